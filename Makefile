@@ -1,0 +1,36 @@
+# Build of libmvc_hip.so (gfx950) and the CPU oracle.
+# -ffp-contract=off is part of the numerical spec (include/mvc_pmath.h).
+ROOT := $(abspath $(dir $(lastword $(MAKEFILE_LIST))))
+PKG := $(ROOT)/multiview-clustering_amd
+SRC := $(PKG)/csrc
+LIB := $(PKG)/lib/libmvc_hip.so
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+            -I$(ROOT)/include -I$(SRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-const-variable
+OBJS := $(PKG)/build/mvc_exact.o $(PKG)/build/mvc_parallel.o $(PKG)/build/mvc_spec.o $(PKG)/build/mvc_api.o
+HDRS := $(ROOT)/include/mvc.h $(ROOT)/include/mvc_pmath.h $(ROOT)/include/mvc_philox.h \
+        $(SRC)/mvc_internal.h $(SRC)/mvc_host.h
+
+all: $(LIB) oracle
+
+$(PKG)/build/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(PKG)/build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(PKG)/build/mvc_api.o: $(SRC)/mvc_api.cpp $(HDRS)
+	@mkdir -p $(PKG)/build
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIB): $(OBJS)
+	@mkdir -p $(PKG)/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJS)
+
+oracle:
+	$(MAKE) -C $(ROOT)/oracle
+
+clean:
+	rm -rf $(PKG)/build $(PKG)/lib
+	$(MAKE) -C $(ROOT)/oracle clean
+
+.PHONY: all oracle clean

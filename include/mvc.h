@@ -1,0 +1,152 @@
+/*
+ * mvc.h — C ABI of libmvc_hip.so, the MI355X-native Gibbs sampler for the
+ * two-level Pitman–Yor multiview clustering model of JunR3/Multiview-Clustering.
+ *
+ * Plain C: no torch or HIP types cross this boundary.  Every entry point
+ * returns an int status (MVC_OK == 0) and never throws; on failure the
+ * message is copied into err[0..errlen) and also kept per thread
+ * (mvc_last_error()).
+ *
+ * Reference interfaces replaced:
+ *   mvc_run()              <- Rcpp::List run_gibbs_cpp(const Rcpp::List& data_views,
+ *                              int M, int burn_in, int thin)
+ *                              /root/reference/Multiview/multiview_gibbs.cpp:105-131
+ *                              (decl. multiview_gibbs.h:8-9).  data_views = V numeric
+ *                              vectors of length n -> views[v] (n*dim doubles each).
+ *   mvc_result_*()         <- the named Rcpp::List built at multiview_gibbs.cpp:121-130
+ *                              (table_of, dish_of, loglik, alpha_v, sigma_v, tau_v,
+ *                              alpha_global, sigma_global).
+ *   mvc_sampler_sweep()    <- void gibbs_sampler(int M, int burn_in, int thin)
+ *                              multiview_gibbs.cpp:134-212 (one call = n_sweeps
+ *                              iterations of the loop at :150).
+ *   mvc_sampler_create()   <- static void initialize_state_from_data()
+ *                              multiview_gibbs.cpp:12-103 + the globals of
+ *                              multiview_state.cpp:4-27 (now per-handle state).
+ *   mvc_sampler_get_state()<- void save_state() multiview_utils.cpp:291-303.
+ *   seed                   <- R's RNG under set.seed() (multiview_utils.cpp:305-306,
+ *                              multiview_gibbs.cpp:26,56; multiview_rng.h is dead code).
+ *                              Replaced by counter-based Philox4x32-10 (mvc_philox.h).
+ *
+ * Integration stubs for R (Rcpp + dlopen) and Python (ctypes): INTEGRATION.md.
+ */
+#ifndef MVC_H
+#define MVC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVC_ABI_VERSION 1
+
+/* status codes */
+#define MVC_OK 0
+#define MVC_ERR_ARG 1        /* invalid argument (sizes, mode, NULL)            */
+#define MVC_ERR_HIP 2        /* HIP runtime error (no device, OOM, launch)       */
+#define MVC_ERR_STATE 3      /* sampler state invariant violated (bug)          */
+#define MVC_ERR_UNSUPPORTED 4
+
+/* schedules */
+#define MVC_MODE_EXACT 0     /* reference schedule, bit-exact vs. the CPU oracle  */
+#define MVC_MODE_PARALLEL 1  /* parallel z-resample sweep          */
+
+typedef struct mvc_config {
+  int32_t n;            /* customers (observations)                              */
+  int32_t n_views;      /* V = length(data_views)                                */
+  int32_t dim;          /* D per view (1 in the reference)                        */
+  int32_t n_iter;       /* M                                                      */
+  int32_t burn_in;      /* burn_in                                                */
+  int32_t thin;         /* thin (>= 1)                                            */
+  uint64_t seed;        /* Philox key                                             */
+  int32_t n_chains;     /* independent chains on this device                      */
+  int32_t first_chain;  /* global id of chain 0 (multi-GPU sharding)              */
+  int32_t device;       /* HIP device ordinal                                     */
+  int32_t mode;         /* MVC_MODE_EXACT | MVC_MODE_PARALLEL                     */
+  int32_t table_cap;    /* initial table capacity per chain (0 = auto)            */
+  int32_t dish_cap;     /* initial dish capacity per view per chain (0 = auto)    */
+  int32_t flags;        /* MVC_FLAG_*                                             */
+} mvc_config;
+
+#define MVC_FLAG_TIMING 1   /* record per-kernel HIP-event times (mvc_sampler_kernel_time) */
+#define MVC_FLAG_QUIET  2   /* no progress lines on stderr                                 */
+
+void mvc_config_init(mvc_config *cfg);   /* fills defaults: thin=1, n_chains=1, ... */
+int mvc_abi_version(void);
+const char *mvc_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* One-shot drop-in: the whole run_gibbs_cpp() call.                          */
+/* views[v] -> host array of n*dim doubles ([n][dim] row-major).              */
+/* ------------------------------------------------------------------------ */
+typedef struct mvc_result mvc_result;
+
+int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out,
+            char *err, size_t errlen);
+
+int mvc_result_num_saved(const mvc_result *r);                 /* S */
+int mvc_result_num_chains(const mvc_result *r);
+int mvc_result_num_tables(const mvc_result *r, int chain, int s);               /* T_s */
+const int32_t *mvc_result_table_of(const mvc_result *r, int chain, int s);      /* n     */
+const int32_t *mvc_result_dish_of(const mvc_result *r, int chain, int s);       /* V*T_s, view-major */
+/* hyperparameter traces: which = MVC_TRACE_*; *_v traces are V*S (view-major) */
+#define MVC_TRACE_ALPHA_V 0
+#define MVC_TRACE_SIGMA_V 1
+#define MVC_TRACE_TAU_V 2
+#define MVC_TRACE_ALPHA_GLOBAL 3
+#define MVC_TRACE_SIGMA_GLOBAL 4
+const double *mvc_result_trace(const mvc_result *r, int chain, int which);
+void mvc_result_free(mvc_result *r);
+
+/* ------------------------------------------------------------------------ */
+/* Handle API: data uploaded once, sweeps enqueued on the handle's stream.    */
+/* ------------------------------------------------------------------------ */
+typedef struct mvc_sampler mvc_sampler;
+
+int mvc_sampler_create(const mvc_config *cfg, const double *const *views, mvc_sampler **out,
+                       char *err, size_t errlen);
+/* Run n_sweeps further iterations (sweep index continues across calls). */
+int mvc_sampler_sweep(mvc_sampler *s, int n_sweeps, char *err, size_t errlen);
+int mvc_sampler_synchronize(mvc_sampler *s, char *err, size_t errlen);
+int mvc_sampler_sweeps_done(const mvc_sampler *s);
+/* Copy one chain's current state: table_of[n] (table positions), *n_tables,
+ * dish_of[V * dish_of_cap] (view-major, raw dish ids, first *n_tables per view
+ * are valid), hyper[3V+2] = tau[V], alpha[V], sigma[V], alpha_g, sigma_g.
+ * Any output pointer may be NULL. */
+int mvc_sampler_get_state(mvc_sampler *s, int chain, int32_t *table_of, int32_t *n_tables,
+                          int32_t *dish_of, int32_t dish_of_cap, double *hyper,
+                          char *err, size_t errlen);
+/* Number of live dishes per view (k_out[V]). */
+int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char *err, size_t errlen);
+/* HIP-event kernel timing (needs MVC_FLAG_TIMING): kernel = "zresample",
+ * "commit", "stats", "hyper", "exact_sweep", or "sweep" (whole sweep). */
+int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms,
+                            int64_t *launches);
+void mvc_sampler_reset_timers(mvc_sampler *s);
+/* Opaque HIP stream the handle launches on (hipStream_t as void*). */
+void *mvc_sampler_stream(mvc_sampler *s);
+void mvc_sampler_destroy(mvc_sampler *s);
+
+/* ------------------------------------------------------------------------ */
+/* Spec primitives on the device (parity tests of RNG / math / reductions).   */
+/* x, out are HOST arrays; computed on the device.                             */
+/* op: 0 exp, 1 log, 2 lgamma, 3 qnorm, 4 sqrt                                 */
+/* ------------------------------------------------------------------------ */
+int mvc_device_math(int device, int op, const double *x, double *out, int64_t n,
+                    char *err, size_t errlen);
+int mvc_device_seq_uniforms(int device, uint64_t seed, uint32_t chain, uint64_t start,
+                            double *out, int64_t n, char *err, size_t errlen);
+/* tree64 sum and select of the parallel mode, one wave per row:
+ * x[rows][n] -> sums[rows], sel[rows] for targets r[rows] (r<sum). */
+int mvc_device_tree64(int device, const double *x, int64_t rows, int64_t n, const double *r,
+                      double *sums, int64_t *sel, char *err, size_t errlen);
+/* G = Y * S1^T with the fma-chain order of DESIGN.md §4.1 on the MFMA path
+ * (Y[n][D], S1[K][D], G[n][K]); used to pin the f64 MFMA accumulation order. */
+int mvc_device_gemm_check(int device, const double *Y, const double *S1, int64_t n, int64_t K,
+                          int64_t D, double *G, char *err, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVC_H */

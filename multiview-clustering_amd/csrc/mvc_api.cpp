@@ -1,0 +1,350 @@
+// mvc_api.cpp — C ABI of libmvc_hip.so (declared in include/mvc.h).
+//
+// Thin dispatch: validates arguments, owns result memory, converts C++
+// exceptions into status codes (nothing throws across the ABI).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "mvc.h"
+#include "mvc_host.h"
+
+namespace mvc {
+
+InitState draw_initial_state(const double *y, int n, int V, int D, uint64_t seed, uint32_t chain) {
+  // multiview_gibbs.cpp:12-62: T0 = 4 tables drawn for i ascending, then per
+  // view K0 = 2 dishes for t ascending, all from R::runif(0, K).
+  InitState S;
+  uint64_t k = 0;
+  auto runif = [&](double a, double b) {
+    if (a == b) return a;
+    return a + (b - a) * mvc_seq_uniform(seed, chain, k++);
+  };
+  S.table.resize(n);
+  for (int i = 0; i < n; ++i) {
+    int t = (int)std::floor(runif(0.0, 4.0));
+    if (t < 0) t = 0;
+    if (t >= 4) t = 3;
+    S.table[i] = t;
+  }
+  S.dish_raw.resize((size_t)V * 4);
+  for (int v = 0; v < V; ++v)
+    for (int t = 0; t < 4; ++t) {
+      int kk = (int)std::floor(runif(0.0, 2.0));
+      if (kk < 0) kk = 0;
+      if (kk >= 2) kk = 1;
+      S.dish_raw[v * 4 + t] = kk;
+    }
+  // tau_v = Var_{n-1}(y_v) * 0.25 * 0.01  (multiview_gibbs.cpp:78-94);
+  // for dim > 1 the mean of the per-dimension variances.
+  S.tau.resize(V);
+  for (int v = 0; v < V; ++v) {
+    double vsum = 0.0;
+    for (int d = 0; d < D; ++d) {
+      double s1 = 0.0;
+      for (int i = 0; i < n; ++i) s1 += y[((size_t)v * n + i) * D + d];
+      const double mean = s1 / std::max(1, n);
+      double var = 0.0;
+      if (n > 1) {
+        for (int i = 0; i < n; ++i) {
+          const double df = y[((size_t)v * n + i) * D + d] - mean;
+          var += df * df;
+        }
+        var /= (n - 1);
+      } else {
+        var = 1.0;
+      }
+      if (var <= 0.0) var = 1.0;
+      vsum += var;
+    }
+    const double var = vsum / (double)D;
+    S.tau[v] = var * 0.25 * 0.01;
+  }
+  S.draws = k;
+  return S;
+}
+
+void Timers::begin(const char *, hipEvent_t *ev) {
+  *ev = nullptr;
+  if (!on) return;
+  MVC_HIP(hipEventCreate(ev));
+  MVC_HIP(hipEventRecord(*ev, stream));
+}
+void Timers::end(const char *name, hipEvent_t a) {
+  if (!on || !a) return;
+  hipEvent_t b;
+  MVC_HIP(hipEventCreate(&b));
+  MVC_HIP(hipEventRecord(b, stream));
+  pending.push_back({a, b, name});
+  if (pending.size() > 4096) {
+    MVC_HIP(hipStreamSynchronize(stream));
+    collect();
+  }
+}
+void Timers::collect() {
+  for (auto &r : pending) {
+    MVC_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    MVC_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    auto &e = acc[r.name];
+    e.first += ms;
+    e.second += 1;
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+  pending.clear();
+}
+void Timers::reset() {
+  if (stream) hipStreamSynchronize(stream);
+  collect();
+  acc.clear();
+}
+Timers::~Timers() {
+  for (auto &r : pending) {
+    hipEventDestroy(r.a);
+    hipEventDestroy(r.b);
+  }
+}
+
+}  // namespace mvc
+
+// ---------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg, char *err, size_t errlen) {
+  g_last_error = msg;
+  if (err && errlen) {
+    std::snprintf(err, errlen, "%s", msg.c_str());
+  }
+  return code;
+}
+
+template <class F>
+int guarded(char *err, size_t errlen, F &&f) {
+  (void)hipGetLastError();   // never report a stale error of an earlier call
+  try {
+    f();
+    g_last_error.clear();
+    return MVC_OK;
+  } catch (const mvc::Error &e) {
+    return fail(e.code, e.what(), err, errlen);
+  } catch (const std::bad_alloc &) {
+    return fail(MVC_ERR_HIP, "host allocation failed", err, errlen);
+  } catch (const std::exception &e) {
+    return fail(MVC_ERR_STATE, e.what(), err, errlen);
+  }
+}
+
+void validate(const mvc_config *c, const double *const *views) {
+  using mvc::Error;
+  if (!c) throw Error(MVC_ERR_ARG, "config is NULL");
+  if (c->n < 2) throw Error(MVC_ERR_ARG, "n must be >= 2 (the reference divides by n-1)");
+  if (c->n_views < 1) throw Error(MVC_ERR_ARG, "n_views must be >= 1");
+  if (c->dim < 1) throw Error(MVC_ERR_ARG, "dim must be >= 1");
+  if (c->n_iter < 0 || c->burn_in < 0) throw Error(MVC_ERR_ARG, "n_iter and burn_in must be >= 0");
+  if (c->thin < 1) throw Error(MVC_ERR_ARG, "thin must be >= 1");
+  if (c->n_chains < 1) throw Error(MVC_ERR_ARG, "n_chains must be >= 1");
+  if (c->mode != MVC_MODE_EXACT && c->mode != MVC_MODE_PARALLEL) throw Error(MVC_ERR_ARG, "unknown mode");
+  if (!views) throw Error(MVC_ERR_ARG, "views is NULL");
+  for (int v = 0; v < c->n_views; ++v)
+    if (!views[v]) throw Error(MVC_ERR_ARG, "views[v] is NULL");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw Error(MVC_ERR_HIP, "no HIP device visible");
+  if (c->device < 0 || c->device >= ndev) throw Error(MVC_ERR_ARG, "device ordinal out of range");
+}
+
+}  // namespace
+
+struct mvc_result {
+  int S = 0, C = 0, n = 0, V = 0;
+  // [chain][s]
+  std::vector<std::vector<std::vector<int32_t>>> table_of, dish_of;
+  std::vector<std::vector<int>> T;
+  // [chain][which] traces
+  std::vector<std::vector<std::vector<double>>> traces;
+};
+
+struct mvc_sampler {
+  std::unique_ptr<mvc::Sampler> impl;
+};
+
+extern "C" {
+
+void mvc_config_init(mvc_config *c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->dim = 1;
+  c->thin = 1;
+  c->n_chains = 1;
+  c->mode = MVC_MODE_EXACT;
+}
+
+int mvc_abi_version(void) { return MVC_ABI_VERSION; }
+const char *mvc_last_error(void) { return g_last_error.c_str(); }
+
+int mvc_sampler_create(const mvc_config *cfg, const double *const *views, mvc_sampler **out, char *err,
+                       size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!out) throw mvc::Error(MVC_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    validate(cfg, views);
+    auto *h = new mvc_sampler();
+    try {
+      h->impl.reset(cfg->mode == MVC_MODE_EXACT ? mvc::make_exact_sampler(*cfg, views)
+                                                : mvc::make_parallel_sampler(*cfg, views));
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int mvc_sampler_sweep(mvc_sampler *s, int n_sweeps, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl) throw mvc::Error(MVC_ERR_ARG, "sampler is NULL");
+    if (n_sweeps < 0) throw mvc::Error(MVC_ERR_ARG, "n_sweeps < 0");
+    s->impl->sweep(n_sweeps);
+  });
+}
+
+int mvc_sampler_synchronize(mvc_sampler *s, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl) throw mvc::Error(MVC_ERR_ARG, "sampler is NULL");
+    s->impl->synchronize();
+  });
+}
+
+int mvc_sampler_sweeps_done(const mvc_sampler *s) { return (s && s->impl) ? s->impl->sweeps_done : -1; }
+
+int mvc_sampler_get_state(mvc_sampler *s, int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of,
+                          int32_t dish_of_cap, double *hyper, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl) throw mvc::Error(MVC_ERR_ARG, "sampler is NULL");
+    s->impl->get_state(chain, table_of, n_tables, dish_of, dish_of_cap, hyper);
+  });
+}
+
+int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl || !k_out) throw mvc::Error(MVC_ERR_ARG, "NULL argument");
+    s->impl->get_dish_counts(chain, k_out);
+  });
+}
+
+int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms, int64_t *launches) {
+  if (!s || !s->impl || !kernel) return MVC_ERR_ARG;
+  try {
+    s->impl->synchronize();
+  } catch (...) {
+    return MVC_ERR_HIP;
+  }
+  auto &acc = s->impl->timers.acc;
+  auto it = acc.find(kernel);
+  if (total_ms) *total_ms = it == acc.end() ? 0.0 : it->second.first;
+  if (launches) *launches = it == acc.end() ? 0 : it->second.second;
+  return MVC_OK;
+}
+
+void mvc_sampler_reset_timers(mvc_sampler *s) {
+  if (s && s->impl) s->impl->timers.reset();
+}
+
+void *mvc_sampler_stream(mvc_sampler *s) { return (s && s->impl) ? (void *)s->impl->stream : nullptr; }
+
+void mvc_sampler_destroy(mvc_sampler *s) { delete s; }
+
+int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!out) throw mvc::Error(MVC_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    validate(cfg, views);
+    std::unique_ptr<mvc::Sampler> S(cfg->mode == MVC_MODE_EXACT ? mvc::make_exact_sampler(*cfg, views)
+                                                                : mvc::make_parallel_sampler(*cfg, views));
+    auto R = std::make_unique<mvc_result>();
+    const int C = cfg->n_chains, V = cfg->n_views, n = cfg->n;
+    R->C = C;
+    R->n = n;
+    R->V = V;
+    R->table_of.resize(C);
+    R->dish_of.resize(C);
+    R->T.resize(C);
+    R->traces.assign(C, std::vector<std::vector<double>>(5));
+    std::vector<std::vector<std::vector<double>>> hv(C);   // [chain][s] hyper vectors
+    std::vector<double> hyper(3 * V + 2);
+    const bool quiet = (cfg->flags & MVC_FLAG_QUIET) != 0;
+    for (int iter = 0; iter < cfg->n_iter; ++iter) {
+      if (!quiet && (iter + 1) % 100 == 0)                          // gibbs.cpp:152-155
+        std::fprintf(stderr, "Iteration %d / %d\n", iter + 1, cfg->n_iter);
+      S->sweep(1);
+      if (iter >= cfg->burn_in && ((iter - cfg->burn_in) % cfg->thin == 0)) {   // gibbs.cpp:205
+        for (int c = 0; c < C; ++c) {
+          std::vector<int32_t> t(n);
+          int32_t T = 0;
+          // first query T, then fetch dish_of with an exact capacity
+          S->get_state(c, t.data(), &T, nullptr, 0, hyper.data());
+          std::vector<int32_t> d((size_t)V * std::max(T, 1));
+          S->get_state(c, nullptr, &T, d.data(), std::max(T, 1), nullptr);
+          d.resize((size_t)V * T);
+          R->table_of[c].push_back(std::move(t));
+          R->dish_of[c].push_back(std::move(d));
+          R->T[c].push_back(T);
+          hv[c].push_back(hyper);
+        }
+        R->S++;
+      }
+    }
+    S->synchronize();
+    const int Sn = R->S;
+    for (int c = 0; c < C; ++c) {
+      auto &tr = R->traces[c];
+      tr[MVC_TRACE_ALPHA_V].resize((size_t)V * Sn);
+      tr[MVC_TRACE_SIGMA_V].resize((size_t)V * Sn);
+      tr[MVC_TRACE_TAU_V].resize((size_t)V * Sn);
+      tr[MVC_TRACE_ALPHA_GLOBAL].resize(Sn);
+      tr[MVC_TRACE_SIGMA_GLOBAL].resize(Sn);
+      for (int s = 0; s < Sn; ++s) {
+        const auto &h = hv[c][s];
+        for (int v = 0; v < V; ++v) {
+          tr[MVC_TRACE_TAU_V][(size_t)v * Sn + s] = h[v];
+          tr[MVC_TRACE_ALPHA_V][(size_t)v * Sn + s] = h[V + v];
+          tr[MVC_TRACE_SIGMA_V][(size_t)v * Sn + s] = h[2 * V + v];
+        }
+        tr[MVC_TRACE_ALPHA_GLOBAL][s] = h[3 * V];
+        tr[MVC_TRACE_SIGMA_GLOBAL][s] = h[3 * V + 1];
+      }
+    }
+    *out = R.release();
+  });
+}
+
+int mvc_result_num_saved(const mvc_result *r) { return r ? r->S : -1; }
+int mvc_result_num_chains(const mvc_result *r) { return r ? r->C : -1; }
+int mvc_result_num_tables(const mvc_result *r, int chain, int s) {
+  if (!r || chain < 0 || chain >= r->C || s < 0 || s >= r->S) return -1;
+  return r->T[chain][s];
+}
+const int32_t *mvc_result_table_of(const mvc_result *r, int chain, int s) {
+  if (!r || chain < 0 || chain >= r->C || s < 0 || s >= r->S) return nullptr;
+  return r->table_of[chain][s].data();
+}
+const int32_t *mvc_result_dish_of(const mvc_result *r, int chain, int s) {
+  if (!r || chain < 0 || chain >= r->C || s < 0 || s >= r->S) return nullptr;
+  return r->dish_of[chain][s].data();
+}
+const double *mvc_result_trace(const mvc_result *r, int chain, int which) {
+  if (!r || chain < 0 || chain >= r->C || which < 0 || which > 4) return nullptr;
+  return r->traces[chain][which].data();
+}
+void mvc_result_free(mvc_result *r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,984 @@
+// mvc_exact.hip — the reference's sequential Gibbs schedule on gfx950.
+//
+// One 64-lane workgroup (one wavefront) owns one chain and walks the
+// customer loop of multiview_gibbs.cpp:157-200 in order; lanes parallelise
+// each step over tables (positions), live dishes and views.  Every fp64
+// operation is the reference's, in the reference's order, with the portable
+// exp/log of include/mvc_pmath.h, so the chain is bit-identical to the
+// PortableMath ExactSampler of oracle/mvc_oracle.cpp for the same Philox seed.
+//
+// Many chains run side by side (grid = chains); this is where the GPU's
+// throughput comes from: the schedule itself is a dependent chain of n
+// small steps.
+//
+// Compile with -ffp-contract=off (Makefile).
+#include "mvc_internal.h"
+
+namespace {
+
+// multiview_utils.cpp:307-338 compute_f_vk, literal expression order.
+__device__ __forceinline__ double ref_f_vk(int nk, double S1, double S2, double tau, double yvi) {
+  const double term1_old = -0.5 * S2 / tau;
+  const double term2_old = 0.5 * (S1 * S1) / (tau * (tau + nk));
+  const double log_det_old = -0.5 * nk * mvc_log(2.0 * MVC_PI * tau) - 0.5 * mvc_log(tau * (tau + nk));
+  const int n_new = nk + 1;
+  const double S1_new = S1 + yvi;
+  const double S2_new = S2 + yvi * yvi;
+  const double term1_new = -0.5 * S2_new / tau;
+  const double term2_new = 0.5 * (S1_new * S1_new) / (tau * (tau + n_new));
+  const double log_det_new = -0.5 * n_new * mvc_log(2.0 * MVC_PI * tau) - 0.5 * mvc_log(tau * (tau + n_new));
+  const double lp = (log_det_new + term1_new + term2_new) - (log_det_old + term1_old + term2_old);
+  return mvc_exp(lp);
+}
+
+// multiview_utils.cpp:340-350 compute_f_vk_new
+__device__ __forceinline__ double ref_f_new(double tau, double yvi) {
+  const double log_norm = -0.5 * mvc_log(2.0 * MVC_PI * tau);
+  const double log_exp = -0.5 * (yvi * yvi) / tau;
+  return mvc_exp(log_norm + log_exp);
+}
+
+constexpr double kEps = 1e-6;   // multiview_hyper.cpp:13
+
+struct Shared {
+  int Kact[MVC_MAXV];
+  int next_id[MVC_MAXV];
+  int Koff[MVC_MAXV + 1];
+  int died[MVC_MAXV];
+  int draw_ix[MVC_MAXV];
+  double hyp[3 * MVC_MAXV + 2];
+  double ys[MVC_MAXV];
+  double fnew[MVC_MAXV];
+  double marg[MVC_MAXV];
+  double tw[MVC_MAXV];
+  double buf[MVC_WAVE];
+  double dv[4];
+  int iv[8];
+};
+
+// ---------------------------------------------------------------------------
+// hyperparameter MH (multiview_hyper.cpp:211-292), executed by the wave.
+// Sums are accumulated in the reference's order by lane 0; lanes only
+// produce the addends.
+// ---------------------------------------------------------------------------
+struct MH {
+  ExactChain &C;
+  Shared &sh;
+  int V, n, lane;
+  uint64_t seed;
+
+  __device__ double unif() {   // lane 0 only
+    return mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws++);
+  }
+  __device__ double rnorm(double mu, double sd) {  // lane 0 only
+    const double u1 = unif();
+    const double u2 = unif();
+    return mu + sd * mvc_norm_from_uniforms(u1, u2);
+  }
+  __device__ double bcast(double x) {
+    if (lane == 0) sh.dv[0] = x;
+    __syncthreads();
+    const double r = sh.dv[0];
+    __syncthreads();
+    return r;
+  }
+  static __device__ double prior_alpha(double a) {
+    if (a <= 0.0) return -MVC_PM_INF;
+    return (4.0 - 1.0) * mvc_log(a) - 3.0 * a;
+  }
+  static __device__ double prior_sigma(double s) {
+    if (s <= 0.0 || s >= 1.0) return -MVC_PM_INF;
+    return (1.0 - 1.0) * mvc_log(s) + (5.0 - 1.0) * mvc_log(1.0 - s);
+  }
+  // hyper.cpp:176-209 (all lanes call; result valid on all lanes)
+  __device__ double post_tau(int v, double tau) {
+    if (tau <= 0.0) return -MVC_PM_INF;
+    const int K = sh.Kact[v];
+    const int KC = C.KC;
+    double ll = 0.0;
+    for (int base = 0; base < K; base += MVC_WAVE) {
+      const int j = base + lane;
+      double term = 0.0;
+      if (j < K) {
+        const int nk = C.d_n[v * KC + j];
+        if (nk != 0) {
+          const double sy = C.d_S1[v * KC + j], sy2 = C.d_S2[v * KC + j];
+          double sse = sy2 - (sy * sy) / (double)nk;
+          if (sse < 0.0) sse = 0.0;
+          term = -0.5 * nk * mvc_log(2.0 * MVC_PI * tau) - 0.5 * (sse / tau);
+        }
+      }
+      sh.buf[lane] = term;
+      __syncthreads();
+      if (lane == 0) {
+        const int cnt = min(MVC_WAVE, K - base);
+        for (int q = 0; q < cnt; ++q)
+          if (C.d_n[v * KC + base + q] != 0) ll += sh.buf[q];
+      }
+      __syncthreads();
+    }
+    ll = bcast(ll);
+    const double prior = 2.0 * mvc_log(1.0) - 0.0 - (2.0 + 1.0) * mvc_log(tau) - 1.0 / tau;
+    return ll + prior;
+  }
+  // hyper.cpp:295-342 log_EPPF over live dishes of view v
+  __device__ double eppf_view(int v, double alpha, double sigma) {
+    if (!(sigma > kEps && sigma < 1.0 - kEps)) return -MVC_PM_INF;
+    if (alpha <= -sigma) return -MVC_PM_INF;
+    const int K = sh.Kact[v];
+    const int KC = C.KC;
+    int total = 0;
+    for (int j = 0; j < K; ++j) total += C.d_l[v * KC + j];   // uniform loop
+    if (total == 0) return 0.0;
+    double lp = 0.0;
+    int bad = 0;
+    // sum_j log(alpha + j*sigma), j < K_active
+    for (int base = 0; base < K; base += MVC_WAVE) {
+      const int j = base + lane;
+      double t = 0.0;
+      if (j < K) { const double term = alpha + j * sigma; if (term <= 0.0) bad = 1; t = mvc_log(term); }
+      sh.buf[lane] = t;
+      __syncthreads();
+      if (lane == 0) { const int c = min(MVC_WAVE, K - base); for (int q = 0; q < c; ++q) lp += sh.buf[q]; }
+      __syncthreads();
+    }
+    // - sum_{i=1}^{total-1} log(alpha + i)
+    for (int base = 1; base < total; base += MVC_WAVE) {
+      const int i = base + lane;
+      double t = 0.0;
+      if (i < total) { const double term = alpha + i; if (term <= 0.0) bad = 1; t = mvc_log(term); }
+      sh.buf[lane] = t;
+      __syncthreads();
+      if (lane == 0) { const int c = min(MVC_WAVE, total - base); for (int q = 0; q < c; ++q) lp -= sh.buf[q]; }
+      __syncthreads();
+    }
+    // + sum_k sum_{m=1}^{l_k-1} log(m - sigma), k ascending
+    int maxl = 0;
+    for (int j = 0; j < K; ++j) maxl = max(maxl, C.d_l[v * KC + j]);
+    for (int m = 1 + lane; m < maxl; m += MVC_WAVE) {
+      const double term = (double)m - sigma;
+      if (term <= 0.0) bad = 1;
+      C.mhbuf[m] = mvc_log(term);
+    }
+    __syncthreads();
+    if (lane == 0)
+      for (int j = 0; j < K; ++j) {
+        const int lk = C.d_l[v * KC + j];
+        for (int m = 1; m < lk; ++m) lp += C.mhbuf[m];
+      }
+    __syncthreads();
+    bad = __any(bad);
+    lp = bcast(lp);
+    return bad ? -MVC_PM_INF : lp;
+  }
+  // hyper.cpp:53-83 log_global_EPPF
+  __device__ double eppf_global(double alpha, double sigma) {
+    if (!(sigma > kEps && sigma < 1.0 - kEps)) return -MVC_PM_INF;
+    if (alpha <= -sigma) return -MVC_PM_INF;
+    const int T = C.T;
+    if (T <= 0) return 0.0;
+    double lp = 0.0;
+    int bad = 0;
+    for (int base = 0; base < T; base += MVC_WAVE) {
+      const int j = base + lane;
+      double t = 0.0;
+      if (j < T) { const double term = alpha + j * sigma; if (term <= 0.0) bad = 1; t = mvc_log(term); }
+      sh.buf[lane] = t;
+      __syncthreads();
+      if (lane == 0) { const int c = min(MVC_WAVE, T - base); for (int q = 0; q < c; ++q) lp += sh.buf[q]; }
+      __syncthreads();
+    }
+    for (int base = 1; base < n; base += MVC_WAVE) {
+      const int i = base + lane;
+      double t = 0.0;
+      if (i < n) { const double term = alpha + i; if (term <= 0.0) bad = 1; t = mvc_log(term); }
+      sh.buf[lane] = t;
+      __syncthreads();
+      if (lane == 0) { const int c = min(MVC_WAVE, n - base); for (int q = 0; q < c; ++q) lp -= sh.buf[q]; }
+      __syncthreads();
+    }
+    int maxc = 0;
+    for (int p = lane; p < T; p += MVC_WAVE) maxc = max(maxc, C.n_t[C.slot_at_pos[p]]);
+    for (int m = 32; m >= 1; m >>= 1) maxc = max(maxc, __shfl_xor(maxc, m, 64));
+    for (int m = 1 + lane; m < maxc; m += MVC_WAVE) {
+      const double term = (double)m - sigma;
+      if (term <= 0.0) bad = 1;
+      C.mhbuf[m] = mvc_log(term);
+    }
+    __syncthreads();
+    if (lane == 0)
+      for (int p = 0; p < T; ++p) {   // n_t in position order (hyper.cpp:74)
+        const int c = C.n_t[C.slot_at_pos[p]];
+        for (int m = 1; m < c; ++m) lp += C.mhbuf[m];
+      }
+    __syncthreads();
+    bad = __any(bad);
+    lp = bcast(lp);
+    return bad ? -MVC_PM_INF : lp;
+  }
+  static __device__ double reflect_unit(double value) {   // hyper.cpp:110-122
+    double p = value;
+    while (p <= kEps || p >= 1.0 - kEps) {
+      if (p <= kEps) p = 2.0 * kEps - p;
+      if (p >= 1.0 - kEps) p = 2.0 * (1.0 - kEps) - p;
+    }
+    return p < kEps ? kEps : (p > 1.0 - kEps ? 1.0 - kEps : p);
+  }
+  __device__ double propose_alpha(double a_old) {   // hyper.cpp:100-108, lane 0
+    double la = mvc_log(a_old > kEps ? a_old : kEps);
+    la += rnorm(0.0, 0.1);
+    const double c = mvc_exp(la);
+    return (c > kEps) ? c : kEps;
+  }
+  // hyper.cpp:233-292 update_hyperparameters
+  __device__ void run() {
+    double *tau = sh.hyp, *alpha = sh.hyp + V, *sigma = sh.hyp + 2 * V;
+    double &ag = sh.hyp[3 * V], &sg = sh.hyp[3 * V + 1];
+    for (int v = 0; v < V; ++v) {                                    // :211-231
+      double t_old = tau[v];
+      if (t_old <= 0.0) t_old = kEps;
+      const double l_old = post_tau(v, t_old);
+      double t_prop = 0.0;
+      if (lane == 0) t_prop = mvc_exp(mvc_log(t_old) + rnorm(0.0, 0.3));
+      t_prop = bcast(t_prop);
+      if (t_prop <= 0.0) continue;
+      const double l_new = post_tau(v, t_prop);
+      const double lq = mvc_log(t_prop) - mvc_log(t_old);
+      const double acc = (l_new - l_old) + lq;
+      if (lane == 0 && mvc_log(unif()) < acc) tau[v] = t_prop;
+      __syncthreads();
+    }
+    for (int v = 0; v < V; ++v) {
+      double a_old = alpha[v];
+      if (a_old <= 0.0) a_old = kEps;
+      double a_prop = 0.0;
+      if (lane == 0) a_prop = propose_alpha(a_old);
+      a_prop = bcast(a_prop);
+      const double lo = (a_old <= 0.0) ? -MVC_PM_INF : eppf_view(v, a_old, sigma[v]) + prior_alpha(a_old);
+      const double ln = (a_prop <= 0.0) ? -MVC_PM_INF : eppf_view(v, a_prop, sigma[v]) + prior_alpha(a_prop);
+      const double lq = mvc_log(a_prop) - mvc_log(a_old);
+      if (lane == 0 && mvc_log(unif()) < (ln - lo) + lq) alpha[v] = a_prop;
+      __syncthreads();
+      const double s_old = sigma[v];
+      double s_prop = 0.0, u = 0.0;
+      if (lane == 0) { s_prop = reflect_unit(s_old + rnorm(0.0, 0.05)); u = unif(); }
+      s_prop = bcast(s_prop);
+      const double av = alpha[v];
+      const double pn = (s_prop <= kEps || s_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(v, av, s_prop) + prior_sigma(s_prop);
+      const double po = (s_old <= kEps || s_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(v, av, s_old) + prior_sigma(s_old);
+      if (lane == 0 && mvc_log(u) < pn - po) sigma[v] = s_prop;
+      __syncthreads();
+    }
+    double ag_old = ag;
+    if (ag_old <= 0.0) ag_old = kEps;
+    double ag_prop = 0.0;
+    if (lane == 0) ag_prop = propose_alpha(ag_old);
+    ag_prop = bcast(ag_prop);
+    const double sg0 = sg;
+    const double lo = eppf_global(ag_old, sg0) + prior_alpha(ag_old);
+    const double ln = eppf_global(ag_prop, sg0) + prior_alpha(ag_prop);
+    const double lq = mvc_log(ag_prop) - mvc_log(ag_old);
+    if (lane == 0 && mvc_log(unif()) < (ln - lo) + lq) ag = ag_prop;
+    __syncthreads();
+    const double sg_old = sg;
+    double sg_prop = 0.0, u = 0.0;
+    if (lane == 0) { sg_prop = reflect_unit(sg_old + rnorm(0.0, 0.05)); u = unif(); }
+    sg_prop = bcast(sg_prop);
+    const double a_g = ag;
+    const double pn = (sg_prop <= kEps || sg_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_prop) + prior_sigma(sg_prop);
+    const double po = (sg_old <= kEps || sg_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_old) + prior_sigma(sg_old);
+    if (lane == 0 && mvc_log(u) < pn - po) sg = sg_prop;
+    __syncthreads();
+  }
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// One sweep (or the rest of one) for every chain: grid = chains, block = 64.
+// ---------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
+    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed) {
+  __shared__ Shared sh;
+  ExactChain &Cg = chains[blockIdx.x];
+  ExactChain C = Cg;               // pointers + scalars in registers
+  const int lane = threadIdx.x;
+  if (C.status == MVC_ST_DONE || C.status == MVC_ST_ERROR) return;
+  const int TC = C.TC, KC = C.KC;
+
+  for (int v = lane; v < V; v += MVC_WAVE) {
+    sh.Kact[v] = C.Kact[v];
+    sh.next_id[v] = C.next_id[v];
+  }
+  for (int q = lane; q < 3 * V + 2; q += MVC_WAVE) sh.hyp[q] = C.hyper[q];
+  __syncthreads();
+
+  int T = C.T;
+  int n_free = C.n_free;
+  const double *tau = sh.hyp, *alpha = sh.hyp + V, *sigma = sh.hyp + 2 * V;
+  const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];
+  int status = MVC_ST_RUNNING;
+  int i = C.resume_i;
+
+  for (; i < n; ++i) {
+    // -------- capacity guard (every step may add 1 table and 1 dish/view)
+    int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
+    for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
+    if (need) { status = MVC_ST_OVERFLOW; break; }
+
+    if (lane < V) sh.ys[lane] = y[(size_t)lane * n + i];
+    // ---------------- remove_customer(i)   utils.cpp:138-192
+    const int s = C.z[i];
+    __syncthreads();
+    if (lane < V) {
+      const int k = C.dish[lane * TC + s];
+      const double yv = sh.ys[lane];
+      C.d_n[lane * KC + k] -= 1;
+      C.d_S1[lane * KC + k] -= yv;
+      C.d_S2[lane * KC + k] -= yv * yv;
+    }
+    int nt_s = C.n_t[s] - 1;
+    __syncthreads();
+    if (lane == 0) C.n_t[s] = nt_s;
+    if (nt_s == 0) {
+      // table dies: l_vk-- (:170-173), swap-and-pop (:175-190)
+      if (lane < V) {
+        const int k = C.dish[lane * TC + s];
+        int dead = -1;
+        if (k >= 0) {
+          const int l = C.d_l[lane * KC + k];
+          if (l > 0) {
+            C.d_l[lane * KC + k] = l - 1;
+            if (l - 1 == 0) dead = k;
+          }
+        }
+        sh.died[lane] = dead;
+      }
+      const int pos = C.pos_of_slot[s];
+      const int last = T - 1;
+      __syncthreads();
+      if (lane == 0) {
+        if (pos != last) {
+          const int sl = C.slot_at_pos[last];
+          C.slot_at_pos[pos] = sl;
+          C.pos_of_slot[sl] = pos;
+        }
+        C.free_slots[n_free] = s;
+      }
+      T -= 1;
+      n_free += 1;
+      __syncthreads();
+      // compact the live dish list of every view whose dish died
+      for (int v = 0; v < V; ++v) {
+        const int k = sh.died[v];
+        if (k < 0) continue;
+        const int K = sh.Kact[v];
+        // shift entries k+1..K-1 down by one (read all, barrier, write)
+        for (int base = k + 1; base < K; base += MVC_WAVE) {
+          const int j = base + lane;
+          int id = 0, nn = 0, ll = 0;
+          double s1 = 0.0, s2 = 0.0;
+          if (j < K) {
+            id = C.d_id[v * KC + j]; nn = C.d_n[v * KC + j]; ll = C.d_l[v * KC + j];
+            s1 = C.d_S1[v * KC + j]; s2 = C.d_S2[v * KC + j];
+          }
+          __syncthreads();
+          if (j < K) {
+            C.d_id[v * KC + j - 1] = id; C.d_n[v * KC + j - 1] = nn; C.d_l[v * KC + j - 1] = ll;
+            C.d_S1[v * KC + j - 1] = s1; C.d_S2[v * KC + j - 1] = s2;
+          }
+          __syncthreads();
+        }
+        for (int p = lane; p < T; p += MVC_WAVE) {
+          const int sl = C.slot_at_pos[p];
+          const int dk = C.dish[v * TC + sl];
+          if (dk > k) C.dish[v * TC + sl] = dk - 1;
+        }
+        __syncthreads();
+        if (lane == 0) sh.Kact[v] = K - 1;
+        __syncthreads();
+      }
+    }
+
+    // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
+    if (lane == 0) {
+      int acc = 0;
+      for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
+      sh.Koff[V] = acc;
+    }
+    __syncthreads();
+    const int Ktot = sh.Koff[V];
+    for (int e = lane; e < Ktot; e += MVC_WAVE) {
+      int v = 0;
+      while (sh.Koff[v + 1] <= e) ++v;
+      const int j = e - sh.Koff[v];
+      const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v]);
+      C.f[v * KC + j] = f;
+      C.logf[v * KC + j] = mvc_log(f);
+    }
+    if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane]);
+    __syncthreads();
+
+    // ---------------- marginal of a new table per view (utils.cpp:40-69)
+    if (lane < V) {
+      const int v = lane;
+      const int K = sh.Kact[v];
+      double total = 0.0;
+      for (int j = 0; j < K; ++j) total += C.d_l[v * KC + j];
+      const double denom = alpha[v] + total;
+      double m;
+      if (denom <= 0.0) {
+        m = sh.fnew[v];
+      } else {
+        double acc = 0.0;
+        for (int j = 0; j < K; ++j) {
+          double w = (C.d_l[v * KC + j] - sigma[v]);
+          if (w < 0.0) w = 0.0;
+          acc += w * C.f[v * KC + j];
+        }
+        double wn = (alpha[v] + K * sigma[v]);
+        if (wn < 0.0) wn = 0.0;
+        acc += wn * sh.fnew[v];
+        m = acc / denom;
+      }
+      sh.marg[v] = m;
+    }
+
+    // ---------------- table probabilities (utils.cpp:83-116)
+    int tne = 0;
+    for (int p = lane; p < T; p += MVC_WAVE) {
+      const int sl = C.slot_at_pos[p];
+      const int nt = C.n_t[sl];
+      double pr = 0.0;
+      if (nt != 0) {
+        ++tne;
+        double lpt = 0.0;
+        for (int v = 0; v < V; ++v) lpt += C.logf[v * KC + C.dish[v * TC + sl]];
+        const double mass = nt - sg;
+        pr = (mass <= 0.0) ? 0.0 : mass * mvc_exp(lpt);
+      }
+      C.P[p] = pr;
+    }
+    for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
+    __syncthreads();
+
+    // ---------------- normaliser, draw (gibbs.cpp:169-191)
+    if (lane == 0) {
+      double lnew = 0.0;
+      for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
+      const double mass_new = ag + sg * tne;                          // :124-135
+      const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
+      double sum_p = p_new;
+      for (int p = 0; p < T; ++p) sum_p += C.P[p];
+      sh.dv[1] = sum_p;
+    }
+    __syncthreads();
+    const double sum_p = sh.dv[1];
+    int t_star;
+    if (sum_p <= 0.0) {
+      t_star = -2;                       // gibbs.cpp:172-176 -> table at position 0
+    } else {
+      for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
+      __syncthreads();
+      if (lane == 0) {
+        const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
+        double cum = 0.0;
+        int ts = -1;
+        for (int p = 0; p < T; ++p) {
+          cum += C.P[p];
+          if (u < cum) { ts = p; break; }
+        }
+        sh.iv[0] = ts;
+      }
+      C.draws += 1;
+      __syncthreads();
+      t_star = sh.iv[0];
+    }
+
+    if (t_star != -1) {
+      // add_customer_to_existing_table (utils.cpp:194-207)
+      const int sl = C.slot_at_pos[t_star < 0 ? 0 : t_star];
+      __syncthreads();
+      if (lane == 0) { C.z[i] = sl; C.n_t[sl] = C.n_t[sl] + 1; }
+      if (lane < V) {
+        const int k = C.dish[lane * TC + sl];
+        const double yv = sh.ys[lane];
+        C.d_n[lane * KC + k] += 1;
+        C.d_S1[lane * KC + k] += yv;
+        C.d_S2[lane * KC + k] += yv * yv;
+      }
+      __syncthreads();
+    } else {
+      // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
+      n_free -= 1;
+      const int sl = C.free_slots[n_free];
+      const int pos = T;
+      __syncthreads();
+      if (lane == 0) {
+        C.slot_at_pos[pos] = sl;
+        C.pos_of_slot[sl] = pos;
+        C.n_t[sl] = 1;
+        C.z[i] = sl;
+      }
+      T += 1;
+      // assign_dishes_new_table (utils.cpp:278-289): per view weights
+      if (lane < V) {
+        const int v = lane;
+        const int K = sh.Kact[v];
+        double total = 0.0;
+        for (int j = 0; j < K; ++j) {
+          double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
+          if (w < 0) w = 0;
+          total += w;
+        }
+        double wn = (alpha[v] + sigma[v] * K) * sh.fnew[v];
+        if (wn < 0) wn = 0;
+        total += wn;
+        sh.tw[v] = total;
+      }
+      __syncthreads();
+      if (lane == 0) {                       // draws are consumed in view order
+        uint64_t d = C.draws;
+        for (int v = 0; v < V; ++v) sh.draw_ix[v] = (sh.tw[v] <= 0) ? -1 : (int)(d++ - C.draws);
+        sh.iv[1] = (int)(d - C.draws);
+      }
+      __syncthreads();
+      if (lane < V) {
+        const int v = lane;
+        const int K = sh.Kact[v];
+        int kk = -1;
+        const double total = sh.tw[v];
+        if (total > 0) {
+          const double u = 0.0 + (total - 0.0) * mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws + (uint64_t)sh.draw_ix[v]);
+          double cum = 0;
+          for (int j = 0; j < K; ++j) {
+            double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
+            if (w < 0) w = 0;
+            cum += w;
+            if (u < cum) { kk = j; break; }
+          }
+        }
+        if (kk < 0) {                        // fresh dish slot (utils.cpp:250-258,268-275)
+          kk = K;
+          C.d_id[v * KC + kk] = sh.next_id[v];
+          C.d_n[v * KC + kk] = 0;
+          C.d_l[v * KC + kk] = 0;
+          C.d_S1[v * KC + kk] = 0.0;
+          C.d_S2[v * KC + kk] = 0.0;
+          sh.next_id[v] += 1;
+          sh.Kact[v] = K + 1;
+        }
+        const double yv = sh.ys[v];
+        C.dish[v * TC + sl] = kk;
+        C.d_l[v * KC + kk] += 1;
+        C.d_n[v * KC + kk] += 1;
+        C.d_S1[v * KC + kk] += yv;
+        C.d_S2[v * KC + kk] += yv * yv;
+      }
+      C.draws += (uint64_t)sh.iv[1];
+      __syncthreads();
+    }
+  }
+
+  if (status == MVC_ST_RUNNING) {
+    // end of sweep: hyperparameters (gibbs.cpp:202)
+    C.T = T;
+    MH mh{C, sh, V, n, lane, seed};
+    mh.run();
+    status = MVC_ST_DONE;
+    i = n;
+  }
+  __syncthreads();
+  for (int v = lane; v < V; v += MVC_WAVE) {
+    C.Kact[v] = sh.Kact[v];
+    C.next_id[v] = sh.next_id[v];
+  }
+  for (int q = lane; q < 3 * V + 2; q += MVC_WAVE) C.hyper[q] = sh.hyp[q];
+  if (lane == 0) {
+    Cg.T = T;
+    Cg.n_free = n_free;
+    Cg.draws = C.draws;
+    Cg.resume_i = i;
+    Cg.status = status;
+  }
+}
+
+// Snapshot of one chain in reference output form (utils.cpp:291-303):
+// table_of[i] = position of i's table; dish_of[v][p] = raw dish id.
+extern "C" __global__ void mvc_exact_snapshot_kernel(int n, int V, const ExactChain *chains, int chain,
+                                                     int32_t *table_of, int32_t *dish_of, int dish_cap) {
+  const ExactChain &C = chains[chain];
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int stride = gridDim.x * blockDim.x;
+  for (int i = tid; i < n; i += stride) table_of[i] = C.pos_of_slot[C.z[i]];
+  const int T = C.T;
+  for (int e = tid; e < V * T; e += stride) {
+    const int v = e / T, p = e % T;
+    if (p < dish_cap) dish_of[v * dish_cap + p] = C.d_id[v * C.KC + C.dish[v * C.TC + C.slot_at_pos[p]]];
+  }
+}
+
+// ===========================================================================
+// Host side of the exact schedule.
+// ===========================================================================
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "mvc_host.h"
+
+namespace mvc {
+
+namespace {
+
+// Device allocation of one chain at capacities (TC, KC); host mirror of the
+// struct keeps the device pointers.
+struct ExactAlloc {
+  ExactChain h{};          // host copy of the device struct
+  void *block = nullptr;   // single device allocation
+};
+
+size_t exact_bytes(int n, int V, int TC, int KC) {
+  size_t b = 0;
+  auto add = [&](size_t x) { b += (x + 255) & ~(size_t)255; };
+  add(sizeof(int32_t) * n);                 // z
+  for (int k = 0; k < 4; ++k) add(sizeof(int32_t) * TC);  // n_t pos slot free
+  add(sizeof(int32_t) * (size_t)V * TC);    // dish
+  for (int k = 0; k < 3; ++k) add(sizeof(int32_t) * (size_t)V * KC);
+  for (int k = 0; k < 4; ++k) add(sizeof(double) * (size_t)V * KC);  // S1 S2 f logf
+  add(sizeof(double) * TC);                 // P
+  add(sizeof(double) * (size_t)(n + 1));    // mhbuf
+  add(sizeof(int32_t) * V);                 // Kact
+  add(sizeof(int32_t) * V);                 // next_id
+  add(sizeof(double) * (3 * V + 2));        // hyper
+  return b;
+}
+
+void carve(ExactAlloc &A, int n, int V, int TC, int KC) {
+  char *p = (char *)A.block;
+  auto take = [&](size_t x) { char *r = p; p += (x + 255) & ~(size_t)255; return (void *)r; };
+  ExactChain &C = A.h;
+  C.TC = TC;
+  C.KC = KC;
+  C.z = (int32_t *)take(sizeof(int32_t) * n);
+  C.n_t = (int32_t *)take(sizeof(int32_t) * TC);
+  C.pos_of_slot = (int32_t *)take(sizeof(int32_t) * TC);
+  C.slot_at_pos = (int32_t *)take(sizeof(int32_t) * TC);
+  C.free_slots = (int32_t *)take(sizeof(int32_t) * TC);
+  C.dish = (int32_t *)take(sizeof(int32_t) * (size_t)V * TC);
+  C.d_id = (int32_t *)take(sizeof(int32_t) * (size_t)V * KC);
+  C.d_n = (int32_t *)take(sizeof(int32_t) * (size_t)V * KC);
+  C.d_l = (int32_t *)take(sizeof(int32_t) * (size_t)V * KC);
+  C.d_S1 = (double *)take(sizeof(double) * (size_t)V * KC);
+  C.d_S2 = (double *)take(sizeof(double) * (size_t)V * KC);
+  C.f = (double *)take(sizeof(double) * (size_t)V * KC);
+  C.logf = (double *)take(sizeof(double) * (size_t)V * KC);
+  C.P = (double *)take(sizeof(double) * TC);
+  C.mhbuf = (double *)take(sizeof(double) * (size_t)(n + 1));
+  C.Kact = (int32_t *)take(sizeof(int32_t) * V);
+  C.next_id = (int32_t *)take(sizeof(int32_t) * V);
+  C.hyper = (double *)take(sizeof(double) * (3 * V + 2));
+}
+
+// Host-side image of a chain's state (used for init and capacity growth).
+struct ExactImage {
+  int TC, KC, T, n_free;
+  std::vector<int32_t> z, n_t, pos_of_slot, slot_at_pos, free_slots, dish;
+  std::vector<int32_t> d_id, d_n, d_l, Kact, next_id;
+  std::vector<double> d_S1, d_S2, hyper;
+};
+
+void upload(ExactAlloc &A, const ExactImage &I, int n, int V, hipStream_t st) {
+  ExactChain &C = A.h;
+  auto cp = [&](void *dst, const void *src, size_t bytes) {
+    MVC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st));
+  };
+  cp(C.z, I.z.data(), sizeof(int32_t) * n);
+  cp(C.n_t, I.n_t.data(), sizeof(int32_t) * I.TC);
+  cp(C.pos_of_slot, I.pos_of_slot.data(), sizeof(int32_t) * I.TC);
+  cp(C.slot_at_pos, I.slot_at_pos.data(), sizeof(int32_t) * I.TC);
+  cp(C.free_slots, I.free_slots.data(), sizeof(int32_t) * I.TC);
+  cp(C.dish, I.dish.data(), sizeof(int32_t) * (size_t)V * I.TC);
+  cp(C.d_id, I.d_id.data(), sizeof(int32_t) * (size_t)V * I.KC);
+  cp(C.d_n, I.d_n.data(), sizeof(int32_t) * (size_t)V * I.KC);
+  cp(C.d_l, I.d_l.data(), sizeof(int32_t) * (size_t)V * I.KC);
+  cp(C.d_S1, I.d_S1.data(), sizeof(double) * (size_t)V * I.KC);
+  cp(C.d_S2, I.d_S2.data(), sizeof(double) * (size_t)V * I.KC);
+  cp(C.Kact, I.Kact.data(), sizeof(int32_t) * V);
+  cp(C.next_id, I.next_id.data(), sizeof(int32_t) * V);
+  cp(C.hyper, I.hyper.data(), sizeof(double) * (3 * V + 2));
+  C.T = I.T;
+  C.n_free = I.n_free;
+}
+
+void download(const ExactAlloc &A, ExactImage &I, int n, int V, hipStream_t st) {
+  const ExactChain &C = A.h;
+  I.TC = C.TC; I.KC = C.KC; I.T = C.T; I.n_free = C.n_free;
+  auto rs = [&](std::vector<int32_t> &v, size_t k, const void *src) {
+    v.resize(k);
+    MVC_HIP(hipMemcpyAsync(v.data(), src, sizeof(int32_t) * k, hipMemcpyDeviceToHost, st));
+  };
+  auto rd = [&](std::vector<double> &v, size_t k, const void *src) {
+    v.resize(k);
+    MVC_HIP(hipMemcpyAsync(v.data(), src, sizeof(double) * k, hipMemcpyDeviceToHost, st));
+  };
+  rs(I.z, n, C.z);
+  rs(I.n_t, C.TC, C.n_t);
+  rs(I.pos_of_slot, C.TC, C.pos_of_slot);
+  rs(I.slot_at_pos, C.TC, C.slot_at_pos);
+  rs(I.free_slots, C.TC, C.free_slots);
+  rs(I.dish, (size_t)V * C.TC, C.dish);
+  rs(I.d_id, (size_t)V * C.KC, C.d_id);
+  rs(I.d_n, (size_t)V * C.KC, C.d_n);
+  rs(I.d_l, (size_t)V * C.KC, C.d_l);
+  rd(I.d_S1, (size_t)V * C.KC, C.d_S1);
+  rd(I.d_S2, (size_t)V * C.KC, C.d_S2);
+  rs(I.Kact, V, C.Kact);
+  rs(I.next_id, V, C.next_id);
+  rd(I.hyper, 3 * V + 2, C.hyper);
+  MVC_HIP(hipStreamSynchronize(st));
+}
+
+// Re-stride an image to larger capacities.  Free slots are appended so that
+// the slots TC_old..TC_new-1 become available (LIFO order preserved below).
+void grow(ExactImage &I, int V, int TC2, int KC2) {
+  if (TC2 > I.TC) {
+    std::vector<int32_t> dish2((size_t)V * TC2, 0);
+    for (int v = 0; v < V; ++v)
+      std::copy(I.dish.begin() + (size_t)v * I.TC, I.dish.begin() + (size_t)(v + 1) * I.TC,
+                dish2.begin() + (size_t)v * TC2);
+    I.dish.swap(dish2);
+    I.n_t.resize(TC2, 0);
+    I.pos_of_slot.resize(TC2, -1);
+    I.slot_at_pos.resize(TC2, -1);
+    // free stack: new slots go below the existing free ones so the existing
+    // LIFO order (which decides which slot a new table takes) is irrelevant
+    // to results anyway -- slots are internal names.
+    std::vector<int32_t> fs;
+    for (int s = TC2 - 1; s >= I.TC; --s) fs.push_back(s);
+    for (int k = 0; k < I.n_free; ++k) fs.push_back(I.free_slots[k]);
+    I.free_slots = fs;
+    I.free_slots.resize(TC2, -1);
+    I.n_free += TC2 - I.TC;
+    I.TC = TC2;
+  }
+  if (KC2 > I.KC) {
+    auto re = [&](auto &vec) {
+      using Tv = typename std::decay<decltype(vec)>::type::value_type;
+      std::vector<Tv> out((size_t)V * KC2, Tv(0));
+      for (int v = 0; v < V; ++v)
+        std::copy(vec.begin() + (size_t)v * I.KC, vec.begin() + (size_t)(v + 1) * I.KC,
+                  out.begin() + (size_t)v * KC2);
+      vec.swap(out);
+    };
+    re(I.d_id); re(I.d_n); re(I.d_l); re(I.d_S1); re(I.d_S2);
+    I.KC = KC2;
+  }
+}
+
+}  // namespace
+
+class ExactSampler : public Sampler {
+ public:
+  int n, V;
+  double *y_dev = nullptr;
+  std::vector<ExactAlloc> chains;
+  ExactChain *chains_dev = nullptr;
+
+  ExactSampler(const mvc_config &c, const double *const *views) {
+    cfg = c;
+    n = c.n;
+    V = c.n_views;
+    if (c.dim != 1) throw Error(MVC_ERR_UNSUPPORTED, "exact mode requires dim == 1 (the reference's scalar views)");
+    if (V > MVC_MAXV) throw Error(MVC_ERR_UNSUPPORTED, "exact mode supports at most 64 views");
+    MVC_HIP(hipSetDevice(c.device));
+    MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    timers.stream = stream;
+    timers.on = (c.flags & MVC_FLAG_TIMING) != 0;
+    std::vector<double> y((size_t)V * n);
+    for (int v = 0; v < V; ++v) std::memcpy(&y[(size_t)v * n], views[v], sizeof(double) * n);
+    MVC_HIP(hipMalloc(&y_dev, sizeof(double) * y.size()));
+    MVC_HIP(hipMemcpyAsync(y_dev, y.data(), sizeof(double) * y.size(), hipMemcpyHostToDevice, stream));
+    const int TC = std::max(c.table_cap > 0 ? c.table_cap : 64, 8);
+    const int KC = std::max(c.dish_cap > 0 ? c.dish_cap : 32, 4);
+    chains.resize(c.n_chains);
+    for (int ch = 0; ch < c.n_chains; ++ch) {
+      const uint32_t gid = (uint32_t)(c.first_chain + ch);
+      InitState S = draw_initial_state(y.data(), n, V, 1, c.seed, gid);
+      ExactImage I = image_from_init(S, y.data(), TC, KC);
+      ExactAlloc &A = chains[ch];
+      MVC_HIP(hipMalloc(&A.block, exact_bytes(n, V, TC, KC)));
+      carve(A, n, V, TC, KC);
+      upload(A, I, n, V, stream);
+      MVC_HIP(hipStreamSynchronize(stream));   // I is a temporary
+      A.h.draws = S.draws;
+      A.h.resume_i = 0;
+      A.h.status = MVC_ST_RUNNING;
+      A.h.chain_id = (int32_t)gid;
+    }
+    MVC_HIP(hipMalloc(&chains_dev, sizeof(ExactChain) * chains.size()));
+    push_structs();
+    MVC_HIP(hipStreamSynchronize(stream));
+  }
+
+  ~ExactSampler() override {
+    if (stream) hipStreamSynchronize(stream);
+    for (auto &A : chains) if (A.block) hipFree(A.block);
+    if (chains_dev) hipFree(chains_dev);
+    if (y_dev) hipFree(y_dev);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  ExactImage image_from_init(const InitState &S, const double *y, int TC, int KC) {
+    // multiview_gibbs.cpp:12-103 in slot/live-list form
+    ExactImage I;
+    I.TC = TC; I.KC = KC; I.T = 4;
+    I.z = S.table;
+    I.n_t.assign(TC, 0);
+    for (int i = 0; i < n; ++i) I.n_t[S.table[i]]++;
+    I.pos_of_slot.assign(TC, -1);
+    I.slot_at_pos.assign(TC, -1);
+    for (int p = 0; p < 4; ++p) { I.pos_of_slot[p] = p; I.slot_at_pos[p] = p; }
+    I.n_free = TC - 4;
+    I.free_slots.assign(TC, -1);
+    for (int k = 0; k < I.n_free; ++k) I.free_slots[k] = TC - 1 - k;   // pop gives slot 4 first
+    I.dish.assign((size_t)V * TC, 0);
+    I.d_id.assign((size_t)V * KC, 0); I.d_n.assign((size_t)V * KC, 0); I.d_l.assign((size_t)V * KC, 0);
+    I.d_S1.assign((size_t)V * KC, 0.0); I.d_S2.assign((size_t)V * KC, 0.0);
+    I.Kact.assign(V, 0);
+    I.next_id.assign(V, 2);
+    I.hyper.assign(3 * V + 2, 0.0);
+    for (int v = 0; v < V; ++v) {
+      int l2[2] = {0, 0}, n2[2] = {0, 0};
+      double s1[2] = {0.0, 0.0}, s2[2] = {0.0, 0.0};
+      for (int t = 0; t < 4; ++t) l2[S.dish_raw[v * 4 + t]]++;
+      for (int i = 0; i < n; ++i) {          // :64-73, ascending i
+        const int k = S.dish_raw[v * 4 + S.table[i]];
+        const double val = y[(size_t)v * n + i];
+        n2[k]++;
+        s1[k] += val;
+        s2[k] += val * val;
+      }
+      int map2[2] = {-1, -1};
+      for (int k = 0; k < 2; ++k)
+        if (l2[k] > 0) {
+          const int j = I.Kact[v]++;
+          map2[k] = j;
+          I.d_id[v * KC + j] = k; I.d_n[v * KC + j] = n2[k]; I.d_l[v * KC + j] = l2[k];
+          I.d_S1[v * KC + j] = s1[k]; I.d_S2[v * KC + j] = s2[k];
+        }
+      for (int t = 0; t < 4; ++t) I.dish[(size_t)v * TC + t] = map2[S.dish_raw[v * 4 + t]];
+      I.hyper[v] = S.tau[v];
+      I.hyper[V + v] = 1.0;
+      I.hyper[2 * V + v] = 0.5;
+    }
+    I.hyper[3 * V] = 1.0;
+    I.hyper[3 * V + 1] = 0.6;
+    return I;
+  }
+
+  void push_structs() {
+    std::vector<ExactChain> hs(chains.size());
+    for (size_t k = 0; k < chains.size(); ++k) hs[k] = chains[k].h;
+    MVC_HIP(hipMemcpyAsync(chains_dev, hs.data(), sizeof(ExactChain) * hs.size(), hipMemcpyHostToDevice, stream));
+    MVC_HIP(hipStreamSynchronize(stream));
+  }
+  void pull_structs() {
+    std::vector<ExactChain> hs(chains.size());
+    MVC_HIP(hipMemcpyAsync(hs.data(), chains_dev, sizeof(ExactChain) * hs.size(), hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipStreamSynchronize(stream));
+    for (size_t k = 0; k < chains.size(); ++k) {
+      ExactChain &C = chains[k].h;
+      C.T = hs[k].T; C.n_free = hs[k].n_free; C.draws = hs[k].draws;
+      C.resume_i = hs[k].resume_i; C.status = hs[k].status;
+    }
+  }
+
+  void grow_chain(ExactAlloc &A) {
+    ExactImage I;
+    download(A, I, n, V, stream);
+    int TC2 = I.TC, KC2 = I.KC;
+    if (I.n_free < 1) TC2 = I.TC * 2;
+    for (int v = 0; v < V; ++v) if (I.Kact[v] + 1 > I.KC) KC2 = I.KC * 2;
+    grow(I, V, TC2, KC2);
+    ExactAlloc B;
+    B.h = A.h;
+    MVC_HIP(hipMalloc(&B.block, exact_bytes(n, V, TC2, KC2)));
+    carve(B, n, V, TC2, KC2);
+    upload(B, I, n, V, stream);
+    MVC_HIP(hipStreamSynchronize(stream));
+    MVC_HIP(hipFree(A.block));
+    B.h.status = MVC_ST_RUNNING;
+    A = B;
+  }
+
+  void sweep(int n_sweeps) override {
+    for (int it = 0; it < n_sweeps; ++it) {
+      for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; }
+      push_structs();
+      hipEvent_t ev0 = nullptr;
+      timers.begin("sweep", &ev0);
+      for (int round = 0;; ++round) {
+        hipEvent_t ev = nullptr;
+        timers.begin("exact_sweep", &ev);
+        hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), 0, stream,
+                           (const double *)y_dev, n, V, chains_dev, cfg.seed);
+        MVC_HIP(hipGetLastError());
+        timers.end("exact_sweep", ev);
+        pull_structs();
+        bool again = false;
+        for (auto &A : chains) {
+          if (A.h.status == MVC_ST_OVERFLOW) { grow_chain(A); again = true; }
+          else if (A.h.status != MVC_ST_DONE) throw Error(MVC_ERR_STATE, "exact sweep kernel left a chain unfinished");
+        }
+        if (!again) break;
+        push_structs();
+        if (round > 64) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
+      }
+      timers.end("sweep", ev0);
+      ++sweeps_done;
+    }
+  }
+
+  void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
+
+  void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of, int32_t dish_cap,
+                 double *hyper) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    pull_structs();
+    const ExactChain &C = chains[chain].h;
+    const int T = C.T;
+    if (n_tables) *n_tables = T;
+    int32_t *t_dev = nullptr, *d_dev = nullptr;
+    const int cap = std::max(T, 1);
+    MVC_HIP(hipMalloc(&t_dev, sizeof(int32_t) * n));
+    MVC_HIP(hipMalloc(&d_dev, sizeof(int32_t) * (size_t)V * cap));
+    hipLaunchKernelGGL(mvc_exact_snapshot_kernel, dim3(std::min(1024, (n + 255) / 256 + 1)), dim3(256), 0, stream,
+                       n, V, (const ExactChain *)chains_dev, chain, t_dev, d_dev, cap);
+    MVC_HIP(hipGetLastError());
+    std::vector<int32_t> dd((size_t)V * cap);
+    if (table_of) MVC_HIP(hipMemcpyAsync(table_of, t_dev, sizeof(int32_t) * n, hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipMemcpyAsync(dd.data(), d_dev, sizeof(int32_t) * dd.size(), hipMemcpyDeviceToHost, stream));
+    std::vector<double> hy(3 * V + 2);
+    MVC_HIP(hipMemcpyAsync(hy.data(), C.hyper, sizeof(double) * hy.size(), hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipStreamSynchronize(stream));
+    hipFree(t_dev);
+    hipFree(d_dev);
+    if (dish_of)
+      for (int v = 0; v < V; ++v)
+        for (int p = 0; p < std::min(T, (int)dish_cap); ++p) dish_of[(size_t)v * dish_cap + p] = dd[(size_t)v * cap + p];
+    if (hyper) std::copy(hy.begin(), hy.end(), hyper);
+  }
+
+  void get_dish_counts(int chain, int32_t *k_out) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    MVC_HIP(hipMemcpyAsync(k_out, chains[chain].h.Kact, sizeof(int32_t) * V, hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipStreamSynchronize(stream));
+  }
+};
+
+Sampler *make_exact_sampler(const mvc_config &cfg, const double *const *views) {
+  return new ExactSampler(cfg, views);
+}
+
+}  // namespace mvc

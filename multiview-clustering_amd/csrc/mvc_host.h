@@ -1,0 +1,71 @@
+// mvc_host.h — host-side sampler classes behind the C ABI (include/mvc.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mvc.h"
+#include "mvc_internal.h"
+
+namespace mvc {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define MVC_HIP(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      throw ::mvc::Error(MVC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// Initial state draws of multiview_gibbs.cpp:12-62 on the sequential Philox
+// stream (shared by both schedules), plus tau_v of :78-94.
+struct InitState {
+  std::vector<int32_t> table;            // [n] position 0..3
+  std::vector<int32_t> dish_raw;         // [V*4] raw dish id (0/1) of each initial table
+  std::vector<double> tau;               // [V]
+  uint64_t draws = 0;                    // sequential draws consumed
+};
+InitState draw_initial_state(const double *y /*[V][n][D]*/, int n, int V, int D, uint64_t seed,
+                             uint32_t chain);
+
+// Per-kernel HIP-event timers (MVC_FLAG_TIMING).
+struct Timers {
+  bool on = false;
+  hipStream_t stream = nullptr;
+  struct Rec { hipEvent_t a, b; std::string name; };
+  std::vector<Rec> pending;
+  std::map<std::string, std::pair<double, int64_t>> acc;
+  void begin(const char *name, hipEvent_t *ev);
+  void end(const char *name, hipEvent_t a);
+  void collect();
+  void reset();
+  ~Timers();
+};
+
+class Sampler {
+ public:
+  virtual ~Sampler() {}
+  virtual void sweep(int n_sweeps) = 0;
+  virtual void synchronize() = 0;
+  virtual void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of,
+                         int32_t dish_cap, double *hyper) = 0;
+  virtual void get_dish_counts(int chain, int32_t *k_out) = 0;
+  mvc_config cfg;
+  int sweeps_done = 0;
+  hipStream_t stream = nullptr;
+  Timers timers;
+};
+
+Sampler *make_exact_sampler(const mvc_config &cfg, const double *const *views);
+Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views);
+
+}  // namespace mvc

@@ -1,0 +1,1164 @@
+// mvc_parallel.hip — the parallel ("mode P") sweep on gfx950.
+//
+// Per sweep:
+//   zresample : every customer draws its table against the state frozen at
+//               sweep start (virtual self-removal), one wavefront per
+//               customer, log-space probabilities, tree64 sums, Philox
+//               counters (chain, sweep, customer).
+//   births    : customers that chose a new table draw one dish per view.
+//   commit    : survivors + births -> dense positions, live-dish lists,
+//               counts (integer atomics: order independent).
+//   stats     : S1/S2 rebuilt in a fixed chunked order (bit-reproducible).
+//   hyper     : one workgroup: ||S1||^2, the MH updates of
+//               multiview_hyper.cpp:233-292 (EPPF sums via lgamma + size
+//               histograms, tree64 order), then next sweep's coefficients.
+// Every fp64 expression matches ParallelSampler in oracle/mvc_oracle.cpp.
+// Compile with -ffp-contract=off.
+#include <hipcub/hipcub.hpp>
+
+#include "mvc_internal.h"
+
+namespace {
+
+constexpr double kEps = 1e-6;
+constexpr int kStatsChunk = 4096;   // must equal oracle kStatsChunk
+constexpr int kMaxChunks = 64;      // two-level tree64: <= 4096 elements
+
+struct Coef { double c0, cb; };
+__device__ __forceinline__ Coef coef(int n_, double Q, double tau, double L2pt, int D) {
+  const double a = tau + (double)n_;
+  const double b = tau + (double)(n_ + 1);
+  Coef c;
+  c.c0 = (double)D * ((-0.5 * L2pt) - 0.5 * mvc_log(b / a)) - (0.5 * Q) / ((tau * a) * b);
+  c.cb = 1.0 / (tau * b);
+  return c;
+}
+
+// Kernel argument bundle (passed by value).
+struct Sweep {
+  ParState P;
+  const double *y;        // [V][n][D]
+  const double *Y2;       // [V][n]
+  const double *L2pt;     // [V]  log(2 pi tau)
+  const double *cnew;     // [V]  D * (-0.5 L2pt)
+  const int32_t *Koff;    // [V+1] prefix of Kact
+  double *scratch;        // per wave: [sumK]
+  int32_t *choice;        // [n] position or -1 (birth)
+  int32_t *bdish;         // [n*V] birth dish choices (by birth rank)
+  const int32_t *blist;   // [NB] birth customers, ascending
+  const int32_t *nbirth;  // [1]
+  const int32_t *status;  // [V+4]; status[V+3] = tables with n_t > 0
+  int32_t T, sumK;
+  uint64_t seed;
+  uint32_t chain, sweep;
+};
+
+// Per-view mixture of the new-table marginal for customer i.
+// Writes lp of every live dish into lp[0..K); returns lmarg; outputs the max
+// m, the tree sum S and (lane c) the level-0 chunk partial of chunk c.
+struct ViewOut { double lmarg, m, S, part; int nc; double lf_new, w_new; };
+
+__device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p0, bool alive, double *lp) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63;
+  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
+  const int K = P.Kact[v];
+  const int j0 = P.dish[v * P.TC + p0];
+  const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+  const double Y2i = A.Y2[(size_t)v * n + i];
+  const double hy = 0.5 * Y2i;
+  const double h = (-0.5 * Y2i) / tau;
+  const double *yrow = A.y + ((size_t)v * n + i) * D;
+  const double *S1v = P.S1T + (size_t)v * D * KC;
+  const int l0 = P.d_l[v * KC + j0];
+  const int l0p = alive ? l0 : l0 - 1;
+  double mx = -MVC_PM_INF;
+  for (int base = 0; base < K; base += 64) {
+    const int j = base + lane;
+    if (j < K) {
+      double G = 0.0;
+      for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S1v[(size_t)d * KC + j], G);
+      double val;
+      int l;
+      if (j == j0) {
+        l = l0p;
+        const double Gp = G - Y2i;
+        const double Qp = (P.Q[v * KC + j] - 2.0 * G) + Y2i;
+        const Coef c = coef(P.d_n[v * KC + j] - 1, Qp, tau, A.L2pt[v], D);
+        val = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
+      } else {
+        l = P.d_l[v * KC + j];
+        val = __builtin_fma(G + hy, P.cb[v * KC + j], P.c0[v * KC + j]) + h;
+      }
+      lp[j] = val;
+      if (l > 0 && val > mx) mx = val;
+    }
+  }
+  ViewOut o;
+  o.lf_new = A.cnew[v] + h;
+  const int Kact_i = K - ((l0p == 0) ? 1 : 0);
+  double wn = alpha + (double)Kact_i * sigma;
+  if (wn < 0.0) wn = 0.0;
+  o.w_new = wn;
+  mx = wave_max(mx);
+  if (o.lf_new > mx) mx = o.lf_new;
+  o.m = mx;
+  const int nel = K + 1;
+  o.nc = (nel + 63) >> 6;
+  double part = 0.0;
+  for (int c = 0; c < o.nc; ++c) {
+    const int e = c * 64 + lane;
+    double leaf = 0.0;
+    if (e < K) {
+      const int l = (e == j0) ? l0p : P.d_l[v * KC + e];
+      if (l > 0) {
+        double w = (double)l - sigma;
+        if (w < 0.0) w = 0.0;
+        leaf = w * mvc_exp(lp[e] - mx);
+      }
+    } else if (e == K) {
+      leaf = wn * mvc_exp(o.lf_new - mx);
+    }
+    const double cs = wave_tree_sum(leaf);
+    if (lane == c) part = cs;
+  }
+  o.part = part;
+  o.S = (o.nc == 1) ? __shfl(part, 0, 64) : wave_tree_sum(lane < o.nc ? part : 0.0);
+  const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
+  o.lmarg = (denom <= 0.0) ? o.lf_new : (mx + mvc_log(o.S)) - mvc_log(denom);
+  return o;
+}
+
+__device__ __forceinline__ int view_select(const Sweep &A, int i, int v, int p0, bool alive, const double *lp,
+                                           const ViewOut &o, double r) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63;
+  const int V = P.V, KC = P.KC;
+  const int K = P.Kact[v];
+  const int j0 = P.dish[v * P.TC + p0];
+  const double sigma = P.hyper[2 * V + v];
+  const int l0p = alive ? P.d_l[v * KC + j0] : P.d_l[v * KC + j0] - 1;
+  int c = 0;
+  if (o.nc > 1) {
+    Tree64Levels L;
+    const double pv = lane < o.nc ? o.part : 0.0;
+    wave_tree_sum_levels(pv, L);
+    c = wave_tree_select(L, pv, r);
+  }
+  const int e = c * 64 + lane;
+  double leaf = 0.0;
+  if (e < K) {
+    const int l = (e == j0) ? l0p : P.d_l[v * KC + e];
+    if (l > 0) {
+      double w = (double)l - sigma;
+      if (w < 0.0) w = 0.0;
+      leaf = w * mvc_exp(lp[e] - o.m);
+    }
+  } else if (e == K) {
+    leaf = o.w_new * mvc_exp(o.lf_new - o.m);
+  }
+  Tree64Levels L2;
+  wave_tree_sum_levels(leaf, L2);
+  const int l = wave_tree_select(L2, leaf, r);
+  return c * 64 + l;
+}
+
+// table score s_p (or -inf if excluded) for customer with own table p0
+__device__ __forceinline__ double table_score(const Sweep &A, int p, int p0, double sg, const double *lpall) {
+  const ParState &P = A.P;
+  const int np = P.n_t[p] - (p == p0 ? 1 : 0);
+  if (np < 1) return -MVC_PM_INF;
+  const double mass = (double)np - sg;
+  if (mass <= 0.0) return -MVC_PM_INF;
+  double sp = (p == p0) ? mvc_log(mass) : P.lmass[p];
+  for (int v = 0; v < P.V; ++v) sp = sp + lpall[A.Koff[v] + P.dish[v * P.TC + p]];
+  return sp;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// zresample: one wavefront per customer (grid-stride), block = 256.
+// ---------------------------------------------------------------------------
+extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep A) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63;
+  const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  double *lpall = A.scratch + (size_t)wid * A.sumK;
+  const int V = P.V, T = A.T;
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const int T_ne = A.status[V + 3];
+  for (int i = wid; i < P.n; i += nw) {
+    const int p0 = P.z[i];
+    const bool alive = (P.n_t[p0] - 1) > 0;
+    double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+    for (int v = 0; v < V; ++v) {
+      const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v]);
+      s_new = s_new + o.lmarg;
+    }
+    // pass 1: max
+    double M = s_new;
+    for (int base = 0; base < T; base += 64) {
+      const int p = base + lane;
+      if (p < T) {
+        const double sp = table_score(A, p, p0, sg, lpall);
+        if (sp > M) M = sp;
+      }
+    }
+    M = wave_max(M);
+    // pass 2: leaves, chunk partials (T <= 4096)
+    const int nc = (T + 63) >> 6;
+    double part = 0.0;
+    for (int c = 0; c < nc; ++c) {
+      const int p = c * 64 + lane;
+      double leaf = 0.0;
+      if (p < T) {
+        const double sp = table_score(A, p, p0, sg, lpall);
+        if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
+      }
+      const double cs = wave_tree_sum(leaf);
+      if (lane == c) part = cs;
+    }
+    double B;
+    if (nc == 0) B = 0.0;
+    else if (nc == 1) B = __shfl(part, 0, 64);
+    else B = wave_tree_sum(lane < nc ? part : 0.0);
+    const double e_new = mvc_exp(s_new - M);
+    const double W = e_new + B;
+    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+    int pick = -1;
+    if (r < B) {
+      int c = 0;
+      if (nc > 1) {
+        Tree64Levels L;
+        const double pv = lane < nc ? part : 0.0;
+        wave_tree_sum_levels(pv, L);
+        c = wave_tree_select(L, pv, r);
+      }
+      const int p = c * 64 + lane;
+      double leaf = 0.0;
+      if (p < T) {
+        const double sp = table_score(A, p, p0, sg, lpall);
+        if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
+      }
+      Tree64Levels L2;
+      wave_tree_sum_levels(leaf, L2);
+      pick = c * 64 + wave_tree_select(L2, leaf, r);
+    }
+    if (lane == 0) A.choice[i] = pick;
+  }
+}
+
+// births: one wavefront per birth customer; per view dish draw
+extern "C" __global__ __launch_bounds__(256) void mvc_par_birth_kernel(Sweep A) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63;
+  const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  double *lpall = A.scratch + (size_t)wid * A.sumK;
+  const int NB = *A.nbirth;
+  for (int b = wid; b < NB; b += nw) {
+    const int i = A.blist[b];
+    const int p0 = P.z[i];
+    const bool alive = (P.n_t[p0] - 1) > 0;
+    for (int v = 0; v < P.V; ++v) {
+      double *lp = lpall + A.Koff[v];
+      const ViewOut o = view_eval(A, i, v, p0, alive, lp);
+      int e;
+      if (!(o.S > 0.0)) {
+        e = P.Kact[v];
+      } else {
+        const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_DISH + 1u + (uint32_t)v) * o.S;
+        e = view_select(A, i, v, p0, alive, lp, o, r);
+      }
+      if (lane == 0) A.bdish[(size_t)b * P.V + v] = e;
+    }
+  }
+}
+
+// commit step 1: table counts and birth flags
+extern "C" __global__ void mvc_par_count_kernel(int n, const int32_t *choice, int32_t *cnt, int32_t *flag) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c = choice[i];
+    flag[i] = c < 0 ? 1 : 0;
+    if (c >= 0) atomicAdd(&cnt[c], 1);
+  }
+}
+
+// commit step 2 (one workgroup of 256): new tables, dish lists, counts.
+// status[0] = T_new, status[1..V] = K_new, status[V+1] = error flag,
+// status[V+2] = births.
+extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
+    ParState P, int T, const int32_t *cnt, const int32_t *nbirth, const int32_t *bdish, int32_t *pos_new,
+    int32_t *tmp_dish /*[V*TC]*/, int32_t *tmp_nt /*[TC]*/, int32_t *lcnt /*[V*KC]*/, int32_t *jmap /*[V*KC]*/,
+    int32_t *status) {
+  __shared__ int s_scan[256];
+  __shared__ int s_tot;
+  const int tid = threadIdx.x;
+  const int V = P.V, TC = P.TC, KC = P.KC;
+  const int NB = *nbirth;
+  auto block_scan = [&](int x, int &total) {   // exclusive scan of x over the block
+    s_scan[tid] = x;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      const int t = tid >= off ? s_scan[tid - off] : 0;
+      __syncthreads();
+      s_scan[tid] += t;
+      __syncthreads();
+    }
+    const int incl = s_scan[tid];
+    total = s_scan[255];
+    __syncthreads();
+    return incl - x;
+  };
+  // survivors in ascending position
+  int run = 0;
+  for (int base = 0; base < T; base += 256) {
+    const int p = base + tid;
+    const int alive = (p < T && cnt[p] > 0) ? 1 : 0;
+    int tot;
+    const int ex = block_scan(alive, tot);
+    if (p < T) pos_new[p] = alive ? run + ex : -1;
+    run += tot;
+  }
+  const int Tsurv = run;
+  const int Tn = Tsurv + NB;
+  if (tid == 0) { status[0] = Tn; status[V + 1] = 0; status[V + 2] = NB; }
+  if (Tn > TC) { if (tid == 0) status[V + 1] = 1; return; }
+  __syncthreads();
+  // extended dish index of every new table, per view
+  for (int v = 0; v < V; ++v) {
+    const int Kold = P.Kact[v];
+    int nnew = 0;
+    for (int base = 0; base < NB; base += 256) {
+      const int b = base + tid;
+      const int e = b < NB ? bdish[(size_t)b * V + v] : 0;
+      const int isnew = (b < NB && e >= Kold) ? 1 : 0;
+      int tot;
+      const int ex = block_scan(isnew, tot);
+      if (b < NB) tmp_dish[v * TC + Tsurv + b] = isnew ? Kold + nnew + ex : e;
+      nnew += tot;
+    }
+    if (Kold + nnew > KC) { if (tid == 0) status[V + 1] = 2; return; }
+    for (int p = tid; p < T; p += 256)
+      if (pos_new[p] >= 0) tmp_dish[v * TC + pos_new[p]] = P.dish[v * TC + p];
+    for (int j = tid; j < Kold + nnew; j += 256) lcnt[v * KC + j] = 0;
+    __syncthreads();
+    for (int p = tid; p < Tn; p += 256) atomicAdd(&lcnt[v * KC + tmp_dish[v * TC + p]], 1);
+    __syncthreads();
+    // compact surviving dishes (ascending extended index == ascending raw id)
+    const int Kext = Kold + nnew;
+    int kr = 0;
+    for (int base = 0; base < Kext; base += 256) {
+      const int j = base + tid;
+      const int live = (j < Kext && lcnt[v * KC + j] > 0) ? 1 : 0;
+      int tot;
+      const int ex = block_scan(live, tot);
+      if (j < Kext) jmap[v * KC + j] = live ? kr + ex : -1;
+      kr += tot;
+    }
+    __syncthreads();
+    // write the compacted dish arrays in place: ids ascend, so a stable
+    // left-shift is safe when done in increasing j by a single pass per chunk
+    const int next = P.next_id[v];
+    for (int base = 0; base < Kext; base += 256) {
+      const int j = base + tid;
+      int id = 0, l = 0, keep = 0;
+      if (j < Kext) {
+        keep = jmap[v * KC + j] >= 0;
+        id = j < Kold ? P.d_id[v * KC + j] : next + (j - Kold);
+        l = lcnt[v * KC + j];
+      }
+      __syncthreads();
+      if (keep) {
+        const int jn = jmap[v * KC + j];
+        P.d_id[v * KC + jn] = id;
+        P.d_l[v * KC + jn] = l;
+        P.d_n[v * KC + jn] = 0;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      P.next_id[v] = next + nnew;
+      P.Kact[v] = kr;
+      status[1 + v] = kr;
+    }
+    __syncthreads();
+    for (int p = tid; p < Tn; p += 256) {
+      const int jn = jmap[v * KC + tmp_dish[v * TC + p]];
+      P.dish[v * TC + p] = jn;
+    }
+    __syncthreads();
+  }
+  // table counts, n_vk
+  for (int p = tid; p < T; p += 256)
+    if (pos_new[p] >= 0) tmp_nt[pos_new[p]] = cnt[p];
+  for (int b = tid; b < NB; b += 256) tmp_nt[Tsurv + b] = 1;
+  __syncthreads();
+  for (int p = tid; p < Tn; p += 256) {
+    const int c = tmp_nt[p];
+    P.n_t[p] = c;
+    for (int v = 0; v < V; ++v) atomicAdd(&P.d_n[v * KC + P.dish[v * TC + p]], c);
+  }
+  if (tid == 0) s_tot = Tsurv;
+  (void)s_tot;
+}
+
+// commit step 3: relabel customers (births numbered by birth rank)
+extern "C" __global__ void mvc_par_relabel_kernel(int n, int V, const int32_t *choice, const int32_t *pos_new,
+                                                  const int32_t *brank, const int32_t *status, int32_t *z) {
+  const int32_t Tn = status[0];
+  const int32_t NB = status[V + 2];
+  const int32_t Tsurv = Tn - NB;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c = choice[i];
+    z[i] = c >= 0 ? pos_new[c] : Tsurv + brank[i];
+  }
+}
+
+// Y2[v][i] = sum_d y^2, fma chain in d order (oracle ParallelSampler::fma_dot)
+extern "C" __global__ void mvc_par_y2_kernel(int n, int V, int D, const double *y, double *Y2) {
+  const size_t total = (size_t)n * V;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const double *r = y + e * D;
+    double acc = 0.0;
+    for (int d = 0; d < D; ++d) acc = __builtin_fma(r[d], r[d], acc);
+    Y2[e] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Stats rebuild, chunked ordered sums.  Block (chunk c,
+// view v): thread d owns dimension d and walks the chunk's customers in
+// ascending order, accumulating into acc[j][d] in LDS; thread D (or thread
+// 0 after the dims) does the same for Y2 -> S2.
+// part1[c][Koff[v]+j][d], part2[c][Koff[v]+j]
+// ---------------------------------------------------------------------------
+#define MVC_STATS_SUB 64
+extern "C" __global__ __launch_bounds__(256) void mvc_par_stats_partial_kernel(
+    ParState P, const double *y, const double *Y2, const int32_t *Koff, int sumK, int dgroup,
+    double *part1, double *part2) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int c = blockIdx.x, v = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int n = P.n, D = P.D, TC = P.TC;
+  const int K = P.Kact[v];
+  const int i0 = c * kStatsChunk, i1 = min(n, i0 + kStatsChunk);
+  // LDS: acc[K][dgroup] | acc2[K] | ysub[SUB][dgroup] | y2sub[SUB] | jsub[SUB]
+  double *acc = (double *)smem;
+  double *acc2 = acc + (size_t)K * dgroup;
+  double *ysub = acc2 + K;
+  double *y2sub = ysub + (size_t)MVC_STATS_SUB * dgroup;
+  int *jsub = (int *)(y2sub + MVC_STATS_SUB);
+  for (int d0 = 0; d0 < D; d0 += dgroup) {
+    const int dg = min(dgroup, D - d0);
+    const bool do_y2 = (d0 == 0);
+    for (int e = tid; e < K * dgroup; e += 256) acc[e] = 0.0;
+    for (int e = tid; e < K; e += 256) acc2[e] = 0.0;
+    __syncthreads();
+    for (int s0 = i0; s0 < i1; s0 += MVC_STATS_SUB) {
+      const int cnt = min(MVC_STATS_SUB, i1 - s0);
+      for (int e = tid; e < cnt * dg; e += 256) {
+        const int q = e / dg, d = e % dg;
+        ysub[q * dgroup + d] = y[((size_t)v * n + s0 + q) * D + d0 + d];
+      }
+      for (int q = tid; q < cnt; q += 256) {
+        jsub[q] = P.dish[v * TC + P.z[s0 + q]];
+        y2sub[q] = Y2[(size_t)v * n + s0 + q];
+      }
+      __syncthreads();
+      if (tid < dg) {
+        for (int q = 0; q < cnt; ++q) {
+          const int j = jsub[q];
+          acc[j * dgroup + tid] = acc[j * dgroup + tid] + ysub[q * dgroup + tid];
+        }
+      } else if (do_y2 && tid == (dg < 256 ? dg : 0)) {
+        for (int q = 0; q < cnt; ++q) acc2[jsub[q]] = acc2[jsub[q]] + y2sub[q];
+      }
+      __syncthreads();
+      if (do_y2 && dg == 256 && tid == 0) {   // all threads busy with dims: Y2 afterwards
+        for (int q = 0; q < cnt; ++q) acc2[jsub[q]] = acc2[jsub[q]] + y2sub[q];
+      }
+      __syncthreads();
+    }
+    const size_t base = ((size_t)c * sumK + Koff[v]);
+    for (int e = tid; e < K * dg; e += 256) {
+      const int j = e / dg, d = e % dg;
+      part1[(base + j) * D + d0 + d] = acc[j * dgroup + d];
+    }
+    if (do_y2)
+      for (int j = tid; j < K; j += 256) part2[base + j] = acc2[j];
+    __syncthreads();
+  }
+}
+
+// S1T[v][d][j] = sum_c part1[c][..] (ascending c, from 0.0); same for S2.
+// stride = dish-row stride of the partial buffers (>= Koff[V]).
+extern "C" __global__ void mvc_par_stats_combine_kernel(ParState P, const int32_t *Koff, int stride, int nchunk,
+                                                        const double *part1, const double *part2) {
+  const int D = P.D, KC = P.KC, V = P.V;
+  const size_t tot = (size_t)Koff[V] * (D + 1);
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e / (D + 1));
+    const int d = (int)(e % (D + 1));
+    int v = 0;
+    while (v + 1 < V && Koff[v + 1] <= k) ++v;
+    const int j = k - Koff[v];
+    double s = 0.0;
+    if (d < D) {
+      for (int c = 0; c < nchunk; ++c) s = s + part1[((size_t)c * stride + k) * D + d];
+      P.S1T[((size_t)v * D + d) * KC + j] = s;
+    } else {
+      for (int c = 0; c < nchunk; ++c) s = s + part2[(size_t)c * stride + k];
+      P.S2[v * KC + j] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Hyperparameter MH + next-sweep coefficients, ONE workgroup of 256.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct BlockCtx {
+  double *red;      // LDS [4]
+  double *scratch;  // global, >= leaves/64 + ... per level (two halves)
+  size_t half;      // scratch half size
+};
+
+// tree64 over n leaves produced by leaf(e), executed by the whole block.
+// Level partials ping-pong between the two halves of ctx.scratch.
+template <class F>
+__device__ double block_tree64(const BlockCtx &ctx, int64_t n, F leaf) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ double s_root;
+  if (n <= 0) return 0.0;
+  double *src = nullptr;
+  double *dst = ctx.scratch;
+  int64_t m = (n + 63) / 64;
+  for (int64_t c = w; c < m; c += 4) {
+    const int64_t e = c * 64 + lane;
+    const double x = e < n ? leaf(e) : 0.0;
+    const double s = wave_tree_sum(x);
+    if (lane == 0) dst[c] = s;
+  }
+  __syncthreads();
+  while (m > 1) {
+    src = dst;
+    dst = (src == ctx.scratch) ? ctx.scratch + ctx.half : ctx.scratch;
+    const int64_t m2 = (m + 63) / 64;
+    for (int64_t c = w; c < m2; c += 4) {
+      const int64_t e = c * 64 + lane;
+      const double x = e < m ? src[e] : 0.0;
+      const double s = wave_tree_sum(x);
+      if (lane == 0) dst[c] = s;
+    }
+    __syncthreads();
+    m = m2;
+  }
+  if (tid == 0) s_root = dst[0];
+  __syncthreads();
+  const double r = s_root;
+  __syncthreads();
+  return r;
+}
+
+struct MHArgs {
+  ParState P;
+  int32_t *status;        // [V+3]: T, K[V], err, NB  -> we add T_ne at status[V+3]
+  int32_t *Koff;          // [V+1] (output)
+  double *L2pt, *cnew;    // [V] (output)
+  int32_t *histT;         // [n+2] scratch: c_m for tables
+  int32_t *histL;         // [V*(TC+2)] scratch: c_m for dishes
+  double *scratch;        // tree levels
+  size_t half;
+  uint64_t seed;
+  uint32_t chain, sweep;
+  int do_mh;
+};
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A) {
+  ParState &P = A.P;
+  const int tid = threadIdx.x;
+  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
+  __shared__ double s_red[8];
+  __shared__ double s_b[4];
+  __shared__ int s_i[8];
+  BlockCtx ctx{s_red, A.scratch, A.half};
+  const int T = A.status[0];
+  // ---- Q = ||S1||^2 per live dish, Ltot, Koff ----
+  for (int v = 0; v < V; ++v) {
+    const int K = P.Kact[v];
+    for (int j = tid; j < K; j += 256) {
+      double q = 0.0;
+      for (int d = 0; d < D; ++d) {
+        const double s = P.S1T[((size_t)v * D + d) * KC + j];
+        q = __builtin_fma(s, s, q);
+      }
+      P.Q[v * KC + j] = q;
+    }
+  }
+  if (tid == 0) {
+    for (int v = 0; v < V; ++v) {
+      int lt = 0;
+      for (int j = 0; j < P.Kact[v]; ++j) lt += P.d_l[v * KC + j];
+      P.Ltot[v] = lt;
+    }
+    int tne = 0, maxn = 0;
+    for (int p = 0; p < T; ++p) { if (P.n_t[p] > 0) ++tne; maxn = max(maxn, P.n_t[p]); }
+    s_i[0] = tne;
+    s_i[1] = maxn;
+    A.status[V + 3] = tne;
+  }
+  __syncthreads();
+  const int maxn = s_i[1];
+  double *hyp = P.hyper;
+  if (A.do_mh) {
+    // c_m = #{tables with n_t > m}, m = 0..maxn
+    for (int m = tid; m <= maxn + 1; m += 256) A.histT[m] = 0;
+    __syncthreads();
+    for (int p = tid; p < T; p += 256) atomicAdd(&A.histT[P.n_t[p]], 1);
+    __syncthreads();
+    if (tid == 0) {   // suffix counts, exclusive: c_m = sum_{s > m} hist[s]
+      int run = 0;
+      for (int m = maxn; m >= 0; --m) { const int h = A.histT[m]; A.histT[m] = run; run += h; }
+    }
+    for (int v = 0; v < V; ++v) {
+      int *hl = A.histL + (size_t)v * (TC + 2);
+      for (int m = tid; m < TC + 2; m += 256) hl[m] = 0;
+    }
+    __syncthreads();
+    int maxl_loc = 0;
+    for (int v = 0; v < V; ++v) {
+      int *hl = A.histL + (size_t)v * (TC + 2);
+      for (int j = tid; j < P.Kact[v]; j += 256) atomicAdd(&hl[P.d_l[v * KC + j]], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int v = 0; v < V; ++v) {
+        int *hl = A.histL + (size_t)v * (TC + 2);
+        int run = 0, mx = 0;
+        for (int j = 0; j < P.Kact[v]; ++j) mx = max(mx, P.d_l[v * KC + j]);
+        for (int m = mx; m >= 0; --m) { const int h = hl[m]; hl[m] = run; run += h; }
+        hl[TC + 1] = mx;   // stash max l
+        maxl_loc = max(maxl_loc, mx);
+      }
+    }
+    __syncthreads();
+    (void)maxl_loc;
+
+    uint32_t kdraw = 0;
+    auto unif = [&]() -> double {   // block-uniform
+      if (tid == 0) s_b[0] = mvc_uniform(A.seed, kdraw, A.sweep, A.chain, MVC_TAG_MH);
+      __syncthreads();
+      const double u = s_b[0];
+      __syncthreads();
+      ++kdraw;
+      return u;
+    };
+    auto rnorm = [&](double mu, double sd) -> double {
+      const double u1 = unif();
+      const double u2 = unif();
+      return mu + sd * mvc_norm_from_uniforms(u1, u2);
+    };
+    auto prior_alpha = [](double a) -> double {
+      if (a <= 0.0) return -MVC_PM_INF;
+      return (4.0 - 1.0) * mvc_log(a) - 3.0 * a;
+    };
+    auto prior_sigma = [](double s) -> double {
+      if (s <= 0.0 || s >= 1.0) return -MVC_PM_INF;
+      return (1.0 - 1.0) * mvc_log(s) + (5.0 - 1.0) * mvc_log(1.0 - s);
+    };
+    auto reflect_unit = [](double value) -> double {
+      double p = value;
+      while (p <= kEps || p >= 1.0 - kEps) {
+        if (p <= kEps) p = 2.0 * kEps - p;
+        if (p >= 1.0 - kEps) p = 2.0 * (1.0 - kEps) - p;
+      }
+      return p < kEps ? kEps : (p > 1.0 - kEps ? 1.0 - kEps : p);
+    };
+    // EPPF of a partition: K blocks, total tot, counts c_m (exclusive suffix),
+    // max block size mx.
+    auto eppf = [&](int K, int tot, const int *cm, int mx, double a, double s) -> double {
+      if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
+      if (a <= -s) return -MVC_PM_INF;
+      // any term a + j s <= 0 ?  (monotone in j for s > 0: check j = 0)
+      if (K > 0 && !(a + 0.0 * s > 0.0)) return -MVC_PM_INF;
+      const double P1 = block_tree64(ctx, K, [&](int64_t j) { return mvc_log(a + (double)j * s); });
+      const double P2 = mvc_lgamma_pos(a + (double)tot) - mvc_lgamma_pos(a + 1.0);
+      const double P3 = block_tree64(ctx, mx > 1 ? mx - 1 : 0,
+                                     [&](int64_t e) { const int m = (int)e + 1; return (double)cm[m] * mvc_log((double)m - s); });
+      return (P1 - P2) + P3;
+    };
+    auto eppf_view = [&](int v, double a, double s) -> double {
+      if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
+      if (a <= -s) return -MVC_PM_INF;
+      if (P.Ltot[v] == 0) return 0.0;
+      const int *hl = A.histL + (size_t)v * (TC + 2);
+      return eppf(P.Kact[v], P.Ltot[v], hl, hl[TC + 1], a, s);
+    };
+    auto eppf_global = [&](double a, double s) -> double {
+      if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
+      if (a <= -s) return -MVC_PM_INF;
+      if (T <= 0) return 0.0;
+      return eppf(T, n, A.histT, maxn, a, s);
+    };
+    auto post_tau = [&](int v, double t) -> double {
+      if (t <= 0.0) return -MVC_PM_INF;
+      const double L = mvc_log((2.0 * MVC_PI) * t);
+      const double ll = block_tree64(ctx, P.Kact[v], [&](int64_t j) {
+        const int nk = P.d_n[v * KC + j];
+        if (nk == 0) return 0.0;
+        double sse = P.S2[v * KC + j] - P.Q[v * KC + j] / (double)nk;
+        if (sse < 0.0) sse = 0.0;
+        return ((-0.5 * (double)nk) * (double)D) * L - 0.5 * (sse / t);
+      });
+      const double prior = (-3.0 * mvc_log(t)) - 1.0 / t;
+      return ll + prior;
+    };
+    // ---- multiview_hyper.cpp:211-231 ----
+    for (int v = 0; v < V; ++v) {
+      double t_old = hyp[v];
+      if (t_old <= 0.0) t_old = kEps;
+      const double l_old = post_tau(v, t_old);
+      const double t_prop = mvc_exp(mvc_log(t_old) + rnorm(0.0, 0.3));
+      if (t_prop <= 0.0) continue;
+      const double l_new = post_tau(v, t_prop);
+      const double acc = (l_new - l_old) + (mvc_log(t_prop) - mvc_log(t_old));
+      const double u = unif();
+      if (mvc_log(u) < acc) { if (tid == 0) hyp[v] = t_prop; }
+      __syncthreads();
+    }
+    // ---- :239-266 ----
+    for (int v = 0; v < V; ++v) {
+      double a_old = hyp[V + v];
+      if (a_old <= 0.0) a_old = kEps;
+      const double la = mvc_log(a_old > kEps ? a_old : kEps) + rnorm(0.0, 0.1);
+      double a_prop = mvc_exp(la);
+      if (!(a_prop > kEps)) a_prop = kEps;
+      const double sv = hyp[2 * V + v];
+      const double lo = (a_old <= 0.0) ? -MVC_PM_INF : eppf_view(v, a_old, sv) + prior_alpha(a_old);
+      const double ln = (a_prop <= 0.0) ? -MVC_PM_INF : eppf_view(v, a_prop, sv) + prior_alpha(a_prop);
+      const double lq = mvc_log(a_prop) - mvc_log(a_old);
+      const double u = unif();
+      if (mvc_log(u) < (ln - lo) + lq) { if (tid == 0) hyp[V + v] = a_prop; }
+      __syncthreads();
+      const double s_old = hyp[2 * V + v];
+      const double s_prop = reflect_unit(s_old + rnorm(0.0, 0.05));
+      const double u2 = unif();
+      const double av = hyp[V + v];
+      const double pn = (s_prop <= kEps || s_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(v, av, s_prop) + prior_sigma(s_prop);
+      const double po = (s_old <= kEps || s_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(v, av, s_old) + prior_sigma(s_old);
+      if (mvc_log(u2) < pn - po) { if (tid == 0) hyp[2 * V + v] = s_prop; }
+      __syncthreads();
+    }
+    // ---- :268-291 ----
+    {
+      double ag_old = hyp[3 * V];
+      if (ag_old <= 0.0) ag_old = kEps;
+      const double la = mvc_log(ag_old > kEps ? ag_old : kEps) + rnorm(0.0, 0.1);
+      double ag_prop = mvc_exp(la);
+      if (!(ag_prop > kEps)) ag_prop = kEps;
+      const double sg0 = hyp[3 * V + 1];
+      const double lo = eppf_global(ag_old, sg0) + prior_alpha(ag_old);
+      const double ln = eppf_global(ag_prop, sg0) + prior_alpha(ag_prop);
+      const double lq = mvc_log(ag_prop) - mvc_log(ag_old);
+      const double u = unif();
+      if (mvc_log(u) < (ln - lo) + lq) { if (tid == 0) hyp[3 * V] = ag_prop; }
+      __syncthreads();
+      const double sg_old = hyp[3 * V + 1];
+      const double sg_prop = reflect_unit(sg_old + rnorm(0.0, 0.05));
+      const double u2 = unif();
+      const double a_g = hyp[3 * V];
+      const double pn = (sg_prop <= kEps || sg_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_prop) + prior_sigma(sg_prop);
+      const double po = (sg_old <= kEps || sg_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_old) + prior_sigma(sg_old);
+      if (mvc_log(u2) < pn - po) { if (tid == 0) hyp[3 * V + 1] = sg_prop; }
+      __syncthreads();
+    }
+  }
+  // ---- coefficients of the next sweep (frozen state) ----
+  for (int v = 0; v < V; ++v) {
+    const double tau = hyp[v];
+    const double L = mvc_log((2.0 * MVC_PI) * tau);
+    if (tid == 0) { A.L2pt[v] = L; A.cnew[v] = (double)D * (-0.5 * L); }
+    for (int j = tid; j < P.Kact[v]; j += 256) {
+      const Coef c = coef(P.d_n[v * KC + j], P.Q[v * KC + j], tau, L, D);
+      P.c0[v * KC + j] = c.c0;
+      P.cb[v * KC + j] = c.cb;
+    }
+  }
+  const double sg = hyp[3 * V + 1];
+  for (int p = tid; p < T; p += 256) P.lmass[p] = mvc_log((double)P.n_t[p] - sg);
+}
+
+// ===========================================================================
+// Host side of the parallel schedule.
+// ===========================================================================
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "mvc_host.h"
+
+namespace mvc {
+
+namespace {
+constexpr int kParTC = 4096;   // table capacity (two-level tree64)
+constexpr int kParKC = 4095;   // live dishes per view (+1 new element <= 4096)
+constexpr int kZGrid = 2048;   // zresample / birth grid (4 waves per block)
+
+template <class Tp>
+Tp *dmalloc(size_t count) {
+  void *p = nullptr;
+  MVC_HIP(hipMalloc(&p, sizeof(Tp) * std::max<size_t>(count, 1)));
+  return (Tp *)p;
+}
+}  // namespace
+
+class ParallelSampler : public Sampler {
+ public:
+  int n, V, D, TC, KC, nchunk;
+  double *y = nullptr, *Y2 = nullptr;
+  struct Chain {
+    ParState P{};
+    double *L2pt = nullptr, *cnew = nullptr;
+    int32_t *Koff = nullptr, *status = nullptr;
+    int32_t *choice = nullptr, *flags = nullptr, *brank = nullptr, *blist = nullptr, *nbirth = nullptr;
+    int32_t *bdish = nullptr, *cnt = nullptr, *pos_new = nullptr, *tmp_dish = nullptr, *tmp_nt = nullptr;
+    int32_t *lcnt = nullptr, *jmap = nullptr, *histT = nullptr, *histL = nullptr;
+    double *mh_scratch = nullptr;
+    size_t mh_half = 0;
+    int T = 0;
+    std::vector<int32_t> K;
+    uint32_t gid = 0;
+    std::vector<void *> owned;
+  };
+  std::vector<Chain> chains;
+  double *lp_scratch = nullptr;
+  size_t lp_cap = 0;               // doubles per wave
+  double *part1 = nullptr, *part2 = nullptr;
+  size_t part_cap = 0;             // sumK capacity of partials
+  void *cub_tmp = nullptr;
+  size_t cub_bytes = 0;
+  std::vector<int32_t> st_host;
+
+  template <class Tp>
+  Tp *own(Chain &c, size_t count) {
+    Tp *p = dmalloc<Tp>(count);
+    c.owned.push_back(p);
+    return p;
+  }
+
+  ParallelSampler(const mvc_config &cf, const double *const *views) {
+    cfg = cf;
+    n = cf.n; V = cf.n_views; D = cf.dim;
+    TC = kParTC; KC = kParKC;
+    nchunk = (n + 4095) / 4096;
+    if (V > MVC_MAXV) throw Error(MVC_ERR_UNSUPPORTED, "at most 64 views");
+    MVC_HIP(hipSetDevice(cf.device));
+    MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    timers.stream = stream;
+    timers.on = (cf.flags & MVC_FLAG_TIMING) != 0;
+    std::vector<double> yh((size_t)V * n * D);
+    for (int v = 0; v < V; ++v) std::memcpy(&yh[(size_t)v * n * D], views[v], sizeof(double) * (size_t)n * D);
+    y = dmalloc<double>(yh.size());
+    Y2 = dmalloc<double>((size_t)V * n);
+    MVC_HIP(hipMemcpyAsync(y, yh.data(), sizeof(double) * yh.size(), hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
+    MVC_HIP(hipGetLastError());
+    // hipcub temp storage (scan + select over n)
+    size_t b1 = 0, b2 = 0;
+    MVC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (int32_t *)nullptr, (int32_t *)nullptr, n, stream));
+    hipcub::CountingInputIterator<int32_t> it(0);
+    MVC_HIP(hipcub::DeviceSelect::Flagged(nullptr, b2, it, (int32_t *)nullptr, (int32_t *)nullptr,
+                                          (int32_t *)nullptr, n, stream));
+    cub_bytes = std::max(b1, b2);
+    MVC_HIP(hipMalloc(&cub_tmp, cub_bytes));
+    st_host.assign(V + 4, 0);
+    chains.resize(cf.n_chains);
+    for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh.data());
+    MVC_HIP(hipStreamSynchronize(stream));
+  }
+
+  ~ParallelSampler() override {
+    if (stream) hipStreamSynchronize(stream);
+    for (auto &c : chains)
+      for (void *p : c.owned) hipFree(p);
+    for (void *p : {(void *)y, (void *)Y2, (void *)lp_scratch, (void *)part1, (void *)part2, cub_tmp})
+      if (p) hipFree(p);
+    if (stream) hipStreamDestroy(stream);
+  }
+
+  void alloc_chain(Chain &c) {
+    ParState &P = c.P;
+    P.n = n; P.V = V; P.D = D; P.TC = TC; P.KC = KC;
+    P.z = own<int32_t>(c, n);
+    P.n_t = own<int32_t>(c, TC);
+    P.dish = own<int32_t>(c, (size_t)V * TC);
+    P.d_id = own<int32_t>(c, (size_t)V * KC);
+    P.d_n = own<int32_t>(c, (size_t)V * KC);
+    P.d_l = own<int32_t>(c, (size_t)V * KC);
+    P.S1T = own<double>(c, (size_t)V * D * KC);
+    P.S2 = own<double>(c, (size_t)V * KC);
+    P.Q = own<double>(c, (size_t)V * KC);
+    P.c0 = own<double>(c, (size_t)V * KC);
+    P.cb = own<double>(c, (size_t)V * KC);
+    P.lmass = own<double>(c, TC);
+    P.hyper = own<double>(c, 3 * V + 2);
+    P.Kact = own<int32_t>(c, V);
+    P.next_id = own<int32_t>(c, V);
+    P.Ltot = own<int32_t>(c, V);
+    c.L2pt = own<double>(c, V);
+    c.cnew = own<double>(c, V);
+    c.Koff = own<int32_t>(c, V + 1);
+    c.status = own<int32_t>(c, V + 4);
+    c.choice = own<int32_t>(c, n);
+    c.flags = own<int32_t>(c, n);
+    c.brank = own<int32_t>(c, n);
+    c.blist = own<int32_t>(c, n);
+    c.nbirth = own<int32_t>(c, 1);
+    c.bdish = own<int32_t>(c, (size_t)n * V);
+    c.cnt = own<int32_t>(c, TC);
+    c.pos_new = own<int32_t>(c, TC);
+    c.tmp_dish = own<int32_t>(c, (size_t)V * TC);
+    c.tmp_nt = own<int32_t>(c, TC);
+    c.lcnt = own<int32_t>(c, (size_t)V * KC);
+    c.jmap = own<int32_t>(c, (size_t)V * KC);
+    c.histT = own<int32_t>(c, (size_t)n + 2);
+    c.histL = own<int32_t>(c, (size_t)V * (TC + 2));
+    c.mh_half = (size_t)n / 64 + 128;
+    c.mh_scratch = own<double>(c, 2 * c.mh_half);
+  }
+
+  void init_chain(Chain &c, uint32_t gid, const double *yh) {
+    c.gid = gid;
+    alloc_chain(c);
+    const InitState S = draw_initial_state(yh, n, V, D, cfg.seed, gid);
+    // multiview_gibbs.cpp:12-98 in dense-position / live-list form
+    std::vector<int32_t> nt(4, 0);
+    for (int i = 0; i < n; ++i) nt[S.table[i]]++;
+    std::vector<int32_t> dish((size_t)V * TC, 0), did((size_t)V * KC, 0), dn((size_t)V * KC, 0), dl((size_t)V * KC, 0);
+    c.K.assign(V, 0);
+    std::vector<int32_t> next(V, 2);
+    std::vector<double> hyp(3 * V + 2);
+    for (int v = 0; v < V; ++v) {
+      int l2[2] = {0, 0}, map2[2] = {-1, -1};
+      for (int t = 0; t < 4; ++t) l2[S.dish_raw[v * 4 + t]]++;
+      for (int k = 0; k < 2; ++k)
+        if (l2[k] > 0) { map2[k] = c.K[v]; did[v * KC + c.K[v]] = k; dl[v * KC + c.K[v]] = l2[k]; c.K[v]++; }
+      for (int t = 0; t < 4; ++t) {
+        const int j = map2[S.dish_raw[v * 4 + t]];
+        dish[(size_t)v * TC + t] = j;
+        dn[v * KC + j] += nt[t];
+      }
+      hyp[v] = S.tau[v];
+      hyp[V + v] = 1.0;
+      hyp[2 * V + v] = 0.5;
+    }
+    hyp[3 * V] = 1.0;
+    hyp[3 * V + 1] = 0.6;
+    c.T = 4;
+    ParState &P = c.P;
+    auto up = [&](void *dst, const void *src, size_t bytes) {
+      MVC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+    };
+    up(P.z, S.table.data(), sizeof(int32_t) * n);
+    up(P.n_t, nt.data(), sizeof(int32_t) * 4);
+    up(P.dish, dish.data(), sizeof(int32_t) * dish.size());
+    up(P.d_id, did.data(), sizeof(int32_t) * did.size());
+    up(P.d_n, dn.data(), sizeof(int32_t) * dn.size());
+    up(P.d_l, dl.data(), sizeof(int32_t) * dl.size());
+    up(P.Kact, c.K.data(), sizeof(int32_t) * V);
+    up(P.next_id, next.data(), sizeof(int32_t) * V);
+    up(P.hyper, hyp.data(), sizeof(double) * hyp.size());
+    std::vector<int32_t> st(V + 4, 0);
+    st[0] = 4;
+    up(c.status, st.data(), sizeof(int32_t) * st.size());
+    MVC_HIP(hipStreamSynchronize(stream));
+    rebuild_stats(c);
+    launch_hyper(c, 0, 0);
+  }
+
+  int sumK(const Chain &c) const {
+    int s = 0;
+    for (int k : c.K) s += k;
+    return s;
+  }
+
+  void upload_koff(Chain &c) {
+    std::vector<int32_t> ko(V + 1, 0);
+    for (int v = 0; v < V; ++v) ko[v + 1] = ko[v] + c.K[v];
+    MVC_HIP(hipMemcpyAsync(c.Koff, ko.data(), sizeof(int32_t) * ko.size(), hipMemcpyHostToDevice, stream));
+    // the copy source must outlive the async copy
+    MVC_HIP(hipStreamSynchronize(stream));
+  }
+
+  void rebuild_stats(Chain &c) {
+    upload_koff(c);
+    const int sk = sumK(c);
+    if ((size_t)sk > part_cap) {
+      if (part1) hipFree(part1);
+      if (part2) hipFree(part2);
+      part_cap = (size_t)sk + 64;
+      part1 = dmalloc<double>((size_t)nchunk * part_cap * D);
+      part2 = dmalloc<double>((size_t)nchunk * part_cap);
+    }
+    int Kmax = 1;
+    for (int k : c.K) Kmax = std::max(Kmax, k);
+    // LDS: acc[K][dg] + acc2[K] + ysub[64][dg] + y2sub[64] + jsub[64]
+    const size_t budget = 96 * 1024;
+    const size_t fixed = sizeof(double) * Kmax + sizeof(double) * 64 + sizeof(int) * 64;
+    if (fixed >= budget) throw Error(MVC_ERR_UNSUPPORTED, "too many dishes for the stats kernel");
+    int dg = (int)((budget - fixed) / (sizeof(double) * (Kmax + 64)));
+    dg = std::max(1, std::min({dg, D, 256}));
+    const size_t lds = sizeof(double) * ((size_t)Kmax * dg + Kmax + 64 * dg + 64) + sizeof(int) * 64;
+    hipEvent_t ev = nullptr;
+    timers.begin("stats", &ev);
+    hipLaunchKernelGGL(mvc_par_stats_partial_kernel, dim3(nchunk, V), dim3(256), lds, stream, c.P, (const double *)y,
+                       (const double *)Y2, (const int32_t *)c.Koff, (int)part_cap, dg, part1, part2);
+    MVC_HIP(hipGetLastError());
+    const size_t tot = (size_t)sk * (D + 1);
+    hipLaunchKernelGGL(mvc_par_stats_combine_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256),
+                       0, stream, c.P, (const int32_t *)c.Koff, (int)part_cap, nchunk, (const double *)part1,
+                       (const double *)part2);
+    MVC_HIP(hipGetLastError());
+    timers.end("stats", ev);
+  }
+
+  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix) {
+    MHArgs A;
+    A.P = c.P;
+    A.status = c.status;
+    A.Koff = c.Koff;
+    A.L2pt = c.L2pt;
+    A.cnew = c.cnew;
+    A.histT = c.histT;
+    A.histL = c.histL;
+    A.scratch = c.mh_scratch;
+    A.half = c.mh_half;
+    A.seed = cfg.seed;
+    A.chain = c.gid;
+    A.sweep = sweep_ix;
+    A.do_mh = do_mh;
+    hipEvent_t ev = nullptr;
+    timers.begin("hyper", &ev);
+    hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(256), 0, stream, A);
+    MVC_HIP(hipGetLastError());
+    timers.end("hyper", ev);
+  }
+
+  void ensure_lp(size_t per_wave) {
+    if (per_wave <= lp_cap) return;
+    if (lp_scratch) hipFree(lp_scratch);
+    lp_cap = per_wave + 64;
+    lp_scratch = dmalloc<double>((size_t)kZGrid * 4 * lp_cap);
+  }
+
+  Sweep make_sweep(Chain &c, uint32_t s) {
+    Sweep A;
+    A.P = c.P;
+    A.y = y;
+    A.Y2 = Y2;
+    A.L2pt = c.L2pt;
+    A.cnew = c.cnew;
+    A.Koff = c.Koff;
+    A.scratch = lp_scratch;
+    A.choice = c.choice;
+    A.bdish = c.bdish;
+    A.blist = c.blist;
+    A.nbirth = c.nbirth;
+    A.status = c.status;
+    A.T = c.T;
+    A.sumK = (int32_t)lp_cap;
+    A.seed = cfg.seed;
+    A.chain = c.gid;
+    A.sweep = s;
+    return A;
+  }
+
+  void sweep_chain(Chain &c, uint32_t s) {
+    ensure_lp((size_t)sumK(c));
+    upload_koff(c);
+    Sweep A = make_sweep(c, s);
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    timers.begin("zresample", &e0);
+    hipLaunchKernelGGL(mvc_par_zresample_kernel, dim3(std::min(kZGrid, (n + 3) / 4)), dim3(256), 0, stream, A);
+    MVC_HIP(hipGetLastError());
+    timers.end("zresample", e0);
+    timers.begin("commit", &e1);
+    MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
+    hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n,
+                       (const int32_t *)c.choice, c.cnt, c.flags);
+    MVC_HIP(hipGetLastError());
+    size_t bytes = cub_bytes;
+    MVC_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, bytes, c.flags, c.brank, n, stream));
+    bytes = cub_bytes;
+    hipcub::CountingInputIterator<int32_t> it(0);
+    MVC_HIP(hipcub::DeviceSelect::Flagged(cub_tmp, bytes, it, c.flags, c.blist, c.nbirth, n, stream));
+    hipLaunchKernelGGL(mvc_par_birth_kernel, dim3(std::min(kZGrid, (n + 3) / 4)), dim3(256), 0, stream, A);
+    MVC_HIP(hipGetLastError());
+    hipLaunchKernelGGL(mvc_par_commit_kernel, dim3(1), dim3(256), 0, stream, c.P, c.T, (const int32_t *)c.cnt,
+                       (const int32_t *)c.nbirth, (const int32_t *)c.bdish, c.pos_new, c.tmp_dish, c.tmp_nt, c.lcnt,
+                       c.jmap, c.status);
+    MVC_HIP(hipGetLastError());
+    hipLaunchKernelGGL(mvc_par_relabel_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n, V,
+                       (const int32_t *)c.choice, (const int32_t *)c.pos_new, (const int32_t *)c.brank,
+                       (const int32_t *)c.status, c.P.z);
+    MVC_HIP(hipGetLastError());
+    timers.end("commit", e1);
+    // the one host synchronisation of a sweep: new T and dish counts
+    MVC_HIP(hipMemcpyAsync(st_host.data(), c.status, sizeof(int32_t) * (V + 4), hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipStreamSynchronize(stream));
+    if (st_host[V + 1] == 1) throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: table capacity (4096) exceeded");
+    if (st_host[V + 1] == 2) throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: dish capacity (4095 per view) exceeded");
+    c.T = st_host[0];
+    for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
+    rebuild_stats(c);
+    launch_hyper(c, 1, s);
+    (void)e2;
+  }
+
+  void sweep(int n_sweeps) override {
+    for (int it = 0; it < n_sweeps; ++it) {
+      hipEvent_t ev = nullptr;
+      timers.begin("sweep", &ev);
+      for (auto &c : chains) sweep_chain(c, (uint32_t)sweeps_done);
+      timers.end("sweep", ev);
+      ++sweeps_done;
+    }
+  }
+
+  void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
+
+  void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of, int32_t dish_cap,
+                 double *hyper) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    Chain &c = chains[chain];
+    MVC_HIP(hipStreamSynchronize(stream));
+    if (n_tables) *n_tables = c.T;
+    if (table_of) MVC_HIP(hipMemcpy(table_of, c.P.z, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+    if (dish_of) {
+      std::vector<int32_t> dish((size_t)V * TC), did((size_t)V * KC);
+      MVC_HIP(hipMemcpy(dish.data(), c.P.dish, sizeof(int32_t) * dish.size(), hipMemcpyDeviceToHost));
+      MVC_HIP(hipMemcpy(did.data(), c.P.d_id, sizeof(int32_t) * did.size(), hipMemcpyDeviceToHost));
+      for (int v = 0; v < V; ++v)
+        for (int p = 0; p < std::min(c.T, (int)dish_cap); ++p)
+          dish_of[(size_t)v * dish_cap + p] = did[(size_t)v * KC + dish[(size_t)v * TC + p]];
+    }
+    if (hyper) MVC_HIP(hipMemcpy(hyper, c.P.hyper, sizeof(double) * (3 * V + 2), hipMemcpyDeviceToHost));
+  }
+
+  void get_dish_counts(int chain, int32_t *k_out) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    for (int v = 0; v < V; ++v) k_out[v] = chains[chain].K[v];
+  }
+};
+
+Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views) {
+  return new ParallelSampler(cfg, views);
+}
+
+}  // namespace mvc

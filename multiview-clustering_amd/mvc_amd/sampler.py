@@ -1,0 +1,246 @@
+"""Python host mirror of the reference's R entry point.
+
+``run_gibbs_cpp(data_views, M, burn_in, thin)`` has the argument meaning and
+the output list of ``Rcpp::List run_gibbs_cpp(const Rcpp::List& data_views,
+int M, int burn_in, int thin)`` (/root/reference/Multiview/multiview_gibbs.cpp:
+105-131): a dict with ``table_of`` (list over saved iterations of int32[n],
+0-based table positions), ``dish_of`` (list over saved iterations of a list
+over views of int32[T_s], raw dish ids), ``loglik`` (empty: the reference
+declares compute_log_likelihood but never defines it, multiview_gibbs.h:13),
+``alpha_v``/``sigma_v``/``tau_v`` (list over views of float64[S]) and
+``alpha_global``/``sigma_global`` (float64[S]).
+
+The RNG is Philox4x32-10 keyed by ``seed`` instead of R's global RNG
+(multiview_utils.cpp:305-306); everything runs on the GPU through
+libmvc_hip.so.  Errors from the library raise ``MvcError`` (the reference
+raises R conditions via Rcpp::stop, multiview_utils.cpp:141,145).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _views_to_array(data_views):
+    """List of V arrays of n (or n x D) floats -> float64 [V][n][D]."""
+    if isinstance(data_views, np.ndarray):
+        arr = np.asarray(data_views, dtype=np.float64)
+        if arr.ndim == 2:
+            arr = arr[:, :, None]
+        return np.ascontiguousarray(arr)
+    views = [np.asarray(v, dtype=np.float64) for v in data_views]
+    if not views:
+        raise ValueError("data_views must hold at least one view")
+    n = views[0].shape[0]       # n is taken from view 0 (multiview_gibbs.cpp:110)
+    out = []
+    for v in views:
+        if v.shape[0] != n:
+            raise ValueError("all views must have the same number of observations")
+        out.append(v.reshape(n, -1))
+    D = out[0].shape[1]
+    if any(v.shape[1] != D for v in out):
+        raise ValueError("all views must have the same dimension")
+    return np.ascontiguousarray(np.stack(out))
+
+
+def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_chain=0, device=0,
+                mode="exact", table_cap=0, dish_cap=0, timing=False, quiet=True):
+    cfg = L.Config()
+    L.lib().mvc_config_init(ctypes.byref(cfg))
+    cfg.n, cfg.n_views, cfg.dim = n, V, D
+    cfg.n_iter, cfg.burn_in, cfg.thin = M, burn_in, thin
+    cfg.seed = seed & 0xFFFFFFFFFFFFFFFF
+    cfg.n_chains, cfg.first_chain, cfg.device = n_chains, first_chain, device
+    cfg.mode = {"exact": L.MODE_EXACT, "parallel": L.MODE_PARALLEL}[mode]
+    cfg.table_cap, cfg.dish_cap = table_cap, dish_cap
+    cfg.flags = (L.FLAG_TIMING if timing else 0) | (L.FLAG_QUIET if quiet else 0)
+    return cfg
+
+
+def _view_ptrs(y):
+    V = y.shape[0]
+    arr = (ctypes.POINTER(ctypes.c_double) * V)()
+    for v in range(V):
+        arr[v] = y[v].ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+    return arr
+
+
+def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chains=1, device=0,
+                  first_chain=0, quiet=False):
+    """Drop-in for the reference's ``run_gibbs_cpp`` (see module docstring).
+
+    With ``n_chains > 1`` a list of per-chain result dicts is returned.
+    """
+    y = _views_to_array(data_views)
+    V, n, D = y.shape
+    cfg = make_config(n, V, D, M, burn_in, thin, seed, n_chains, first_chain, device, mode, quiet=quiet)
+    lib = L.lib()
+    res = ctypes.c_void_p()
+    buf = L.errbuf()
+    L.check(lib.mvc_run(ctypes.byref(cfg), _view_ptrs(y), ctypes.byref(res), buf, len(buf)), buf)
+    try:
+        S = lib.mvc_result_num_saved(res)
+        outs = []
+        for c in range(n_chains):
+            table_of, dish_of = [], []
+            for s in range(S):
+                T = lib.mvc_result_num_tables(res, c, s)
+                t = np.ctypeslib.as_array(lib.mvc_result_table_of(res, c, s), shape=(n,)).copy()
+                d = np.ctypeslib.as_array(lib.mvc_result_dish_of(res, c, s), shape=(V * max(T, 1),))[: V * T]
+                d = d.copy().reshape(V, T)
+                table_of.append(t)
+                dish_of.append([d[v] for v in range(V)])
+
+            def tr(which, per_view):
+                p = lib.mvc_result_trace(res, c, which)
+                k = V * S if per_view else S
+                a = np.ctypeslib.as_array(p, shape=(max(k, 1),))[:k].copy() if k else np.zeros(0)
+                return [a[v * S:(v + 1) * S] for v in range(V)] if per_view else a
+
+            outs.append({
+                "table_of": table_of,
+                "dish_of": dish_of,
+                "loglik": np.zeros(0),
+                "alpha_v": tr(L.TRACE_ALPHA_V, True),
+                "sigma_v": tr(L.TRACE_SIGMA_V, True),
+                "tau_v": tr(L.TRACE_TAU_V, True),
+                "alpha_global": tr(L.TRACE_ALPHA_GLOBAL, False),
+                "sigma_global": tr(L.TRACE_SIGMA_GLOBAL, False),
+            })
+        return outs[0] if n_chains == 1 else outs
+    finally:
+        lib.mvc_result_free(res)
+
+
+def get_final_clusters(res):
+    """Port of New_Simulation.R:135-149: per-view cluster labels of the last
+    saved iteration, shape [n, V]."""
+    t = res["table_of"][-1]
+    dishes = res["dish_of"][-1]
+    return np.stack([np.asarray(d)[t] for d in dishes], axis=1)
+
+
+class Sampler:
+    """Handle API: data uploaded once; sweeps run on the handle's HIP stream."""
+
+    def __init__(self, data_views, seed=1999, mode="exact", n_chains=1, first_chain=0, device=0,
+                 table_cap=0, dish_cap=0, timing=False):
+        self.y = _views_to_array(data_views)
+        self.V, self.n, self.D = self.y.shape
+        self.n_chains = n_chains
+        cfg = make_config(self.n, self.V, self.D, 0, 0, 1, seed, n_chains, first_chain, device, mode,
+                          table_cap, dish_cap, timing)
+        self._lib = L.lib()
+        self._h = ctypes.c_void_p()
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_create(ctypes.byref(cfg), _view_ptrs(self.y), ctypes.byref(self._h), buf,
+                                             len(buf)), buf)
+
+    def sweep(self, n_sweeps=1):
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_sweep(self._h, n_sweeps, buf, len(buf)), buf)
+
+    def synchronize(self):
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_synchronize(self._h, buf, len(buf)), buf)
+
+    @property
+    def sweeps_done(self):
+        return self._lib.mvc_sampler_sweeps_done(self._h)
+
+    def state(self, chain=0):
+        """(table_of[n], dish_of[V][T], hyper dict) of one chain."""
+        buf = L.errbuf()
+        T = ctypes.c_int32()
+        t = np.empty(self.n, dtype=np.int32)
+        hy = np.empty(3 * self.V + 2)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.check(self._lib.mvc_sampler_get_state(self._h, chain, t.ctypes.data_as(ip), ctypes.byref(T), None, 0,
+                                                hy.ctypes.data_as(dp), buf, len(buf)), buf)
+        cap = max(T.value, 1)
+        d = np.empty(self.V * cap, dtype=np.int32)
+        L.check(self._lib.mvc_sampler_get_state(self._h, chain, None, ctypes.byref(T), d.ctypes.data_as(ip), cap,
+                                                None, buf, len(buf)), buf)
+        V = self.V
+        hyper = {"tau_v": hy[:V].copy(), "alpha_v": hy[V:2 * V].copy(), "sigma_v": hy[2 * V:3 * V].copy(),
+                 "alpha_global": float(hy[3 * V]), "sigma_global": float(hy[3 * V + 1])}
+        return t, d.reshape(V, cap)[:, :T.value].copy(), hyper
+
+    def dish_counts(self, chain=0):
+        buf = L.errbuf()
+        k = np.empty(self.V, dtype=np.int32)
+        L.check(self._lib.mvc_sampler_get_dish_counts(self._h, chain, k.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                      buf, len(buf)), buf)
+        return k
+
+    def kernel_time(self, name):
+        """(total_ms, launches) recorded with HIP events on the handle's stream."""
+        ms = ctypes.c_double()
+        cnt = ctypes.c_int64()
+        st = self._lib.mvc_sampler_kernel_time(self._h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt))
+        if st != L.MVC_OK:
+            raise L.MvcError(st, "kernel_time failed")
+        return ms.value, cnt.value
+
+    def reset_timers(self):
+        self._lib.mvc_sampler_reset_timers(self._h)
+
+    def close(self):
+        if self._h:
+            self._lib.mvc_sampler_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- spec primitives on the device (parity tests) ----
+def device_math(op, x, device=0):
+    ops = {"exp": 0, "log": 1, "lgamma": 2, "qnorm": 3, "sqrt": 4}
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    o = np.empty_like(x)
+    buf = L.errbuf()
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.check(L.lib().mvc_device_math(device, ops[op], x.ctypes.data_as(dp), o.ctypes.data_as(dp), x.size, buf,
+                                    len(buf)), buf)
+    return o
+
+
+def device_seq_uniforms(seed, chain, start, n, device=0):
+    o = np.empty(n)
+    buf = L.errbuf()
+    L.check(L.lib().mvc_device_seq_uniforms(device, seed, chain, start,
+                                            o.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n, buf, len(buf)), buf)
+    return o
+
+
+def device_tree64(x, r, device=0):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    rows, n = x.shape
+    r = np.ascontiguousarray(r, dtype=np.float64)
+    sums = np.empty(rows)
+    sel = np.empty(rows, dtype=np.int64)
+    buf = L.errbuf()
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.check(L.lib().mvc_device_tree64(device, x.ctypes.data_as(dp), rows, n, r.ctypes.data_as(dp),
+                                      sums.ctypes.data_as(dp), sel.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                      buf, len(buf)), buf)
+    return sums, sel
+
+
+def device_gemm_check(Y, S1, device=0):
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    S1 = np.ascontiguousarray(S1, dtype=np.float64)
+    n, D = Y.shape
+    K = S1.shape[0]
+    G = np.empty((n, K))
+    buf = L.errbuf()
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.check(L.lib().mvc_device_gemm_check(device, Y.ctypes.data_as(dp), S1.ctypes.data_as(dp), n, K, D,
+                                          G.ctypes.data_as(dp), buf, len(buf)), buf)
+    return G

@@ -1,0 +1,159 @@
+"""ctypes binding of the CPU oracle (oracle/build/libmvc_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py.  The product never imports this module.
+
+Parity status: "parity unpinned" against the reference binary (the reference
+needs Rcpp/R, absent here; see mvc_oracle.cpp header and DESIGN.md §3).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libmvc_oracle.so")
+_lib = None
+
+EXACT, PARALLEL = 0, 1
+LIBM, PORTABLE = 0, 1
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i32, u64, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int64
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int)
+        L.mvo_run.restype = vp
+        L.mvo_run.argtypes = [dp, i32, i32, i32, i32, i32, i32, u64, i32, i32, i32]
+        L.mvo_error.restype = ctypes.c_char_p
+        L.mvo_error.argtypes = [vp]
+        for f in ("mvo_num_saved", "mvo_num_sweeps"):
+            getattr(L, f).restype = i32
+            getattr(L, f).argtypes = [vp]
+        L.mvo_sample_T.restype = i32
+        L.mvo_sample_T.argtypes = [vp, i32]
+        L.mvo_copy_table_of.argtypes = [vp, i32, ip]
+        L.mvo_copy_dish_of.argtypes = [vp, i32, ip]
+        L.mvo_copy_hyper.argtypes = [vp, dp, dp, dp, dp, dp]
+        L.mvo_copy_trace.argtypes = [vp, ip, ctypes.POINTER(ctypes.c_uint64)]
+        L.mvo_free.argtypes = [vp]
+        for f in ("mvo_pm_exp", "mvo_pm_log", "mvo_pm_lgamma", "mvo_pm_qnorm"):
+            getattr(L, f).argtypes = [dp, dp, i64]
+        L.mvo_philox.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.POINTER(ctypes.c_uint32)]
+        L.mvo_seq_uniforms.argtypes = [u64, ctypes.c_uint32, u64, dp, i64]
+        L.mvo_tree64_sum.restype = ctypes.c_double
+        L.mvo_tree64_sum.argtypes = [dp, i64]
+        L.mvo_tree64_select.restype = i64
+        L.mvo_tree64_select.argtypes = [dp, i64, ctypes.c_double]
+        _lib = L
+    return _lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE):
+    """Run one chain.  y: float64 array [V][n] (D=1) or [V][n][D].
+
+    Returns a dict shaped like the reference's Rcpp::List
+    (multiview_gibbs.cpp:121-130) plus per-sweep traces.
+    """
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    if y.ndim == 2:
+        y = y[:, :, None]
+    V, n, D = y.shape
+    L = lib()
+    h = L.mvo_run(_dp(y), n, V, D, M, burn_in, thin, ctypes.c_uint64(seed), chain, mode, math)
+    try:
+        err = L.mvo_error(h)
+        if err:
+            raise RuntimeError(err.decode())
+        S = L.mvo_num_saved(h)
+        table_of, dish_of = [], []
+        for s in range(S):
+            t = np.empty(n, dtype=np.int32)
+            L.mvo_copy_table_of(h, s, t.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            T = L.mvo_sample_T(h, s)
+            dd = np.empty(V * T, dtype=np.int32)
+            L.mvo_copy_dish_of(h, s, dd.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+            table_of.append(t)
+            dish_of.append(dd.reshape(V, T))
+        av, sv, tv = (np.empty(S * V) for _ in range(3))
+        ag, sg = np.empty(S), np.empty(S)
+        L.mvo_copy_hyper(h, _dp(av), _dp(sv), _dp(tv), _dp(ag), _dp(sg))
+        nsw = L.mvo_num_sweeps(h)
+        tT = np.empty(nsw, dtype=np.int32)
+        td = np.empty(nsw, dtype=np.uint64)
+        L.mvo_copy_trace(h, tT.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                         td.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        return {
+            "table_of": table_of,
+            "dish_of": dish_of,
+            "alpha_v": av.reshape(S, V).T.copy(),
+            "sigma_v": sv.reshape(S, V).T.copy(),
+            "tau_v": tv.reshape(S, V).T.copy(),
+            "alpha_global": ag,
+            "sigma_global": sg,
+            "trace_T": tT,
+            "trace_draws": td,
+        }
+    finally:
+        L.mvo_free(h)
+
+
+def _vec(fn, x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    o = np.empty_like(x)
+    fn(_dp(x), _dp(o), x.size)
+    return o
+
+
+def pm_exp(x):
+    return _vec(lib().mvo_pm_exp, x)
+
+
+def pm_log(x):
+    return _vec(lib().mvo_pm_log, x)
+
+
+def pm_lgamma(x):
+    return _vec(lib().mvo_pm_lgamma, x)
+
+
+def pm_qnorm(x):
+    return _vec(lib().mvo_pm_qnorm, x)
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    o = (ctypes.c_uint32 * 4)()
+    lib().mvo_philox(c, ctypes.c_uint32(key[0]), ctypes.c_uint32(key[1]), o)
+    return tuple(o)
+
+
+def seq_uniforms(seed, chain, start, n):
+    o = np.empty(n)
+    lib().mvo_seq_uniforms(ctypes.c_uint64(seed), chain, ctypes.c_uint64(start), _dp(o), n)
+    return o
+
+
+def tree64_sum(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return lib().mvo_tree64_sum(_dp(x), x.size)
+
+
+def tree64_select(x, r):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return int(lib().mvo_tree64_select(_dp(x), x.size, r))
