@@ -17,6 +17,8 @@
  *                  uniform.  This stands in for R's unif_rand() stream.
  *   MVC_TAG_Z    : parallel-mode table draw of customer i in sweep s,
  *                  counter {i, s, chain, TAG}.
+ *   MVC_TAG_Z2   : parallel-mode birth resolution (join a table born
+ *                  earlier in the sweep or open one), counter {i, s, chain, TAG}.
  *   MVC_TAG_DISH : parallel-mode birth dish draw, counter {i, s, chain,
  *                  TAG + 1 + v}.
  *   MVC_TAG_MH   : parallel-mode hyperparameter stream, counter
@@ -35,6 +37,7 @@
 
 #define MVC_TAG_SEQ  0x4D564345u /* 'MVCE' */
 #define MVC_TAG_Z    0x4D565A30u /* 'MVZ0' */
+#define MVC_TAG_Z2   0x4D565A32u /* 'MVZ2' birth resolution */
 #define MVC_TAG_DISH 0x4D564400u /* 'MVD\0' + 1 + view */
 #define MVC_TAG_MH   0x4D564D48u /* 'MVMH' */
 

@@ -44,8 +44,15 @@ struct Sweep {
   const int32_t *Koff;    // [V+1] prefix of Kact
   double *scratch;        // per wave: [sumK]
   int32_t *choice;        // [n] position or -1 (birth)
-  int32_t *bdish;         // [n*V] birth dish choices (by birth rank)
   const int32_t *blist;   // [NB] birth customers, ascending
+  // birth resolution (phase 2) state
+  int32_t *p2meta;        // [V+2]: T2, K2[V], error
+  int32_t *p2_c;          // [TC] customers of phase-2 table t
+  int32_t *p2_tup;        // [TC*V] extended dish index (frozen j or K_v + q)
+  int32_t *n2, *l2;       // [V*KC]
+  double *S1_2T;          // [(v*D + d)*KC + q]
+  double *lp2;            // [V*KC] lp of phase-2 dishes for the current birth
+  int32_t *btab;          // [NB] phase-2 table of each birth
   const int32_t *nbirth;  // [1]
   const int32_t *status;  // [V+4]; status[V+3] = tables with n_t > 0
   int32_t T, sumK;
@@ -58,11 +65,13 @@ struct Sweep {
 // m, the tree sum S and (lane c) the level-0 chunk partial of chunk c.
 struct ViewOut { double lmarg, m, S, part; int nc; double lf_new, w_new; };
 
-__device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p0, bool alive, double *lp) {
+__device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p0, bool alive, double *lp,
+                                            bool with_p2 = false) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
   const int V = P.V, D = P.D, KC = P.KC, n = P.n;
   const int K = P.Kact[v];
+  const int K2 = with_p2 ? A.p2meta[1 + v] : 0;
   const int j0 = P.dish[v * P.TC + p0];
   const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
   const double Y2i = A.Y2[(size_t)v * n + i];
@@ -94,17 +103,37 @@ __device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p
       if (l > 0 && val > mx) mx = val;
     }
   }
+  int L2sum = 0;
+  if (with_p2) {
+    const double *S2v = A.S1_2T + (size_t)v * D * KC;
+    for (int base = 0; base < K2; base += 64) {
+      const int q = base + lane;
+      if (q < K2) {
+        double G = 0.0, Q = 0.0;
+        for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S2v[(size_t)d * KC + q], G);
+        for (int d = 0; d < D; ++d) {
+          const double sq = S2v[(size_t)d * KC + q];
+          Q = __builtin_fma(sq, sq, Q);
+        }
+        const Coef c = coef(A.n2[v * KC + q], Q, tau, A.L2pt[v], D);
+        const double val = __builtin_fma(G + hy, c.cb, c.c0) + h;
+        A.lp2[v * KC + q] = val;
+        if (val > mx) mx = val;
+      }
+    }
+    for (int q = 0; q < K2; ++q) L2sum += A.l2[v * KC + q];
+  }
   ViewOut o;
   o.lf_new = A.cnew[v] + h;
-  const int Kact_i = K - ((l0p == 0) ? 1 : 0);
+  const int Kact_i = K - ((l0p == 0) ? 1 : 0) + K2;
   double wn = alpha + (double)Kact_i * sigma;
   if (wn < 0.0) wn = 0.0;
   o.w_new = wn;
   mx = wave_max(mx);
   if (o.lf_new > mx) mx = o.lf_new;
   o.m = mx;
-  const int nel = K + 1;
-  o.nc = (nel + 63) >> 6;
+  const int NE = K + K2;
+  o.nc = (NE + 1 + 63) >> 6;
   double part = 0.0;
   for (int c = 0; c < o.nc; ++c) {
     const int e = c * 64 + lane;
@@ -116,7 +145,11 @@ __device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p
         if (w < 0.0) w = 0.0;
         leaf = w * mvc_exp(lp[e] - mx);
       }
-    } else if (e == K) {
+    } else if (e < NE) {
+      double w = (double)A.l2[v * KC + (e - K)] - sigma;
+      if (w < 0.0) w = 0.0;
+      leaf = w * mvc_exp(A.lp2[v * KC + (e - K)] - mx);
+    } else if (e == NE) {
       leaf = wn * mvc_exp(o.lf_new - mx);
     }
     const double cs = wave_tree_sum(leaf);
@@ -124,17 +157,19 @@ __device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p
   }
   o.part = part;
   o.S = (o.nc == 1) ? __shfl(part, 0, 64) : wave_tree_sum(lane < o.nc ? part : 0.0);
-  const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
+  const double denom = alpha + (double)((P.Ltot[v] - (alive ? 0 : 1)) + L2sum);
   o.lmarg = (denom <= 0.0) ? o.lf_new : (mx + mvc_log(o.S)) - mvc_log(denom);
   return o;
 }
 
-__device__ __forceinline__ int view_select(const Sweep &A, int i, int v, int p0, bool alive, const double *lp,
-                                           const ViewOut &o, double r) {
+__device__ __forceinline__ int view_select(const Sweep &A, int v, int p0, bool alive, const double *lp,
+                                           const ViewOut &o, double r, bool with_p2) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
   const int V = P.V, KC = P.KC;
   const int K = P.Kact[v];
+  const int K2 = with_p2 ? A.p2meta[1 + v] : 0;
+  const int NE = K + K2;
   const int j0 = P.dish[v * P.TC + p0];
   const double sigma = P.hyper[2 * V + v];
   const int l0p = alive ? P.d_l[v * KC + j0] : P.d_l[v * KC + j0] - 1;
@@ -154,7 +189,11 @@ __device__ __forceinline__ int view_select(const Sweep &A, int i, int v, int p0,
       if (w < 0.0) w = 0.0;
       leaf = w * mvc_exp(lp[e] - o.m);
     }
-  } else if (e == K) {
+  } else if (e < NE) {
+    double w = (double)A.l2[v * KC + (e - K)] - sigma;
+    if (w < 0.0) w = 0.0;
+    leaf = w * mvc_exp(A.lp2[v * KC + (e - K)] - o.m);
+  } else if (e == NE) {
     leaf = o.w_new * mvc_exp(o.lf_new - o.m);
   }
   Tree64Levels L2;
@@ -250,30 +289,135 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep
   }
 }
 
-// births: one wavefront per birth customer; per view dish draw
-extern "C" __global__ __launch_bounds__(256) void mvc_par_birth_kernel(Sweep A) {
+// Phase 2: births resolved sequentially in ascending
+// customer order by ONE wavefront.  Each birth joins a table born earlier in
+// this sweep or opens one (dish per view from frozen + phase-2 + new dishes).
+extern "C" __global__ __launch_bounds__(64) void mvc_par_births_kernel(Sweep A) {
   const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * blockDim.x) >> 6;
-  double *lpall = A.scratch + (size_t)wid * A.sumK;
+  const int lane = threadIdx.x;
+  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC;
+  double *lpall = A.scratch;
   const int NB = *A.nbirth;
-  for (int b = wid; b < NB; b += nw) {
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const int T_ne = A.status[V + 3];
+  if (lane == 0) {
+    A.p2meta[0] = 0;
+    for (int v = 0; v < V; ++v) A.p2meta[1 + v] = 0;
+    A.p2meta[V + 1] = 0;
+  }
+  __syncthreads();
+  for (int b = 0; b < NB; ++b) {
     const int i = A.blist[b];
     const int p0 = P.z[i];
     const bool alive = (P.n_t[p0] - 1) > 0;
-    for (int v = 0; v < P.V; ++v) {
-      double *lp = lpall + A.Koff[v];
-      const ViewOut o = view_eval(A, i, v, p0, alive, lp);
-      int e;
-      if (!(o.S > 0.0)) {
-        e = P.Kact[v];
-      } else {
-        const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_DISH + 1u + (uint32_t)v) * o.S;
-        e = view_select(A, i, v, p0, alive, lp, o, r);
-      }
-      if (lane == 0) A.bdish[(size_t)b * P.V + v] = e;
+    const int T2 = A.p2meta[0];
+    // capacity: one more table and one more dish per view
+    int bad = (A.T + T2 + 1 > TC) ? 1 : 0;
+    for (int v = 0; v < V; ++v) bad |= (P.Kact[v] + A.p2meta[1 + v] + 1 > KC) ? 1 : 0;
+    if (bad) {
+      if (lane == 0) A.p2meta[V + 1] = 1;
+      return;
     }
+    double s_new = mvc_log(ag + sg * (double)((T_ne - (alive ? 0 : 1)) + T2));
+    for (int v = 0; v < V; ++v) {
+      const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v], true);
+      s_new = s_new + o.lmarg;
+    }
+    __syncthreads();
+    auto lpx = [&](int v, int ex) -> double {
+      const int K = P.Kact[v];
+      return ex < K ? lpall[A.Koff[v] + ex] : A.lp2[v * KC + (ex - K)];
+    };
+    auto score = [&](int t) -> double {
+      double st = mvc_log((double)A.p2_c[t] - sg);
+      for (int v = 0; v < V; ++v) st = st + lpx(v, A.p2_tup[t * V + v]);
+      return st;
+    };
+    double M = s_new;
+    for (int base = 0; base < T2; base += 64) {
+      const int t = base + lane;
+      if (t < T2) { const double st = score(t); if (st > M) M = st; }
+    }
+    M = wave_max(M);
+    const int nc = (T2 + 63) >> 6;
+    double part = 0.0;
+    for (int c = 0; c < nc; ++c) {
+      const int t = c * 64 + lane;
+      const double leaf = t < T2 ? mvc_exp(score(t) - M) : 0.0;
+      const double cs = wave_tree_sum(leaf);
+      if (lane == c) part = cs;
+    }
+    double B;
+    if (nc == 0) B = 0.0;
+    else if (nc == 1) B = __shfl(part, 0, 64);
+    else B = wave_tree_sum(lane < nc ? part : 0.0);
+    const double W = mvc_exp(s_new - M) + B;
+    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z2) * W;
+    int t_pick;
+    if (r < B) {
+      int c = 0;
+      if (nc > 1) {
+        Tree64Levels L;
+        const double pv = lane < nc ? part : 0.0;
+        wave_tree_sum_levels(pv, L);
+        c = wave_tree_select(L, pv, r);
+      }
+      const int t = c * 64 + lane;
+      const double leaf = t < T2 ? mvc_exp(score(t) - M) : 0.0;
+      Tree64Levels L2;
+      wave_tree_sum_levels(leaf, L2);
+      t_pick = c * 64 + wave_tree_select(L2, leaf, r);
+      __syncthreads();
+      if (lane == 0) A.p2_c[t_pick] += 1;
+      for (int v = 0; v < V; ++v) {
+        const int K = P.Kact[v];
+        const int ex = A.p2_tup[t_pick * V + v];
+        if (ex >= K) {
+          const int q = ex - K;
+          if (lane == 0) A.n2[v * KC + q] += 1;
+          const double *yrow = A.y + ((size_t)v * P.n + i) * D;
+          for (int d = lane; d < D; d += 64) {
+            double *cell = A.S1_2T + ((size_t)v * D + d) * KC + q;
+            *cell = *cell + yrow[d];
+          }
+        }
+      }
+    } else {
+      t_pick = T2;
+      for (int v = 0; v < V; ++v) {
+        const int K = P.Kact[v];
+        const int K2 = A.p2meta[1 + v];
+        int ex;
+        // recompute this view's mixture (identical arithmetic) for the draw
+        const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v], true);
+        if (!(o.S > 0.0)) {
+          ex = K + K2;
+        } else {
+          const double rv = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_DISH + 1u + (uint32_t)v) * o.S;
+          ex = view_select(A, v, p0, alive, lpall + A.Koff[v], o, rv, true);
+        }
+        __syncthreads();
+        const double *yrow = A.y + ((size_t)v * P.n + i) * D;
+        if (ex == K + K2) {     // brand-new phase-2 dish
+          if (lane == 0) { A.n2[v * KC + K2] = 0; A.l2[v * KC + K2] = 0; A.p2meta[1 + v] = K2 + 1; }
+          for (int d = lane; d < D; d += 64) A.S1_2T[((size_t)v * D + d) * KC + K2] = 0.0;
+          __syncthreads();
+        }
+        if (ex >= K) {
+          const int q = ex - K;
+          if (lane == 0) { A.l2[v * KC + q] += 1; A.n2[v * KC + q] += 1; }
+          for (int d = lane; d < D; d += 64) {
+            double *cell = A.S1_2T + ((size_t)v * D + d) * KC + q;
+            *cell = *cell + yrow[d];
+          }
+        }
+        if (lane == 0) A.p2_tup[T2 * V + v] = ex;
+        __syncthreads();
+      }
+      if (lane == 0) { A.p2_c[T2] = 1; A.p2meta[0] = T2 + 1; }
+    }
+    if (lane == 0) A.btab[b] = t_pick;
+    __syncthreads();
   }
 }
 
@@ -288,16 +432,15 @@ extern "C" __global__ void mvc_par_count_kernel(int n, const int32_t *choice, in
 
 // commit step 2 (one workgroup of 256): new tables, dish lists, counts.
 // status[0] = T_new, status[1..V] = K_new, status[V+1] = error flag,
-// status[V+2] = births.
+// status[V+2] = tables opened by the birth resolution.
 extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
-    ParState P, int T, const int32_t *cnt, const int32_t *nbirth, const int32_t *bdish, int32_t *pos_new,
-    int32_t *tmp_dish /*[V*TC]*/, int32_t *tmp_nt /*[TC]*/, int32_t *lcnt /*[V*KC]*/, int32_t *jmap /*[V*KC]*/,
-    int32_t *status) {
+    ParState P, int T, const int32_t *cnt, const int32_t *p2meta, const int32_t *p2_c, const int32_t *p2_tup,
+    int32_t *pos_new, int32_t *tmp_dish /*[V*TC]*/, int32_t *tmp_nt /*[TC]*/, int32_t *lcnt /*[V*KC]*/,
+    int32_t *jmap /*[V*KC]*/, int32_t *status) {
   __shared__ int s_scan[256];
-  __shared__ int s_tot;
   const int tid = threadIdx.x;
   const int V = P.V, TC = P.TC, KC = P.KC;
-  const int NB = *nbirth;
+  const int T2 = p2meta[0];
   auto block_scan = [&](int x, int &total) {   // exclusive scan of x over the block
     s_scan[tid] = x;
     __syncthreads();
@@ -312,6 +455,10 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
     __syncthreads();
     return incl - x;
   };
+  if (p2meta[V + 1] != 0) {
+    if (tid == 0) status[V + 1] = 1;
+    return;
+  }
   // survivors in ascending position
   int run = 0;
   for (int base = 0; base < T; base += 256) {
@@ -323,24 +470,14 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
     run += tot;
   }
   const int Tsurv = run;
-  const int Tn = Tsurv + NB;
-  if (tid == 0) { status[0] = Tn; status[V + 1] = 0; status[V + 2] = NB; }
+  const int Tn = Tsurv + T2;
+  if (tid == 0) { status[0] = Tn; status[V + 1] = 0; status[V + 2] = T2; }
   if (Tn > TC) { if (tid == 0) status[V + 1] = 1; return; }
   __syncthreads();
-  // extended dish index of every new table, per view
   for (int v = 0; v < V; ++v) {
     const int Kold = P.Kact[v];
-    int nnew = 0;
-    for (int base = 0; base < NB; base += 256) {
-      const int b = base + tid;
-      const int e = b < NB ? bdish[(size_t)b * V + v] : 0;
-      const int isnew = (b < NB && e >= Kold) ? 1 : 0;
-      int tot;
-      const int ex = block_scan(isnew, tot);
-      if (b < NB) tmp_dish[v * TC + Tsurv + b] = isnew ? Kold + nnew + ex : e;
-      nnew += tot;
-    }
-    if (Kold + nnew > KC) { if (tid == 0) status[V + 1] = 2; return; }
+    const int nnew = p2meta[1 + v];
+    for (int t = tid; t < T2; t += 256) tmp_dish[v * TC + Tsurv + t] = p2_tup[t * V + v];
     for (int p = tid; p < T; p += 256)
       if (pos_new[p] >= 0) tmp_dish[v * TC + pos_new[p]] = P.dish[v * TC + p];
     for (int j = tid; j < Kold + nnew; j += 256) lcnt[v * KC + j] = 0;
@@ -359,8 +496,8 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
       kr += tot;
     }
     __syncthreads();
-    // write the compacted dish arrays in place: ids ascend, so a stable
-    // left-shift is safe when done in increasing j by a single pass per chunk
+    // in-place left compaction, one 256-chunk at a time (writes never reach
+    // entries of a later chunk)
     const int next = P.next_id[v];
     for (int base = 0; base < Kext; base += 256) {
       const int j = base + tid;
@@ -385,35 +522,31 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
       status[1 + v] = kr;
     }
     __syncthreads();
-    for (int p = tid; p < Tn; p += 256) {
-      const int jn = jmap[v * KC + tmp_dish[v * TC + p]];
-      P.dish[v * TC + p] = jn;
-    }
+    for (int p = tid; p < Tn; p += 256) P.dish[v * TC + p] = jmap[v * KC + tmp_dish[v * TC + p]];
     __syncthreads();
   }
   // table counts, n_vk
   for (int p = tid; p < T; p += 256)
     if (pos_new[p] >= 0) tmp_nt[pos_new[p]] = cnt[p];
-  for (int b = tid; b < NB; b += 256) tmp_nt[Tsurv + b] = 1;
+  for (int t = tid; t < T2; t += 256) tmp_nt[Tsurv + t] = p2_c[t];
   __syncthreads();
   for (int p = tid; p < Tn; p += 256) {
     const int c = tmp_nt[p];
     P.n_t[p] = c;
     for (int v = 0; v < V; ++v) atomicAdd(&P.d_n[v * KC + P.dish[v * TC + p]], c);
   }
-  if (tid == 0) s_tot = Tsurv;
-  (void)s_tot;
 }
 
-// commit step 3: relabel customers (births numbered by birth rank)
+// commit step 3: relabel customers (births -> Tsurv + their phase-2 table)
 extern "C" __global__ void mvc_par_relabel_kernel(int n, int V, const int32_t *choice, const int32_t *pos_new,
-                                                  const int32_t *brank, const int32_t *status, int32_t *z) {
+                                                  const int32_t *brank, const int32_t *btab, const int32_t *status,
+                                                  int32_t *z) {
   const int32_t Tn = status[0];
-  const int32_t NB = status[V + 2];
-  const int32_t Tsurv = Tn - NB;
+  const int32_t T2 = status[V + 2];
+  const int32_t Tsurv = Tn - T2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int c = choice[i];
-    z[i] = c >= 0 ? pos_new[c] : Tsurv + brank[i];
+    z[i] = c >= 0 ? pos_new[c] : Tsurv + btab[brank[i]];
   }
 }
 
@@ -827,7 +960,9 @@ class ParallelSampler : public Sampler {
     double *L2pt = nullptr, *cnew = nullptr;
     int32_t *Koff = nullptr, *status = nullptr;
     int32_t *choice = nullptr, *flags = nullptr, *brank = nullptr, *blist = nullptr, *nbirth = nullptr;
-    int32_t *bdish = nullptr, *cnt = nullptr, *pos_new = nullptr, *tmp_dish = nullptr, *tmp_nt = nullptr;
+    int32_t *cnt = nullptr, *pos_new = nullptr, *tmp_dish = nullptr, *tmp_nt = nullptr;
+    int32_t *p2meta = nullptr, *p2_c = nullptr, *p2_tup = nullptr, *n2 = nullptr, *l2 = nullptr, *btab = nullptr;
+    double *S1_2T = nullptr, *lp2 = nullptr;
     int32_t *lcnt = nullptr, *jmap = nullptr, *histT = nullptr, *histL = nullptr;
     double *mh_scratch = nullptr;
     size_t mh_half = 0;
@@ -920,7 +1055,14 @@ class ParallelSampler : public Sampler {
     c.brank = own<int32_t>(c, n);
     c.blist = own<int32_t>(c, n);
     c.nbirth = own<int32_t>(c, 1);
-    c.bdish = own<int32_t>(c, (size_t)n * V);
+    c.p2meta = own<int32_t>(c, V + 2);
+    c.p2_c = own<int32_t>(c, TC);
+    c.p2_tup = own<int32_t>(c, (size_t)TC * V);
+    c.n2 = own<int32_t>(c, (size_t)V * KC);
+    c.l2 = own<int32_t>(c, (size_t)V * KC);
+    c.S1_2T = own<double>(c, (size_t)V * D * KC);
+    c.lp2 = own<double>(c, (size_t)V * KC);
+    c.btab = own<int32_t>(c, n);
     c.cnt = own<int32_t>(c, TC);
     c.pos_new = own<int32_t>(c, TC);
     c.tmp_dish = own<int32_t>(c, (size_t)V * TC);
@@ -1067,8 +1209,15 @@ class ParallelSampler : public Sampler {
     A.Koff = c.Koff;
     A.scratch = lp_scratch;
     A.choice = c.choice;
-    A.bdish = c.bdish;
     A.blist = c.blist;
+    A.p2meta = c.p2meta;
+    A.p2_c = c.p2_c;
+    A.p2_tup = c.p2_tup;
+    A.n2 = c.n2;
+    A.l2 = c.l2;
+    A.S1_2T = c.S1_2T;
+    A.lp2 = c.lp2;
+    A.btab = c.btab;
     A.nbirth = c.nbirth;
     A.status = c.status;
     A.T = c.T;
@@ -1098,22 +1247,27 @@ class ParallelSampler : public Sampler {
     bytes = cub_bytes;
     hipcub::CountingInputIterator<int32_t> it(0);
     MVC_HIP(hipcub::DeviceSelect::Flagged(cub_tmp, bytes, it, c.flags, c.blist, c.nbirth, n, stream));
-    hipLaunchKernelGGL(mvc_par_birth_kernel, dim3(std::min(kZGrid, (n + 3) / 4)), dim3(256), 0, stream, A);
+    timers.end("commit", e1);
+    hipEvent_t eb = nullptr;
+    timers.begin("births", &eb);
+    hipLaunchKernelGGL(mvc_par_births_kernel, dim3(1), dim3(64), 0, stream, A);
     MVC_HIP(hipGetLastError());
+    timers.end("births", eb);
+    timers.begin("commit", &e1);
     hipLaunchKernelGGL(mvc_par_commit_kernel, dim3(1), dim3(256), 0, stream, c.P, c.T, (const int32_t *)c.cnt,
-                       (const int32_t *)c.nbirth, (const int32_t *)c.bdish, c.pos_new, c.tmp_dish, c.tmp_nt, c.lcnt,
-                       c.jmap, c.status);
+                       (const int32_t *)c.p2meta, (const int32_t *)c.p2_c, (const int32_t *)c.p2_tup, c.pos_new,
+                       c.tmp_dish, c.tmp_nt, c.lcnt, c.jmap, c.status);
     MVC_HIP(hipGetLastError());
     hipLaunchKernelGGL(mvc_par_relabel_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n, V,
                        (const int32_t *)c.choice, (const int32_t *)c.pos_new, (const int32_t *)c.brank,
-                       (const int32_t *)c.status, c.P.z);
+                       (const int32_t *)c.btab, (const int32_t *)c.status, c.P.z);
     MVC_HIP(hipGetLastError());
     timers.end("commit", e1);
     // the one host synchronisation of a sweep: new T and dish counts
     MVC_HIP(hipMemcpyAsync(st_host.data(), c.status, sizeof(int32_t) * (V + 4), hipMemcpyDeviceToHost, stream));
     MVC_HIP(hipStreamSynchronize(stream));
-    if (st_host[V + 1] == 1) throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: table capacity (4096) exceeded");
-    if (st_host[V + 1] == 2) throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: dish capacity (4095 per view) exceeded");
+    if (st_host[V + 1] != 0)
+      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: table (4096) or dish (4095 per view) capacity exceeded");
     c.T = st_host[0];
     for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
     rebuild_stats(c);

@@ -824,13 +824,25 @@ struct ParallelSampler {
       if (n_t[p] > 0) ++T_ne;
   }
 
-  void eval_view(int i, int v, bool alive, int j0, ViewEval &E) const {
+  // Dishes created earlier in the same sweep by the birth resolution
+  // (DESIGN.md §4.5): per view counts and sums, extended index K_v + q.
+  struct Phase2 {
+    int T2 = 0;
+    std::vector<int> c;                       // [t] customers
+    std::vector<std::vector<int>> tup;        // [t][v] extended dish index
+    std::vector<std::vector<int>> n2, l2;     // [v][q]
+    std::vector<std::vector<double>> S1_2;    // [v][q*D + d]
+  };
+
+  void eval_view(int i, int v, bool alive, int j0, ViewEval &E, const Phase2 *P2 = nullptr) const {
     const int K = (int)ids[v].size();
+    const int K2 = P2 ? (int)P2->n2[v].size() : 0;
+    const int NE = K + K2;
     const double Y2i = Y2[(size_t)v * n + i];
     const double hy = 0.5 * Y2i;
     const double h = (-0.5 * Y2i) / tau[v];
     const double *yi = y + ((size_t)v * n + i) * D;
-    E.lv.assign(K + 1, 0.0); E.w.assign(K + 1, 0.0); E.inc.assign(K + 1, 0);
+    E.lv.assign(NE + 1, 0.0); E.w.assign(NE + 1, 0.0); E.inc.assign(NE + 1, 0);
     int Kact = K;
     for (int j = 0; j < K; ++j) {
       const double G = fma_dot(yi, &S1[v][(size_t)j * D], D);
@@ -855,33 +867,45 @@ struct ParallelSampler {
         Kact -= 1;
       }
     }
-    E.lv[K] = cnew[v] + h;
-    double wn = alpha[v] + (double)Kact * sigma[v];
+    int L2sum = 0;
+    for (int q = 0; q < K2; ++q) {
+      const double *s2 = &P2->S1_2[v][(size_t)q * D];
+      const double G = fma_dot(yi, s2, D);
+      const double Q = fma_dot(s2, s2, D);
+      const Coef c = coef(P2->n2[v][q], Q, tau[v], L2pt[v]);
+      E.lv[K + q] = __builtin_fma(G + hy, c.cb, c.c0) + h;
+      E.inc[K + q] = 1;
+      double w = (double)P2->l2[v][q] - sigma[v];
+      if (w < 0.0) w = 0.0;
+      E.w[K + q] = w;
+      L2sum += P2->l2[v][q];
+    }
+    E.lv[NE] = cnew[v] + h;
+    double wn = alpha[v] + (double)(Kact + K2) * sigma[v];
     if (wn < 0.0) wn = 0.0;
-    E.w[K] = wn;
-    E.inc[K] = 1;
+    E.w[NE] = wn;
+    E.inc[NE] = 1;
     double m = -MVC_PM_INF;
-    for (int e = 0; e <= K; ++e)
+    for (int e = 0; e <= NE; ++e)
       if (E.inc[e] && E.lv[e] > m) m = E.lv[e];
     E.m = m;
-    E.leaves.assign(K + 1, 0.0);
-    for (int e = 0; e <= K; ++e)
+    E.leaves.assign(NE + 1, 0.0);
+    for (int e = 0; e <= NE; ++e)
       if (E.inc[e]) E.leaves[e] = E.w[e] * mvc_exp(E.lv[e] - m);
     E.S = tree64_sum(E.leaves);
-    const double denom = alpha[v] + (double)(Ltot[v] - (alive ? 0 : 1));
+    const double denom = alpha[v] + (double)((Ltot[v] - (alive ? 0 : 1)) + L2sum);
     if (denom <= 0.0)
-      E.lmarg = E.lv[K];
+      E.lmarg = E.lv[NE];
     else
       E.lmarg = (m + mvc_log(E.S)) - mvc_log(denom);
   }
 
-  // returns chosen position (>= 0) or -1 for a birth; births also fill choice[v]
-  int resample_customer(int i, int s, std::vector<int> &dish_choice) const {
+  // Phase 1: table against the frozen state; -1 = birth.
+  int resample_customer(int i, int s) const {
     const int p0 = z[i];
     const bool alive = (n_t[p0] - 1) > 0;
     std::vector<ViewEval> E(V);
     for (int v = 0; v < V; ++v) eval_view(i, v, alive, dish[v][p0], E[v]);
-    // table scores
     std::vector<double> sc(T, 0.0);
     std::vector<char> inc(T, 0);
     double M = -MVC_PM_INF;
@@ -910,46 +934,109 @@ struct ParallelSampler {
     const double W = e_new + B;
     const double r = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_Z) * W;
     if (r < B) return (int)tb.select(r);
-    // birth: one dish per view from the marginal mixture
-    dish_choice.assign(V, -1);
-    for (int v = 0; v < V; ++v) {
-      const int K = (int)ids[v].size();
-      if (!(E[v].S > 0.0)) { dish_choice[v] = K; continue; }
-      Tree64 td;
-      td.build(E[v].leaves);
-      const double rv = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_DISH + 1u + (uint32_t)v) * E[v].S;
-      dish_choice[v] = (int)td.select(rv);
-    }
     return -1;
   }
 
-  void commit(const std::vector<int> &choice, const std::vector<std::vector<int>> &birth_dish) {
-    // births in ascending i
-    std::vector<int> birth_cust;
-    for (int i = 0; i < n; ++i)
-      if (choice[i] < 0) birth_cust.push_back(i);
-    const int NB = (int)birth_cust.size();
+  // Phase 2: births in ascending customer order either join
+  // a table born earlier in this sweep or open a new one with one dish per
+  // view drawn from the mixture over frozen, phase-2 and brand-new dishes.
+  // Returns for every birth (ascending) its phase-2 table.
+  std::vector<int> resolve_births(const std::vector<int> &births, int s, Phase2 &P2) const {
+    P2 = Phase2();
+    P2.n2.assign(V, {}); P2.l2.assign(V, {}); P2.S1_2.assign(V, {});
+    std::vector<int> btab(births.size());
+    std::vector<ViewEval> E(V);
+    for (size_t b = 0; b < births.size(); ++b) {
+      const int i = births[b];
+      const int p0 = z[i];
+      const bool alive = (n_t[p0] - 1) > 0;
+      for (int v = 0; v < V; ++v) eval_view(i, v, alive, dish[v][p0], E[v], &P2);
+      double M = -MVC_PM_INF;
+      std::vector<double> sc(P2.T2);
+      for (int t = 0; t < P2.T2; ++t) {
+        double st = mvc_log((double)P2.c[t] - sg);
+        for (int v = 0; v < V; ++v) st = st + E[v].lv[P2.tup[t][v]];
+        sc[t] = st;
+        if (st > M) M = st;
+      }
+      const int Tne_i = T_ne - (alive ? 0 : 1);
+      double s_new = mvc_log(ag + sg * (double)(Tne_i + P2.T2));
+      for (int v = 0; v < V; ++v) s_new = s_new + E[v].lmarg;
+      if (s_new > M) M = s_new;
+      std::vector<double> e(P2.T2);
+      for (int t = 0; t < P2.T2; ++t) e[t] = mvc_exp(sc[t] - M);
+      Tree64 tb;
+      const double B = tb.build(e);
+      const double W = mvc_exp(s_new - M) + B;
+      const double r = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_Z2) * W;
+      int t;
+      if (r < B) {
+        t = (int)tb.select(r);
+        P2.c[t] += 1;
+        for (int v = 0; v < V; ++v) {
+          const int K = (int)ids[v].size();
+          const int ex = P2.tup[t][v];
+          if (ex >= K) {
+            const int q = ex - K;
+            P2.n2[v][q] += 1;
+            for (int d = 0; d < D; ++d)
+              P2.S1_2[v][(size_t)q * D + d] = P2.S1_2[v][(size_t)q * D + d] + yv(v, i, d);
+          }
+        }
+      } else {
+        std::vector<int> tup(V);
+        for (int v = 0; v < V; ++v) {
+          const int K = (int)ids[v].size();
+          const int K2 = (int)P2.n2[v].size();
+          int ex;
+          if (!(E[v].S > 0.0)) {
+            ex = K + K2;
+          } else {
+            Tree64 td;
+            td.build(E[v].leaves);
+            const double rv = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_DISH + 1u + (uint32_t)v) * E[v].S;
+            ex = (int)td.select(rv);
+          }
+          if (ex == K + K2) {
+            P2.n2[v].push_back(0);
+            P2.l2[v].push_back(0);
+            P2.S1_2[v].resize((size_t)(K2 + 1) * D, 0.0);
+          }
+          if (ex >= K) {
+            const int q = ex - K;
+            P2.l2[v][q] += 1;
+            P2.n2[v][q] += 1;
+            for (int d = 0; d < D; ++d)
+              P2.S1_2[v][(size_t)q * D + d] = P2.S1_2[v][(size_t)q * D + d] + yv(v, i, d);
+          }
+          tup[v] = ex;
+        }
+        t = P2.T2++;
+        P2.c.push_back(1);
+        P2.tup.push_back(tup);
+      }
+      btab[b] = t;
+    }
+    return btab;
+  }
+
+  void commit(const std::vector<int> &choice, const std::vector<int> &births, const std::vector<int> &btab,
+              const Phase2 &P2) {
     std::vector<int> cnt(T, 0);
     for (int i = 0; i < n; ++i)
       if (choice[i] >= 0) cnt[choice[i]]++;
-    // extended dish lists: new dishes per view in ascending birth order
-    std::vector<std::vector<int>> bd(V, std::vector<int>(NB));
-    std::vector<int> Kold(V), nnew(V, 0);
+    std::vector<int> Kold(V), nnew(V);
     for (int v = 0; v < V; ++v) {
       Kold[v] = (int)ids[v].size();
-      for (int b = 0; b < NB; ++b) {
-        int e = birth_dish[b][v];
-        if (e >= Kold[v]) e = Kold[v] + nnew[v]++;
-        bd[v][b] = e;
-      }
+      nnew[v] = (int)P2.n2[v].size();
     }
-    // surviving tables: old in ascending position, then births
+    // surviving tables: old in ascending position, then phase-2 tables
     std::vector<int> pos_new(T, -1);
     int Tn = 0;
     for (int p = 0; p < T; ++p)
       if (cnt[p] > 0) pos_new[p] = Tn++;
     const int Tsurv = Tn;
-    Tn += NB;
+    Tn += P2.T2;
     std::vector<int> nt_new(Tn);
     std::vector<std::vector<int>> dext(V, std::vector<int>(Tn));
     for (int p = 0; p < T; ++p)
@@ -957,16 +1044,16 @@ struct ParallelSampler {
         nt_new[pos_new[p]] = cnt[p];
         for (int v = 0; v < V; ++v) dext[v][pos_new[p]] = dish[v][p];
       }
-    for (int b = 0; b < NB; ++b) {
-      nt_new[Tsurv + b] = 1;
-      for (int v = 0; v < V; ++v) dext[v][Tsurv + b] = bd[v][b];
+    for (int t = 0; t < P2.T2; ++t) {
+      nt_new[Tsurv + t] = P2.c[t];
+      for (int v = 0; v < V; ++v) dext[v][Tsurv + t] = P2.tup[t][v];
     }
     std::vector<int> z_new(n);
     {
-      int b = 0;
-      for (int i = 0; i < n; ++i) z_new[i] = choice[i] >= 0 ? pos_new[choice[i]] : Tsurv + b++;
+      size_t b = 0;
+      for (int i = 0; i < n; ++i) z_new[i] = choice[i] >= 0 ? pos_new[choice[i]] : Tsurv + btab[b++];
     }
-    // dishes: recount l, compact survivors
+    (void)births;
     for (int v = 0; v < V; ++v) {
       const int Kext = Kold[v] + nnew[v];
       std::vector<int> l(Kext, 0);
@@ -1140,17 +1227,17 @@ struct ParallelSampler {
 
   void run(int M, int burn_in, int thin, Result &R) {
     R.dish_off.push_back(0);
-    std::vector<int> choice(n);
-    std::vector<std::vector<int>> bdish;
-    std::vector<int> dc;
+    std::vector<int> choice(n), births;
+    Phase2 P2;
     for (int s = 0; s < M; ++s) {
       sweep_constants();
-      bdish.clear();
+      births.clear();
       for (int i = 0; i < n; ++i) {
-        choice[i] = resample_customer(i, s, dc);
-        if (choice[i] < 0) bdish.push_back(dc);
+        choice[i] = resample_customer(i, s);
+        if (choice[i] < 0) births.push_back(i);
       }
-      commit(choice, bdish);
+      const std::vector<int> btab = resolve_births(births, s, P2);
+      commit(choice, births, btab, P2);
       update_hyper(s);
       R.trace_T.push_back(T);
       R.trace_draws.push_back(init_rng.draws);
