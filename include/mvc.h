@@ -117,6 +117,12 @@ int mvc_sampler_sweeps_done(const mvc_sampler *s);
 int mvc_sampler_get_state(mvc_sampler *s, int chain, int32_t *table_of, int32_t *n_tables,
                           int32_t *dish_of, int32_t dish_of_cap, double *hyper,
                           char *err, size_t errlen);
+/* Warm start / resume: replace one chain's state.  table_of[n] = table
+ * position in [0, n_tables) (every table non-empty), dish_of[V*n_tables]
+ * (view-major) = raw dish id of each table, hyper[3V+2] as in get_state.
+ * The chain's RNG stream restarts at draw 0; the sweep counter is kept. */
+int mvc_sampler_set_state(mvc_sampler *s, int chain, const int32_t *table_of, int32_t n_tables,
+                          const int32_t *dish_of, const double *hyper, char *err, size_t errlen);
 /* Number of live dishes per view (k_out[V]). */
 int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char *err, size_t errlen);
 /* HIP-event kernel timing (needs MVC_FLAG_TIMING): kernel = "zresample",

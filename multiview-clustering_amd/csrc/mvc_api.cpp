@@ -70,6 +70,39 @@ InitState draw_initial_state(const double *y, int n, int V, int D, uint64_t seed
   return S;
 }
 
+UserState check_user_state(int n, int V, const int32_t *table_of, int32_t T, const int32_t *dish_of) {
+  if (!table_of || !dish_of) throw Error(MVC_ERR_ARG, "set_state: NULL table_of / dish_of");
+  if (T < 1) throw Error(MVC_ERR_ARG, "set_state: n_tables must be >= 1");
+  UserState U;
+  U.T = T;
+  U.n_t.assign(T, 0);
+  for (int i = 0; i < n; ++i) {
+    if (table_of[i] < 0 || table_of[i] >= T) throw Error(MVC_ERR_ARG, "set_state: table_of out of range");
+    U.n_t[table_of[i]]++;
+  }
+  for (int p = 0; p < T; ++p)
+    if (U.n_t[p] == 0) throw Error(MVC_ERR_ARG, "set_state: every table must hold at least one customer");
+  U.ids.resize(V); U.l.resize(V); U.dish.resize(V); U.next_id.resize(V);
+  for (int v = 0; v < V; ++v) {
+    std::vector<int32_t> raw(dish_of + (size_t)v * T, dish_of + (size_t)(v + 1) * T);
+    for (int32_t r : raw)
+      if (r < 0) throw Error(MVC_ERR_ARG, "set_state: negative dish id");
+    std::vector<int32_t> srt = raw;
+    std::sort(srt.begin(), srt.end());
+    srt.erase(std::unique(srt.begin(), srt.end()), srt.end());
+    U.ids[v] = srt;
+    U.l[v].assign(srt.size(), 0);
+    U.dish[v].resize(T);
+    for (int p = 0; p < T; ++p) {
+      const int j = (int)(std::lower_bound(srt.begin(), srt.end(), raw[p]) - srt.begin());
+      U.dish[v][p] = j;
+      U.l[v][j]++;
+    }
+    U.next_id[v] = srt.back() + 1;
+  }
+  return U;
+}
+
 void Timers::begin(const char *, hipEvent_t *ev) {
   *ev = nullptr;
   if (!on) return;
@@ -231,6 +264,14 @@ int mvc_sampler_get_state(mvc_sampler *s, int chain, int32_t *table_of, int32_t 
   return guarded(err, errlen, [&] {
     if (!s || !s->impl) throw mvc::Error(MVC_ERR_ARG, "sampler is NULL");
     s->impl->get_state(chain, table_of, n_tables, dish_of, dish_of_cap, hyper);
+  });
+}
+
+int mvc_sampler_set_state(mvc_sampler *s, int chain, const int32_t *table_of, int32_t n_tables,
+                          const int32_t *dish_of, const double *hyper, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl || !hyper) throw mvc::Error(MVC_ERR_ARG, "NULL argument");
+    s->impl->set_state(chain, table_of, n_tables, dish_of, hyper);
   });
 }
 

@@ -970,6 +970,60 @@ class ExactSampler : public Sampler {
     if (hyper) std::copy(hy.begin(), hy.end(), hyper);
   }
 
+  void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of, const double *hyper) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    const UserState U = check_user_state(n, V, table_of, T, dish_of);
+    std::vector<double> yh((size_t)V * n);
+    MVC_HIP(hipMemcpy(yh.data(), y_dev, sizeof(double) * yh.size(), hipMemcpyDeviceToHost));
+    int TC = chains[chain].h.TC, KC = chains[chain].h.KC;
+    while (TC < T + 1) TC *= 2;
+    for (int v = 0; v < V; ++v)
+      while (KC < (int)U.ids[v].size() + 1) KC *= 2;
+    ExactImage I;
+    I.TC = TC; I.KC = KC; I.T = T;
+    I.z.assign(table_of, table_of + n);           // slot p == position p
+    I.n_t.assign(TC, 0);
+    for (int p = 0; p < T; ++p) I.n_t[p] = U.n_t[p];
+    I.pos_of_slot.assign(TC, -1);
+    I.slot_at_pos.assign(TC, -1);
+    for (int p = 0; p < T; ++p) { I.pos_of_slot[p] = p; I.slot_at_pos[p] = p; }
+    I.n_free = TC - T;
+    I.free_slots.assign(TC, -1);
+    for (int k = 0; k < I.n_free; ++k) I.free_slots[k] = TC - 1 - k;
+    I.dish.assign((size_t)V * TC, 0);
+    I.d_id.assign((size_t)V * KC, 0); I.d_n.assign((size_t)V * KC, 0); I.d_l.assign((size_t)V * KC, 0);
+    I.d_S1.assign((size_t)V * KC, 0.0); I.d_S2.assign((size_t)V * KC, 0.0);
+    I.Kact.assign(V, 0);
+    I.next_id = U.next_id;
+    I.hyper.assign(hyper, hyper + 3 * V + 2);
+    for (int v = 0; v < V; ++v) {
+      const int K = (int)U.ids[v].size();
+      I.Kact[v] = K;
+      for (int j = 0; j < K; ++j) { I.d_id[v * KC + j] = U.ids[v][j]; I.d_l[v * KC + j] = U.l[v][j]; }
+      for (int p = 0; p < T; ++p) I.dish[(size_t)v * TC + p] = U.dish[v][p];
+      for (int i = 0; i < n; ++i) {        // sufficient statistics, ascending i
+        const int j = U.dish[v][table_of[i]];
+        const double val = yh[(size_t)v * n + i];
+        I.d_n[v * KC + j]++;
+        I.d_S1[v * KC + j] += val;
+        I.d_S2[v * KC + j] += val * val;
+      }
+    }
+    ExactAlloc &A = chains[chain];
+    ExactAlloc B;
+    B.h = A.h;
+    MVC_HIP(hipMalloc(&B.block, exact_bytes(n, V, TC, KC)));
+    carve(B, n, V, TC, KC);
+    upload(B, I, n, V, stream);
+    MVC_HIP(hipStreamSynchronize(stream));
+    MVC_HIP(hipFree(A.block));
+    B.h.draws = 0;
+    B.h.resume_i = 0;
+    B.h.status = MVC_ST_RUNNING;
+    A = B;
+    push_structs();
+  }
+
   void get_dish_counts(int chain, int32_t *k_out) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
     MVC_HIP(hipMemcpyAsync(k_out, chains[chain].h.Kact, sizeof(int32_t) * V, hipMemcpyDeviceToHost, stream));

@@ -59,11 +59,24 @@ class Sampler {
   virtual void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of,
                          int32_t dish_cap, double *hyper) = 0;
   virtual void get_dish_counts(int chain, int32_t *k_out) = 0;
+  virtual void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of,
+                         const double *hyper) = 0;
   mvc_config cfg;
   int sweeps_done = 0;
   hipStream_t stream = nullptr;
   Timers timers;
 };
+
+// Validated host view of a user-supplied state (warm start / resume).
+struct UserState {
+  int T = 0;
+  std::vector<int32_t> n_t;                  // [T]
+  std::vector<std::vector<int32_t>> ids;     // [v] live raw ids, ascending
+  std::vector<std::vector<int32_t>> l;       // [v] tables per live dish
+  std::vector<std::vector<int32_t>> dish;    // [v][T] live index
+  std::vector<int32_t> next_id;              // [v] max id + 1
+};
+UserState check_user_state(int n, int V, const int32_t *table_of, int32_t T, const int32_t *dish_of);
 
 Sampler *make_exact_sampler(const mvc_config &cfg, const double *const *views);
 Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views);

@@ -202,22 +202,88 @@ __device__ __forceinline__ int view_select(const Sweep &A, int v, int p0, bool a
   return c * 64 + l;
 }
 
-// table score s_p (or -inf if excluded) for customer with own table p0
-__device__ __forceinline__ double table_score(const Sweep &A, int p, int p0, double sg, const double *lpall) {
+// table score s_p (or -inf if excluded) for customer with own table p0;
+// lp of view v dish j is lp[(Koff[v] + j) * stride]
+__device__ __forceinline__ double table_score(const Sweep &A, int p, int p0, double sg, const double *lp,
+                                             int stride) {
   const ParState &P = A.P;
   const int np = P.n_t[p] - (p == p0 ? 1 : 0);
   if (np < 1) return -MVC_PM_INF;
   const double mass = (double)np - sg;
   if (mass <= 0.0) return -MVC_PM_INF;
   double sp = (p == p0) ? mvc_log(mass) : P.lmass[p];
-  for (int v = 0; v < P.V; ++v) sp = sp + lpall[A.Koff[v] + P.dish[v * P.TC + p]];
+  for (int v = 0; v < P.V; ++v) sp = sp + lp[(size_t)(A.Koff[v] + P.dish[v * P.TC + p]) * stride];
   return sp;
+}
+
+// Table draw of one customer (wave-uniform), DESIGN.md §4.3: lane = table
+// slot, tree64 over the table leaves, birth iff r >= B.  Returns the
+// position or -1.
+__device__ __forceinline__ int choose_table(const Sweep &A, int i, int p0, double s_new, const double *lp,
+                                            int stride) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63;
+  const int T = A.T;
+  const double sg = P.hyper[3 * P.V + 1];
+  double M = s_new;
+  for (int base = 0; base < T; base += 64) {
+    const int p = base + lane;
+    if (p < T) {
+      const double sp = table_score(A, p, p0, sg, lp, stride);
+      if (sp > M) M = sp;
+    }
+  }
+  M = wave_max(M);
+  const int nc = (T + 63) >> 6;
+  double part = 0.0;
+  for (int c = 0; c < nc; ++c) {
+    const int p = c * 64 + lane;
+    double leaf = 0.0;
+    if (p < T) {
+      const double sp = table_score(A, p, p0, sg, lp, stride);
+      if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
+    }
+    const double cs = wave_tree_sum(leaf);
+    if (lane == c) part = cs;
+  }
+  double B;
+  if (nc == 0) B = 0.0;
+  else if (nc == 1) B = __shfl(part, 0, 64);
+  else B = wave_tree_sum(lane < nc ? part : 0.0);
+  const double e_new = mvc_exp(s_new - M);
+  const double W = e_new + B;
+  double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+  if (!(r < B)) return -1;
+  int c = 0;
+  if (nc > 1) {
+    Tree64Levels L;
+    const double pv = lane < nc ? part : 0.0;
+    wave_tree_sum_levels(pv, L);
+    c = wave_tree_select(L, pv, r);
+  }
+  const int p = c * 64 + lane;
+  double leaf = 0.0;
+  if (p < T) {
+    const double sp = table_score(A, p, p0, sg, lp, stride);
+    if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
+  }
+  Tree64Levels L2;
+  wave_tree_sum_levels(leaf, L2);
+  return c * 64 + wave_tree_select(L2, leaf, r);
+}
+
+__device__ __forceinline__ double grp16_max(double x) {
+  for (int m = 8; m >= 1; m >>= 1) {
+    const double o = __shfl_xor(x, m, 64);
+    x = o > x ? o : x;
+  }
+  return x;
 }
 
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// zresample: one wavefront per customer (grid-stride), block = 256.
+// zresample, generic path (any D): one wavefront per customer, grid-stride.
 // ---------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep A) {
   const ParState &P = A.P;
@@ -225,7 +291,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep
   const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   double *lpall = A.scratch + (size_t)wid * A.sumK;
-  const int V = P.V, T = A.T;
+  const int V = P.V;
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
   const int T_ne = A.status[V + 3];
   for (int i = wid; i < P.n; i += nw) {
@@ -236,56 +302,181 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep
       const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v]);
       s_new = s_new + o.lmarg;
     }
-    // pass 1: max
-    double M = s_new;
-    for (int base = 0; base < T; base += 64) {
-      const int p = base + lane;
-      if (p < T) {
-        const double sp = table_score(A, p, p0, sg, lpall);
-        if (sp > M) M = sp;
-      }
-    }
-    M = wave_max(M);
-    // pass 2: leaves, chunk partials (T <= 4096)
-    const int nc = (T + 63) >> 6;
-    double part = 0.0;
-    for (int c = 0; c < nc; ++c) {
-      const int p = c * 64 + lane;
-      double leaf = 0.0;
-      if (p < T) {
-        const double sp = table_score(A, p, p0, sg, lpall);
-        if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
-      }
-      const double cs = wave_tree_sum(leaf);
-      if (lane == c) part = cs;
-    }
-    double B;
-    if (nc == 0) B = 0.0;
-    else if (nc == 1) B = __shfl(part, 0, 64);
-    else B = wave_tree_sum(lane < nc ? part : 0.0);
-    const double e_new = mvc_exp(s_new - M);
-    const double W = e_new + B;
-    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-    int pick = -1;
-    if (r < B) {
-      int c = 0;
-      if (nc > 1) {
-        Tree64Levels L;
-        const double pv = lane < nc ? part : 0.0;
-        wave_tree_sum_levels(pv, L);
-        c = wave_tree_select(L, pv, r);
-      }
-      const int p = c * 64 + lane;
-      double leaf = 0.0;
-      if (p < T) {
-        const double sp = table_score(A, p, p0, sg, lpall);
-        if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
-      }
-      Tree64Levels L2;
-      wave_tree_sum_levels(leaf, L2);
-      pick = c * 64 + wave_tree_select(L2, leaf, r);
-    }
+    const int pick = choose_table(A, i, p0, s_new, lpall, 1);
     if (lane == 0) A.choice[i] = pick;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// zresample, MFMA path (D % 4 == 0, D >= 16, every K_v <= 256).  One
+// wavefront per tile of 16 customers.  G = Y_tile * S1^T with
+// v_mfma_f64_16x16x4_f64 (a k-ordered fma chain, bitwise equal to the
+// spec's fma_dot), then the per-view mixture is evaluated in the MFMA C
+// layout (lane = 16 * row-group + dish column, 4 customers per lane): the
+// tree64 butterfly over dish slot e = 16 t + col maps to in-register adds
+// for offsets 32 and 16 and xor-8/4/2/1 shuffles inside each 16-lane group.
+// lp of every (customer, dish) goes to LDS for the table draw, which then
+// runs per customer exactly as in the generic path (choose_table).
+// ---------------------------------------------------------------------------
+typedef double mvc_d4 __attribute__((ext_vector_type(4)));
+
+extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_mfma_kernel(Sweep A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
+  const int sumK = A.Koff[V];
+  double *lpw = (double *)smem + (size_t)w * ((size_t)sumK * 16 + (size_t)V * 16);
+  double *lmw = lpw + (size_t)sumK * 16;
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const int T_ne = A.status[V + 3];
+  const int ntile = (n + 15) >> 4;
+  for (int tile = blockIdx.x * 4 + w; tile < ntile; tile += gridDim.x * 4) {
+    const int i0 = tile * 16;
+    int p0r[4];
+    bool alr[4];
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + grp + 4 * r;
+      p0r[r] = i < n ? P.z[i] : 0;
+      alr[r] = i < n ? (P.n_t[p0r[r]] - 1) > 0 : true;
+    }
+    for (int v = 0; v < V; ++v) {
+      const int K = P.Kact[v];
+      const int koff = A.Koff[v];
+      const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+      const double L2pt = A.L2pt[v];
+      double hy[4], h[4], Y2r[4], mx[4], lfn[4];
+      int j0[4], l0p[4];
+      for (int r = 0; r < 4; ++r) {
+        const int i = i0 + grp + 4 * r;
+        Y2r[r] = i < n ? A.Y2[(size_t)v * n + i] : 0.0;
+        hy[r] = 0.5 * Y2r[r];
+        h[r] = (-0.5 * Y2r[r]) / tau;
+        j0[r] = P.dish[v * TC + p0r[r]];
+        const int l0 = P.d_l[v * KC + j0[r]];
+        l0p[r] = alr[r] ? l0 : l0 - 1;
+        mx[r] = -MVC_PM_INF;
+        lfn[r] = A.cnew[v] + h[r];
+      }
+      const double *S1v = P.S1T + (size_t)v * D * KC;
+      const int arow = i0 + col;
+      const double *yrow = A.y + ((size_t)v * n + (arow < n ? arow : 0)) * D;
+      const int ng = (K + 63) >> 6;
+      for (int g = 0; g < ng; ++g) {
+        mvc_d4 acc[4];
+        for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+        for (int d = 0; d < D; d += 4) {
+          const double a = arow < n ? yrow[d + grp] : 0.0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const int j = g * 64 + t * 16 + col;
+            const double b = j < K ? S1v[(size_t)(d + grp) * KC + j] : 0.0;
+            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = g * 64 + t * 16 + col;
+          if (j < K) {
+            const int lj = P.d_l[v * KC + j];
+            const double c0j = P.c0[v * KC + j], cbj = P.cb[v * KC + j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const double G = acc[t][r];
+              double val;
+              int l;
+              if (j == j0[r]) {
+                l = l0p[r];
+                const double Gp = G - Y2r[r];
+                const double Qp = (P.Q[v * KC + j] - 2.0 * G) + Y2r[r];
+                const Coef c = coef(P.d_n[v * KC + j] - 1, Qp, tau, L2pt, D);
+                val = __builtin_fma(Gp + hy[r], c.cb, c.c0) + h[r];
+              } else {
+                l = lj;
+                val = __builtin_fma(G + hy[r], cbj, c0j) + h[r];
+              }
+              lpw[(size_t)(koff + j) * 16 + grp + 4 * r] = val;
+              if (l > 0 && val > mx[r]) mx[r] = val;
+            }
+          }
+        }
+      }
+      double m[4], wn[4];
+      for (int r = 0; r < 4; ++r) {
+        m[r] = grp16_max(mx[r]);
+        if (lfn[r] > m[r]) m[r] = lfn[r];
+        const int Kact_i = K - ((l0p[r] == 0) ? 1 : 0);
+        double ww = alpha + (double)Kact_i * sigma;
+        if (ww < 0.0) ww = 0.0;
+        wn[r] = ww;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const int nc = (K + 1 + 63) >> 6;
+      double part[4][4];
+      for (int g = 0; g < 4; ++g)
+        for (int r = 0; r < 4; ++r) part[g][r] = 0.0;
+      for (int g = 0; g < nc; ++g) {
+        double x[4][4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int e = g * 64 + t * 16 + col;
+          const int le = e < K ? P.d_l[v * KC + e] : 0;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            double leaf = 0.0;
+            if (e < K) {
+              const int l = (e == j0[r]) ? l0p[r] : le;
+              if (l > 0) {
+                double ww = (double)l - sigma;
+                if (ww < 0.0) ww = 0.0;
+                leaf = ww * mvc_exp(lpw[(size_t)(koff + e) * 16 + grp + 4 * r] - m[r]);
+              }
+            } else if (e == K) {
+              leaf = wn[r] * mvc_exp(lfn[r] - m[r]);
+            }
+            x[t][r] = leaf;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double a0 = x[0][r] + x[2][r];    // offset 32
+          const double a1 = x[1][r] + x[3][r];
+          double s0 = a0 + a1;                    // offset 16
+          s0 = s0 + __shfl_xor(s0, 8, 64);        // offsets 8, 4, 2, 1
+          s0 = s0 + __shfl_xor(s0, 4, 64);
+          s0 = s0 + __shfl_xor(s0, 2, 64);
+          s0 = s0 + __shfl_xor(s0, 1, 64);
+          if (g == 0) part[0][r] = s0;
+          else if (g == 1) part[1][r] = s0;
+          else if (g == 2) part[2][r] = s0;
+          else part[3][r] = s0;
+        }
+      }
+      for (int r = 0; r < 4; ++r) {
+        double S;
+        if (nc == 1) S = part[0][r];
+        else S = (part[0][r] + part[2][r]) + (part[1][r] + part[3][r]);
+        const double denom = alpha + (double)(P.Ltot[v] - (alr[r] ? 0 : 1));
+        const double lm = (denom <= 0.0) ? lfn[r] : (m[r] + mvc_log(S)) - mvc_log(denom);
+        if (col == 0) lmw[v * 16 + grp + 4 * r] = lm;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int c = 0; c < 16; ++c) {
+      const int i = i0 + c;
+      if (i >= n) break;
+      const int p0 = P.z[i];
+      const bool alive = (P.n_t[p0] - 1) > 0;
+      double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+      for (int v = 0; v < V; ++v) s_new = s_new + lmw[v * 16 + c];
+      const int pick = choose_table(A, i, p0, s_new, lpw + c, 16);
+      if (lane == 0) A.choice[i] = pick;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -931,6 +1122,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
 // Host side of the parallel schedule.
 // ===========================================================================
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -979,6 +1171,8 @@ class ParallelSampler : public Sampler {
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;
   std::vector<int32_t> st_host;
+  bool force_generic = false;
+  bool last_path_mfma = false;
 
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
@@ -1013,6 +1207,12 @@ class ParallelSampler : public Sampler {
     cub_bytes = std::max(b1, b2);
     MVC_HIP(hipMalloc(&cub_tmp, cub_bytes));
     st_host.assign(V + 4, 0);
+    const char *fg = getenv("MVC_FORCE_GENERIC");
+    force_generic = fg && fg[0] == '1';
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_mfma_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_stats_partial_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh.data());
     MVC_HIP(hipStreamSynchronize(stream));
@@ -1233,10 +1433,22 @@ class ParallelSampler : public Sampler {
     upload_koff(c);
     Sweep A = make_sweep(c, s);
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    // MFMA path when the view width allows it
+    int Kmax = 0;
+    for (int k : c.K) Kmax = std::max(Kmax, k);
+    const size_t mfma_lds = 4 * ((size_t)sumK(c) * 16 + (size_t)V * 16) * sizeof(double);
+    const bool use_mfma = !force_generic && D % 4 == 0 && D >= 16 && Kmax <= 255 && mfma_lds <= 160 * 1024;
     timers.begin("zresample", &e0);
-    hipLaunchKernelGGL(mvc_par_zresample_kernel, dim3(std::min(kZGrid, (n + 3) / 4)), dim3(256), 0, stream, A);
+    if (use_mfma) {
+      const int ntile = (n + 15) / 16;
+      hipLaunchKernelGGL(mvc_par_zresample_mfma_kernel, dim3(std::min(2048, (ntile + 3) / 4)), dim3(256), mfma_lds,
+                         stream, A);
+    } else {
+      hipLaunchKernelGGL(mvc_par_zresample_kernel, dim3(std::min(kZGrid, (n + 3) / 4)), dim3(256), 0, stream, A);
+    }
     MVC_HIP(hipGetLastError());
     timers.end("zresample", e0);
+    last_path_mfma = use_mfma;
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
     hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n,
@@ -1308,6 +1520,47 @@ class ParallelSampler : public Sampler {
   void get_dish_counts(int chain, int32_t *k_out) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
     for (int v = 0; v < V; ++v) k_out[v] = chains[chain].K[v];
+  }
+
+  void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of, const double *hyper) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    const UserState U = check_user_state(n, V, table_of, T, dish_of);
+    if (T > TC) throw Error(MVC_ERR_UNSUPPORTED, "set_state: more tables than the parallel-mode capacity (4096)");
+    Chain &c = chains[chain];
+    std::vector<int32_t> dish((size_t)V * TC, 0), did((size_t)V * KC, 0), dn((size_t)V * KC, 0), dl((size_t)V * KC, 0);
+    c.K.assign(V, 0);
+    for (int v = 0; v < V; ++v) {
+      const int K = (int)U.ids[v].size();
+      if (K > KC) throw Error(MVC_ERR_UNSUPPORTED, "set_state: too many dishes for the parallel-mode capacity");
+      c.K[v] = K;
+      for (int j = 0; j < K; ++j) { did[v * KC + j] = U.ids[v][j]; dl[v * KC + j] = U.l[v][j]; }
+      for (int p = 0; p < T; ++p) {
+        dish[(size_t)v * TC + p] = U.dish[v][p];
+        dn[v * KC + U.dish[v][p]] += U.n_t[p];
+      }
+    }
+    MVC_HIP(hipStreamSynchronize(stream));
+    ParState &P = c.P;
+    auto up = [&](void *dst, const void *src, size_t bytes) {
+      MVC_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream));
+    };
+    up(P.z, table_of, sizeof(int32_t) * n);
+    up(P.n_t, U.n_t.data(), sizeof(int32_t) * T);
+    up(P.dish, dish.data(), sizeof(int32_t) * dish.size());
+    up(P.d_id, did.data(), sizeof(int32_t) * did.size());
+    up(P.d_n, dn.data(), sizeof(int32_t) * dn.size());
+    up(P.d_l, dl.data(), sizeof(int32_t) * dl.size());
+    up(P.Kact, c.K.data(), sizeof(int32_t) * V);
+    up(P.next_id, U.next_id.data(), sizeof(int32_t) * V);
+    up(P.hyper, hyper, sizeof(double) * (3 * V + 2));
+    std::vector<int32_t> st(V + 4, 0);
+    st[0] = T;
+    up(c.status, st.data(), sizeof(int32_t) * st.size());
+    MVC_HIP(hipStreamSynchronize(stream));
+    c.T = T;
+    rebuild_stats(c);
+    launch_hyper(c, 0, 0);
+    MVC_HIP(hipStreamSynchronize(stream));
   }
 };
 

@@ -168,6 +168,21 @@ class Sampler:
                  "alpha_global": float(hy[3 * V]), "sigma_global": float(hy[3 * V + 1])}
         return t, d.reshape(V, cap)[:, :T.value].copy(), hyper
 
+    def set_state(self, table_of, dish_of, hyper, chain=0):
+        """Warm start / resume one chain (see mvc_sampler_set_state).
+        table_of[n]: table positions; dish_of[V][T]: raw dish ids; hyper:
+        dict as returned by state() or a flat array tau, alpha, sigma, ag, sg."""
+        if isinstance(hyper, dict):
+            hyper = np.concatenate([hyper["tau_v"], hyper["alpha_v"], hyper["sigma_v"],
+                                    [hyper["alpha_global"], hyper["sigma_global"]]])
+        t = np.ascontiguousarray(table_of, dtype=np.int32)
+        d = np.ascontiguousarray(dish_of, dtype=np.int32)
+        h = np.ascontiguousarray(hyper, dtype=np.float64)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_set_state(self._h, chain, t.ctypes.data_as(ip), d.shape[1], d.ctypes.data_as(ip),
+                                                h.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), buf, len(buf)), buf)
+
     def dish_counts(self, chain=0):
         buf = L.errbuf()
         k = np.empty(self.V, dtype=np.int32)

@@ -172,6 +172,39 @@ struct ExactSampler {
     sigma_global = 0.6;
   }
 
+  // Warm start (mvc_sampler_set_state): tables at positions, raw dish ids,
+  // sufficient statistics as ascending-i sums (the init order :64-73).
+  void load_state(const int *tab, int T_, const int *dish_raw, const double *hyper) {
+    T = T_;
+    table_of.assign(tab, tab + n);
+    n_t.assign(T, 0);
+    members.assign(T, {});
+    for (int i = 0; i < n; ++i) { n_t[table_of[i]]++; members[table_of[i]].push_back(i); }
+    dish_of.assign(d, std::vector<int>(T));
+    views.assign(d, View());
+    for (int v = 0; v < d; ++v) {
+      View &W = views[v];
+      int mx = 0;
+      for (int t = 0; t < T; ++t) { dish_of[v][t] = dish_raw[(size_t)v * T + t]; mx = std::max(mx, dish_of[v][t]); }
+      W.K = mx + 1;
+      W.n_vk.assign(W.K, 0); W.l_vk.assign(W.K, 0);
+      W.sum_y.assign(W.K, 0.0); W.sum_y2.assign(W.K, 0.0);
+      for (int t = 0; t < T; ++t) W.l_vk[dish_of[v][t]]++;
+      for (int i = 0; i < n; ++i) {
+        const int k = dish_of[v][table_of[i]];
+        const double val = y[v][i];
+        W.n_vk[k]++;
+        W.sum_y[k] += val;
+        W.sum_y2[k] += val * val;
+      }
+      W.tau_v = hyper[v];
+      W.alpha_v = hyper[d + v];
+      W.sigma_v = hyper[2 * d + v];
+    }
+    alpha_global = hyper[3 * d];
+    sigma_global = hyper[3 * d + 1];
+  }
+
   // ---- multiview_utils.cpp:307-338 compute_f_vk ----
   double f_vk(int v, int k, int i) const {
     const View &W = views[v];
@@ -773,6 +806,44 @@ struct ParallelSampler {
     rebuild_stats();
   }
 
+  void load_state(const int *tab, int T_, const int *dish_raw, const double *hyper) {
+    Y2.assign((size_t)V * n, 0.0);
+    for (int v = 0; v < V; ++v)
+      for (int i = 0; i < n; ++i) {
+        const double *r = y + ((size_t)v * n + i) * D;
+        Y2[(size_t)v * n + i] = fma_dot(r, r, D);
+      }
+    T = T_;
+    z.assign(tab, tab + n);
+    n_t.assign(T, 0);
+    for (int i = 0; i < n; ++i) n_t[z[i]]++;
+    dish.assign(V, std::vector<int>(T));
+    ids.assign(V, {}); nk.assign(V, {}); lk.assign(V, {});
+    S1.assign(V, {}); S2.assign(V, {});
+    next_id.assign(V, 0);
+    tau.assign(V, 0.0); alpha.assign(V, 0.0); sigma.assign(V, 0.0);
+    for (int v = 0; v < V; ++v) {
+      std::vector<int> raw(dish_raw + (size_t)v * T, dish_raw + (size_t)(v + 1) * T);
+      std::vector<int> srt = raw;
+      std::sort(srt.begin(), srt.end());
+      srt.erase(std::unique(srt.begin(), srt.end()), srt.end());
+      ids[v] = srt;
+      lk[v].assign(srt.size(), 0);
+      for (int p = 0; p < T; ++p) {
+        const int j = (int)(std::lower_bound(srt.begin(), srt.end(), raw[p]) - srt.begin());
+        dish[v][p] = j;
+        lk[v][j]++;
+      }
+      next_id[v] = srt.back() + 1;
+      tau[v] = hyper[v];
+      alpha[v] = hyper[V + v];
+      sigma[v] = hyper[2 * V + v];
+    }
+    ag = hyper[3 * V];
+    sg = hyper[3 * V + 1];
+    rebuild_stats();
+  }
+
   struct Coef { double c0, cb; };
   Coef coef(int n_, double Q, double tau_v, double L2pt) const {
     const double a = tau_v + (double)n_;
@@ -1284,6 +1355,42 @@ void *mvo_run(const double *y, int n, int V, int D, int M, int burn_in, int thin
       P.seed = seed; P.chain = (uint32_t)chain;
       P.init_rng = SeqRng{seed, (uint32_t)chain, 0};
       P.initialize();
+      P.run(M, burn_in, thin, *R);
+    }
+  } catch (const std::exception &e) {
+    R->error = e.what();
+  }
+  return R;
+}
+
+// Same as mvo_run, but the chain starts from a given state instead of the
+// reference initialisation (mirrors mvc_sampler_set_state: RNG draw 0).
+void *mvo_run_from(const double *y, int n, int V, int D, int M, int burn_in, int thin, uint64_t seed, int chain,
+                   int mode, int math, const int *table_of, int T, const int *dish_of, const double *hyper) {
+  Result *R = new Result();
+  R->n = n;
+  R->V = V;
+  try {
+    if (mode == 0) {
+      if (D != 1) throw std::runtime_error("exact mode requires D == 1");
+      auto go = [&](auto &S) {
+        S.n = n;
+        S.d = V;
+        S.y.assign(V, std::vector<double>(n));
+        for (int v = 0; v < V; ++v)
+          for (int i = 0; i < n; ++i) S.y[v][i] = y[(size_t)v * n + i];
+        S.rng = SeqRng{seed, (uint32_t)chain, 0};
+        S.load_state(table_of, T, dish_of, hyper);
+        S.run(M, burn_in, thin, *R);
+      };
+      if (math == 0) { ExactSampler<LibmMath> S; go(S); }
+      else { ExactSampler<PortableMath> S; go(S); }
+    } else {
+      ParallelSampler P;
+      P.n = n; P.V = V; P.D = D; P.y = y;
+      P.seed = seed; P.chain = (uint32_t)chain;
+      P.init_rng = SeqRng{seed, (uint32_t)chain, 0};
+      P.load_state(table_of, T, dish_of, hyper);
       P.run(M, burn_in, thin, *R);
     }
   } catch (const std::exception &e) {

@@ -35,6 +35,8 @@ def lib():
         ip = ctypes.POINTER(ctypes.c_int)
         L.mvo_run.restype = vp
         L.mvo_run.argtypes = [dp, i32, i32, i32, i32, i32, i32, u64, i32, i32, i32]
+        L.mvo_run_from.restype = vp
+        L.mvo_run_from.argtypes = [dp, i32, i32, i32, i32, i32, i32, u64, i32, i32, i32, ip, i32, ip, dp]
         L.mvo_error.restype = ctypes.c_char_p
         L.mvo_error.argtypes = [vp]
         for f in ("mvo_num_saved", "mvo_num_sweeps"):
@@ -64,8 +66,12 @@ def _dp(a):
     return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
 
 
-def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE):
+def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=None):
     """Run one chain.  y: float64 array [V][n] (D=1) or [V][n][D].
+
+    state = (table_of[n], dish_of[V][T], hyper[3V+2]) starts the chain from
+    that state (mirror of mvc_sampler_set_state) instead of the reference
+    initialisation.
 
     Returns a dict shaped like the reference's Rcpp::List
     (multiview_gibbs.cpp:121-130) plus per-sweep traces.
@@ -75,7 +81,15 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE):
         y = y[:, :, None]
     V, n, D = y.shape
     L = lib()
-    h = L.mvo_run(_dp(y), n, V, D, M, burn_in, thin, ctypes.c_uint64(seed), chain, mode, math)
+    if state is None:
+        h = L.mvo_run(_dp(y), n, V, D, M, burn_in, thin, ctypes.c_uint64(seed), chain, mode, math)
+    else:
+        tab = np.ascontiguousarray(state[0], dtype=np.int32)
+        dsh = np.ascontiguousarray(state[1], dtype=np.int32)
+        hyp = np.ascontiguousarray(state[2], dtype=np.float64)
+        ipt = ctypes.POINTER(ctypes.c_int)
+        h = L.mvo_run_from(_dp(y), n, V, D, M, burn_in, thin, ctypes.c_uint64(seed), chain, mode, math,
+                           tab.ctypes.data_as(ipt), dsh.shape[1], dsh.ctypes.data_as(ipt), _dp(hyp))
     try:
         err = L.mvo_error(h)
         if err:

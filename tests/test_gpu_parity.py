@@ -194,3 +194,78 @@ def test_dropin_output_shape():
     assert res["loglik"].size == 0
     cl = m.get_final_clusters(res)
     assert cl.shape == (200, 5)
+
+
+# ---------------------------------------------------------------- MFMA path, warm start
+def _warm_state(z, V, K):
+    from mvc_amd import data  # noqa: F401
+    T = int(z.max()) + 1
+    dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
+    hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
+    return z.astype(np.int32), dish, hyper
+
+
+@pytest.mark.parametrize("D", [16, 32])
+def test_parallel_mfma_path_cold(D):
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.synthetic(1200, 3, D, 8, seed=D)
+    gpu = m.run_gibbs_cpp(y, 6, 0, 1, seed=21, mode="parallel", quiet=True)
+    ref = O.run(y, 6, 0, 1, seed=21, mode=O.PARALLEL)
+    _compare(gpu, ref)
+
+
+@pytest.mark.parametrize("D", [1, 4, 64])
+def test_parallel_warm_start(D):
+    m = _mvc()
+    from mvc_amd import data
+    V, K = 4, 16
+    y, z = data.synthetic(3000, V, D, K, seed=100 + D)
+    st = _warm_state(z, V, K)
+    s = m.Sampler(y, seed=77, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 5, 0, 1, seed=77, mode=O.PARALLEL, state=st)
+    for it in range(5):
+        s.sweep(1)
+        t, d, h = s.state()
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+        assert np.array_equal(h["tau_v"], ref["tau_v"][:, it]), it
+        assert h["sigma_global"] == ref["sigma_global"][it]
+    s.close()
+
+
+def test_mfma_and_generic_paths_identical(monkeypatch):
+    m = _mvc()
+    from mvc_amd import data
+    V, K, D = 3, 8, 32
+    y, z = data.synthetic(2000, V, D, K, seed=5)
+    st = _warm_state(z, V, K)
+    out = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MVC_FORCE_GENERIC", flag)
+        s = m.Sampler(y, seed=9, mode="parallel")
+        s.set_state(*st)
+        s.sweep(3)
+        out.append(s.state())
+        s.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+
+
+def test_exact_warm_start():
+    m = _mvc()
+    from mvc_amd import data
+    y, z = data.config1(4, n=400)
+    dish = np.array([[0, 1, 2], [0, 1, 0]], dtype=np.int32)
+    hyper = np.array([1.69, 1.69, 1.0, 1.0, 0.5, 0.5, 1.0, 0.6])
+    s = m.Sampler(y, seed=8, mode="exact")
+    s.set_state(z.astype(np.int32), dish, hyper)
+    ref = O.run(y, 6, 0, 1, seed=8, mode=O.EXACT, math=O.PORTABLE, state=(z.astype(np.int32), dish, hyper))
+    for it in range(6):
+        s.sweep(1)
+        t, d, h = s.state()
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+        assert h["alpha_global"] == ref["alpha_global"][it]
+    s.close()
