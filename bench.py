@@ -1,0 +1,189 @@
+"""bench.py — Gibbs sweeps/s of the MI355X sampler (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[3], one shard per GPU): synthetic data
+N = 1,000,000 customers, V = 4 views, D = 128 dims, K = 64 generating
+clusters (per-view K_v = 64, 32, 16, 8), fp64; one independent chain per
+GPU (chain id = rank, weak scaling).  A "step" is one full parallel sweep
+(z-resample of all N customers + birth resolution + commit + stats rebuild +
+hyperparameter MH).  The chain is warm-started at the generating partition so
+the measured state has ~K tables (the reference's cold initialisation has a
+long transient); every timed sweep does the complete work.
+
+Multi-GPU: launched by torch.distributed.run, one process per GPU, chains
+shard embarrassingly (no collective in the sweep); the timed region is
+bracketed by barrier + device sync and the max over ranks is reported.
+
+Output: one JSON line on rank 0 (driver contract), including the roofline of
+the dominant kernel (zresample) measured with HIP events on the sampler's
+stream, and a CPU baseline (the oracle's port of the same sweep, timed on a
+bounded subsample on one host core).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # name: (N, V, D, K, description)
+    "c4": (1_000_000, 4, 128, 64, "BASELINE configs[3] shard: synthetic N=1M V=4 D=128 K=64, 1 chain/GPU"),
+    "c2": (100_000, 2, 64, 16, "BASELINE configs[1]: synthetic N=100k V=2 D=64 K=16, 1 chain"),
+    "ns": (1_000_000, 4, 1, 64, "north_star literal: synthetic N=1M V=4 D=1 K=64, 1 chain/GPU"),
+}
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_F64_TFLOPS = 78.6       # fp64 MFMA / vector dense peak (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=1999)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="customers in the CPU baseline sample (0 = auto)")
+    return ap.parse_args()
+
+
+def warm_state(z, V, K):
+    """Generating partition: table t = global cluster t, dish_v(t) = t mod K_v."""
+    uniq = np.unique(z)
+    remap = np.full(int(z.max()) + 1, -1, dtype=np.int64)
+    remap[uniq] = np.arange(uniq.size)
+    table_of = remap[z].astype(np.int32)
+    dish = np.stack([uniq % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
+    hyper = np.concatenate([np.full(V, 1.69), np.ones(V), np.full(V, 0.5), [1.0, 0.6]])
+    return table_of, dish, hyper
+
+
+def cpu_baseline(y, z, V, K, D, seed, n_sample=0, target_s=12.0):
+    """Oracle port of the same parallel sweep on a bounded subsample, 1 core.
+    The sample size is calibrated on a 2000-customer probe to ~target_s."""
+    from oracle import oracle as O
+    if not n_sample:
+        m = min(2000, y.shape[1])
+        t0 = time.perf_counter()
+        O.run(np.ascontiguousarray(y[:, :m]), 1, 0, 1, seed, chain=0, mode=O.PARALLEL, state=warm_state(z[:m], V, K))
+        per = (time.perf_counter() - t0) / m
+        n_sample = int(min(y.shape[1], max(m, target_s / max(per, 1e-9))))
+    ys = np.ascontiguousarray(y[:, :n_sample])
+    st = warm_state(z[:n_sample], V, K)
+    t0 = time.perf_counter()
+    O.run(ys, 1, 0, 1, seed, chain=0, mode=O.PARALLEL, state=st)
+    dt = time.perf_counter() - t0
+    sweeps_per_s = 1.0 / (dt * (y.shape[1] / n_sample))   # cost is linear in N at fixed K, T
+    return {"value": sweeps_per_s, "unit": "sweeps/s", "cores": 1, "kind": "port",
+            "sample": f"1 parallel sweep of the oracle (oracle/mvc_oracle.cpp ParallelSampler, g++ -O2, "
+                      f"portable math) over the first {n_sample} of {y.shape[1]} customers from the same warm "
+                      f"state, {dt:.2f} s, extrapolated linearly to N"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    N, V, D, K, desc = CONFIGS[args.config]
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    from mvc_amd import data
+    from mvc_amd.sampler import Sampler
+
+    t_gen = time.perf_counter()
+    y, z = data.synthetic(N, V, D, K, seed=args.seed)
+    t_gen = time.perf_counter() - t_gen
+    s = Sampler(y, seed=args.seed, mode="parallel", first_chain=rank, device=local, timing=True)
+    s.set_state(*warm_state(z, V, K))
+    s.sweep(args.warmup)
+    s.synchronize()
+    s.reset_timers()
+
+    barrier_sync()
+    t0 = time.perf_counter()
+    s.sweep(args.steps)
+    s.synchronize()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    kms, kcnt = s.kernel_time("zresample")
+    sweep_ms, _ = s.kernel_time("sweep")
+    parts = {k: s.kernel_time(k)[0] / max(1, args.steps) for k in ("zresample", "births", "commit", "stats", "hyper")}
+    kdish = s.dish_counts()
+    T = s.state()[1].shape[1]
+    s.close()
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    k_avg_s = (kms / max(1, kcnt)) / 1e3
+    bytes_alg = N * (8 * V * D + 8)                 # y read once + z read + choice write
+    flops_alg = 2.0 * N * float(kdish.sum()) * D    # G = Y S1^T per view (MFMA fp64)
+    hbm_gbs = bytes_alg / k_avg_s / 1e9
+    tflops = flops_alg / k_avg_s / 1e12
+    mfma_bound = D >= 16
+    roof = ({"bound": "mfma", "achieved": round(tflops, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(tflops / PEAK_F64_TFLOPS, 4), "traffic": None}
+            if mfma_bound else
+            {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+             "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "traffic": None})
+    value = world * args.steps / elapsed
+    out = {
+        "metric": "Gibbs sweeps/sec (N×V×K) at 1/2/4/8 MI355X; % HBM roofline",
+        "value": round(value, 4),
+        "unit": "sweeps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": desc, "N": N, "V": V, "D": D, "K": K, "chains": world,
+                   "schedule": "parallel z-resample (DESIGN.md §4)", "parallelism": f"chains{world}",
+                   "tables_at_end": int(T), "dishes_at_end": kdish.tolist()},
+        "roofline": roof,
+        "hbm": {"kernel": "zresample", "achieved_gbs": round(hbm_gbs, 1), "peak_gbs": PEAK_HBM_GBS,
+                "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": bytes_alg,
+                "flops_per_launch": flops_alg, "kernel_ms": round(k_avg_s * 1e3, 4)},
+        "nvk_sweeps_per_s": round(value * N * V * K, 1),
+        "kernel_ms_per_sweep": {k: round(v, 4) for k, v in parts.items()},
+        "data_gen_s": round(t_gen, 2),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(y, z, V, K, D, args.seed, args.cpu_sample)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
