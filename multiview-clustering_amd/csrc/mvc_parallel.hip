@@ -308,27 +308,82 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep
 }
 
 // ---------------------------------------------------------------------------
-// zresample, MFMA path (D % 4 == 0, D >= 16, every K_v <= 256).  One
-// wavefront per tile of 16 customers.  G = Y_tile * S1^T with
-// v_mfma_f64_16x16x4_f64 (a k-ordered fma chain, bitwise equal to the
-// spec's fma_dot), then the per-view mixture is evaluated in the MFMA C
-// layout (lane = 16 * row-group + dish column, 4 customers per lane): the
-// tree64 butterfly over dish slot e = 16 t + col maps to in-register adds
-// for offsets 32 and 16 and xor-8/4/2/1 shuffles inside each 16-lane group.
-// lp of every (customer, dish) goes to LDS for the table draw, which then
-// runs per customer exactly as in the generic path (choose_table).
+// zresample, MFMA path (D % 4 == 0, D >= 16, every K_v <= 255, T <= 256).
+// One wavefront per tile of 16 customers; 4 wavefronts per block.
+//   * table descriptors (log mass, size, per-view lp row index) and dish
+//     descriptors (c0, cb, Q, n, l) of the frozen state are staged in LDS once
+//     per block;
+//   * G = Y_tile * S1^T with v_mfma_f64_16x16x4_f64 (a k-ordered fma chain,
+//     bitwise equal to the spec's fma_dot);
+//   * the per-view mixture is evaluated in the MFMA C layout (lane = 16 *
+//     row-group + dish column, 4 customers per lane): the tree64 butterfly
+//     over dish slot e = 16 t + col is in-register for offsets 32 and 16 and
+//     xor-8/4/2/1 shuffles inside each 16-lane group;
+//   * lp of every (customer, dish) goes to per-wave LDS; the table draw then
+//     runs per customer with lane = table slot, keeping scores and the tree
+//     levels in registers (one pass, no recomputation).
+// Bitwise identical to the generic path (tests/test_gpu_parity.py).
 // ---------------------------------------------------------------------------
 typedef double mvc_d4 __attribute__((ext_vector_type(4)));
+
+#define MVC_MFMA_TMAX 256
+
+struct MfmaLds {          // carve of the dynamic LDS
+  double *t_lmass;        // [T]
+  int *t_n;               // [T]
+  int *t_idx;             // [V*T]  Koff[v] + dish[v][p]
+  double *d_c0, *d_cb, *d_Q;   // [sumK]
+  int *d_n, *d_l;         // [sumK]
+  double *lpw, *lmw;      // per wave
+};
+
+__device__ __forceinline__ size_t mfma_shared_bytes(int T, int V, int sumK) {
+  return (size_t)T * 8 + (size_t)T * 4 + (size_t)V * T * 4 + (size_t)sumK * (3 * 8 + 2 * 4) + 64;
+}
 
 extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_mfma_kernel(Sweep A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
+  const int T = A.T;
   const int sumK = A.Koff[V];
-  double *lpw = (double *)smem + (size_t)w * ((size_t)sumK * 16 + (size_t)V * 16);
-  double *lmw = lpw + (size_t)sumK * 16;
+  // ---- carve: doubles first (8-byte aligned), ints after
+  MfmaLds L;
+  {
+    double *dp = (double *)smem;
+    L.t_lmass = dp; dp += T;
+    L.d_c0 = dp; dp += sumK;
+    L.d_cb = dp; dp += sumK;
+    L.d_Q = dp; dp += sumK;
+    int *ip = (int *)dp;
+    L.t_n = ip; ip += T;
+    L.t_idx = ip; ip += V * T;
+    L.d_n = ip; ip += sumK;
+    L.d_l = ip; ip += sumK;
+    char *cp = (char *)(((uintptr_t)ip + 15) & ~(uintptr_t)15);
+    L.lpw = (double *)cp + (size_t)w * ((size_t)sumK * 16 + (size_t)V * 16);
+    L.lmw = L.lpw + (size_t)sumK * 16;
+  }
+  for (int p = tid; p < T; p += 256) {
+    L.t_lmass[p] = P.lmass[p];
+    L.t_n[p] = P.n_t[p];
+    for (int v = 0; v < V; ++v) L.t_idx[v * T + p] = A.Koff[v] + P.dish[v * TC + p];
+  }
+  for (int k = tid; k < sumK; k += 256) {
+    int v = 0;
+    while (v + 1 < V && A.Koff[v + 1] <= k) ++v;
+    const int j = k - A.Koff[v];
+    L.d_c0[k] = P.c0[v * KC + j];
+    L.d_cb[k] = P.cb[v * KC + j];
+    L.d_Q[k] = P.Q[v * KC + j];
+    L.d_n[k] = P.d_n[v * KC + j];
+    L.d_l[k] = P.d_l[v * KC + j];
+  }
+  __syncthreads();
+  double *lpw = L.lpw, *lmw = L.lmw;
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
   const int T_ne = A.status[V + 3];
   const int ntile = (n + 15) >> 4;
@@ -336,40 +391,61 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_mfma_kernel(
     const int i0 = tile * 16;
     int p0r[4];
     bool alr[4];
+#pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int i = i0 + grp + 4 * r;
       p0r[r] = i < n ? P.z[i] : 0;
-      alr[r] = i < n ? (P.n_t[p0r[r]] - 1) > 0 : true;
+      alr[r] = i < n ? (L.t_n[p0r[r]] - 1) > 0 : true;
     }
     for (int v = 0; v < V; ++v) {
       const int K = P.Kact[v];
       const int koff = A.Koff[v];
       const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
       const double L2pt = A.L2pt[v];
-      double hy[4], h[4], Y2r[4], mx[4], lfn[4];
-      int j0[4], l0p[4];
+      const double cnew = A.cnew[v];
+      double Y2r[4], mx[4];
+      int j0[4];
+#pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int i = i0 + grp + 4 * r;
         Y2r[r] = i < n ? A.Y2[(size_t)v * n + i] : 0.0;
-        hy[r] = 0.5 * Y2r[r];
-        h[r] = (-0.5 * Y2r[r]) / tau;
-        j0[r] = P.dish[v * TC + p0r[r]];
-        const int l0 = P.d_l[v * KC + j0[r]];
-        l0p[r] = alr[r] ? l0 : l0 - 1;
+        j0[r] = L.t_idx[v * T + p0r[r]] - koff;
         mx[r] = -MVC_PM_INF;
-        lfn[r] = A.cnew[v] + h[r];
       }
       const double *S1v = P.S1T + (size_t)v * D * KC;
       const int arow = i0 + col;
-      const double *yrow = A.y + ((size_t)v * n + (arow < n ? arow : 0)) * D;
+      const bool rowok = arow < n;
+      const double *yrow = A.y + ((size_t)v * n + (rowok ? arow : 0)) * D;
       const int ng = (K + 63) >> 6;
       for (int g = 0; g < ng; ++g) {
         mvc_d4 acc[4];
+#pragma unroll
         for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
-        for (int d = 0; d < D; d += 4) {
-          const double a = arow < n ? yrow[d + grp] : 0.0;
+        const int nt = min(4, (K - g * 64 + 15) >> 4);
+        int d = 0;
+        for (; d + 8 <= D; d += 8) {            // 2 k-steps per iteration
+          double a0 = rowok ? yrow[d + grp] : 0.0;
+          double a1 = rowok ? yrow[d + 4 + grp] : 0.0;
+          double b0[4], b1[4];
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
+            const int j = g * 64 + t * 16 + col;
+            const bool ok = t < nt && j < K;
+            b0[t] = ok ? S1v[(size_t)(d + grp) * KC + j] : 0.0;
+            b1[t] = ok ? S1v[(size_t)(d + 4 + grp) * KC + j] : 0.0;
+          }
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (t < nt) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[t], acc[t], 0, 0, 0);
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (t < nt) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[t], acc[t], 0, 0, 0);
+        }
+        for (; d < D; d += 4) {
+          const double a = rowok ? yrow[d + grp] : 0.0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if (t >= nt) continue;
             const int j = g * 64 + t * 16 + col;
             const double b = j < K ? S1v[(size_t)(d + grp) * KC + j] : 0.0;
             acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
@@ -378,101 +454,140 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_mfma_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           const int j = g * 64 + t * 16 + col;
-          if (j < K) {
-            const int lj = P.d_l[v * KC + j];
-            const double c0j = P.c0[v * KC + j], cbj = P.cb[v * KC + j];
+          if (t < nt && j < K) {
+            const int k = koff + j;
+            const int lj = L.d_l[k];
+            const double c0j = L.d_c0[k], cbj = L.d_cb[k];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const double G = acc[t][r];
+              const double hy = 0.5 * Y2r[r];
+              const double h = (-0.5 * Y2r[r]) / tau;
               double val;
-              int l;
+              int l = lj;
               if (j == j0[r]) {
-                l = l0p[r];
+                if (!alr[r]) l -= 1;
                 const double Gp = G - Y2r[r];
-                const double Qp = (P.Q[v * KC + j] - 2.0 * G) + Y2r[r];
-                const Coef c = coef(P.d_n[v * KC + j] - 1, Qp, tau, L2pt, D);
-                val = __builtin_fma(Gp + hy[r], c.cb, c.c0) + h[r];
+                const double Qp = (L.d_Q[k] - 2.0 * G) + Y2r[r];
+                const Coef c = coef(L.d_n[k] - 1, Qp, tau, L2pt, D);
+                val = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
               } else {
-                l = lj;
-                val = __builtin_fma(G + hy[r], cbj, c0j) + h[r];
+                val = __builtin_fma(G + hy, cbj, c0j) + h;
               }
-              lpw[(size_t)(koff + j) * 16 + grp + 4 * r] = val;
+              lpw[(size_t)k * 16 + grp + 4 * r] = val;
               if (l > 0 && val > mx[r]) mx[r] = val;
             }
           }
         }
       }
-      double m[4], wn[4];
-      for (int r = 0; r < 4; ++r) {
-        m[r] = grp16_max(mx[r]);
-        if (lfn[r] > m[r]) m[r] = lfn[r];
-        const int Kact_i = K - ((l0p[r] == 0) ? 1 : 0);
-        double ww = alpha + (double)Kact_i * sigma;
-        if (ww < 0.0) ww = 0.0;
-        wn[r] = ww;
-      }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int nc = (K + 1 + 63) >> 6;
-      double part[4][4];
-      for (int g = 0; g < 4; ++g)
-        for (int r = 0; r < 4; ++r) part[g][r] = 0.0;
-      for (int g = 0; g < nc; ++g) {
-        double x[4][4];
+#pragma unroll 1
+      for (int r = 0; r < 4; ++r) {
+        const int row = grp + 4 * r;
+        const double h = (-0.5 * Y2r[r]) / tau;
+        const double lfn = cnew + h;
+        const int l0 = L.d_l[koff + j0[r]];
+        const int l0p = alr[r] ? l0 : l0 - 1;
+        double m = grp16_max(mx[r]);
+        if (lfn > m) m = lfn;
+        const int Kact_i = K - ((l0p == 0) ? 1 : 0);
+        double wn = alpha + (double)Kact_i * sigma;
+        if (wn < 0.0) wn = 0.0;
+        double part[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int g = 0; g < nc; ++g) {
+          double x[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int e = g * 64 + t * 16 + col;
-          const int le = e < K ? P.d_l[v * KC + e] : 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
+          for (int t = 0; t < 4; ++t) {
+            const int e = g * 64 + t * 16 + col;
             double leaf = 0.0;
             if (e < K) {
-              const int l = (e == j0[r]) ? l0p[r] : le;
+              const int l = (e == j0[r]) ? l0p : L.d_l[koff + e];
               if (l > 0) {
                 double ww = (double)l - sigma;
                 if (ww < 0.0) ww = 0.0;
-                leaf = ww * mvc_exp(lpw[(size_t)(koff + e) * 16 + grp + 4 * r] - m[r]);
+                leaf = ww * mvc_exp(lpw[(size_t)(koff + e) * 16 + row] - m);
               }
             } else if (e == K) {
-              leaf = wn[r] * mvc_exp(lfn[r] - m[r]);
+              leaf = wn * mvc_exp(lfn - m);
             }
-            x[t][r] = leaf;
+            x[t] = leaf;
           }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const double a0 = x[0][r] + x[2][r];    // offset 32
-          const double a1 = x[1][r] + x[3][r];
-          double s0 = a0 + a1;                    // offset 16
-          s0 = s0 + __shfl_xor(s0, 8, 64);        // offsets 8, 4, 2, 1
+          double s0 = (x[0] + x[2]) + (x[1] + x[3]);   // offsets 32, 16
+          s0 = s0 + __shfl_xor(s0, 8, 64);             // offsets 8, 4, 2, 1
           s0 = s0 + __shfl_xor(s0, 4, 64);
           s0 = s0 + __shfl_xor(s0, 2, 64);
           s0 = s0 + __shfl_xor(s0, 1, 64);
-          if (g == 0) part[0][r] = s0;
-          else if (g == 1) part[1][r] = s0;
-          else if (g == 2) part[2][r] = s0;
-          else part[3][r] = s0;
+          if (g == 0) part[0] = s0;
+          else if (g == 1) part[1] = s0;
+          else if (g == 2) part[2] = s0;
+          else part[3] = s0;
         }
-      }
-      for (int r = 0; r < 4; ++r) {
-        double S;
-        if (nc == 1) S = part[0][r];
-        else S = (part[0][r] + part[2][r]) + (part[1][r] + part[3][r]);
+        const double S = (nc == 1) ? part[0] : (part[0] + part[2]) + (part[1] + part[3]);
         const double denom = alpha + (double)(P.Ltot[v] - (alr[r] ? 0 : 1));
-        const double lm = (denom <= 0.0) ? lfn[r] : (m[r] + mvc_log(S)) - mvc_log(denom);
-        if (col == 0) lmw[v * 16 + grp + 4 * r] = lm;
+        const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
+        if (col == 0) lmw[v * 16 + row] = lm;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    // ---- table draw per customer: lane = table slot, one pass (T <= 256)
+    const int nct = (T + 63) >> 6;
     for (int c = 0; c < 16; ++c) {
       const int i = i0 + c;
       if (i >= n) break;
       const int p0 = P.z[i];
-      const bool alive = (P.n_t[p0] - 1) > 0;
+      const bool alive = (L.t_n[p0] - 1) > 0;
       double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
       for (int v = 0; v < V; ++v) s_new = s_new + lmw[v * 16 + c];
-      const int pick = choose_table(A, i, p0, s_new, lpw + c, 16);
+      double sc[4];
+      double M = s_new;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int p = q * 64 + lane;
+        double sp = -MVC_PM_INF;
+        if (q < nct && p < T) {
+          const int np = L.t_n[p] - (p == p0 ? 1 : 0);
+          const double mass = (double)np - sg;
+          if (np >= 1 && mass > 0.0) {
+            sp = (p == p0) ? mvc_log(mass) : L.t_lmass[p];
+            for (int v = 0; v < V; ++v) sp = sp + lpw[(size_t)L.t_idx[v * T + p] * 16 + c];
+          }
+        }
+        sc[q] = sp;
+        if (sp > M) M = sp;
+      }
+      M = wave_max(M);
+      double leafq[4], part = 0.0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        leafq[q] = (q < nct && sc[q] != -MVC_PM_INF) ? mvc_exp(sc[q] - M) : 0.0;
+        if (q < nct) {
+          const double cs = wave_tree_sum(leafq[q]);
+          if (lane == q) part = cs;
+        }
+      }
+      double B;
+      if (nct == 0) B = 0.0;
+      else if (nct == 1) B = __shfl(part, 0, 64);
+      else B = wave_tree_sum(lane < nct ? part : 0.0);
+      const double W = mvc_exp(s_new - M) + B;
+      double rr = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+      int pick = -1;
+      if (rr < B) {
+        int cq = 0;
+        if (nct > 1) {
+          Tree64Levels Lv;
+          const double pv = lane < nct ? part : 0.0;
+          wave_tree_sum_levels(pv, Lv);
+          cq = wave_tree_select(Lv, pv, rr);
+        }
+        const double leaf = cq == 0 ? leafq[0] : (cq == 1 ? leafq[1] : (cq == 2 ? leafq[2] : leafq[3]));
+        Tree64Levels L2;
+        wave_tree_sum_levels(leaf, L2);
+        pick = cq * 64 + wave_tree_select(L2, leaf, rr);
+      }
       if (lane == 0) A.choice[i] = pick;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -613,12 +728,21 @@ extern "C" __global__ __launch_bounds__(64) void mvc_par_births_kernel(Sweep A) 
 }
 
 // commit step 1: table counts and birth flags
-extern "C" __global__ void mvc_par_count_kernel(int n, const int32_t *choice, int32_t *cnt, int32_t *flag) {
+// (per-block LDS histogram, then one global add per touched table: integer
+// counts, so the result is independent of the order)
+extern "C" __global__ __launch_bounds__(256) void mvc_par_count_kernel(int n, int T, const int32_t *choice,
+                                                                      int32_t *cnt, int32_t *flag) {
+  __shared__ int h[4096];
+  for (int p = threadIdx.x; p < T; p += blockDim.x) h[p] = 0;
+  __syncthreads();
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int c = choice[i];
     flag[i] = c < 0 ? 1 : 0;
-    if (c >= 0) atomicAdd(&cnt[c], 1);
+    if (c >= 0) atomicAdd(&h[c], 1);
   }
+  __syncthreads();
+  for (int p = threadIdx.x; p < T; p += blockDim.x)
+    if (h[p]) atomicAdd(&cnt[p], h[p]);
 }
 
 // commit step 2 (one workgroup of 256): new tables, dish lists, counts.
@@ -754,66 +878,74 @@ extern "C" __global__ void mvc_par_y2_kernel(int n, int V, int D, const double *
 
 // ---------------------------------------------------------------------------
 // Stats rebuild, chunked ordered sums.  Block (chunk c,
-// view v): thread d owns dimension d and walks the chunk's customers in
-// ascending order, accumulating into acc[j][d] in LDS; thread D (or thread
-// 0 after the dims) does the same for Y2 -> S2.
-// part1[c][Koff[v]+j][d], part2[c][Koff[v]+j]
+// view v): (1) dish of every customer of the chunk into LDS; (2) thread j
+// builds the ascending member list of dish j by one broadcast pass over the
+// chunk; (3) thread per (dish j, dim d), d fastest, accumulates y over the
+// members in ascending order in a register (the spec's sequential sum) with
+// 8 loads in flight.  part1[c][Koff[v]+j][d], part2[c][Koff[v]+j].
 // ---------------------------------------------------------------------------
-#define MVC_STATS_SUB 64
 extern "C" __global__ __launch_bounds__(256) void mvc_par_stats_partial_kernel(
-    ParState P, const double *y, const double *Y2, const int32_t *Koff, int sumK, int dgroup,
+    ParState P, const double *y, const double *Y2, const int32_t *Koff, int stride, int unused,
     double *part1, double *part2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  (void)unused;
   const int c = blockIdx.x, v = blockIdx.y;
   const int tid = threadIdx.x;
   const int n = P.n, D = P.D, TC = P.TC;
   const int K = P.Kact[v];
-  const int i0 = c * kStatsChunk, i1 = min(n, i0 + kStatsChunk);
-  // LDS: acc[K][dgroup] | acc2[K] | ysub[SUB][dgroup] | y2sub[SUB] | jsub[SUB]
-  double *acc = (double *)smem;
-  double *acc2 = acc + (size_t)K * dgroup;
-  double *ysub = acc2 + K;
-  double *y2sub = ysub + (size_t)MVC_STATS_SUB * dgroup;
-  int *jsub = (int *)(y2sub + MVC_STATS_SUB);
-  for (int d0 = 0; d0 < D; d0 += dgroup) {
-    const int dg = min(dgroup, D - d0);
-    const bool do_y2 = (d0 == 0);
-    for (int e = tid; e < K * dgroup; e += 256) acc[e] = 0.0;
-    for (int e = tid; e < K; e += 256) acc2[e] = 0.0;
-    __syncthreads();
-    for (int s0 = i0; s0 < i1; s0 += MVC_STATS_SUB) {
-      const int cnt = min(MVC_STATS_SUB, i1 - s0);
-      for (int e = tid; e < cnt * dg; e += 256) {
-        const int q = e / dg, d = e % dg;
-        ysub[q * dgroup + d] = y[((size_t)v * n + s0 + q) * D + d0 + d];
-      }
-      for (int q = tid; q < cnt; q += 256) {
-        jsub[q] = P.dish[v * TC + P.z[s0 + q]];
-        y2sub[q] = Y2[(size_t)v * n + s0 + q];
-      }
-      __syncthreads();
-      if (tid < dg) {
-        for (int q = 0; q < cnt; ++q) {
-          const int j = jsub[q];
-          acc[j * dgroup + tid] = acc[j * dgroup + tid] + ysub[q * dgroup + tid];
-        }
-      } else if (do_y2 && tid == (dg < 256 ? dg : 0)) {
-        for (int q = 0; q < cnt; ++q) acc2[jsub[q]] = acc2[jsub[q]] + y2sub[q];
-      }
-      __syncthreads();
-      if (do_y2 && dg == 256 && tid == 0) {   // all threads busy with dims: Y2 afterwards
-        for (int q = 0; q < cnt; ++q) acc2[jsub[q]] = acc2[jsub[q]] + y2sub[q];
-      }
-      __syncthreads();
+  const int i0 = c * kStatsChunk, cnt = min(n, i0 + kStatsChunk) - i0;
+  int *jsub = (int *)smem;               // [kStatsChunk]
+  int *list = jsub + kStatsChunk;        // [kStatsChunk]
+  int *off = list + kStatsChunk;         // [K + 1]
+  for (int q = tid; q < cnt; q += 256) jsub[q] = P.dish[v * TC + P.z[i0 + q]];
+  __syncthreads();
+  // member counts -> offsets (thread j counts; single pass per dish chunk)
+  for (int j0 = 0; j0 < K; j0 += 256) {
+    const int j = j0 + tid;
+    int m = 0;
+    if (j < K)
+      for (int q = 0; q < cnt; ++q) m += (jsub[q] == j) ? 1 : 0;
+    if (j < K) off[j + 1] = m;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    off[0] = 0;
+    for (int j = 0; j < K; ++j) off[j + 1] += off[j];
+  }
+  __syncthreads();
+  for (int j0 = 0; j0 < K; j0 += 256) {
+    const int j = j0 + tid;
+    if (j < K) {
+      int w = off[j];
+      for (int q = 0; q < cnt; ++q)
+        if (jsub[q] == j) list[w++] = q;
     }
-    const size_t base = ((size_t)c * sumK + Koff[v]);
-    for (int e = tid; e < K * dg; e += 256) {
-      const int j = e / dg, d = e % dg;
-      part1[(base + j) * D + d0 + d] = acc[j * dgroup + d];
+  }
+  __syncthreads();
+  const size_t base = (size_t)c * stride + Koff[v];
+  const double *yv = y + ((size_t)v * n + i0) * D;
+  const int items = K * D;
+  for (int it = tid; it < items + K; it += 256) {
+    if (it < items) {
+      const int j = it / D, d = it - (it / D) * D;
+      const int m0 = off[j], m1 = off[j + 1];
+      double acc = 0.0;
+      int m = m0;
+      for (; m + 8 <= m1; m += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = yv[(size_t)list[m + u] * D + d];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + x[u];
+      }
+      for (; m < m1; ++m) acc = acc + yv[(size_t)list[m] * D + d];
+      part1[(base + j) * D + d] = acc;
+    } else {
+      const int j = it - items;
+      double acc = 0.0;
+      for (int m = off[j]; m < off[j + 1]; ++m) acc = acc + Y2[(size_t)v * n + i0 + list[m]];
+      part2[base + j] = acc;
     }
-    if (do_y2)
-      for (int j = tid; j < K; j += 256) part2[base + j] = acc2[j];
-    __syncthreads();
   }
 }
 
@@ -888,6 +1020,34 @@ __device__ double block_tree64(const BlockCtx &ctx, int64_t n, F leaf) {
   return r;
 }
 
+// In-place exclusive SUFFIX scan of a[0..len) by the whole block:
+// a[m] <- sum_{s > m} a[s].  Integer, so any order gives the same result.
+__device__ void block_suffix_exclusive(int32_t *a, int len) {
+  __shared__ int sc[256];
+  __shared__ int carry;
+  const int tid = threadIdx.x;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int top = len - 1; top >= 0; top -= 256) {
+    const int m = top - tid;              // descending within the chunk
+    const int x = m >= 0 ? a[m] : 0;
+    sc[tid] = x;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      const int t = tid >= off ? sc[tid - off] : 0;
+      __syncthreads();
+      sc[tid] += t;
+      __syncthreads();
+    }
+    const int incl = sc[tid];
+    const int c0 = carry;
+    __syncthreads();
+    if (m >= 0) a[m] = c0 + incl - x;
+    if (tid == 255) carry = c0 + incl;
+    __syncthreads();
+  }
+}
+
 struct MHArgs {
   ParState P;
   int32_t *status;        // [V+3]: T, K[V], err, NB  -> we add T_ne at status[V+3]
@@ -946,10 +1106,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
     __syncthreads();
     for (int p = tid; p < T; p += 256) atomicAdd(&A.histT[P.n_t[p]], 1);
     __syncthreads();
-    if (tid == 0) {   // suffix counts, exclusive: c_m = sum_{s > m} hist[s]
-      int run = 0;
-      for (int m = maxn; m >= 0; --m) { const int h = A.histT[m]; A.histT[m] = run; run += h; }
-    }
+    block_suffix_exclusive(A.histT, maxn + 1);   // c_m = sum_{s > m} hist[s]
     for (int v = 0; v < V; ++v) {
       int *hl = A.histL + (size_t)v * (TC + 2);
       for (int m = tid; m < TC + 2; m += 256) hl[m] = 0;
@@ -961,17 +1118,19 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       for (int j = tid; j < P.Kact[v]; j += 256) atomicAdd(&hl[P.d_l[v * KC + j]], 1);
     }
     __syncthreads();
-    if (tid == 0) {
-      for (int v = 0; v < V; ++v) {
-        int *hl = A.histL + (size_t)v * (TC + 2);
-        int run = 0, mx = 0;
-        for (int j = 0; j < P.Kact[v]; ++j) mx = max(mx, P.d_l[v * KC + j]);
-        for (int m = mx; m >= 0; --m) { const int h = hl[m]; hl[m] = run; run += h; }
-        hl[TC + 1] = mx;   // stash max l
-        maxl_loc = max(maxl_loc, mx);
-      }
+    for (int v = 0; v < V; ++v) {
+      int *hl = A.histL + (size_t)v * (TC + 2);
+      int mx = 0;
+      for (int j = tid; j < P.Kact[v]; j += 256) mx = max(mx, P.d_l[v * KC + j]);
+      for (int m = 32; m >= 1; m >>= 1) mx = max(mx, __shfl_xor(mx, m, 64));
+      if ((tid & 63) == 0) s_i[2 + (tid >> 6)] = mx;
+      __syncthreads();
+      mx = max(max(s_i[2], s_i[3]), max(s_i[4], s_i[5]));
+      __syncthreads();
+      block_suffix_exclusive(hl, mx + 1);
+      if (tid == 0) hl[TC + 1] = mx;   // stash max l
+      __syncthreads();
     }
-    __syncthreads();
     (void)maxl_loc;
 
     uint32_t kdraw = 0;
@@ -1350,13 +1509,8 @@ class ParallelSampler : public Sampler {
     }
     int Kmax = 1;
     for (int k : c.K) Kmax = std::max(Kmax, k);
-    // LDS: acc[K][dg] + acc2[K] + ysub[64][dg] + y2sub[64] + jsub[64]
-    const size_t budget = 96 * 1024;
-    const size_t fixed = sizeof(double) * Kmax + sizeof(double) * 64 + sizeof(int) * 64;
-    if (fixed >= budget) throw Error(MVC_ERR_UNSUPPORTED, "too many dishes for the stats kernel");
-    int dg = (int)((budget - fixed) / (sizeof(double) * (Kmax + 64)));
-    dg = std::max(1, std::min({dg, D, 256}));
-    const size_t lds = sizeof(double) * ((size_t)Kmax * dg + Kmax + 64 * dg + 64) + sizeof(int) * 64;
+    const size_t lds = sizeof(int) * (2 * 4096 + (size_t)Kmax + 1);
+    const int dg = 0;
     hipEvent_t ev = nullptr;
     timers.begin("stats", &ev);
     hipLaunchKernelGGL(mvc_par_stats_partial_kernel, dim3(nchunk, V), dim3(256), lds, stream, c.P, (const double *)y,
@@ -1436,8 +1590,11 @@ class ParallelSampler : public Sampler {
     // MFMA path when the view width allows it
     int Kmax = 0;
     for (int k : c.K) Kmax = std::max(Kmax, k);
-    const size_t mfma_lds = 4 * ((size_t)sumK(c) * 16 + (size_t)V * 16) * sizeof(double);
-    const bool use_mfma = !force_generic && D % 4 == 0 && D >= 16 && Kmax <= 255 && mfma_lds <= 160 * 1024;
+    const int sk = sumK(c);
+    const size_t mfma_lds = ((size_t)c.T * 8 + (size_t)c.T * 4 + (size_t)V * c.T * 4 + (size_t)sk * 32 + 64) +
+                            4 * ((size_t)sk * 16 + (size_t)V * 16) * sizeof(double);
+    const bool use_mfma = !force_generic && D % 4 == 0 && D >= 16 && Kmax <= 255 && c.T <= MVC_MFMA_TMAX &&
+                          mfma_lds <= 160 * 1024;
     timers.begin("zresample", &e0);
     if (use_mfma) {
       const int ntile = (n + 15) / 16;
@@ -1451,7 +1608,7 @@ class ParallelSampler : public Sampler {
     last_path_mfma = use_mfma;
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
-    hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n,
+    hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, n, c.T,
                        (const int32_t *)c.choice, c.cnt, c.flags);
     MVC_HIP(hipGetLastError());
     size_t bytes = cub_bytes;
