@@ -300,6 +300,8 @@ void mvc_sampler_reset_timers(mvc_sampler *s) {
   if (s && s->impl) s->impl->timers.reset();
 }
 
+int mvc_sampler_zpath(mvc_sampler *s) { return (s && s->impl) ? s->impl->zpath : -1; }
+
 void *mvc_sampler_stream(mvc_sampler *s) { return (s && s->impl) ? (void *)s->impl->stream : nullptr; }
 
 void mvc_sampler_destroy(mvc_sampler *s) { delete s; }

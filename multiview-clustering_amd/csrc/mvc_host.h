@@ -63,6 +63,7 @@ class Sampler {
                          const double *hyper) = 0;
   mvc_config cfg;
   int sweeps_done = 0;
+  int zpath = -1;                        // mvc_sampler_zpath
   hipStream_t stream = nullptr;
   Timers timers;
 };

@@ -82,45 +82,114 @@ __device__ __forceinline__ double shfl_xor_d(double x, int m) {
 __device__ __forceinline__ double shfl_d(double x, int src) {
   return __shfl(x, src, 64);
 }
+// Cross-lane moves for fp64 values, gfx950 (no LDS traffic):
+//   down<h>(x), h = 1,2,4,8 : DPP row_shl:h, lane l receives lane l+h of its
+//                             16-lane row (0 past the row end);
+//   down16(x) / down32(x)   : v_permlane16_swap / v_permlane32_swap, lane l
+//                             receives lane l+16 (even rows) / l+32 (l < 32).
+// The reductions below are prefix trees: after the step with offset h only
+// lanes l < h hold tree values, which is all the tree64 association needs
+// (node l at offset h = lane l + lane l+h, oracle butterfly64()); the root
+// is read back with v_readlane.  Callers keep the whole wave converged.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int H>
+__device__ __forceinline__ double down_d(double x) {
+  static_assert(H == 1 || H == 2 || H == 4 || H == 8, "row shift");
+  return dpp_d<0x100 + H>(x);
+}
+__device__ __forceinline__ double down16_d(double x) {
+  const long long b = __double_as_longlong(x);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __longlong_as_double(((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+__device__ __forceinline__ double down32_d(double x) {
+  const long long b = __double_as_longlong(x);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+  return __longlong_as_double(((long long)hi[1] << 32) | (unsigned)lo[1]);
+}
+// broadcast lane 0 of each 16-lane row to the row (DPP row_newbcast:0)
+__device__ __forceinline__ double row_bcast0_d(double x) { return dpp_d<0x150>(x); }
+// wave-uniform read of lane `l` (l wave-uniform)
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ int readlane_i(int x, int l) { return __builtin_amdgcn_readlane(x, l); }
+
+__device__ __forceinline__ double dmax(double a, double b) { return b > a ? b : a; }
+
 __device__ __forceinline__ double wave_max(double x) {
-  for (int m = 32; m >= 1; m >>= 1) {
-    const double o = shfl_xor_d(x, m);
-    x = o > x ? o : x;
-  }
-  return x;
+  x = dmax(x, down32_d(x));
+  x = dmax(x, down16_d(x));
+  x = dmax(x, down_d<8>(x));
+  x = dmax(x, down_d<4>(x));
+  x = dmax(x, down_d<2>(x));
+  x = dmax(x, down_d<1>(x));
+  return readlane_d(x, 0);
 }
-// tree64 butterfly over the 64 lanes (slot = lane); every lane gets the sum.
-// Identical association to butterfly64() in oracle/mvc_oracle.cpp: at offset
-// h lane l adds lane l^h, i.e. pairs (l, l+h) for l < h.
+// max over each 16-lane row, broadcast to the row
+__device__ __forceinline__ double row16_max(double x) {
+  x = dmax(x, down_d<8>(x));
+  x = dmax(x, down_d<4>(x));
+  x = dmax(x, down_d<2>(x));
+  x = dmax(x, down_d<1>(x));
+  return row_bcast0_d(x);
+}
+// tree64 over the 64 lanes (slot = lane); returns the root, wave-uniform.
+// Same association as butterfly64() in oracle/mvc_oracle.cpp: at offset h
+// node l = node l + node l+h.
 __device__ __forceinline__ double wave_tree_sum(double x) {
-  for (int m = 32; m >= 1; m >>= 1) x = x + shfl_xor_d(x, m);
-  return x;
+  x = x + down32_d(x);
+  x = x + down16_d(x);
+  x = x + down_d<8>(x);
+  x = x + down_d<4>(x);
+  x = x + down_d<2>(x);
+  x = x + down_d<1>(x);
+  return readlane_d(x, 0);
 }
-// Same butterfly, keeping the value each lane holds after every step; used
-// for the descent.  In the oracle's notation lvl[5] = v32, lvl[4] = v16,
-// lvl[3] = v8, lvl[2] = v4, lvl[1] = v2, lvl[0] = v1 (root), lvl[6] = leaves.
+// tree16 over each row's 16 lanes (tree64 of a chunk whose upper 48 slots
+// were already folded in by the caller), root broadcast to the row.
+__device__ __forceinline__ double row16_tree_sum(double x) {
+  x = x + down_d<8>(x);
+  x = x + down_d<4>(x);
+  x = x + down_d<2>(x);
+  x = x + down_d<1>(x);
+  return row_bcast0_d(x);
+}
+// Same tree, keeping the node values of every level for the descent.  In
+// the oracle's notation lvl[5] = v32, lvl[4] = v16, ..., lvl[1] = v2,
+// lvl[0] = root (returned), lvl[6] = leaves; node l of lvl[k] sits in lane l.
 struct Tree64Levels {
-  double v32, v16, v8, v4, v2, v1;   // value after the step with that offset
+  double v32, v16, v8, v4, v2;
 };
 __device__ __forceinline__ double wave_tree_sum_levels(double x, Tree64Levels &L) {
-  x = x + shfl_xor_d(x, 32); L.v32 = x;
-  x = x + shfl_xor_d(x, 16); L.v16 = x;
-  x = x + shfl_xor_d(x, 8);  L.v8 = x;
-  x = x + shfl_xor_d(x, 4);  L.v4 = x;
-  x = x + shfl_xor_d(x, 2);  L.v2 = x;
-  x = x + shfl_xor_d(x, 1);  L.v1 = x;
-  return x;
+  x = x + down32_d(x);   L.v32 = x;
+  x = x + down16_d(x);   L.v16 = x;
+  x = x + down_d<8>(x);  L.v8 = x;
+  x = x + down_d<4>(x);  L.v4 = x;
+  x = x + down_d<2>(x);  L.v2 = x;
+  x = x + down_d<1>(x);
+  return readlane_d(x, 0);
 }
-// Descent (oracle Tree64::select_chunk).  lvl[k][l] (2^k entries) equals the
-// value lane l holds after the step with offset 2^k, for l < 2^k; leaves are
-// the inputs (level 6).  Wave-uniform r; returns the selected slot.
+// Descent (oracle Tree64::select_chunk) on wave-uniform values: node l at
+// offset h has children lvl[k+1][l] and lvl[k+1][l+h]; go right unless the
+// right child is 0 or r < left.  Returns the slot; r is updated.
 __device__ __forceinline__ int wave_tree_select(const Tree64Levels &L, double leaf, double &r) {
   int l = 0;
-  // node at level kk (h = 2^kk) has children lvl[kk+1][l] and lvl[kk+1][l+h]
 #define MVC_DESCEND(VAL, H)                                   \
   {                                                           \
-    const double a = __shfl((VAL), l, 64);                    \
-    const double b = __shfl((VAL), l + (H), 64);              \
+    const double a = readlane_d((VAL), l);                    \
+    const double b = readlane_d((VAL), l + (H));              \
     if (!(b == 0.0 || r < a)) { r = r - a; l = l + (H); }     \
   }
   MVC_DESCEND(L.v2, 1)

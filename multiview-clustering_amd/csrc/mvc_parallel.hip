@@ -55,6 +55,9 @@ struct Sweep {
   int32_t *btab;          // [NB] phase-2 table of each birth
   const int32_t *nbirth;  // [1]
   const int32_t *status;  // [V+4]; status[V+3] = tables with n_t > 0
+  const double *yt;       // MFMA A-fragment layout of y (mvc_par_ytile_kernel)
+  const double *S1t;      // MFMA B-fragment layout of S1 (mvc_par_s1tile_kernel)
+  int32_t SP;             // k-steps per view in yt/S1t (D/4 rounded up to MVC_Z_KS)
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
@@ -593,6 +596,458 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_mfma_kernel(
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// ---------------------------------------------------------------------------
+// zresample, block-lockstep MFMA path.  Conditions: D % 4 ==
+// 0, D >= 16, every K_v <= 64, T <= 128, V <= 8.
+//
+// A block of MVC_Z_NW wavefronts walks MVC_Z_NW tiles of 16 customers at a
+// time, all waves in step over (view, k-chunk).  Per chunk of MVC_Z_KS
+// k-steps (4 dims each):
+//   * the S1 B-fragments of the chunk (S1t, <= 16 KB) are staged into a
+//     double-buffered LDS slot shared by the block -- loaded from L2 one
+//     chunk ahead, so every wave reads B from LDS;
+//   * each wave's A-fragments (yt: one 512-byte coalesced row of 64 lanes per
+//     k-step) are prefetched one chunk ahead into registers, so the HBM
+//     stream of y has a chunk of MFMA work to hide behind;
+//   * G += A * B with v_mfma_f64_16x16x4_f64 (k-ordered fma chain = the
+//     spec's fma_dot), accumulators in registers across the view's chunks.
+// After a view's last chunk the wave evaluates the view's mixture in the MFMA
+// C layout (lane = 16 * row-group + dish column, rows grp + 4r), the self-dish
+// coefficients once per row, and adds the view's lp of each table's dish into
+// per-lane table scores (lane = table slot).  After the last view the table
+// draw runs per customer on those scores (DPP trees, readlane descent).
+// Bitwise identical to the generic path (tests/test_gpu_parity.py).
+// ---------------------------------------------------------------------------
+#define MVC_Z_NW 8            // wavefronts per block
+#define MVC_Z_KS 8            // k-steps per staged chunk
+#define MVC_Z_LS 80           // lp row stride (doubles): odd multiple of 16
+#define MVC_Z_TMAX 128
+#define MVC_Z_KMAX 64
+#define MVC_Z_VMAX 8
+#define MVC_Z_BUFD (MVC_Z_KS * 4 * 64)   // doubles per S1 chunk buffer
+
+__host__ __device__ inline size_t z_shared_bytes(int T, int V, int sumK) {
+  return 8 * ((size_t)2 * T + 3 * (size_t)sumK + 2 * MVC_Z_BUFD +
+              (size_t)MVC_Z_NW * (16 * MVC_Z_LS + 4 * 16 + 16 * MVC_Z_VMAX)) +
+         4 * ((size_t)T + (size_t)V * T + 2 * (size_t)sumK + 2 * (size_t)V + (size_t)MVC_Z_NW * 16) + 64;
+}
+
+// A-fragment layout: yt[((v*ntile + tile)*SP + s)*64 + lane] = y[v][16 tile +
+// (lane & 15)][4 s + (lane >> 4)], zero outside n x D.
+extern "C" __global__ void mvc_par_ytile_kernel(int n, int V, int D, int SP, const double *y, double *yt) {
+  const int ntile = (n + 15) >> 4;
+  const size_t total = (size_t)V * ntile * SP * 64;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
+    const int ln = (int)(e & 63);
+    const size_t q = e >> 6;
+    const int s = (int)(q % SP);
+    const size_t vt = q / SP;
+    const int tile = (int)(vt % ntile);
+    const int v = (int)(vt / ntile);
+    const int row = tile * 16 + (ln & 15), d = 4 * s + (ln >> 4);
+    yt[e] = (row < n && d < D) ? y[((size_t)v * n + row) * D + d] : 0.0;
+  }
+}
+
+// B-fragment layout per view (ncolt_v = ceil(K_v / 16) column tiles):
+// S1t[S1o_v + (s * ncolt_v + ct) * 64 + lane] = S1[v][d = 4 s + (lane >> 4)]
+// [j = 16 ct + (lane & 15)], zero outside D x K_v; S1o_v = SP*64*sum_{u<v}
+// ncolt_u.
+extern "C" __global__ void mvc_par_s1tile_kernel(ParState P, const int32_t *Koff, int SP, double *S1t) {
+  const int V = P.V, D = P.D, KC = P.KC;
+  size_t off[MVC_Z_VMAX + 1];
+  off[0] = 0;
+  for (int v = 0; v < V; ++v) off[v + 1] = off[v] + (size_t)SP * 64 * ((Koff[v + 1] - Koff[v] + 15) >> 4);
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < off[V]; e += (size_t)gridDim.x * blockDim.x) {
+    int v = 0;
+    while (e >= off[v + 1]) ++v;
+    const int K = Koff[v + 1] - Koff[v];
+    const int nct = (K + 15) >> 4;
+    const size_t loc = e - off[v];
+    const int ln = (int)(loc & 63);
+    const size_t q = loc >> 6;
+    const int ct = (int)(q % nct), s = (int)(q / nct);
+    const int d = 4 * s + (ln >> 4), j = 16 * ct + (ln & 15);
+    S1t[e] = (d < D && j < K) ? P.S1T[((size_t)v * D + d) * KC + j] : 0.0;
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void z_mfma_chunk(const double (&a)[MVC_Z_KS], const double *__restrict__ buf,
+                                             mvc_d4 (&acc)[4]) {
+#pragma unroll
+  for (int s = 0; s < MVC_Z_KS; ++s) {
+    double b[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) b[t] = buf[(s * NT + t) * 64];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[t], acc[t], 0, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+typedef double mvc_d2 __attribute__((ext_vector_type(2)));
+struct ZStage {
+  mvc_d2 st[2];          // this thread's share of the next S1 chunk
+  double an[MVC_Z_KS];    // next chunk's A fragments
+  int pz;                 // z of row (lane & 15) of the next tile
+  double y2[2];           // Y2[grp + 4q][row] of the next tile
+};
+struct ZGeom { int per_it, nCC, ntile, SP, n, V, nblk, blk, w, tid, lane, col, grp; };
+
+// issue the global loads of flat chunk X (tile iteration, view, k-chunk)
+__device__ __forceinline__ void z_issue(const Sweep &A, const ZGeom &g, const int *s_nct, const int *s_S1o, int X,
+                                        ZStage &o) {
+  const int it = X / g.per_it;
+  const int rem = X - it * g.per_it;
+  const int v = rem / g.nCC, cc = rem - v * g.nCC;
+  const int tile = min((it * g.nblk + g.blk) * MVC_Z_NW + g.w, g.ntile - 1);
+  const int nct = s_nct[v];
+  const mvc_d2 *src = (const mvc_d2 *)(A.S1t + ((size_t)s_S1o[v] + (size_t)cc * MVC_Z_KS * nct) * 64);
+  const int units = MVC_Z_KS * nct * 32;
+  // unconditional loads (clamped to the chunk) keep the stage in registers
+  o.st[0] = src[min(g.tid, units - 1)];
+  o.st[1] = src[min(g.tid + MVC_Z_NW * 64, units - 1)];
+  const double *ap = A.yt + (((size_t)v * g.ntile + tile) * g.SP + (size_t)cc * MVC_Z_KS) * 64 + g.lane;
+#pragma unroll
+  for (int s = 0; s < MVC_Z_KS; ++s) o.an[s] = ap[s * 64];
+  if (rem == 0) {   // first chunk of a tile: its customers' z and Y2
+    const int i = min(tile * 16 + g.col, g.n - 1);
+    o.pz = A.P.z[i];
+    o.y2[0] = (g.grp < g.V) ? A.Y2[(size_t)g.grp * g.n + i] : 0.0;
+    o.y2[1] = (g.grp + 4 < g.V) ? A.Y2[(size_t)(g.grp + 4) * g.n + i] : 0.0;
+  }
+}
+// write the staged S1 chunk X into its LDS buffer; block barrier
+__device__ __forceinline__ void z_commit(const ZGeom &g, const int *s_nct, double *sbuf, int X, const ZStage &o) {
+  const int it = X / g.per_it;
+  const int rem = X - it * g.per_it;
+  const int v = rem / g.nCC;
+  const int units = MVC_Z_KS * s_nct[v] * 32;
+  mvc_d2 *dst = (mvc_d2 *)(sbuf + (X & 1) * MVC_Z_BUFD);
+  if (g.tid < units) dst[g.tid] = o.st[0];
+  if (g.tid + MVC_Z_NW * 64 < units) dst[g.tid + MVC_Z_NW * 64] = o.st[1];
+  __syncthreads();
+}
+
+template <int QT>
+__device__ __forceinline__ void z_kernel_body(const Sweep &A, char *smem) {
+  const ParState &P = A.P;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int V = P.V, D = P.D, TC = P.TC, KC = P.KC, n = P.n;
+  const int T = A.T;
+  const int SP = A.SP;
+  const int sumK = A.Koff[V];
+  const int ntile = (n + 15) >> 4;
+  // ---- LDS carve (doubles first)
+  double *dp = (double *)smem;
+  double *sbuf = dp; dp += 2 * MVC_Z_BUFD;   // first: 16-byte aligned (double2)
+  double *t_b0 = dp; dp += T;            // base score of table p (p != p0)
+  double *t_b1 = dp; dp += T;            // base score of table p when p == p0
+  double *d_c0 = dp; dp += sumK;
+  double *d_cb = dp; dp += sumK;
+  double *d_Q = dp; dp += sumK;
+  double *wbase = dp + (size_t)w * (16 * MVC_Z_LS + 4 * 16 + 16 * MVC_Z_VMAX);
+  dp += (size_t)MVC_Z_NW * (16 * MVC_Z_LS + 4 * 16 + 16 * MVC_Z_VMAX);
+  double *lpv = wbase;                   // [16][LS] lp of the current view
+  double *selfG = lpv + 16 * MVC_Z_LS;   // [16]
+  double *selfv = selfG + 16;            // [16]
+  double *rowS = selfv + 16;             // [16]
+  double *rowM = rowS + 16;              // [16]
+  double *y2s = rowM + 16;               // [VMAX][16] Y2 of the tile's rows
+  int *ip = (int *)dp;
+  int *t_n = ip; ip += T;
+  int *t_dish = ip; ip += V * T;
+  int *d_n = ip; ip += sumK;
+  int *d_l = ip; ip += sumK;
+  int *s_nct = ip; ip += V;
+  int *s_S1o = ip; ip += V;              // in units of 64 doubles
+  int *zs = ip + w * 16;                 // [16] z of the tile's rows
+
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  for (int p = tid; p < T; p += blockDim.x) {
+    const int np = P.n_t[p];
+    t_n[p] = np;
+    t_b0[p] = (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
+    const double m1 = (double)(np - 1) - sg;
+    t_b1[p] = (np - 1 >= 1 && m1 > 0.0) ? mvc_log(m1) : -MVC_PM_INF;
+    for (int v = 0; v < V; ++v) t_dish[v * T + p] = P.dish[v * TC + p];
+  }
+  for (int k = tid; k < sumK; k += blockDim.x) {
+    int v = 0;
+    while (v + 1 < V && A.Koff[v + 1] <= k) ++v;
+    const int j = k - A.Koff[v];
+    d_c0[k] = P.c0[v * KC + j];
+    d_cb[k] = P.cb[v * KC + j];
+    d_Q[k] = P.Q[v * KC + j];
+    d_n[k] = P.d_n[v * KC + j];
+    d_l[k] = P.d_l[v * KC + j];
+  }
+  if (tid == 0) {
+    int o = 0;
+    for (int v = 0; v < V; ++v) {
+      const int nct = (A.Koff[v + 1] - A.Koff[v] + 15) >> 4;
+      s_nct[v] = nct;
+      s_S1o[v] = o;
+      o += SP * nct;
+    }
+  }
+  __syncthreads();
+
+  const int T_ne = A.status[V + 3];
+  const double snewA = mvc_log(ag + sg * (double)T_ne);
+  const double snewD = mvc_log(ag + sg * (double)(T_ne - 1));
+  const int nCC = SP / MVC_Z_KS;
+  const int per_it = V * nCC;
+  const int stride_t = gridDim.x * MVC_Z_NW;
+  const int nIt = (ntile - (int)blockIdx.x * MVC_Z_NW + stride_t - 1) / stride_t;
+  const int nX = nIt > 0 ? nIt * per_it : 0;
+  if (nX == 0) return;
+
+  // ---- pipeline registers
+  double a[MVC_Z_KS];
+  ZStage stg;
+  stg.pz = 0;
+  stg.y2[0] = stg.y2[1] = 0.0;
+  const ZGeom geo{per_it, nCC, ntile, SP, n, V, (int)gridDim.x, (int)blockIdx.x, w, tid, lane, col, grp};
+  // ---- per-tile state
+  int i0 = 0, i_row = 0, p0_row = 0;     // row = lane & 15
+  bool alive_row = false, tile_active = false;
+  double u_row = 0.0, snew_acc = 0.0;
+  double sc[16][QT];
+  // ---- per-view state
+  mvc_d4 acc[4];
+
+  z_issue(A, geo, s_nct, s_S1o, 0, stg);
+  z_commit(geo, s_nct, sbuf, 0, stg);
+#pragma unroll
+  for (int s = 0; s < MVC_Z_KS; ++s) a[s] = stg.an[s];
+
+  for (int X = 0; X < nX; ++X) {
+    const int it = X / per_it;
+    const int rem = X - it * per_it;
+    const int v = rem / nCC, cc = rem - v * nCC;
+    const int K = A.Koff[v + 1] - A.Koff[v];
+    const int koff = A.Koff[v];
+    const int NT = s_nct[v];
+    if (rem == 0) {
+      // ---- tile setup (z, Y2 arrived with the chunk-0 prefetch)
+      const int tile = (it * (int)gridDim.x + (int)blockIdx.x) * MVC_Z_NW + w;
+      tile_active = tile < ntile;
+      i0 = min(tile, ntile - 1) * 16;
+      i_row = i0 + col;
+      if (grp == 0) zs[col] = stg.pz;
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        if (grp + 4 * q < V) y2s[(grp + 4 * q) * 16 + col] = stg.y2[q];
+      wave_lds_sync();
+      p0_row = stg.pz;
+      alive_row = (t_n[p0_row] - 1) > 0;
+      u_row = mvc_uniform(A.seed, (uint32_t)i_row, A.sweep, A.chain, MVC_TAG_Z);
+      snew_acc = alive_row ? snewA : snewD;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int p0c = zs[c];
+#pragma unroll
+        for (int q = 0; q < QT; ++q) {
+          const int p = q * 64 + lane;
+          sc[c][q] = p < T ? (p == p0c ? t_b1[p] : t_b0[p]) : -MVC_PM_INF;
+        }
+      }
+    }
+    if (cc == 0) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+    }
+    if (X + 1 < nX) z_issue(A, geo, s_nct, s_S1o, X + 1, stg);
+    const double *bufl = sbuf + (X & 1) * MVC_Z_BUFD + lane;
+    switch (NT) {
+      case 1: z_mfma_chunk<1>(a, bufl, acc); break;
+      case 2: z_mfma_chunk<2>(a, bufl, acc); break;
+      case 3: z_mfma_chunk<3>(a, bufl, acc); break;
+      default: z_mfma_chunk<4>(a, bufl, acc); break;
+    }
+    if (cc == nCC - 1) {
+      // ================= view epilogue =================
+      const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+      const double L2pt = A.L2pt[v], cnew = A.cnew[v];
+      double hy[4], hr[4];
+      int j0[4];
+      bool alr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double y2r = y2s[v * 16 + grp + 4 * r];
+        hy[r] = 0.5 * y2r;
+        hr[r] = (-0.5 * y2r) / tau;
+        const int p0 = zs[grp + 4 * r];
+        j0[r] = t_dish[v * T + p0];
+        alr[r] = (t_n[p0] - 1) > 0;
+      }
+      // self dish: G of (row, j0) to LDS (coefficients once per row below)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int jt = j0[r] >> 4;
+        double g = acc[0][r];
+        if (jt == 1) g = acc[1][r];
+        if (jt == 2) g = acc[2][r];
+        if (jt == 3) g = acc[3][r];
+        if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
+      }
+      // acc -> lp in place (frozen-dish coefficients)
+      int lj[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = 16 * t + col;
+        const int k = koff + min(j, K - 1);
+        const double c0j = d_c0[k], cbj = d_cb[k];
+        lj[t] = j < K ? d_l[k] : 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[t][r] = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+      }
+      wave_lds_sync();
+      {
+        const double G = selfG[col];
+        const double y2 = y2s[v * 16 + col];
+        const int k0 = koff + t_dish[v * T + p0_row];
+        const double Gp = G - y2;
+        const double Qp = (d_Q[k0] - 2.0 * G) + y2;
+        const Coef cf = coef(d_n[k0] - 1, Qp, tau, L2pt, D);
+        const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
+        if (lane < 16) selfv[col] = sv;
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = grp + 4 * r;
+        const double svr = selfv[row];
+        const int l0 = d_l[koff + j0[r]];
+        const int l0p = alr[r] ? l0 : l0 - 1;
+        double mx = -MVC_PM_INF;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = 16 * t + col;
+          const bool self = (j == j0[r]);
+          if (self) acc[t][r] = svr;
+          const int l = self ? l0p : lj[t];
+          if (j < K && l > 0) mx = dmax(mx, acc[t][r]);
+        }
+        double m = row16_max(mx);
+        const double lfn = cnew + hr[r];
+        if (lfn > m) m = lfn;
+        const int Kact_i = K - ((l0p == 0) ? 1 : 0);
+        double wn = alpha + (double)Kact_i * sigma;
+        if (wn < 0.0) wn = 0.0;
+        const double xnew = wn * mvc_exp(lfn - m);
+        double x[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = 16 * t + col;
+          const int l = (j == j0[r]) ? l0p : lj[t];
+          const bool ok = j < K && l > 0;
+          double ww = (double)l - sigma;
+          if (ww < 0.0) ww = 0.0;
+          const double ex = mvc_exp(ok ? acc[t][r] - m : 0.0);
+          x[t] = ok ? ww * ex : (j == K ? xnew : 0.0);
+        }
+        const double S0 = row16_tree_sum((x[0] + x[2]) + (x[1] + x[3]));
+        const double S = (K == 64) ? S0 + xnew : S0;
+        if (col == 0) { rowS[row] = S; rowM[row] = m; }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const int j = 16 * t + col;
+          if (j < K) lpv[row * MVC_Z_LS + j] = acc[t][r];
+        }
+      }
+      wave_lds_sync();
+      {   // lane-parallel per-row marginal (row = lane & 15)
+        const double S = rowS[col], m = rowM[col];
+        const double y2 = y2s[v * 16 + col];
+        const double lfn = cnew + (-0.5 * y2) / tau;
+        const double denom = alpha + (double)(P.Ltot[v] - (alive_row ? 0 : 1));
+        const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
+        snew_acc = snew_acc + lm;
+      }
+      // table scores: lane = table slot
+#pragma unroll
+      for (int q = 0; q < QT; ++q) {
+        const int p = q * 64 + lane;
+        const int dj = p < T ? t_dish[v * T + p] : 0;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) sc[c][q] = sc[c][q] + lpv[c * MVC_Z_LS + dj];
+      }
+      if (v == V - 1) {
+        // ================= table draw =================
+        const int nct = (T + 63) >> 6;
+        wave_lds_sync();   // rowS/rowM of the marginal step are consumed
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const double snc = readlane_d(snew_acc, c);
+          double M = -MVC_PM_INF;
+#pragma unroll
+          for (int q = 0; q < QT; ++q) M = dmax(M, sc[c][q]);
+          M = wave_max(M);
+          if (!(M > snc)) M = snc;
+          double B = 0.0;
+#pragma unroll
+          for (int q = 0; q < QT; ++q) {
+            const double lf = sc[c][q] != -MVC_PM_INF ? mvc_exp(sc[c][q] - M) : 0.0;
+            sc[c][q] = lf;
+            if (q < nct) {
+              const double cs = wave_tree_sum(lf);
+              B = (q == 0) ? cs : B + cs;
+            }
+          }
+          if (lane == 0) { rowM[c] = M; rowS[c] = B; }
+        }
+        wave_lds_sync();
+        const double Mc = rowM[col], Bc = rowS[col];
+        const double W = mvc_exp(snew_acc - Mc) + Bc;
+        const double rr_row = u_row * W;
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          double rr = readlane_d(rr_row, c);
+          const double Bu = readlane_d(Bc, c);
+          int pick = -1;
+          if (rr < Bu) {
+            int cq = 0;
+            if (QT > 1 && nct > 1) {
+              // two-chunk partial tree: node values p0 = part[0], p1 = part[1]
+              const double p0s = wave_tree_sum(sc[c][0]);
+              const double p1s = wave_tree_sum(sc[c][QT - 1]);
+              if (!(p1s == 0.0 || rr < p0s)) { rr = rr - p0s; cq = 1; }
+            }
+            Tree64Levels Lv;
+            const double leaf = (cq == 0) ? sc[c][0] : sc[c][QT - 1];
+            wave_tree_sum_levels(leaf, Lv);
+            pick = cq * 64 + wave_tree_select(Lv, leaf, rr);
+          }
+          if (lane == 0 && tile_active && i0 + c < n) A.choice[i0 + c] = pick;
+        }
+      }
+    }
+    if (X + 1 < nX) {
+      z_commit(geo, s_nct, sbuf, X + 1, stg);
+#pragma unroll
+      for (int s = 0; s < MVC_Z_KS; ++s) a[s] = stg.an[s];
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(MVC_Z_NW * 64) void mvc_par_zresample_z1_kernel(Sweep A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  z_kernel_body<1>(A, smem);
+}
+extern "C" __global__ __launch_bounds__(MVC_Z_NW * 64) void mvc_par_zresample_z2_kernel(Sweep A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  z_kernel_body<2>(A, smem);
 }
 
 // Phase 2: births resolved sequentially in ascending
@@ -1306,6 +1761,8 @@ class ParallelSampler : public Sampler {
  public:
   int n, V, D, TC, KC, nchunk;
   double *y = nullptr, *Y2 = nullptr;
+  double *yt = nullptr;            // MFMA A-fragment layout of y (z-kernel)
+  int SP = 0;                      // k-steps per view in yt / S1t (0: no MFMA path)
   struct Chain {
     ParState P{};
     double *L2pt = nullptr, *cnew = nullptr;
@@ -1317,6 +1774,8 @@ class ParallelSampler : public Sampler {
     int32_t *lcnt = nullptr, *jmap = nullptr, *histT = nullptr, *histL = nullptr;
     double *mh_scratch = nullptr;
     size_t mh_half = 0;
+    double *S1t = nullptr;         // MFMA B-fragment layout of S1 (K_v <= 64)
+    bool s1t_ok = false;
     int T = 0;
     std::vector<int32_t> K;
     uint32_t gid = 0;
@@ -1331,6 +1790,8 @@ class ParallelSampler : public Sampler {
   size_t cub_bytes = 0;
   std::vector<int32_t> st_host;
   bool force_generic = false;
+  bool force_mfma1 = false;
+  int n_cu = 256;
   bool last_path_mfma = false;
 
   template <class Tp>
@@ -1357,6 +1818,13 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipMemcpyAsync(y, yh.data(), sizeof(double) * yh.size(), hipMemcpyHostToDevice, stream));
     hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
     MVC_HIP(hipGetLastError());
+    if (D % 4 == 0 && D >= 16 && V <= MVC_Z_VMAX) {
+      SP = ((D / 4 + MVC_Z_KS - 1) / MVC_Z_KS) * MVC_Z_KS;
+      const size_t ntile = ((size_t)n + 15) / 16;
+      yt = dmalloc<double>((size_t)V * ntile * SP * 64);
+      hipLaunchKernelGGL(mvc_par_ytile_kernel, dim3(4096), dim3(256), 0, stream, n, V, D, SP, (const double *)y, yt);
+      MVC_HIP(hipGetLastError());
+    }
     // hipcub temp storage (scan + select over n)
     size_t b1 = 0, b2 = 0;
     MVC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (int32_t *)nullptr, (int32_t *)nullptr, n, stream));
@@ -1368,7 +1836,18 @@ class ParallelSampler : public Sampler {
     st_host.assign(V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
+    const char *f1 = getenv("MVC_FORCE_MFMA1");
+    force_mfma1 = f1 && f1[0] == '1';
+    {
+      hipDeviceProp_t prop;
+      MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
+      n_cu = std::max(1, prop.multiProcessorCount);
+    }
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_mfma_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_z1_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_z2_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_stats_partial_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1381,7 +1860,7 @@ class ParallelSampler : public Sampler {
     if (stream) hipStreamSynchronize(stream);
     for (auto &c : chains)
       for (void *p : c.owned) hipFree(p);
-    for (void *p : {(void *)y, (void *)Y2, (void *)lp_scratch, (void *)part1, (void *)part2, cub_tmp})
+    for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)part1, (void *)part2, cub_tmp})
       if (p) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -1521,6 +2000,14 @@ class ParallelSampler : public Sampler {
                        0, stream, c.P, (const int32_t *)c.Koff, (int)part_cap, nchunk, (const double *)part1,
                        (const double *)part2);
     MVC_HIP(hipGetLastError());
+    c.s1t_ok = false;
+    if (SP > 0 && Kmax <= MVC_Z_KMAX) {
+      if (!c.S1t) c.S1t = own<double>(c, (size_t)V * SP * 4 * 64);
+      hipLaunchKernelGGL(mvc_par_s1tile_kernel, dim3(256), dim3(256), 0, stream, c.P, (const int32_t *)c.Koff, SP,
+                         c.S1t);
+      MVC_HIP(hipGetLastError());
+      c.s1t_ok = true;
+    }
     timers.end("stats", ev);
   }
 
@@ -1574,6 +2061,9 @@ class ParallelSampler : public Sampler {
     A.btab = c.btab;
     A.nbirth = c.nbirth;
     A.status = c.status;
+    A.yt = yt;
+    A.S1t = c.S1t;
+    A.SP = SP;
     A.T = c.T;
     A.sumK = (int32_t)lp_cap;
     A.seed = cfg.seed;
@@ -1588,15 +2078,26 @@ class ParallelSampler : public Sampler {
     Sweep A = make_sweep(c, s);
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     // MFMA path when the view width allows it
-    int Kmax = 0;
-    for (int k : c.K) Kmax = std::max(Kmax, k);
+    int Kmax = 0, Kmin = 1 << 30;
+    for (int k : c.K) { Kmax = std::max(Kmax, k); Kmin = std::min(Kmin, k); }
     const int sk = sumK(c);
     const size_t mfma_lds = ((size_t)c.T * 8 + (size_t)c.T * 4 + (size_t)V * c.T * 4 + (size_t)sk * 32 + 64) +
                             4 * ((size_t)sk * 16 + (size_t)V * 16) * sizeof(double);
     const bool use_mfma = !force_generic && D % 4 == 0 && D >= 16 && Kmax <= 255 && c.T <= MVC_MFMA_TMAX &&
                           mfma_lds <= 160 * 1024;
+    const size_t z_lds = z_shared_bytes(c.T, V, sk);
+    const bool use_z = !force_generic && !force_mfma1 && c.s1t_ok && Kmin >= 1 && Kmax <= MVC_Z_KMAX && c.T <= MVC_Z_TMAX &&
+                       z_lds <= 160 * 1024;
     timers.begin("zresample", &e0);
-    if (use_mfma) {
+    if (use_z) {
+      // one block of MVC_Z_NW waves per CU
+      const int ntile = (n + 15) / 16;
+      const int grid = std::max(1, std::min(n_cu, (ntile + MVC_Z_NW - 1) / MVC_Z_NW));
+      if (c.T <= 64)
+        hipLaunchKernelGGL(mvc_par_zresample_z1_kernel, dim3(grid), dim3(MVC_Z_NW * 64), z_lds, stream, A);
+      else
+        hipLaunchKernelGGL(mvc_par_zresample_z2_kernel, dim3(grid), dim3(MVC_Z_NW * 64), z_lds, stream, A);
+    } else if (use_mfma) {
       const int ntile = (n + 15) / 16;
       hipLaunchKernelGGL(mvc_par_zresample_mfma_kernel, dim3(std::min(2048, (ntile + 3) / 4)), dim3(256), mfma_lds,
                          stream, A);
@@ -1605,7 +2106,8 @@ class ParallelSampler : public Sampler {
     }
     MVC_HIP(hipGetLastError());
     timers.end("zresample", e0);
-    last_path_mfma = use_mfma;
+    last_path_mfma = use_mfma || use_z;
+    zpath = use_z ? 2 : (use_mfma ? 1 : 0);
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
     hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, n, c.T,

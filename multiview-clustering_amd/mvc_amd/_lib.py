@@ -87,6 +87,7 @@ def lib():
         "mvc_sampler_set_state": (i32, [vp, i32, ip, ctypes.c_int32, ip, dp, cp, sz]),
         "mvc_sampler_kernel_time": (i32, [vp, cp, dp, lp]),
         "mvc_sampler_reset_timers": (None, [vp]),
+        "mvc_sampler_zpath": (i32, [vp]),
         "mvc_sampler_stream": (vp, [vp]),
         "mvc_sampler_destroy": (None, [vp]),
         "mvc_device_math": (i32, [i32, i32, dp, dp, i64, cp, sz]),

@@ -199,6 +199,11 @@ class Sampler:
             raise L.MvcError(st, "kernel_time failed")
         return ms.value, cnt.value
 
+    def zpath(self):
+        """z-resample kernel of the last parallel sweep (0 generic, 1 per-wave
+        MFMA, 2 block-lockstep MFMA; -1 exact schedule / no sweep yet)."""
+        return int(self._lib.mvc_sampler_zpath(self._h))
+
     def reset_timers(self):
         self._lib.mvc_sampler_reset_timers(self._h)
 

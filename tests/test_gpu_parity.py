@@ -235,22 +235,59 @@ def test_parallel_warm_start(D):
     s.close()
 
 
+def _run_path(m, y, st, seed, sweeps, path, monkeypatch):
+    """Run `sweeps` warm-started sweeps forcing z-path 0/1/2; check the path."""
+    monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
+    monkeypatch.setenv("MVC_FORCE_MFMA1", "1" if path == 1 else "0")
+    s = m.Sampler(y, seed=seed, mode="parallel")
+    s.set_state(*st)
+    states = []
+    for it in range(sweeps):
+        s.sweep(1)
+        if it == 0:          # later sweeps may leave the path's limits (births)
+            assert s.zpath() == path
+        states.append(s.state())
+    s.close()
+    return states
+
+
 def test_mfma_and_generic_paths_identical(monkeypatch):
     m = _mvc()
     from mvc_amd import data
     V, K, D = 3, 8, 32
     y, z = data.synthetic(2000, V, D, K, seed=5)
     st = _warm_state(z, V, K)
-    out = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("MVC_FORCE_GENERIC", flag)
-        s = m.Sampler(y, seed=9, mode="parallel")
-        s.set_state(*st)
-        s.sweep(3)
-        out.append(s.state())
-        s.close()
-    assert np.array_equal(out[0][0], out[1][0])
-    assert np.array_equal(out[0][1], out[1][1])
+    out = [_run_path(m, y, st, 9, 3, p, monkeypatch) for p in (0, 1, 2)]
+    for a in out[1:]:
+        for sa, sb in zip(out[0], a):
+            assert np.array_equal(sa[0], sb[0])
+            assert np.array_equal(sa[1], sb[1])
+            assert np.array_equal(sa[2]["tau_v"], sb[2]["tau_v"])
+
+
+# block-lockstep MFMA kernel (path 2): ragged tiles (n % 16 != 0), fewer tiles
+# than waves, D not a multiple of 32 (zero-padded k-steps), T in (64, 128]
+# (two table chunks), K_v of 64 (new-dish leaf in the second chunk)
+@pytest.mark.parametrize("n,V,D,K,T", [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96),
+                                       (2500, 2, 128, 64, 64)])
+def test_zpath2_vs_oracle(n, V, D, K, T, monkeypatch):
+    m = _mvc()
+    from mvc_amd import data
+    y, z = data.synthetic(n, V, D, T, seed=n + D)
+    uniq, table_of = np.unique(z, return_inverse=True)   # generating partition
+    table_of = table_of.astype(np.int32)
+    T = uniq.size
+    dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
+    hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
+    st = (table_of, dish, hyper)
+    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch)
+    ref = O.run(y, 3, 0, 1, seed=31, mode=O.PARALLEL, state=st)
+    for it in range(3):
+        t, d, h = gpu[it]
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+        assert np.array_equal(h["tau_v"], ref["tau_v"][:, it]), it
+        assert h["sigma_global"] == ref["sigma_global"][it]
 
 
 def test_exact_warm_start():
