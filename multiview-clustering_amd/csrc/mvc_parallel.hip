@@ -205,433 +205,38 @@ __device__ __forceinline__ int view_select(const Sweep &A, int v, int p0, bool a
   return c * 64 + l;
 }
 
-// table score s_p (or -inf if excluded) for customer with own table p0;
-// lp of view v dish j is lp[(Koff[v] + j) * stride]
-__device__ __forceinline__ double table_score(const Sweep &A, int p, int p0, double sg, const double *lp,
-                                             int stride) {
-  const ParState &P = A.P;
-  const int np = P.n_t[p] - (p == p0 ? 1 : 0);
-  if (np < 1) return -MVC_PM_INF;
-  const double mass = (double)np - sg;
-  if (mass <= 0.0) return -MVC_PM_INF;
-  double sp = (p == p0) ? mvc_log(mass) : P.lmass[p];
-  for (int v = 0; v < P.V; ++v) sp = sp + lp[(size_t)(A.Koff[v] + P.dish[v * P.TC + p]) * stride];
-  return sp;
-}
-
-// Table draw of one customer (wave-uniform), DESIGN.md §4.3: lane = table
-// slot, tree64 over the table leaves, birth iff r >= B.  Returns the
-// position or -1.
-__device__ __forceinline__ int choose_table(const Sweep &A, int i, int p0, double s_new, const double *lp,
-                                            int stride) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int T = A.T;
-  const double sg = P.hyper[3 * P.V + 1];
-  double M = s_new;
-  for (int base = 0; base < T; base += 64) {
-    const int p = base + lane;
-    if (p < T) {
-      const double sp = table_score(A, p, p0, sg, lp, stride);
-      if (sp > M) M = sp;
-    }
-  }
-  M = wave_max(M);
-  const int nc = (T + 63) >> 6;
-  double part = 0.0;
-  for (int c = 0; c < nc; ++c) {
-    const int p = c * 64 + lane;
-    double leaf = 0.0;
-    if (p < T) {
-      const double sp = table_score(A, p, p0, sg, lp, stride);
-      if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
-    }
-    const double cs = wave_tree_sum(leaf);
-    if (lane == c) part = cs;
-  }
-  double B;
-  if (nc == 0) B = 0.0;
-  else if (nc == 1) B = __shfl(part, 0, 64);
-  else B = wave_tree_sum(lane < nc ? part : 0.0);
-  const double e_new = mvc_exp(s_new - M);
-  const double W = e_new + B;
-  double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-  if (!(r < B)) return -1;
-  int c = 0;
-  if (nc > 1) {
-    Tree64Levels L;
-    const double pv = lane < nc ? part : 0.0;
-    wave_tree_sum_levels(pv, L);
-    c = wave_tree_select(L, pv, r);
-  }
-  const int p = c * 64 + lane;
-  double leaf = 0.0;
-  if (p < T) {
-    const double sp = table_score(A, p, p0, sg, lp, stride);
-    if (sp != -MVC_PM_INF) leaf = mvc_exp(sp - M);
-  }
-  Tree64Levels L2;
-  wave_tree_sum_levels(leaf, L2);
-  return c * 64 + wave_tree_select(L2, leaf, r);
-}
-
-__device__ __forceinline__ double grp16_max(double x) {
-  for (int m = 8; m >= 1; m >>= 1) {
-    const double o = __shfl_xor(x, m, 64);
-    x = o > x ? o : x;
-  }
-  return x;
-}
-
 }  // namespace
 
-// ---------------------------------------------------------------------------
-// zresample, generic path (any D): one wavefront per customer, grid-stride.
-// ---------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_kernel(Sweep A) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int nw = (gridDim.x * blockDim.x) >> 6;
-  double *lpall = A.scratch + (size_t)wid * A.sumK;
-  const int V = P.V;
-  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
-  const int T_ne = A.status[V + 3];
-  for (int i = wid; i < P.n; i += nw) {
-    const int p0 = P.z[i];
-    const bool alive = (P.n_t[p0] - 1) > 0;
-    double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
-    for (int v = 0; v < V; ++v) {
-      const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v]);
-      s_new = s_new + o.lmarg;
-    }
-    const int pick = choose_table(A, i, p0, s_new, lpall, 1);
-    if (lane == 0) A.choice[i] = pick;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// zresample, MFMA path (D % 4 == 0, D >= 16, every K_v <= 255, T <= 256).
-// One wavefront per tile of 16 customers; 4 wavefronts per block.
-//   * table descriptors (log mass, size, per-view lp row index) and dish
-//     descriptors (c0, cb, Q, n, l) of the frozen state are staged in LDS once
-//     per block;
-//   * G = Y_tile * S1^T with v_mfma_f64_16x16x4_f64 (a k-ordered fma chain,
-//     bitwise equal to the spec's fma_dot);
-//   * the per-view mixture is evaluated in the MFMA C layout (lane = 16 *
-//     row-group + dish column, 4 customers per lane): the tree64 butterfly
-//     over dish slot e = 16 t + col is in-register for offsets 32 and 16 and
-//     xor-8/4/2/1 shuffles inside each 16-lane group;
-//   * lp of every (customer, dish) goes to per-wave LDS; the table draw then
-//     runs per customer with lane = table slot, keeping scores and the tree
-//     levels in registers (one pass, no recomputation).
-// Bitwise identical to the generic path (tests/test_gpu_parity.py).
-// ---------------------------------------------------------------------------
 typedef double mvc_d4 __attribute__((ext_vector_type(4)));
 
-#define MVC_MFMA_TMAX 256
-
-struct MfmaLds {          // carve of the dynamic LDS
-  double *t_lmass;        // [T]
-  int *t_n;               // [T]
-  int *t_idx;             // [V*T]  Koff[v] + dish[v][p]
-  double *d_c0, *d_cb, *d_Q;   // [sumK]
-  int *d_n, *d_l;         // [sumK]
-  double *lpw, *lmw;      // per wave
-};
-
-__device__ __forceinline__ size_t mfma_shared_bytes(int T, int V, int sumK) {
-  return (size_t)T * 8 + (size_t)T * 4 + (size_t)V * T * 4 + (size_t)sumK * (3 * 8 + 2 * 4) + 64;
-}
-
-extern "C" __global__ __launch_bounds__(256) void mvc_par_zresample_mfma_kernel(Sweep A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const ParState &P = A.P;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, w = tid >> 6;
-  const int col = lane & 15, grp = lane >> 4;
-  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
-  const int T = A.T;
-  const int sumK = A.Koff[V];
-  // ---- carve: doubles first (8-byte aligned), ints after
-  MfmaLds L;
-  {
-    double *dp = (double *)smem;
-    L.t_lmass = dp; dp += T;
-    L.d_c0 = dp; dp += sumK;
-    L.d_cb = dp; dp += sumK;
-    L.d_Q = dp; dp += sumK;
-    int *ip = (int *)dp;
-    L.t_n = ip; ip += T;
-    L.t_idx = ip; ip += V * T;
-    L.d_n = ip; ip += sumK;
-    L.d_l = ip; ip += sumK;
-    char *cp = (char *)(((uintptr_t)ip + 15) & ~(uintptr_t)15);
-    L.lpw = (double *)cp + (size_t)w * ((size_t)sumK * 16 + (size_t)V * 16);
-    L.lmw = L.lpw + (size_t)sumK * 16;
-  }
-  for (int p = tid; p < T; p += 256) {
-    L.t_lmass[p] = P.lmass[p];
-    L.t_n[p] = P.n_t[p];
-    for (int v = 0; v < V; ++v) L.t_idx[v * T + p] = A.Koff[v] + P.dish[v * TC + p];
-  }
-  for (int k = tid; k < sumK; k += 256) {
-    int v = 0;
-    while (v + 1 < V && A.Koff[v + 1] <= k) ++v;
-    const int j = k - A.Koff[v];
-    L.d_c0[k] = P.c0[v * KC + j];
-    L.d_cb[k] = P.cb[v * KC + j];
-    L.d_Q[k] = P.Q[v * KC + j];
-    L.d_n[k] = P.d_n[v * KC + j];
-    L.d_l[k] = P.d_l[v * KC + j];
-  }
-  __syncthreads();
-  double *lpw = L.lpw, *lmw = L.lmw;
-  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
-  const int T_ne = A.status[V + 3];
-  const int ntile = (n + 15) >> 4;
-  for (int tile = blockIdx.x * 4 + w; tile < ntile; tile += gridDim.x * 4) {
-    const int i0 = tile * 16;
-    int p0r[4];
-    bool alr[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = i0 + grp + 4 * r;
-      p0r[r] = i < n ? P.z[i] : 0;
-      alr[r] = i < n ? (L.t_n[p0r[r]] - 1) > 0 : true;
-    }
-    for (int v = 0; v < V; ++v) {
-      const int K = P.Kact[v];
-      const int koff = A.Koff[v];
-      const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-      const double L2pt = A.L2pt[v];
-      const double cnew = A.cnew[v];
-      double Y2r[4], mx[4];
-      int j0[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = i0 + grp + 4 * r;
-        Y2r[r] = i < n ? A.Y2[(size_t)v * n + i] : 0.0;
-        j0[r] = L.t_idx[v * T + p0r[r]] - koff;
-        mx[r] = -MVC_PM_INF;
-      }
-      const double *S1v = P.S1T + (size_t)v * D * KC;
-      const int arow = i0 + col;
-      const bool rowok = arow < n;
-      const double *yrow = A.y + ((size_t)v * n + (rowok ? arow : 0)) * D;
-      const int ng = (K + 63) >> 6;
-      for (int g = 0; g < ng; ++g) {
-        mvc_d4 acc[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
-        const int nt = min(4, (K - g * 64 + 15) >> 4);
-        int d = 0;
-        for (; d + 8 <= D; d += 8) {            // 2 k-steps per iteration
-          double a0 = rowok ? yrow[d + grp] : 0.0;
-          double a1 = rowok ? yrow[d + 4 + grp] : 0.0;
-          double b0[4], b1[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int j = g * 64 + t * 16 + col;
-            const bool ok = t < nt && j < K;
-            b0[t] = ok ? S1v[(size_t)(d + grp) * KC + j] : 0.0;
-            b1[t] = ok ? S1v[(size_t)(d + 4 + grp) * KC + j] : 0.0;
-          }
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            if (t < nt) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0[t], acc[t], 0, 0, 0);
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            if (t < nt) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1[t], acc[t], 0, 0, 0);
-        }
-        for (; d < D; d += 4) {
-          const double a = rowok ? yrow[d + grp] : 0.0;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            if (t >= nt) continue;
-            const int j = g * 64 + t * 16 + col;
-            const double b = j < K ? S1v[(size_t)(d + grp) * KC + j] : 0.0;
-            acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[t], 0, 0, 0);
-          }
-        }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = g * 64 + t * 16 + col;
-          if (t < nt && j < K) {
-            const int k = koff + j;
-            const int lj = L.d_l[k];
-            const double c0j = L.d_c0[k], cbj = L.d_cb[k];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const double G = acc[t][r];
-              const double hy = 0.5 * Y2r[r];
-              const double h = (-0.5 * Y2r[r]) / tau;
-              double val;
-              int l = lj;
-              if (j == j0[r]) {
-                if (!alr[r]) l -= 1;
-                const double Gp = G - Y2r[r];
-                const double Qp = (L.d_Q[k] - 2.0 * G) + Y2r[r];
-                const Coef c = coef(L.d_n[k] - 1, Qp, tau, L2pt, D);
-                val = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
-              } else {
-                val = __builtin_fma(G + hy, cbj, c0j) + h;
-              }
-              lpw[(size_t)k * 16 + grp + 4 * r] = val;
-              if (l > 0 && val > mx[r]) mx[r] = val;
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      const int nc = (K + 1 + 63) >> 6;
-#pragma unroll 1
-      for (int r = 0; r < 4; ++r) {
-        const int row = grp + 4 * r;
-        const double h = (-0.5 * Y2r[r]) / tau;
-        const double lfn = cnew + h;
-        const int l0 = L.d_l[koff + j0[r]];
-        const int l0p = alr[r] ? l0 : l0 - 1;
-        double m = grp16_max(mx[r]);
-        if (lfn > m) m = lfn;
-        const int Kact_i = K - ((l0p == 0) ? 1 : 0);
-        double wn = alpha + (double)Kact_i * sigma;
-        if (wn < 0.0) wn = 0.0;
-        double part[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int g = 0; g < nc; ++g) {
-          double x[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int e = g * 64 + t * 16 + col;
-            double leaf = 0.0;
-            if (e < K) {
-              const int l = (e == j0[r]) ? l0p : L.d_l[koff + e];
-              if (l > 0) {
-                double ww = (double)l - sigma;
-                if (ww < 0.0) ww = 0.0;
-                leaf = ww * mvc_exp(lpw[(size_t)(koff + e) * 16 + row] - m);
-              }
-            } else if (e == K) {
-              leaf = wn * mvc_exp(lfn - m);
-            }
-            x[t] = leaf;
-          }
-          double s0 = (x[0] + x[2]) + (x[1] + x[3]);   // offsets 32, 16
-          s0 = s0 + __shfl_xor(s0, 8, 64);             // offsets 8, 4, 2, 1
-          s0 = s0 + __shfl_xor(s0, 4, 64);
-          s0 = s0 + __shfl_xor(s0, 2, 64);
-          s0 = s0 + __shfl_xor(s0, 1, 64);
-          if (g == 0) part[0] = s0;
-          else if (g == 1) part[1] = s0;
-          else if (g == 2) part[2] = s0;
-          else part[3] = s0;
-        }
-        const double S = (nc == 1) ? part[0] : (part[0] + part[2]) + (part[1] + part[3]);
-        const double denom = alpha + (double)(P.Ltot[v] - (alr[r] ? 0 : 1));
-        const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
-        if (col == 0) lmw[v * 16 + row] = lm;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    // ---- table draw per customer: lane = table slot, one pass (T <= 256)
-    const int nct = (T + 63) >> 6;
-    for (int c = 0; c < 16; ++c) {
-      const int i = i0 + c;
-      if (i >= n) break;
-      const int p0 = P.z[i];
-      const bool alive = (L.t_n[p0] - 1) > 0;
-      double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
-      for (int v = 0; v < V; ++v) s_new = s_new + lmw[v * 16 + c];
-      double sc[4];
-      double M = s_new;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int p = q * 64 + lane;
-        double sp = -MVC_PM_INF;
-        if (q < nct && p < T) {
-          const int np = L.t_n[p] - (p == p0 ? 1 : 0);
-          const double mass = (double)np - sg;
-          if (np >= 1 && mass > 0.0) {
-            sp = (p == p0) ? mvc_log(mass) : L.t_lmass[p];
-            for (int v = 0; v < V; ++v) sp = sp + lpw[(size_t)L.t_idx[v * T + p] * 16 + c];
-          }
-        }
-        sc[q] = sp;
-        if (sp > M) M = sp;
-      }
-      M = wave_max(M);
-      double leafq[4], part = 0.0;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        leafq[q] = (q < nct && sc[q] != -MVC_PM_INF) ? mvc_exp(sc[q] - M) : 0.0;
-        if (q < nct) {
-          const double cs = wave_tree_sum(leafq[q]);
-          if (lane == q) part = cs;
-        }
-      }
-      double B;
-      if (nct == 0) B = 0.0;
-      else if (nct == 1) B = __shfl(part, 0, 64);
-      else B = wave_tree_sum(lane < nct ? part : 0.0);
-      const double W = mvc_exp(s_new - M) + B;
-      double rr = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-      int pick = -1;
-      if (rr < B) {
-        int cq = 0;
-        if (nct > 1) {
-          Tree64Levels Lv;
-          const double pv = lane < nct ? part : 0.0;
-          wave_tree_sum_levels(pv, Lv);
-          cq = wave_tree_select(Lv, pv, rr);
-        }
-        const double leaf = cq == 0 ? leafq[0] : (cq == 1 ? leafq[1] : (cq == 2 ? leafq[2] : leafq[3]));
-        Tree64Levels L2;
-        wave_tree_sum_levels(leaf, L2);
-        pick = cq * 64 + wave_tree_select(L2, leaf, rr);
-      }
-      if (lane == 0) A.choice[i] = pick;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
 // ---------------------------------------------------------------------------
-// zresample, block-lockstep MFMA path.  Conditions: D % 4 ==
-// 0, D >= 16, every K_v <= 64, T <= 128, V <= 8.
-//
-// A block of MVC_Z_NW wavefronts walks MVC_Z_NW tiles of 16 customers at a
-// time, all waves in step over (view, k-chunk).  Per chunk of MVC_Z_KS
-// k-steps (4 dims each):
-//   * the S1 B-fragments of the chunk (S1t, <= 16 KB) are staged into a
-//     double-buffered LDS slot shared by the block -- loaded from L2 one
-//     chunk ahead, so every wave reads B from LDS;
-//   * each wave's A-fragments (yt: one 512-byte coalesced row of 64 lanes per
-//     k-step) are prefetched one chunk ahead into registers, so the HBM
-//     stream of y has a chunk of MFMA work to hide behind;
-//   * G += A * B with v_mfma_f64_16x16x4_f64 (k-ordered fma chain = the
-//     spec's fma_dot), accumulators in registers across the view's chunks.
-// After a view's last chunk the wave evaluates the view's mixture in the MFMA
-// C layout (lane = 16 * row-group + dish column, rows grp + 4r), the self-dish
-// coefficients once per row, and adds the view's lp of each table's dish into
-// per-lane table scores (lane = table slot).  After the last view the table
-// draw runs per customer on those scores (DPP trees, readlane descent).
-// Bitwise identical to the generic path (tests/test_gpu_parity.py).
+// Phase 1 runs as two kernels per batch of customers:
+//   1. an lp producer writes lp[i][Koff[v] + j] (frozen dish j of view v,
+//      self-removal applied to the customer's own dish) into the lp buffer,
+//      slabs of 16 customers, dish-major:  lpb[(li >> 4) * sumK * 16 +
+//      k * 16 + (li & 15)],  li = i - b0;
+//        * MFMA producer (D % 4 == 0, D >= 16, K_v <= 64): G = Y S1^T tiles
+//          with v_mfma_f64_16x16x4_f64, S1 B-fragments staged through LDS by
+//          the block, y A-fragments streamed from the tiled copy yt;
+//        * generic producer (any D): one lane per customer, fma_dot loops;
+//   2. the draw kernel: one lane per customer, sequential reductions over
+//      dishes and tables (the spec of oracle eval_view_seq /
+//      resample_customer), no cross-lane traffic.
 // ---------------------------------------------------------------------------
-#define MVC_Z_NW 8            // wavefronts per block
-#define MVC_Z_KS 8            // k-steps per staged chunk
-#define MVC_Z_LS 80           // lp row stride (doubles): odd multiple of 16
-#define MVC_Z_TMAX 128
+#define MVC_Z_NW 8            // wavefronts per block of the MFMA producer
+#define MVC_Z_KS 4            // k-steps per staged S1 chunk
+#define MVC_Z_PF 4            // L2 warm-up distance (chunks past the register prefetch)
 #define MVC_Z_KMAX 64
 #define MVC_Z_VMAX 8
 #define MVC_Z_BUFD (MVC_Z_KS * 4 * 64)   // doubles per S1 chunk buffer
 
-__host__ __device__ inline size_t z_shared_bytes(int T, int V, int sumK) {
-  return 8 * ((size_t)2 * T + 3 * (size_t)sumK + 2 * MVC_Z_BUFD +
-              (size_t)MVC_Z_NW * (16 * MVC_Z_LS + 4 * 16 + 16 * MVC_Z_VMAX)) +
-         4 * ((size_t)T + (size_t)V * T + 2 * (size_t)sumK + 2 * (size_t)V + (size_t)MVC_Z_NW * 16) + 64;
+__host__ __device__ inline size_t lpb_index(int li, int k, int sumK) {
+  return ((size_t)(li >> 4) * (size_t)sumK + (size_t)k) * 16 + (size_t)(li & 15);
+}
+__host__ __device__ inline size_t zlp_shared_bytes(int V, int sumK, int T) {
+  return 8 * (2 * (size_t)MVC_Z_BUFD + 3 * (size_t)sumK + 2 * (size_t)V +
+              (size_t)MVC_Z_NW * (16 + 16 * (size_t)V + 16 * ((size_t)sumK + 1))) +
+         4 * ((size_t)sumK + 3 * (size_t)V + 1 + (size_t)V * T + (size_t)MVC_Z_NW * 16) + 64;
 }
 
 // A-fragment layout: yt[((v*ntile + tile)*SP + s)*64 + lane] = y[v][16 tile +
@@ -687,41 +292,68 @@ __device__ __forceinline__ void z_mfma_chunk(const double (&a)[MVC_Z_KS], const 
   }
 }
 
+// LDS hand-off between lanes of one wavefront: a wave's LDS instructions
+// execute in order, so only the compiler must not reorder across this point
+// (a memory fence here would also wait for every outstanding global load,
+// i.e. drain the y prefetch).
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  asm volatile("" ::: "memory");
   __builtin_amdgcn_wave_barrier();
+}
+// Block barrier for LDS hand-off only: waits for this wave's LDS ops, not
+// for its global loads in flight (__syncthreads would emit vmcnt(0)).
+__device__ __forceinline__ void block_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 typedef double mvc_d2 __attribute__((ext_vector_type(2)));
 struct ZStage {
-  mvc_d2 st[2];          // this thread's share of the next S1 chunk
+  mvc_d2 st;              // this thread's share (16 B) of the next S1 chunk
   double an[MVC_Z_KS];    // next chunk's A fragments
   int pz;                 // z of row (lane & 15) of the next tile
   double y2[2];           // Y2[grp + 4q][row] of the next tile
+  double pf;              // L2 warm-up load (consumed one chunk later)
 };
-struct ZGeom { int per_it, nCC, ntile, SP, n, V, nblk, blk, w, tid, lane, col, grp; };
+// tile0: first global 16-row tile of the batch; ntile: tiles in the batch
+struct ZGeom { int per_it, nCC, ntile, tile0, ntile_all, SP, n, V, nblk, blk, w, tid, lane, col, grp, nX; };
+
+__device__ __forceinline__ int z_tile(const ZGeom &g, int it) {
+  return min((it * g.nblk + g.blk) * MVC_Z_NW + g.w, g.ntile - 1);
+}
+__device__ __forceinline__ size_t z_aoff(const ZGeom &g, int X, int &rem) {
+  const int it = X / g.per_it;
+  rem = X - it * g.per_it;
+  const int v = rem / g.nCC, cc = rem - v * g.nCC;
+  const int tile = g.tile0 + z_tile(g, it);
+  return (((size_t)v * g.ntile_all + tile) * g.SP + (size_t)cc * MVC_Z_KS) * 64;
+}
 
 // issue the global loads of flat chunk X (tile iteration, view, k-chunk)
 __device__ __forceinline__ void z_issue(const Sweep &A, const ZGeom &g, const int *s_nct, const int *s_S1o, int X,
                                         ZStage &o) {
-  const int it = X / g.per_it;
-  const int rem = X - it * g.per_it;
+  int rem;
+  const size_t aoff = z_aoff(g, X, rem);
   const int v = rem / g.nCC, cc = rem - v * g.nCC;
-  const int tile = min((it * g.nblk + g.blk) * MVC_Z_NW + g.w, g.ntile - 1);
   const int nct = s_nct[v];
   const mvc_d2 *src = (const mvc_d2 *)(A.S1t + ((size_t)s_S1o[v] + (size_t)cc * MVC_Z_KS * nct) * 64);
-  const int units = MVC_Z_KS * nct * 32;
-  // unconditional loads (clamped to the chunk) keep the stage in registers
-  o.st[0] = src[min(g.tid, units - 1)];
-  o.st[1] = src[min(g.tid + MVC_Z_NW * 64, units - 1)];
-  const double *ap = A.yt + (((size_t)v * g.ntile + tile) * g.SP + (size_t)cc * MVC_Z_KS) * 64 + g.lane;
+  const int units = MVC_Z_KS * nct * 32;          // <= MVC_Z_NW * 64
+  o.st = src[min(g.tid, units - 1)];               // unconditional: stays in registers
+  const double *ap = A.yt + aoff + g.lane;
 #pragma unroll
   for (int s = 0; s < MVC_Z_KS; ++s) o.an[s] = ap[s * 64];
-  if (rem == 0) {   // first chunk of a tile: its customers' z and Y2
+  {   // one load per lane, 32 B apart, pulls chunk X + MVC_Z_PF (2 KB per wave) into L2
+    int rem2;
+    const size_t off2 = z_aoff(g, min(X + MVC_Z_PF, g.nX - 1), rem2);
+    o.pf = A.yt[off2 + (size_t)g.lane * 4];
+  }
+  {   // the tile's z and Y2, loaded on every chunk (a load count that
+      // depends on the path would make the compiler drain vmcnt)
+    const int it = X / g.per_it;
+    const int tile = g.tile0 + z_tile(g, it);
     const int i = min(tile * 16 + g.col, g.n - 1);
     o.pz = A.P.z[i];
-    o.y2[0] = (g.grp < g.V) ? A.Y2[(size_t)g.grp * g.n + i] : 0.0;
-    o.y2[1] = (g.grp + 4 < g.V) ? A.Y2[(size_t)(g.grp + 4) * g.n + i] : 0.0;
+    o.y2[0] = A.Y2[(size_t)min(g.grp, g.V - 1) * g.n + i];
+    o.y2[1] = A.Y2[(size_t)min(g.grp + 4, g.V - 1) * g.n + i];
   }
 }
 // write the staged S1 chunk X into its LDS buffer; block barrier
@@ -731,56 +363,195 @@ __device__ __forceinline__ void z_commit(const ZGeom &g, const int *s_nct, doubl
   const int v = rem / g.nCC;
   const int units = MVC_Z_KS * s_nct[v] * 32;
   mvc_d2 *dst = (mvc_d2 *)(sbuf + (X & 1) * MVC_Z_BUFD);
-  if (g.tid < units) dst[g.tid] = o.st[0];
-  if (g.tid + MVC_Z_NW * 64 < units) dst[g.tid + MVC_Z_NW * 64] = o.st[1];
-  __syncthreads();
+  if (g.tid < units) dst[g.tid] = o.st;
+  block_lds_sync();
 }
 
-template <int QT>
-__device__ __forceinline__ void z_kernel_body(const Sweep &A, char *smem) {
+// lp of one view's dishes for the wave's 16 customers: frozen-dish formula
+// from the accumulators (C layout: lane (grp, col) holds rows grp + 4r, dish
+// 16t + col), the own dish with the customer removed (coefficients once per
+// row), transposed through LDS (row stride MVC_Z_TS) and stored as one
+// contiguous K x 16 block of the customers' slab.
+// lp of one view's dishes for the wave's 16 customers into the wave's LDS
+// tile tl[row * (sumK + 1) + Koff[v] + j]: frozen-dish formula from the
+// accumulators (C layout: lane (grp, col) holds rows grp + 4r, dish 16t +
+// col), then the own dish with the customer removed (coefficients once per
+// row).  No global memory traffic here (see zlp_flush).
+template <int NT>
+__device__ __forceinline__ void zlp_store(const mvc_d4 (&acc)[4], const double *y2s, const int *zs, const int *t_dish,
+                                          int T, double tau, double L2pt, int D, int v, int K, int koff, int LSP,
+                                          int lane, int grp, int col, const double *d_c0, const double *d_cb,
+                                          const double *d_Q, const int *d_n, double *selfG, double *tl) {
+  double hy[4], hr[4];
+  int j0[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double y2r = y2s[v * 16 + grp + 4 * r];
+    hy[r] = 0.5 * y2r;
+    hr[r] = (-0.5 * y2r) / tau;
+    j0[r] = t_dish[v * T + zs[grp + 4 * r]];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {   // G of the own dish -> LDS
+    const int jt = j0[r] >> 4;
+    double g = acc[0][r];
+#pragma unroll
+    for (int t = 1; t < NT; ++t)
+      if (jt == t) g = acc[t][r];
+    if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int j = 16 * t + col;
+    const int k = koff + min(j, K - 1);
+    const double c0j = d_c0[k], cbj = d_cb[k];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (j < K) tl[(grp + 4 * r) * LSP + koff + j] = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+  }
+  wave_lds_sync();
+  {   // own dish, one row per lane (row = lane & 15)
+    const double G = selfG[col];
+    const double y2 = y2s[v * 16 + col];
+    const int jj = t_dish[v * T + zs[col]];
+    const int k0 = koff + jj;
+    const double Gp = G - y2;
+    const double Qp = (d_Q[k0] - 2.0 * G) + y2;
+    const Coef cf = coef(d_n[k0] - 1, Qp, tau, L2pt, D);
+    const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
+    if (lane < 16) tl[col * LSP + k0] = sv;
+  }
+  wave_lds_sync();
+}
+
+// the tile's lp (all views) to its slab: sumK x 16 doubles, contiguous
+__device__ __forceinline__ void zlp_flush(const double *tl, int LSP, int sumK, int li0, int lane, double *lpb,
+                                          bool active, int nb) {
+  if (!active) return;
+  if (li0 + 16 <= nb) {
+    double *dst = lpb + lpb_index(li0, 0, sumK);
+    for (int e = 2 * lane; e < 16 * sumK; e += 128) {
+      const int k = e >> 4, row = e & 15;
+      mvc_d2 val;
+      val.x = tl[row * LSP + k];
+      val.y = tl[(row + 1) * LSP + k];
+      *(mvc_d2 *)(dst + e) = val;
+    }
+  } else {
+    for (int e = lane; e < 16 * sumK; e += 64) {
+      const int k = e >> 4, row = e & 15;
+      if (li0 + row < nb) lpb[lpb_index(li0 + row, k, sumK)] = tl[row * LSP + k];
+    }
+  }
+  wave_lds_sync();
+}
+
+struct ZShared {           // LDS carve of the MFMA producer
+  double *sbuf;
+  const double *d_c0, *d_cb, *d_Q, *s_tau, *s_L2pt;
+  double *selfG, *y2s, *tl;
+  const int *d_n, *s_nct, *s_S1o, *t_dish, *s_koff;
+  int *zs;
+};
+struct ZLoop {             // per-wave state carried across chunks
+  mvc_d4 acc[4];
+  int li0;
+  bool active;
+  double pf_sink;
+};
+
+// one flat chunk X: tile setup, next chunk's loads (into nxt), MFMAs from cur,
+// view epilogue, staging of the next S1 chunk
+__device__ __forceinline__ void zlp_chunk(const Sweep &A, const ZGeom &g, const ZShared &Z, int X, ZStage &cur,
+                                          ZStage &nxt, ZLoop &L, double *lpb, int b0, int nb) {
+  const int it = X / g.per_it;
+  const int rem = X - it * g.per_it;
+  const int v = rem / g.nCC, cc = rem - v * g.nCC;
+  const int NT = Z.s_nct[v];
+  const int V = g.V;
+  if (rem == 0) {   // tile setup: z and Y2 arrived with this chunk's loads
+    const int tl_ = (it * g.nblk + g.blk) * MVC_Z_NW + g.w;
+    L.active = tl_ < g.ntile;
+    L.li0 = min(tl_, g.ntile - 1) * 16;
+    if (g.grp == 0) Z.zs[g.col] = cur.pz;
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      if (g.grp + 4 * q < V) Z.y2s[(g.grp + 4 * q) * 16 + g.col] = cur.y2[q];
+    wave_lds_sync();
+  }
+  if (cc == 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) L.acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+  }
+  L.pf_sink = L.pf_sink + cur.pf;   // that warm-up load has had a chunk to land
+  if (X + 1 < g.nX) z_issue(A, g, Z.s_nct, Z.s_S1o, X + 1, nxt);
+  const double *bufl = Z.sbuf + (X & 1) * MVC_Z_BUFD + g.lane;
+  switch (NT) {
+    case 1: z_mfma_chunk<1>(cur.an, bufl, L.acc); break;
+    case 2: z_mfma_chunk<2>(cur.an, bufl, L.acc); break;
+    case 3: z_mfma_chunk<3>(cur.an, bufl, L.acc); break;
+    default: z_mfma_chunk<4>(cur.an, bufl, L.acc); break;
+  }
+  if (cc == g.nCC - 1) {
+    const int K = Z.s_koff[v + 1] - Z.s_koff[v], koff = Z.s_koff[v];
+    const int sumK = Z.s_koff[V];
+    switch (NT) {
+#define MVC_ZLP(NTV) zlp_store<NTV>(L.acc, Z.y2s, Z.zs, Z.t_dish, A.T, Z.s_tau[v], Z.s_L2pt[v], A.P.D, v, K, koff, \
+                                    sumK + 1, g.lane, g.grp, g.col, Z.d_c0, Z.d_cb, Z.d_Q, Z.d_n, Z.selfG, Z.tl)
+      case 1: MVC_ZLP(1); break;
+      case 2: MVC_ZLP(2); break;
+      case 3: MVC_ZLP(3); break;
+      default: MVC_ZLP(4); break;
+#undef MVC_ZLP
+    }
+    if (v == V - 1) zlp_flush(Z.tl, sumK + 1, sumK, L.li0, g.lane, lpb, L.active, nb);
+  }
+  if (X + 1 < g.nX) z_commit(g, Z.s_nct, Z.sbuf, X + 1, nxt);
+}
+
+// MFMA lp producer.  A block of MVC_Z_NW waves walks MVC_Z_NW tiles of 16
+// customers at a time, all waves in step over (view, k-chunk); each chunk's
+// S1 B-fragments are staged once into double-buffered LDS for the block, each
+// wave's A-fragments are prefetched one chunk ahead into registers and
+// MVC_Z_PF chunks ahead into L2.
+extern "C" __global__ __launch_bounds__(MVC_Z_NW * 64) void mvc_par_lpmfma_kernel(Sweep A, int b0, int nb,
+                                                                                   double *lpb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6;
   const int col = lane & 15, grp = lane >> 4;
-  const int V = P.V, D = P.D, TC = P.TC, KC = P.KC, n = P.n;
-  const int T = A.T;
+  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
   const int SP = A.SP;
   const int sumK = A.Koff[V];
-  const int ntile = (n + 15) >> 4;
-  // ---- LDS carve (doubles first)
+  const int ntile = (nb + 15) >> 4;                 // tiles in this batch (b0 % 64 == 0)
   double *dp = (double *)smem;
-  double *sbuf = dp; dp += 2 * MVC_Z_BUFD;   // first: 16-byte aligned (double2)
-  double *t_b0 = dp; dp += T;            // base score of table p (p != p0)
-  double *t_b1 = dp; dp += T;            // base score of table p when p == p0
+  double *sbuf = dp; dp += 2 * MVC_Z_BUFD;          // first: 16-byte aligned
   double *d_c0 = dp; dp += sumK;
   double *d_cb = dp; dp += sumK;
   double *d_Q = dp; dp += sumK;
-  double *wbase = dp + (size_t)w * (16 * MVC_Z_LS + 4 * 16 + 16 * MVC_Z_VMAX);
-  dp += (size_t)MVC_Z_NW * (16 * MVC_Z_LS + 4 * 16 + 16 * MVC_Z_VMAX);
-  double *lpv = wbase;                   // [16][LS] lp of the current view
-  double *selfG = lpv + 16 * MVC_Z_LS;   // [16]
-  double *selfv = selfG + 16;            // [16]
-  double *rowS = selfv + 16;             // [16]
-  double *rowM = rowS + 16;              // [16]
-  double *y2s = rowM + 16;               // [VMAX][16] Y2 of the tile's rows
+  double *s_tau = dp; dp += V;
+  double *s_L2pt = dp; dp += V;
+  const size_t wst = 16 + 16 * (size_t)V + 16 * ((size_t)sumK + 1);
+  double *selfG = dp + (size_t)w * wst;             // [16]
+  double *y2s = selfG + 16;                         // [V][16]
+  double *tl = y2s + 16 * V;                        // [16][sumK + 1] the tile's lp
+  dp += (size_t)MVC_Z_NW * wst;
   int *ip = (int *)dp;
-  int *t_n = ip; ip += T;
-  int *t_dish = ip; ip += V * T;
   int *d_n = ip; ip += sumK;
-  int *d_l = ip; ip += sumK;
   int *s_nct = ip; ip += V;
-  int *s_S1o = ip; ip += V;              // in units of 64 doubles
-  int *zs = ip + w * 16;                 // [16] z of the tile's rows
-
-  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
-  for (int p = tid; p < T; p += blockDim.x) {
-    const int np = P.n_t[p];
-    t_n[p] = np;
-    t_b0[p] = (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
-    const double m1 = (double)(np - 1) - sg;
-    t_b1[p] = (np - 1 >= 1 && m1 > 0.0) ? mvc_log(m1) : -MVC_PM_INF;
-    for (int v = 0; v < V; ++v) t_dish[v * T + p] = P.dish[v * TC + p];
+  int *s_S1o = ip; ip += V;                         // in units of 64 doubles
+  int *t_dish = ip; ip += V * A.T;                  // [V][T] dish of each table
+  int *s_koff = ip; ip += V + 1;                    // Koff
+  int *zs = ip + w * 16;                            // [16]
+  if (tid <= V) s_koff[tid] = A.Koff[tid];
+  // everything the epilogue reads lives in LDS: a global load there would
+  // wait (vmcnt is in order) for the y prefetch issued just before it
+  for (int e = tid; e < V * A.T; e += blockDim.x) {
+    const int v = e / A.T, p = e - v * A.T;
+    t_dish[e] = P.dish[v * P.TC + p];
   }
+  if (tid < V) { s_tau[tid] = P.hyper[tid]; s_L2pt[tid] = A.L2pt[tid]; }
   for (int k = tid; k < sumK; k += blockDim.x) {
     int v = 0;
     while (v + 1 < V && A.Koff[v + 1] <= k) ++v;
@@ -789,7 +560,6 @@ __device__ __forceinline__ void z_kernel_body(const Sweep &A, char *smem) {
     d_cb[k] = P.cb[v * KC + j];
     d_Q[k] = P.Q[v * KC + j];
     d_n[k] = P.d_n[v * KC + j];
-    d_l[k] = P.d_l[v * KC + j];
   }
   if (tid == 0) {
     int o = 0;
@@ -801,10 +571,6 @@ __device__ __forceinline__ void z_kernel_body(const Sweep &A, char *smem) {
     }
   }
   __syncthreads();
-
-  const int T_ne = A.status[V + 3];
-  const double snewA = mvc_log(ag + sg * (double)T_ne);
-  const double snewD = mvc_log(ag + sg * (double)(T_ne - 1));
   const int nCC = SP / MVC_Z_KS;
   const int per_it = V * nCC;
   const int stride_t = gridDim.x * MVC_Z_NW;
@@ -812,242 +578,348 @@ __device__ __forceinline__ void z_kernel_body(const Sweep &A, char *smem) {
   const int nX = nIt > 0 ? nIt * per_it : 0;
   if (nX == 0) return;
 
-  // ---- pipeline registers
-  double a[MVC_Z_KS];
-  ZStage stg;
-  stg.pz = 0;
-  stg.y2[0] = stg.y2[1] = 0.0;
-  const ZGeom geo{per_it, nCC, ntile, SP, n, V, (int)gridDim.x, (int)blockIdx.x, w, tid, lane, col, grp};
-  // ---- per-tile state
-  int i0 = 0, i_row = 0, p0_row = 0;     // row = lane & 15
-  bool alive_row = false, tile_active = false;
-  double u_row = 0.0, snew_acc = 0.0;
-  double sc[16][QT];
-  // ---- per-view state
-  mvc_d4 acc[4];
+  const ZGeom geo{per_it, nCC, ntile, b0 >> 4, (n + 15) >> 4, SP, n, V, (int)gridDim.x, (int)blockIdx.x,
+                  w, tid, lane, col, grp, nX};
+  ZLoop L;
+  L.li0 = 0;
+  L.active = false;
+  L.pf_sink = 0.0;
+  ZStage s0, s1;
+  s0.pz = s1.pz = 0;
+  s0.y2[0] = s0.y2[1] = s1.y2[0] = s1.y2[1] = 0.0;
+  z_issue(A, geo, s_nct, s_S1o, 0, s0);
+  z_commit(geo, s_nct, sbuf, 0, s0);
+  const ZShared Z{sbuf, d_c0, d_cb, d_Q, s_tau, s_L2pt, selfG, y2s, tl, d_n, s_nct, s_S1o, t_dish, s_koff, zs};
+  // two stage register sets: chunk X computes from one while chunk X+1's
+  // loads land in the other (no register copy, so no early wait)
+  for (int X = 0; X < nX; X += 2) {
+    zlp_chunk(A, geo, Z, X, s0, s1, L, lpb, b0, nb);
+    if (X + 1 < nX) zlp_chunk(A, geo, Z, X + 1, s1, s0, L, lpb, b0, nb);
+  }
+  // keep the L2 warm-up loads alive (y is finite, so this never stores)
+  if (L.pf_sink != L.pf_sink) lpb[0] = 0.0;
+}
 
-  z_issue(A, geo, s_nct, s_S1o, 0, stg);
-  z_commit(geo, s_nct, sbuf, 0, stg);
-#pragma unroll
-  for (int s = 0; s < MVC_Z_KS; ++s) a[s] = stg.an[s];
+// MFMA lp producer, one launch per view.  The view's S1
+// B-fragments for every k-step (S1t block, <= 64 KB at D = 128) are staged
+// in LDS once per block; waves then run independently over their 16-customer
+// tiles, streaming the A-fragments (yt, 512 B per k-step per wave) through a
+// ring of MVC_ZR registers: each k-step waits for the oldest load only and
+// issues the load MVC_ZR k-steps ahead (across tile boundaries), so HBM
+// latency hides behind MVC_ZR k-steps of every wave on the CU.  The tile's lp
+// goes straight from the accumulators to the lp buffer (a fixed number of
+// stores per tile).
+#define MVC_ZR 8
+__host__ __device__ inline size_t lpview_shared_bytes(int SP, int NT, int K, int T) {
+  return 8 * ((size_t)SP * NT * 64 + 3 * (size_t)K + 8 * 32) + 4 * ((size_t)K + (size_t)T + 8 * 16) + 64;
+}
 
-  for (int X = 0; X < nX; ++X) {
-    const int it = X / per_it;
-    const int rem = X - it * per_it;
-    const int v = rem / nCC, cc = rem - v * nCC;
-    const int K = A.Koff[v + 1] - A.Koff[v];
-    const int koff = A.Koff[v];
-    const int NT = s_nct[v];
-    if (rem == 0) {
-      // ---- tile setup (z, Y2 arrived with the chunk-0 prefetch)
-      const int tile = (it * (int)gridDim.x + (int)blockIdx.x) * MVC_Z_NW + w;
-      tile_active = tile < ntile;
-      i0 = min(tile, ntile - 1) * 16;
-      i_row = i0 + col;
-      if (grp == 0) zs[col] = stg.pz;
+template <int NT>
+__global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int b0, int nb, double *lpb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int V = P.V, D = P.D, KC = P.KC, n = P.n, T = A.T;
+  const int SP = A.SP;
+  const int koff = A.Koff[v], K = A.Koff[v + 1] - koff, sumK = A.Koff[V];
+  const double tau = P.hyper[v], L2pt = A.L2pt[v];
+  double *Bs = (double *)smem;                     // [SP][NT][64]
+  double *d_c0 = Bs + (size_t)SP * NT * 64;        // [K]
+  double *d_cb = d_c0 + K;
+  double *d_Q = d_cb + K;
+  double *wsp = d_Q + K;                           // per wave: y2s[16], selfG[16]
+  double *y2s = wsp + w * 32;
+  double *selfG = y2s + 16;
+  int *ip = (int *)(wsp + 8 * 32);
+  int *d_n = ip;                                   // [K]
+  int *t_dish = d_n + K;                           // [T]
+  int *zs = t_dish + T + w * 16;                   // per wave [16]
+  {
+    size_t off = 0;
+    for (int u = 0; u < v; ++u) off += (size_t)SP * 64 * ((A.Koff[u + 1] - A.Koff[u] + 15) >> 4);
+    const mvc_d2 *src = (const mvc_d2 *)(A.S1t + off);
+    mvc_d2 *dst = (mvc_d2 *)Bs;
+    for (int e = tid; e < SP * NT * 32; e += blockDim.x) dst[e] = src[e];
+  }
+  for (int j = tid; j < K; j += blockDim.x) {
+    d_c0[j] = P.c0[v * KC + j];
+    d_cb[j] = P.cb[v * KC + j];
+    d_Q[j] = P.Q[v * KC + j];
+    d_n[j] = P.d_n[v * KC + j];
+  }
+  for (int p = tid; p < T; p += blockDim.x) t_dish[p] = P.dish[v * P.TC + p];
+  __syncthreads();
+
+  const int ntile = (nb + 15) >> 4;
+  const int ntile_all = (n + 15) >> 4;
+  const int tile0 = b0 >> 4;
+  const int gw = blockIdx.x * 8 + w, NWT = gridDim.x * 8;
+  if (gw >= ntile) return;                         // whole wave: no barriers below
+  const int nmy = (ntile - gw + NWT - 1) / NWT;    // tiles of this wave
+  const int nq = nmy * SP;                         // k-steps of this wave
+  const double *ybase = A.yt + (size_t)v * ntile_all * SP * 64 + lane;
+  auto aptr = [&](int q) -> const double * {       // A-fragment of flat k-step q (clamped)
+    q = min(q, nq - 1);
+    const int m = q / SP, s = q - m * SP;
+    return ybase + ((size_t)(tile0 + gw + m * NWT) * SP + s) * 64;
+  };
+  double ring[MVC_ZR];
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-        if (grp + 4 * q < V) y2s[(grp + 4 * q) * 16 + col] = stg.y2[q];
-      wave_lds_sync();
-      p0_row = stg.pz;
-      alive_row = (t_n[p0_row] - 1) > 0;
-      u_row = mvc_uniform(A.seed, (uint32_t)i_row, A.sweep, A.chain, MVC_TAG_Z);
-      snew_acc = alive_row ? snewA : snewD;
+  for (int u = 0; u < MVC_ZR; ++u) ring[u] = *aptr(u);
+  const double *Bl = Bs + lane;
+  for (int m = 0; m < nmy; ++m) {
+    const int tile = gw + m * NWT;                 // batch-local tile
+    const int li0 = tile * 16;
+    // this tile's z and Y2 (row = lane & 15); used in the epilogue
+    const int li_row = min(li0 + col, nb - 1);
+    const int pz = P.z[b0 + li_row];
+    const double y2 = A.Y2[(size_t)v * n + b0 + li_row];
+    mvc_d4 acc[4];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int p0c = zs[c];
+    for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+    const int qb = m * SP;
+    for (int s0 = 0; s0 < SP; s0 += MVC_ZR) {
 #pragma unroll
-        for (int q = 0; q < QT; ++q) {
-          const int p = q * 64 + lane;
-          sc[c][q] = p < T ? (p == p0c ? t_b1[p] : t_b0[p]) : -MVC_PM_INF;
-        }
+      for (int u = 0; u < MVC_ZR; ++u) {
+        const double a = ring[u];
+        ring[u] = *aptr(qb + s0 + u + MVC_ZR);     // refill: MVC_ZR k-steps ahead
+        const double *bk = Bl + (size_t)(s0 + u) * NT * 64;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bk[t * 64], acc[t], 0, 0, 0);
       }
     }
-    if (cc == 0) {
+    // ---- epilogue: lp of the tile's 16 customers for this view
+    if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
+    wave_lds_sync();
+    double hy[4], hr[4];
+    int j0[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < 4; ++r) {
+      const double y2r = y2s[grp + 4 * r];
+      hy[r] = 0.5 * y2r;
+      hr[r] = (-0.5 * y2r) / tau;
+      j0[r] = t_dish[zs[grp + 4 * r]];
     }
-    if (X + 1 < nX) z_issue(A, geo, s_nct, s_S1o, X + 1, stg);
-    const double *bufl = sbuf + (X & 1) * MVC_Z_BUFD + lane;
-    switch (NT) {
-      case 1: z_mfma_chunk<1>(a, bufl, acc); break;
-      case 2: z_mfma_chunk<2>(a, bufl, acc); break;
-      case 3: z_mfma_chunk<3>(a, bufl, acc); break;
-      default: z_mfma_chunk<4>(a, bufl, acc); break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // G of the own dish -> LDS
+      const int jt = j0[r] >> 4;
+      double g = acc[0][r];
+#pragma unroll
+      for (int t = 1; t < NT; ++t)
+        if (jt == t) g = acc[t][r];
+      if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
     }
-    if (cc == nCC - 1) {
-      // ================= view epilogue =================
-      const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-      const double L2pt = A.L2pt[v], cnew = A.cnew[v];
-      double hy[4], hr[4];
-      int j0[4];
-      bool alr[4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int j = 16 * t + col;
+      const int jc = min(j, K - 1);
+      const double c0j = d_c0[jc], cbj = d_cb[jc];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const double y2r = y2s[v * 16 + grp + 4 * r];
-        hy[r] = 0.5 * y2r;
-        hr[r] = (-0.5 * y2r) / tau;
-        const int p0 = zs[grp + 4 * r];
-        j0[r] = t_dish[v * T + p0];
-        alr[r] = (t_n[p0] - 1) > 0;
-      }
-      // self dish: G of (row, j0) to LDS (coefficients once per row below)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int jt = j0[r] >> 4;
-        double g = acc[0][r];
-        if (jt == 1) g = acc[1][r];
-        if (jt == 2) g = acc[2][r];
-        if (jt == 3) g = acc[3][r];
-        if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
-      }
-      // acc -> lp in place (frozen-dish coefficients)
-      int lj[4];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int j = 16 * t + col;
-        const int k = koff + min(j, K - 1);
-        const double c0j = d_c0[k], cbj = d_cb[k];
-        lj[t] = j < K ? d_l[k] : 0;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[t][r] = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
-      }
-      wave_lds_sync();
-      {
-        const double G = selfG[col];
-        const double y2 = y2s[v * 16 + col];
-        const int k0 = koff + t_dish[v * T + p0_row];
-        const double Gp = G - y2;
-        const double Qp = (d_Q[k0] - 2.0 * G) + y2;
-        const Coef cf = coef(d_n[k0] - 1, Qp, tau, L2pt, D);
-        const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
-        if (lane < 16) selfv[col] = sv;
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = grp + 4 * r;
-        const double svr = selfv[row];
-        const int l0 = d_l[koff + j0[r]];
-        const int l0p = alr[r] ? l0 : l0 - 1;
-        double mx = -MVC_PM_INF;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = 16 * t + col;
-          const bool self = (j == j0[r]);
-          if (self) acc[t][r] = svr;
-          const int l = self ? l0p : lj[t];
-          if (j < K && l > 0) mx = dmax(mx, acc[t][r]);
-        }
-        double m = row16_max(mx);
-        const double lfn = cnew + hr[r];
-        if (lfn > m) m = lfn;
-        const int Kact_i = K - ((l0p == 0) ? 1 : 0);
-        double wn = alpha + (double)Kact_i * sigma;
-        if (wn < 0.0) wn = 0.0;
-        const double xnew = wn * mvc_exp(lfn - m);
-        double x[4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = 16 * t + col;
-          const int l = (j == j0[r]) ? l0p : lj[t];
-          const bool ok = j < K && l > 0;
-          double ww = (double)l - sigma;
-          if (ww < 0.0) ww = 0.0;
-          const double ex = mvc_exp(ok ? acc[t][r] - m : 0.0);
-          x[t] = ok ? ww * ex : (j == K ? xnew : 0.0);
-        }
-        const double S0 = row16_tree_sum((x[0] + x[2]) + (x[1] + x[3]));
-        const double S = (K == 64) ? S0 + xnew : S0;
-        if (col == 0) { rowS[row] = S; rowM[row] = m; }
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const int j = 16 * t + col;
-          if (j < K) lpv[row * MVC_Z_LS + j] = acc[t][r];
-        }
-      }
-      wave_lds_sync();
-      {   // lane-parallel per-row marginal (row = lane & 15)
-        const double S = rowS[col], m = rowM[col];
-        const double y2 = y2s[v * 16 + col];
-        const double lfn = cnew + (-0.5 * y2) / tau;
-        const double denom = alpha + (double)(P.Ltot[v] - (alive_row ? 0 : 1));
-        const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
-        snew_acc = snew_acc + lm;
-      }
-      // table scores: lane = table slot
-#pragma unroll
-      for (int q = 0; q < QT; ++q) {
-        const int p = q * 64 + lane;
-        const int dj = p < T ? t_dish[v * T + p] : 0;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) sc[c][q] = sc[c][q] + lpv[c * MVC_Z_LS + dj];
-      }
-      if (v == V - 1) {
-        // ================= table draw =================
-        const int nct = (T + 63) >> 6;
-        wave_lds_sync();   // rowS/rowM of the marginal step are consumed
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const double snc = readlane_d(snew_acc, c);
-          double M = -MVC_PM_INF;
-#pragma unroll
-          for (int q = 0; q < QT; ++q) M = dmax(M, sc[c][q]);
-          M = wave_max(M);
-          if (!(M > snc)) M = snc;
-          double B = 0.0;
-#pragma unroll
-          for (int q = 0; q < QT; ++q) {
-            const double lf = sc[c][q] != -MVC_PM_INF ? mvc_exp(sc[c][q] - M) : 0.0;
-            sc[c][q] = lf;
-            if (q < nct) {
-              const double cs = wave_tree_sum(lf);
-              B = (q == 0) ? cs : B + cs;
-            }
-          }
-          if (lane == 0) { rowM[c] = M; rowS[c] = B; }
-        }
-        wave_lds_sync();
-        const double Mc = rowM[col], Bc = rowS[col];
-        const double W = mvc_exp(snew_acc - Mc) + Bc;
-        const double rr_row = u_row * W;
-#pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          double rr = readlane_d(rr_row, c);
-          const double Bu = readlane_d(Bc, c);
-          int pick = -1;
-          if (rr < Bu) {
-            int cq = 0;
-            if (QT > 1 && nct > 1) {
-              // two-chunk partial tree: node values p0 = part[0], p1 = part[1]
-              const double p0s = wave_tree_sum(sc[c][0]);
-              const double p1s = wave_tree_sum(sc[c][QT - 1]);
-              if (!(p1s == 0.0 || rr < p0s)) { rr = rr - p0s; cq = 1; }
-            }
-            Tree64Levels Lv;
-            const double leaf = (cq == 0) ? sc[c][0] : sc[c][QT - 1];
-            wave_tree_sum_levels(leaf, Lv);
-            pick = cq * 64 + wave_tree_select(Lv, leaf, rr);
-          }
-          if (lane == 0 && tile_active && i0 + c < n) A.choice[i0 + c] = pick;
-        }
+        const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+        const int li = li0 + grp + 4 * r;
+        if (j < K && j != j0[r] && li < nb) lpb[lpb_index(li, koff + j, sumK)] = val;
       }
     }
-    if (X + 1 < nX) {
-      z_commit(geo, s_nct, sbuf, X + 1, stg);
-#pragma unroll
-      for (int s = 0; s < MVC_Z_KS; ++s) a[s] = stg.an[s];
+    wave_lds_sync();
+    {   // own dish, one row per lane
+      const double G = selfG[col];
+      const int jj = t_dish[pz];
+      const double Gp = G - y2;
+      const double Qp = (d_Q[jj] - 2.0 * G) + y2;
+      const Coef cf = coef(d_n[jj] - 1, Qp, tau, L2pt, D);
+      const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
+      if (lane < 16 && li0 + col < nb) lpb[lpb_index(li0 + col, koff + jj, sumK)] = sv;
+    }
+    wave_lds_sync();
+  }
+}
+
+// Generic lp producer: one lane per customer (any D).
+extern "C" __global__ __launch_bounds__(256) void mvc_par_lpgen_kernel(Sweep A, int b0, int nb, double *lpb) {
+  const ParState &P = A.P;
+  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
+  const int sumK = A.Koff[V];
+  for (int li = blockIdx.x * blockDim.x + threadIdx.x; li < nb; li += gridDim.x * blockDim.x) {
+    const int i = b0 + li;
+    const int p0 = P.z[i];
+    for (int v = 0; v < V; ++v) {
+      const int K = A.Koff[v + 1] - A.Koff[v], koff = A.Koff[v];
+      const int j0 = P.dish[v * P.TC + p0];
+      const double tau = P.hyper[v];
+      const double Y2i = A.Y2[(size_t)v * n + i];
+      const double hy = 0.5 * Y2i, h = (-0.5 * Y2i) / tau;
+      const double *yrow = A.y + ((size_t)v * n + i) * D;
+      const double *S1v = P.S1T + (size_t)v * D * KC;
+      double G0 = 0.0;
+      for (int j = 0; j < K; ++j) {
+        double G = 0.0;
+        for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S1v[(size_t)d * KC + j], G);
+        if (j == j0) G0 = G;
+        lpb[lpb_index(li, koff + j, sumK)] = __builtin_fma(G + hy, P.cb[v * KC + j], P.c0[v * KC + j]) + h;
+      }
+      // own dish: reduced statistics (same thread, stored after the loop)
+      const double Gp = G0 - Y2i;
+      const double Qp = (P.Q[v * KC + j0] - 2.0 * G0) + Y2i;
+      const Coef c = coef(P.d_n[v * KC + j0] - 1, Qp, tau, A.L2pt[v], D);
+      lpb[lpb_index(li, koff + j0, sumK)] = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
     }
   }
 }
 
-extern "C" __global__ __launch_bounds__(MVC_Z_NW * 64) void mvc_par_zresample_z1_kernel(Sweep A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  z_kernel_body<1>(A, smem);
-}
-extern "C" __global__ __launch_bounds__(MVC_Z_NW * 64) void mvc_par_zresample_z2_kernel(Sweep A) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  z_kernel_body<2>(A, smem);
+// Draw kernel: one lane per customer (oracle ParallelSampler::
+// resample_customer).  Per view: max and sum of w exp(lp - m) in dish order;
+// tables: scores in position order, cumulative weights with a checkpoint
+// every BS tables so the pick re-walks one block only.
+#define MVC_ZD_NCP 16
+extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, int b0, int nb, const double *lpb) {
+  __shared__ double cp_s[MVC_ZD_NCP][256];
+  const ParState &P = A.P;
+  const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
+  const int T = A.T;
+  const int sumK = A.Koff[V];
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const int T_ne = A.status[V + 3];
+  const int BS = max(16, ((T + MVC_ZD_NCP - 1) / MVC_ZD_NCP + 3) & ~3);   // multiple of 4
+  const int nblk = (T + BS - 1) / BS;
+  const int tid = threadIdx.x;
+  for (int li = blockIdx.x * blockDim.x + tid; li < nb; li += gridDim.x * blockDim.x) {
+    const int i = b0 + li;
+    const int p0 = P.z[i];
+    const bool alive = (P.n_t[p0] - 1) > 0;
+    const double *lpi = lpb + lpb_index(li, 0, sumK);   // dish k at lpi[k * 16]
+    double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+    for (int v = 0; v < V; ++v) {
+      const int K = A.Koff[v + 1] - A.Koff[v], koff = A.Koff[v];
+      const int j0 = P.dish[v * TC + p0];
+      const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+      const int l0p = P.d_l[v * KC + j0] - (alive ? 0 : 1);
+      const int *dl = P.d_l + v * KC;
+      const double *lpv = lpi + (size_t)koff * 16;
+      // (loads in batches of 8 so several L2 round trips overlap; the
+      // reductions themselves stay sequential in dish order)
+      double m = -MVC_PM_INF;
+      int j = 0;
+      for (; j + 8 <= K; j += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int l = (j + u == j0) ? l0p : dl[j + u];
+          if (l > 0 && x[u] > m) m = x[u];
+        }
+      }
+      for (; j < K; ++j) {
+        const int l = (j == j0) ? l0p : dl[j];
+        const double x = lpv[(size_t)j * 16];
+        if (l > 0 && x > m) m = x;
+      }
+      if (lfn > m) m = lfn;
+      double S = 0.0;
+      j = 0;
+      for (; j + 8 <= K; j += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int l = (j + u == j0) ? l0p : dl[j + u];
+          double w = (double)l - sigma;
+          if (w < 0.0) w = 0.0;
+          x[u] = l > 0 ? w * mvc_exp(x[u] - m) : -1.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (x[u] >= 0.0) S = S + x[u];
+      }
+      for (; j < K; ++j) {
+        const int l = (j == j0) ? l0p : dl[j];
+        double w = (double)l - sigma;
+        if (w < 0.0) w = 0.0;
+        const double e = mvc_exp(l > 0 ? lpv[(size_t)j * 16] - m : 0.0);
+        if (l > 0) S = S + w * e;
+      }
+      const int Kact = K - ((l0p == 0) ? 1 : 0);
+      double wn = alpha + (double)Kact * sigma;
+      if (wn < 0.0) wn = 0.0;
+      S = S + wn * mvc_exp(lfn - m);
+      const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
+      const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
+      s_new = s_new + lm;
+    }
+    // own table's base score with the customer removed
+    const int np0 = P.n_t[p0] - 1;
+    const double m0 = (double)np0 - sg;
+    const double base_self = (np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
+    auto base = [&](int p) -> double {
+      if (p == p0) return base_self;
+      const int np = P.n_t[p];
+      return (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
+    };
+    // scores of tables p .. p+3 (clamped); view-order sums, 4 gathers in flight
+    auto score4 = [&](int p, double (&sp)[4]) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sp[u] = base(min(p + u, T - 1));
+      for (int v = 0; v < V; ++v) {
+        double x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = lpi[(size_t)(A.Koff[v] + P.dish[v * TC + min(p + u, T - 1)]) * 16];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sp[u] = sp[u] + x[u];
+      }
+    };
+    double M = -MVC_PM_INF;
+    for (int p = 0; p < T; p += 4) {
+      double sp[4];
+      score4(p, sp);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (p + u < T && sp[u] > M) M = sp[u];
+    }
+    if (s_new > M) M = s_new;
+    // cumulative weights; a checkpoint before every block of BS (multiple of 4) tables
+    double cum = 0.0;
+    for (int b = 0; b < nblk; ++b) {
+      cp_s[b][tid] = cum;
+      const int pe = min(T, (b + 1) * BS);
+      for (int p = b * BS; p < pe; p += 4) {
+        double sp[4], e[4];
+        score4(p, sp);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = mvc_exp(sp[u] != -MVC_PM_INF ? sp[u] - M : 0.0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (p + u < pe && sp[u] != -MVC_PM_INF) cum = cum + e[u];
+      }
+    }
+    const double W = mvc_exp(s_new - M) + cum;
+    const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+    int pick = -1;
+    if (r < cum) {
+      int b = 0;
+      while (b + 1 < nblk && !(r < cp_s[b + 1][tid])) ++b;
+      double c = cp_s[b][tid];
+      const int pe = min(T, (b + 1) * BS);
+      for (int p = b * BS; p < pe && pick < 0; p += 4) {
+        double sp[4], e[4];
+        score4(p, sp);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = mvc_exp(sp[u] != -MVC_PM_INF ? sp[u] - M : 0.0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (pick < 0 && p + u < pe) {
+            if (sp[u] != -MVC_PM_INF) c = c + e[u];
+            if (r < c) pick = p + u;
+          }
+        }
+      }
+    }
+    A.choice[i] = pick;
+  }
 }
 
 // Phase 2: births resolved sequentially in ascending
@@ -1747,7 +1619,7 @@ namespace mvc {
 namespace {
 constexpr int kParTC = 4096;   // table capacity (two-level tree64)
 constexpr int kParKC = 4095;   // live dishes per view (+1 new element <= 4096)
-constexpr int kZGrid = 2048;   // zresample / birth grid (4 waves per block)
+constexpr size_t kLpbBudget = (size_t)1 << 28;   // phase-1 lp buffer: 2 GiB of doubles per batch
 
 template <class Tp>
 Tp *dmalloc(size_t count) {
@@ -1782,7 +1654,9 @@ class ParallelSampler : public Sampler {
     std::vector<void *> owned;
   };
   std::vector<Chain> chains;
-  double *lp_scratch = nullptr;
+  double *lp_scratch = nullptr;   // births kernel (one wave)
+  double *lpb = nullptr;          // phase-1 lp buffer (lpb_index layout)
+  size_t lpb_cap = 0;             // doubles
   size_t lp_cap = 0;               // doubles per wave
   double *part1 = nullptr, *part2 = nullptr;
   size_t part_cap = 0;             // sumK capacity of partials
@@ -1790,9 +1664,7 @@ class ParallelSampler : public Sampler {
   size_t cub_bytes = 0;
   std::vector<int32_t> st_host;
   bool force_generic = false;
-  bool force_mfma1 = false;
   int n_cu = 256;
-  bool last_path_mfma = false;
 
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
@@ -1819,7 +1691,7 @@ class ParallelSampler : public Sampler {
     hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
     MVC_HIP(hipGetLastError());
     if (D % 4 == 0 && D >= 16 && V <= MVC_Z_VMAX) {
-      SP = ((D / 4 + MVC_Z_KS - 1) / MVC_Z_KS) * MVC_Z_KS;
+      SP = ((D / 4 + MVC_ZR - 1) / MVC_ZR) * MVC_ZR;
       const size_t ntile = ((size_t)n + 15) / 16;
       yt = dmalloc<double>((size_t)V * ntile * SP * 64);
       hipLaunchKernelGGL(mvc_par_ytile_kernel, dim3(4096), dim3(256), 0, stream, n, V, D, SP, (const double *)y, yt);
@@ -1836,19 +1708,14 @@ class ParallelSampler : public Sampler {
     st_host.assign(V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
-    const char *f1 = getenv("MVC_FORCE_MFMA1");
-    force_mfma1 = f1 && f1[0] == '1';
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
       n_cu = std::max(1, prop.multiProcessorCount);
     }
-    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_mfma_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_z1_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zresample_z2_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (const void *f : {(const void *)mvc_par_lpview_kernel<1>, (const void *)mvc_par_lpview_kernel<2>,
+                          (const void *)mvc_par_lpview_kernel<3>, (const void *)mvc_par_lpview_kernel<4>})
+      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_stats_partial_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     chains.resize(cf.n_chains);
@@ -1860,7 +1727,8 @@ class ParallelSampler : public Sampler {
     if (stream) hipStreamSynchronize(stream);
     for (auto &c : chains)
       for (void *p : c.owned) hipFree(p);
-    for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)part1, (void *)part2, cub_tmp})
+    for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)lpb, (void *)part1, (void *)part2,
+                    cub_tmp})
       if (p) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -2037,7 +1905,7 @@ class ParallelSampler : public Sampler {
     if (per_wave <= lp_cap) return;
     if (lp_scratch) hipFree(lp_scratch);
     lp_cap = per_wave + 64;
-    lp_scratch = dmalloc<double>((size_t)kZGrid * 4 * lp_cap);
+    lp_scratch = dmalloc<double>(lp_cap);   // the births kernel's one wavefront
   }
 
   Sweep make_sweep(Chain &c, uint32_t s) {
@@ -2077,37 +1945,52 @@ class ParallelSampler : public Sampler {
     upload_koff(c);
     Sweep A = make_sweep(c, s);
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-    // MFMA path when the view width allows it
+    // phase 1 in customer batches: lp producer (MFMA or generic), then draw
     int Kmax = 0, Kmin = 1 << 30;
     for (int k : c.K) { Kmax = std::max(Kmax, k); Kmin = std::min(Kmin, k); }
     const int sk = sumK(c);
-    const size_t mfma_lds = ((size_t)c.T * 8 + (size_t)c.T * 4 + (size_t)V * c.T * 4 + (size_t)sk * 32 + 64) +
-                            4 * ((size_t)sk * 16 + (size_t)V * 16) * sizeof(double);
-    const bool use_mfma = !force_generic && D % 4 == 0 && D >= 16 && Kmax <= 255 && c.T <= MVC_MFMA_TMAX &&
-                          mfma_lds <= 160 * 1024;
-    const size_t z_lds = z_shared_bytes(c.T, V, sk);
-    const bool use_z = !force_generic && !force_mfma1 && c.s1t_ok && Kmin >= 1 && Kmax <= MVC_Z_KMAX && c.T <= MVC_Z_TMAX &&
-                       z_lds <= 160 * 1024;
-    timers.begin("zresample", &e0);
-    if (use_z) {
-      // one block of MVC_Z_NW waves per CU
-      const int ntile = (n + 15) / 16;
-      const int grid = std::max(1, std::min(n_cu, (ntile + MVC_Z_NW - 1) / MVC_Z_NW));
-      if (c.T <= 64)
-        hipLaunchKernelGGL(mvc_par_zresample_z1_kernel, dim3(grid), dim3(MVC_Z_NW * 64), z_lds, stream, A);
-      else
-        hipLaunchKernelGGL(mvc_par_zresample_z2_kernel, dim3(grid), dim3(MVC_Z_NW * 64), z_lds, stream, A);
-    } else if (use_mfma) {
-      const int ntile = (n + 15) / 16;
-      hipLaunchKernelGGL(mvc_par_zresample_mfma_kernel, dim3(std::min(2048, (ntile + 3) / 4)), dim3(256), mfma_lds,
-                         stream, A);
-    } else {
-      hipLaunchKernelGGL(mvc_par_zresample_kernel, dim3(std::min(kZGrid, (n + 3) / 4)), dim3(256), 0, stream, A);
+    const bool use_mfma = !force_generic && c.s1t_ok && Kmin >= 1 && Kmax <= MVC_Z_KMAX &&
+                          lpview_shared_bytes(SP, (Kmax + 15) / 16, Kmax, c.T) <= 160 * 1024;
+    // batch: multiple of 64 customers, lp buffer <= kLpbBudget doubles
+    const size_t per64 = (size_t)std::max(1, sk) * 64;
+    const size_t nb_max = std::max<size_t>(64, (kLpbBudget / per64) * 64);
+    const size_t nb_full = ((size_t)n + 63) / 64 * 64;
+    const size_t nbatch_sz = std::min(nb_max, nb_full);
+    const size_t need = (nbatch_sz / 64) * per64;
+    if (need > lpb_cap) {
+      if (lpb) hipFree(lpb);
+      lpb_cap = need;
+      lpb = dmalloc<double>(lpb_cap);
     }
-    MVC_HIP(hipGetLastError());
+    timers.begin("zresample", &e0);
+    for (size_t b0 = 0; b0 < (size_t)n; b0 += nbatch_sz) {
+      const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
+      if (use_mfma) {
+        const int ntile = (nb + 15) / 16;
+        for (int v = 0; v < V; ++v) {
+          const int NT = (c.K[v] + 15) / 16;
+          const size_t lds = lpview_shared_bytes(SP, NT, c.K[v], c.T);
+          const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / std::max<size_t>(lds, 1)));
+          const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + 7) / 8));
+          switch (NT) {
+            case 1: hipLaunchKernelGGL(mvc_par_lpview_kernel<1>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
+            case 2: hipLaunchKernelGGL(mvc_par_lpview_kernel<2>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
+            case 3: hipLaunchKernelGGL(mvc_par_lpview_kernel<3>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
+            default: hipLaunchKernelGGL(mvc_par_lpview_kernel<4>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
+          }
+          MVC_HIP(hipGetLastError());
+        }
+      } else {
+        hipLaunchKernelGGL(mvc_par_lpgen_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256), 0, stream, A,
+                           (int)b0, nb, lpb);
+      }
+      MVC_HIP(hipGetLastError());
+      hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256), 0, stream, A,
+                         (int)b0, nb, (const double *)lpb);
+      MVC_HIP(hipGetLastError());
+    }
     timers.end("zresample", e0);
-    last_path_mfma = use_mfma || use_z;
-    zpath = use_z ? 2 : (use_mfma ? 1 : 0);
+    zpath = use_mfma ? 2 : 0;
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
     hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, n, c.T,

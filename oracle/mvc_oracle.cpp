@@ -21,8 +21,9 @@
 //     (include/mvc_pmath.h, bit-identical to the GPU).
 //   * ParallelSampler — the parallel-z ("mode P") schedule specified in
 //     every customer is resampled against the state frozen at
-//     sweep start, births resolved in index order, deterministic stats rebuild,
-//     log-space probabilities with tree64 reductions, EPPF via lgamma.
+//     sweep start (sequential per-customer reductions), births resolved in
+//     index order (tree64 reductions), deterministic stats rebuild, EPPF via
+//     lgamma.
 //
 // Build: oracle/Makefile  (g++ -O2 -ffp-contract=off, no fast-math).
 #include <stdint.h>
@@ -971,40 +972,92 @@ struct ParallelSampler {
       E.lmarg = (m + mvc_log(E.S)) - mvc_log(denom);
   }
 
+  // Phase 1 per-view marginal: sequential reductions in
+  // dish order, so one GPU lane can own one customer.  lp of every dish goes
+  // to lp_out[0..K); returns lm_v.
+  double eval_view_seq(int i, int v, bool alive, int j0, double *lp_out) const {
+    const int K = (int)ids[v].size();
+    const double Y2i = Y2[(size_t)v * n + i];
+    const double hy = 0.5 * Y2i;
+    const double h = (-0.5 * Y2i) / tau[v];
+    const double *yi = y + ((size_t)v * n + i) * D;
+    int l0p = 0;
+    for (int j = 0; j < K; ++j) {
+      const double G = fma_dot(yi, &S1[v][(size_t)j * D], D);
+      if (j == j0) {
+        l0p = lk[v][j] - (alive ? 0 : 1);
+        const double Gp = G - Y2i;
+        const double Qp = (Qd[v][j] - 2.0 * G) + Y2i;
+        const Coef c = coef(nk[v][j] - 1, Qp, tau[v], L2pt[v]);
+        lp_out[j] = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
+      } else {
+        lp_out[j] = __builtin_fma(G + hy, cf[v][j].cb, cf[v][j].c0) + h;
+      }
+    }
+    const double lfn = cnew[v] + h;
+    // max over included dishes (l' > 0) in dish order, then the new dish
+    double m = -MVC_PM_INF;
+    for (int j = 0; j < K; ++j) {
+      const int l = (j == j0) ? l0p : lk[v][j];
+      if (l > 0 && lp_out[j] > m) m = lp_out[j];
+    }
+    if (lfn > m) m = lfn;
+    // sequential sum of w * exp(lp - m) in dish order, then the new dish
+    double S = 0.0;
+    for (int j = 0; j < K; ++j) {
+      const int l = (j == j0) ? l0p : lk[v][j];
+      if (l > 0) {
+        double w = (double)l - sigma[v];
+        if (w < 0.0) w = 0.0;
+        S = S + w * mvc_exp(lp_out[j] - m);
+      }
+    }
+    const int Kact = K - ((l0p == 0) ? 1 : 0);
+    double wn = alpha[v] + (double)Kact * sigma[v];
+    if (wn < 0.0) wn = 0.0;
+    S = S + wn * mvc_exp(lfn - m);
+    const double denom = alpha[v] + (double)(Ltot[v] - (alive ? 0 : 1));
+    if (denom <= 0.0) return lfn;
+    return (m + mvc_log(S)) - mvc_log(denom);
+  }
+
   // Phase 1: table against the frozen state; -1 = birth.
+  // Table weights e_p = exp(sp_p - M) accumulate in position order
+  // (cum_p = cum_{p-1} + e_p); W = exp(s_new - M) + cum_{T-1}; r = u W picks
+  // the first p with r < cum_p, or a birth when r >= cum_{T-1}.
   int resample_customer(int i, int s) const {
     const int p0 = z[i];
     const bool alive = (n_t[p0] - 1) > 0;
-    std::vector<ViewEval> E(V);
-    for (int v = 0; v < V; ++v) eval_view(i, v, alive, dish[v][p0], E[v]);
-    std::vector<double> sc(T, 0.0);
-    std::vector<char> inc(T, 0);
+    std::vector<std::vector<double>> lp(V);
+    const int Tne_i = T_ne - (alive ? 0 : 1);
+    double s_new = mvc_log(ag + sg * (double)Tne_i);
+    for (int v = 0; v < V; ++v) {
+      lp[v].resize(ids[v].size());
+      s_new = s_new + eval_view_seq(i, v, alive, dish[v][p0], lp[v].data());
+    }
+    std::vector<double> sc(T, -MVC_PM_INF);
     double M = -MVC_PM_INF;
     for (int p = 0; p < T; ++p) {
       const int np = n_t[p] - (p == p0 ? 1 : 0);
-      if (np < 1) continue;
       const double mass = (double)np - sg;
-      if (mass <= 0.0) continue;
+      if (np < 1 || !(mass > 0.0)) continue;
       double sp = mvc_log(mass);
-      for (int v = 0; v < V; ++v) sp = sp + E[v].lv[dish[v][p]];
+      for (int v = 0; v < V; ++v) sp = sp + lp[v][dish[v][p]];
       sc[p] = sp;
-      inc[p] = 1;
       if (sp > M) M = sp;
     }
-    const int Tne_i = T_ne - (alive ? 0 : 1);
-    const double mass_new = ag + sg * (double)Tne_i;
-    double s_new = mvc_log(mass_new);
-    for (int v = 0; v < V; ++v) s_new = s_new + E[v].lmarg;
     if (s_new > M) M = s_new;
-    std::vector<double> e(T, 0.0);
-    for (int p = 0; p < T; ++p)
-      if (inc[p]) e[p] = mvc_exp(sc[p] - M);
-    const double e_new = mvc_exp(s_new - M);
-    Tree64 tb;
-    const double B = tb.build(e);
-    const double W = e_new + B;
+    double cum = 0.0;
+    std::vector<double> cums(T);
+    for (int p = 0; p < T; ++p) {
+      if (sc[p] != -MVC_PM_INF) cum = cum + mvc_exp(sc[p] - M);
+      cums[p] = cum;
+    }
+    const double W = mvc_exp(s_new - M) + cum;
     const double r = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_Z) * W;
-    if (r < B) return (int)tb.select(r);
+    if (r < cum)
+      for (int p = 0; p < T; ++p)
+        if (r < cums[p]) return p;
     return -1;
   }
 

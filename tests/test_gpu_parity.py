@@ -236,9 +236,9 @@ def test_parallel_warm_start(D):
 
 
 def _run_path(m, y, st, seed, sweeps, path, monkeypatch):
-    """Run `sweeps` warm-started sweeps forcing z-path 0/1/2; check the path."""
+    """Run `sweeps` warm-started sweeps forcing the lp producer (0 generic,
+    2 MFMA); check the path on the first sweep."""
     monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
-    monkeypatch.setenv("MVC_FORCE_MFMA1", "1" if path == 1 else "0")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
     states = []
@@ -257,7 +257,7 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
     V, K, D = 3, 8, 32
     y, z = data.synthetic(2000, V, D, K, seed=5)
     st = _warm_state(z, V, K)
-    out = [_run_path(m, y, st, 9, 3, p, monkeypatch) for p in (0, 1, 2)]
+    out = [_run_path(m, y, st, 9, 3, p, monkeypatch) for p in (0, 2)]
     for a in out[1:]:
         for sa, sb in zip(out[0], a):
             assert np.array_equal(sa[0], sb[0])
@@ -265,9 +265,8 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
             assert np.array_equal(sa[2]["tau_v"], sb[2]["tau_v"])
 
 
-# block-lockstep MFMA kernel (path 2): ragged tiles (n % 16 != 0), fewer tiles
-# than waves, D not a multiple of 32 (zero-padded k-steps), T in (64, 128]
-# (two table chunks), K_v of 64 (new-dish leaf in the second chunk)
+# MFMA lp producer (path 2): ragged tiles (n % 16 != 0), fewer tiles than
+# waves, D not a multiple of 16 (zero-padded k-steps), T > 64, K_v of 64
 @pytest.mark.parametrize("n,V,D,K,T", [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96),
                                        (2500, 2, 128, 64, 64)])
 def test_zpath2_vs_oracle(n, V, D, K, T, monkeypatch):
