@@ -772,19 +772,42 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_lpgen_kernel(Sweep A, 
 // Draw kernel: one lane per customer (oracle ParallelSampler::
 // resample_customer).  Per view: max and sum of w exp(lp - m) in dish order;
 // tables: scores in position order, cumulative weights with a checkpoint
-// every BS tables so the pick re-walks one block only.
+// every BS tables so the pick re-walks one block only.  Every uniform
+// per-table / per-dish quantity is staged in LDS first (a gather whose index
+// comes from global memory would pay two dependent memory round trips).
 #define MVC_ZD_NCP 16
+__host__ __device__ inline size_t zdraw_shared_bytes(int V, int T, int sumK) {
+  return 8 * ((size_t)MVC_ZD_NCP * 256 + (size_t)T) + 4 * ((size_t)V * T + (size_t)sumK + (size_t)V + 1) + 64;
+}
 extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, int b0, int nb, const double *lpb) {
-  __shared__ double cp_s[MVC_ZD_NCP][256];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
   const int T = A.T;
-  const int sumK = A.Koff[V];
+  const int tid = threadIdx.x;
+  double *cp_s = (double *)smem;                   // [MVC_ZD_NCP][256]
+  double *s_base = cp_s + MVC_ZD_NCP * 256;        // [T] log mass (or -inf)
+  int *s_tix = (int *)(s_base + T);                // [T][V] Koff[v] + dish_v(p)
+  int *s_koff = s_tix + (size_t)T * V;             // [V+1]
+  int *s_dl = s_koff + V + 1;                      // [sumK] l of each dish
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  if (tid <= V) s_koff[tid] = A.Koff[tid];
+  __syncthreads();
+  const int sumK = s_koff[V];
+  for (int p = tid; p < T; p += blockDim.x) {
+    const int np = P.n_t[p];
+    s_base[p] = (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
+    for (int v = 0; v < V; ++v) s_tix[p * V + v] = s_koff[v] + P.dish[v * TC + p];
+  }
+  for (int k = tid; k < sumK; k += blockDim.x) {
+    int v = 0;
+    while (v + 1 < V && s_koff[v + 1] <= k) ++v;
+    s_dl[k] = P.d_l[v * KC + (k - s_koff[v])];
+  }
+  __syncthreads();
   const int T_ne = A.status[V + 3];
   const int BS = max(16, ((T + MVC_ZD_NCP - 1) / MVC_ZD_NCP + 3) & ~3);   // multiple of 4
   const int nblk = (T + BS - 1) / BS;
-  const int tid = threadIdx.x;
   for (int li = blockIdx.x * blockDim.x + tid; li < nb; li += gridDim.x * blockDim.x) {
     const int i = b0 + li;
     const int p0 = P.z[i];
@@ -792,15 +815,15 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
     const double *lpi = lpb + lpb_index(li, 0, sumK);   // dish k at lpi[k * 16]
     double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
     for (int v = 0; v < V; ++v) {
-      const int K = A.Koff[v + 1] - A.Koff[v], koff = A.Koff[v];
-      const int j0 = P.dish[v * TC + p0];
+      const int koff = s_koff[v], K = s_koff[v + 1] - koff;
+      const int j0 = s_tix[p0 * V + v] - koff;
       const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
       const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
-      const int l0p = P.d_l[v * KC + j0] - (alive ? 0 : 1);
-      const int *dl = P.d_l + v * KC;
+      const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
+      const int *dl = s_dl + koff;
       const double *lpv = lpi + (size_t)koff * 16;
-      // (loads in batches of 8 so several L2 round trips overlap; the
-      // reductions themselves stay sequential in dish order)
+      // loads in batches of 8 (several round trips overlap); the reductions
+      // themselves stay sequential in dish order
       double m = -MVC_PM_INF;
       int j = 0;
       for (; j + 8 <= K; j += 8) {
@@ -855,19 +878,18 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
     const int np0 = P.n_t[p0] - 1;
     const double m0 = (double)np0 - sg;
     const double base_self = (np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
-    auto base = [&](int p) -> double {
-      if (p == p0) return base_self;
-      const int np = P.n_t[p];
-      return (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
-    };
-    // scores of tables p .. p+3 (clamped); view-order sums, 4 gathers in flight
+    // scores of tables p .. p+3 (clamped); view-order sums, 4 V gathers in flight
     auto score4 = [&](int p, double (&sp)[4]) {
+      int pc[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) sp[u] = base(min(p + u, T - 1));
+      for (int u = 0; u < 4; ++u) {
+        pc[u] = min(p + u, T - 1);
+        sp[u] = (pc[u] == p0) ? base_self : s_base[pc[u]];
+      }
       for (int v = 0; v < V; ++v) {
         double x[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x[u] = lpi[(size_t)(A.Koff[v] + P.dish[v * TC + min(p + u, T - 1)]) * 16];
+        for (int u = 0; u < 4; ++u) x[u] = lpi[(size_t)s_tix[pc[u] * V + v] * 16];
 #pragma unroll
         for (int u = 0; u < 4; ++u) sp[u] = sp[u] + x[u];
       }
@@ -881,10 +903,10 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
         if (p + u < T && sp[u] > M) M = sp[u];
     }
     if (s_new > M) M = s_new;
-    // cumulative weights; a checkpoint before every block of BS (multiple of 4) tables
+    // cumulative weights; a checkpoint before every block of BS tables
     double cum = 0.0;
     for (int b = 0; b < nblk; ++b) {
-      cp_s[b][tid] = cum;
+      cp_s[b * 256 + tid] = cum;
       const int pe = min(T, (b + 1) * BS);
       for (int p = b * BS; p < pe; p += 4) {
         double sp[4], e[4];
@@ -901,8 +923,8 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
     int pick = -1;
     if (r < cum) {
       int b = 0;
-      while (b + 1 < nblk && !(r < cp_s[b + 1][tid])) ++b;
-      double c = cp_s[b][tid];
+      while (b + 1 < nblk && !(r < cp_s[(b + 1) * 256 + tid])) ++b;
+      double c = cp_s[b * 256 + tid];
       const int pe = min(T, (b + 1) * BS);
       for (int p = b * BS; p < pe && pick < 0; p += 4) {
         double sp[4], e[4];
@@ -1713,6 +1735,8 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
       n_cu = std::max(1, prop.multiProcessorCount);
     }
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zdraw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024));
     for (const void *f : {(const void *)mvc_par_lpview_kernel<1>, (const void *)mvc_par_lpview_kernel<2>,
                           (const void *)mvc_par_lpview_kernel<3>, (const void *)mvc_par_lpview_kernel<4>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1962,6 +1986,8 @@ class ParallelSampler : public Sampler {
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap);
     }
+    if (zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
+      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: V x tables too large for the draw kernel's LDS tables");
     timers.begin("zresample", &e0);
     for (size_t b0 = 0; b0 < (size_t)n; b0 += nbatch_sz) {
       const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
@@ -1985,8 +2011,8 @@ class ParallelSampler : public Sampler {
                            (int)b0, nb, lpb);
       }
       MVC_HIP(hipGetLastError());
-      hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256), 0, stream, A,
-                         (int)b0, nb, (const double *)lpb);
+      hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
+                         zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb);
       MVC_HIP(hipGetLastError());
     }
     timers.end("zresample", e0);
