@@ -64,6 +64,18 @@ def warm_state(z, V, K):
     return table_of, dish, hyper
 
 
+def measured_traffic(config):
+    """HBM bytes per z-resample pass from the committed rocprofv3 PMC summary
+    (scripts/gpu_pmc_z.sh -> profiles/pmc_traffic.json), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get(config, {}).get("bytes_per_pass")
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(y, z, V, K, D, seed, n_sample=0, target_s=12.0):
     """Oracle port of the same parallel sweep on a bounded subsample, 1 core.
     The sample size is calibrated on a 2000-customer probe to ~target_s."""
@@ -132,10 +144,22 @@ def main():
 
     kms, kcnt = s.kernel_time("zresample")
     sweep_ms, _ = s.kernel_time("sweep")
-    parts = {k: s.kernel_time(k)[0] / max(1, args.steps) for k in ("zresample", "births", "commit", "stats", "hyper")}
+    parts = {k: s.kernel_time(k)[0] / max(1, args.steps)
+             for k in ("zresample", "lp", "draw", "births", "commit", "stats", "hyper")}
     kdish = s.dish_counts()
-    T = s.state()[1].shape[1]
+    _, dish_now, hyper_now = s.state()
+    T = dish_now.shape[1]
+    zpath = s.zpath()
     s.close()
+
+    # optional cross-chain reduce of the hyperparameters (one all-reduce over
+    # RCCL, outside the timed region; reported, never fed back: DESIGN.md §7)
+    from mvc_amd import dist as mdist
+    hv = np.concatenate([hyper_now["alpha_v"], hyper_now["sigma_v"], hyper_now["tau_v"],
+                         [hyper_now["alpha_global"], hyper_now["sigma_global"]]])
+    acc = mdist.HyperAccumulator(hv.size)
+    acc.add(hv[None, :])
+    pooled_mean, _, pooled_n = acc.reduce(device=f"cuda:{local}" if dist is not None else None)
 
     if rank != 0:
         if dist is not None:
@@ -147,12 +171,13 @@ def main():
     flops_alg = 2.0 * N * float(kdish.sum()) * D    # G = Y S1^T per view (MFMA fp64)
     hbm_gbs = bytes_alg / k_avg_s / 1e9
     tflops = flops_alg / k_avg_s / 1e12
-    mfma_bound = D >= 16
+    ridge = PEAK_F64_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
+    traffic = measured_traffic(args.config)
     roof = ({"bound": "mfma", "achieved": round(tflops, 3), "peak": PEAK_F64_TFLOPS, "unit": "TFLOP/s",
-             "frac": round(tflops / PEAK_F64_TFLOPS, 4), "traffic": None}
-            if mfma_bound else
+             "frac": round(tflops / PEAK_F64_TFLOPS, 4), "traffic": traffic}
+            if flops_alg / bytes_alg > ridge else
             {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-             "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "traffic": None})
+             "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "traffic": traffic})
     value = world * args.steps / elapsed
     out = {
         "metric": "Gibbs sweeps/sec (N×V×K) at 1/2/4/8 MI355X; % HBM roofline",
@@ -171,9 +196,14 @@ def main():
                    "schedule": "parallel z-resample (DESIGN.md §4)", "parallelism": f"chains{world}",
                    "tables_at_end": int(T), "dishes_at_end": kdish.tolist()},
         "roofline": roof,
-        "hbm": {"kernel": "zresample", "achieved_gbs": round(hbm_gbs, 1), "peak_gbs": PEAK_HBM_GBS,
-                "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": bytes_alg,
-                "flops_per_launch": flops_alg, "kernel_ms": round(k_avg_s * 1e3, 4)},
+        "hbm": {"pass": "z-resample (lp producer x V + draw, DESIGN.md §5)", "achieved_gbs": round(hbm_gbs, 1),
+                "peak_gbs": PEAK_HBM_GBS, "frac": round(hbm_gbs / PEAK_HBM_GBS, 4),
+                "mfma_tflops": round(tflops, 3), "mfma_frac": round(tflops / PEAK_F64_TFLOPS, 4),
+                "arith_intensity": round(flops_alg / bytes_alg, 3), "ridge": round(ridge, 3),
+                "bytes_per_launch": bytes_alg, "flops_per_launch": flops_alg, "pass_ms": round(k_avg_s * 1e3, 4),
+                "lp_producer": "mfma" if zpath == 2 else "generic"},
+        "hyper_pooled_mean": {"chains": pooled_n, "alpha_global": round(float(pooled_mean[-2]), 6),
+                              "sigma_global": round(float(pooled_mean[-1]), 6)},
         "nvk_sweeps_per_s": round(value * N * V * K, 1),
         "kernel_ms_per_sweep": {k: round(v, 4) for k, v in parts.items()},
         "data_gen_s": round(t_gen, 2),

@@ -1,11 +1,16 @@
-// mvc_parallel.hip — the parallel ("mode P") sweep on gfx950 (DESIGN.md §4).
+// mvc_parallel.hip — the parallel ("mode P") sweep on gfx950 (DESIGN.md §4, §5).
 //
-// Per sweep:
-//   zresample : every customer draws its table against the state frozen at
-//               sweep start (virtual self-removal), one wavefront per
-//               customer, log-space probabilities, tree64 sums, Philox
-//               counters (chain, sweep, customer).
-//   births    : customers that chose a new table draw one dish per view.
+// Per sweep (one stream, one host synchronisation after the commit):
+//   phase 1   : every customer draws its table against the state frozen at
+//               sweep start (virtual self-removal), in two kernels per batch:
+//               an lp producer (per-view MFMA kernel mvc_par_lpview_kernel,
+//               or the generic mvc_par_lpgen_kernel) writes lp of every
+//               (customer, dish) to the lp buffer; the draw kernel
+//               mvc_par_zdraw_kernel (one lane per customer) reduces it in
+//               dish / table order and draws with the Philox counter
+//               (chain, sweep, customer).
+//   births    : customers that chose a new table, resolved in customer order
+//               on one wavefront (tree64 reductions).
 //   commit    : survivors + births -> dense positions, live-dish lists,
 //               counts (integer atomics: order independent).
 //   stats     : S1/S2 rebuilt in a fixed chunked order (bit-reproducible).
@@ -1991,6 +1996,8 @@ class ParallelSampler : public Sampler {
     timers.begin("zresample", &e0);
     for (size_t b0 = 0; b0 < (size_t)n; b0 += nbatch_sz) {
       const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
+      hipEvent_t el = nullptr, ed = nullptr;
+      timers.begin("lp", &el);
       if (use_mfma) {
         const int ntile = (nb + 15) / 16;
         for (int v = 0; v < V; ++v) {
@@ -2011,9 +2018,12 @@ class ParallelSampler : public Sampler {
                            (int)b0, nb, lpb);
       }
       MVC_HIP(hipGetLastError());
+      timers.end("lp", el);
+      timers.begin("draw", &ed);
       hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
                          zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb);
       MVC_HIP(hipGetLastError());
+      timers.end("draw", ed);
     }
     timers.end("zresample", e0);
     zpath = use_mfma ? 2 : 0;

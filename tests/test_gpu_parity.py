@@ -305,3 +305,36 @@ def test_exact_warm_start():
         assert np.array_equal(d, ref["dish_of"][it]), it
         assert h["alpha_global"] == ref["alpha_global"][it]
     s.close()
+
+
+# ------------------------------------------------------ C-ABI from plain C (dlopen)
+def test_c_abi_example_matches_python_path(tmp_path):
+    """examples/mvc_abi_example.c drives libmvc_hip.so through dlopen/dlsym
+    only (the Rcpp drop-in's path); its result equals the ctypes path."""
+    import subprocess
+    m = _mvc()
+    from mvc_amd import data
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "mvc_abi_example"
+    subprocess.run(["gcc", "-O2", "-I", os.path.join(root, "include"), "-o", str(exe),
+                    os.path.join(root, "examples", "mvc_abi_example.c"), "-ldl"], check=True)
+    y, _ = data.new_simulation(11)
+    V, n = y.shape
+    M, burn, thin, mode, seed = 40, 10, 2, 0, 4242
+    inp = tmp_path / "in.bin"
+    with open(inp, "wb") as f:
+        np.array([n, V, 1, M, burn, thin, mode], dtype=np.int32).tofile(f)
+        np.array([seed], dtype=np.uint64).tofile(f)
+        np.ascontiguousarray(y, dtype=np.float64).tofile(f)
+    out = tmp_path / "out.bin"
+    subprocess.run([str(exe), m.LIB_PATH, str(inp), str(out)], check=True, timeout=300)
+    raw = open(out, "rb").read()
+    S, T = np.frombuffer(raw[:8], dtype=np.int32)
+    tab = np.frombuffer(raw[8:8 + 4 * n], dtype=np.int32)
+    dish = np.frombuffer(raw[8 + 4 * n:8 + 4 * n + 4 * V * T], dtype=np.int32).reshape(V, T)
+    ag = np.frombuffer(raw[8 + 4 * n + 4 * V * T:], dtype=np.float64)[:S]
+    ref = m.run_gibbs_cpp(y, M, burn, thin, seed=seed, mode="exact", quiet=True)
+    assert S == len(ref["table_of"])
+    assert np.array_equal(tab, ref["table_of"][-1])
+    assert np.array_equal(dish, np.stack(ref["dish_of"][-1]))
+    assert np.array_equal(ag, ref["alpha_global"])

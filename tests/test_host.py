@@ -1,0 +1,69 @@
+"""CPU tests of the host-side mirror (no GPU): data generators, argument
+handling of the drop-in, get_final_clusters (New_Simulation.R:135-149), the
+bench's warm start and the chain-sharding helpers."""
+import numpy as np
+import pytest
+
+from mvc_amd import data
+from mvc_amd import dist
+from mvc_amd.sampler import _views_to_array, get_final_clusters
+
+
+def test_new_simulation_shape_matches_the_script():
+    y, labels = data.new_simulation(1999)
+    assert y.shape == (5, 200)                       # New_Simulation.R:47-60
+    assert [len(np.unique(lab)) for lab in labels] == [2, 3, 2, 2, 2]
+    y2, _ = data.new_simulation(1999)
+    assert np.array_equal(y, y2)
+
+
+def test_synthetic_generator():
+    y, z = data.synthetic(1000, 3, 8, 16, seed=4)
+    assert y.shape == (3, 1000, 8) and y.dtype == np.float64
+    labels = data.view_labels(z, 3, 16)
+    assert [lab.max() + 1 for lab in labels] == [16, 8, 4]
+    # well-separated clusters: each label's mean differs from the overall mean
+    for v in range(3):
+        m = np.stack([y[v][labels[v] == k].mean(axis=0) for k in range(labels[v].max() + 1)])
+        assert np.linalg.norm(m - m.mean(axis=0), axis=1).min() > 0.5
+
+
+def test_views_to_array_accepts_r_style_lists():
+    a = _views_to_array([np.arange(5.0), np.ones(5)])
+    assert a.shape == (2, 5, 1)
+    b = _views_to_array([np.zeros((5, 3)), np.ones((5, 3))])
+    assert b.shape == (2, 5, 3)
+    with pytest.raises(ValueError):
+        _views_to_array([np.zeros(5), np.zeros(4)])
+    with pytest.raises(ValueError):
+        _views_to_array([])
+
+
+def test_get_final_clusters_maps_tables_to_dishes():
+    res = {"table_of": [np.array([0, 1, 1, 2], dtype=np.int32)],
+           "dish_of": [[np.array([5, 6, 5], dtype=np.int32), np.array([0, 0, 1], dtype=np.int32)]]}
+    cl = get_final_clusters(res)
+    assert cl.shape == (4, 2)
+    assert np.array_equal(cl[:, 0], [5, 6, 6, 5]) and np.array_equal(cl[:, 1], [0, 0, 0, 1])
+
+
+def test_bench_warm_state_is_a_valid_state():
+    import bench
+    _, z = data.synthetic(5000, 4, 4, 64, seed=1)
+    table_of, dish, hyper = bench.warm_state(z, 4, 64)
+    T = dish.shape[1]
+    assert table_of.min() == 0 and table_of.max() == T - 1
+    assert np.all(np.bincount(table_of) > 0)
+    assert [int(d.max()) + 1 for d in dish] == [64, 32, 16, 8]
+    assert hyper.shape == (3 * 4 + 2,)
+
+
+def test_chain_range_and_local_accumulator():
+    assert dist.chain_range(0) == (0, 1)
+    assert dist.chain_range(3, 2) == (6, 2)
+    with pytest.raises(ValueError):
+        dist.chain_range(-1)
+    acc = dist.HyperAccumulator(4)
+    acc.add(np.array([[1.0, 2, 3, 4], [3.0, 2, 1, 0]]))
+    mean, var, cnt = acc.reduce()                   # no process group: local values
+    assert cnt == 2 and np.allclose(mean, [2, 2, 2, 2]) and np.allclose(var, [1, 0, 1, 4])
