@@ -125,6 +125,13 @@ int mvc_sampler_set_state(mvc_sampler *s, int chain, const int32_t *table_of, in
                           const int32_t *dish_of, const double *hyper, char *err, size_t errlen);
 /* Number of live dishes per view (k_out[V]). */
 int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char *err, size_t errlen);
+/* Sufficient statistics of one view (live dishes, ascending raw dish id):
+ * *n_dishes = K; S1[K*dim] (row-major [k][d] sums of y), S2[K] (sums of
+ * |y|^2), n_vk[K] (customers per dish).  Replaces reading ViewState's
+ * sum_y / sum_y2 / n_vk (multiview_state.h:7-18).  Outputs may be NULL;
+ * at most dish_cap dishes are copied. */
+int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes, double *S1, double *S2,
+                          int32_t *n_vk, int32_t dish_cap, char *err, size_t errlen);
 /* HIP-event kernel timing (needs MVC_FLAG_TIMING): kernel = "zresample",
  * "commit", "stats", "hyper", "exact_sweep", or "sweep" (whole sweep). */
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms,

@@ -282,6 +282,16 @@ int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char 
   });
 }
 
+int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes, double *S1, double *S2,
+                          int32_t *n_vk, int32_t dish_cap, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl) throw mvc::Error(MVC_ERR_ARG, "sampler is NULL");
+    if (view < 0 || view >= s->impl->cfg.n_views) throw mvc::Error(MVC_ERR_ARG, "view out of range");
+    if (dish_cap < 0) throw mvc::Error(MVC_ERR_ARG, "dish_cap < 0");
+    s->impl->get_stats(chain, view, n_dishes, S1, S2, n_vk, dish_cap);
+  });
+}
+
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms, int64_t *launches) {
   if (!s || !s->impl || !kernel) return MVC_ERR_ARG;
   try {

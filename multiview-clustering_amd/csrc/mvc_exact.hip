@@ -1029,6 +1029,20 @@ class ExactSampler : public Sampler {
     MVC_HIP(hipMemcpyAsync(k_out, chains[chain].h.Kact, sizeof(int32_t) * V, hipMemcpyDeviceToHost, stream));
     MVC_HIP(hipStreamSynchronize(stream));
   }
+
+  void get_stats(int chain, int view, int32_t *K, double *S1, double *S2, int32_t *n_vk, int32_t cap) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    const ExactChain &h = chains[chain].h;
+    MVC_HIP(hipStreamSynchronize(stream));
+    int32_t k = 0;
+    MVC_HIP(hipMemcpy(&k, h.Kact + view, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (K) *K = k;
+    const int c = std::min<int>(k, cap);
+    const size_t off = (size_t)view * h.KC;
+    if (S1 && c) MVC_HIP(hipMemcpy(S1, h.d_S1 + off, sizeof(double) * c, hipMemcpyDeviceToHost));
+    if (S2 && c) MVC_HIP(hipMemcpy(S2, h.d_S2 + off, sizeof(double) * c, hipMemcpyDeviceToHost));
+    if (n_vk && c) MVC_HIP(hipMemcpy(n_vk, h.d_n + off, sizeof(int32_t) * c, hipMemcpyDeviceToHost));
+  }
 };
 
 Sampler *make_exact_sampler(const mvc_config &cfg, const double *const *views) {

@@ -59,6 +59,8 @@ class Sampler {
   virtual void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of,
                          int32_t dish_cap, double *hyper) = 0;
   virtual void get_dish_counts(int chain, int32_t *k_out) = 0;
+  virtual void get_stats(int chain, int view, int32_t *K, double *S1, double *S2, int32_t *n_vk,
+                         int32_t dish_cap) = 0;
   virtual void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of,
                          const double *hyper) = 0;
   mvc_config cfg;

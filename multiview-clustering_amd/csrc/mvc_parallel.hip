@@ -1105,7 +1105,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_count_kernel(int n, in
 extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
     ParState P, int T, const int32_t *cnt, const int32_t *p2meta, const int32_t *p2_c, const int32_t *p2_tup,
     int32_t *pos_new, int32_t *tmp_dish /*[V*TC]*/, int32_t *tmp_nt /*[TC]*/, int32_t *lcnt /*[V*KC]*/,
-    int32_t *jmap /*[V*KC]*/, int32_t *status) {
+    int32_t *jmap /*[V*KC]*/, int32_t *status, int32_t *dish_old /*[V*TC]*/) {
   __shared__ int s_scan[256];
   const int tid = threadIdx.x;
   const int V = P.V, TC = P.TC, KC = P.KC;
@@ -1146,6 +1146,9 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
   for (int v = 0; v < V; ++v) {
     const int Kold = P.Kact[v];
     const int nnew = p2meta[1 + v];
+    // old table -> dish map, for the incremental statistics (relabel kernel)
+    for (int p = tid; p < T; p += 256) dish_old[v * TC + p] = P.dish[v * TC + p];
+    if (tid == 0) status[V + 4 + v] = 0;
     for (int t = tid; t < T2; t += 256) tmp_dish[v * TC + Tsurv + t] = p2_tup[t * V + v];
     for (int p = tid; p < T; p += 256)
       if (pos_new[p] >= 0) tmp_dish[v * TC + pos_new[p]] = P.dish[v * TC + p];
@@ -1206,16 +1209,121 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
   }
 }
 
-// commit step 3: relabel customers (births -> Tsurv + their phase-2 table)
-extern "C" __global__ void mvc_par_relabel_kernel(int n, int V, const int32_t *choice, const int32_t *pos_new,
-                                                  const int32_t *brank, const int32_t *btab, const int32_t *status,
-                                                  int32_t *z) {
+// commit step 3: relabel customers (births -> Tsurv + their phase-2 table);
+// per view, the customer's old dish (through the compaction map; -1 if the
+// dish died) and new dish, and the per-view count of customers whose dish
+// changed (status[V + 4 + v]) for the incremental statistics
+extern "C" __global__ __launch_bounds__(256) void mvc_par_relabel_kernel(
+    int n, int V, int TC, int KC, const int32_t *choice, const int32_t *pos_new, const int32_t *brank,
+    const int32_t *btab, int32_t *status, int32_t *z, const int32_t *dish_old, const int32_t *jmap,
+    const int32_t *dish_new, int32_t *dold, int32_t *dnew, int32_t *mflag) {
+  __shared__ int s_cnt[MVC_MAXV];
+  for (int v = threadIdx.x; v < V; v += blockDim.x) s_cnt[v] = 0;
+  __syncthreads();
   const int32_t Tn = status[0];
   const int32_t T2 = status[V + 2];
   const int32_t Tsurv = Tn - T2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int c = choice[i];
-    z[i] = c >= 0 ? pos_new[c] : Tsurv + btab[brank[i]];
+    const int zo = z[i];
+    const int zn = c >= 0 ? pos_new[c] : Tsurv + btab[brank[i]];
+    z[i] = zn;
+    for (int v = 0; v < V; ++v) {
+      const int o = jmap[v * KC + dish_old[v * TC + zo]];
+      const int w = dish_new[v * TC + zn];
+      const int m = o != w ? 1 : 0;
+      dold[(size_t)v * n + i] = o;
+      dnew[(size_t)v * n + i] = w;
+      mflag[(size_t)v * n + i] = m;
+      if (m) atomicAdd(&s_cnt[v], 1);
+    }
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < V; v += blockDim.x)
+    if (s_cnt[v]) atomicAdd(&status[V + 4 + v], s_cnt[v]);
+}
+
+// Incremental statistics.  U carries per-view sizes.
+struct StatsUpd {
+  int V, D, KC, n;
+  int Kold[MVC_MAXV], Knew[MVC_MAXV], M[MVC_MAXV];
+};
+// surviving dishes keep their sums under the compaction map; new dishes 0
+extern "C" __global__ void mvc_par_stats_zero_kernel(StatsUpd U, double *S1T, double *S2) {
+  const size_t per = (size_t)(U.D + 1) * U.KC;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < per * U.V; e += (size_t)gridDim.x * blockDim.x) {
+    const int v = (int)(e / per);
+    const size_t r = e - (size_t)v * per;
+    const int dd = (int)(r / U.KC), j = (int)(r % U.KC);
+    if (j >= U.Knew[v]) continue;
+    if (dd < U.D) S1T[((size_t)v * U.D + dd) * U.KC + j] = 0.0;
+    else S2[(size_t)v * U.KC + j] = 0.0;
+  }
+}
+extern "C" __global__ void mvc_par_stats_scatter_kernel(StatsUpd U, const int32_t *jmap, const double *S1T,
+                                                        const double *S2, double *S1T_out, double *S2_out) {
+  const size_t per = (size_t)(U.D + 1) * U.KC;
+  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < per * U.V; e += (size_t)gridDim.x * blockDim.x) {
+    const int v = (int)(e / per);
+    const size_t r = e - (size_t)v * per;
+    const int dd = (int)(r / U.KC), j = (int)(r % U.KC);
+    if (j >= U.Kold[v]) continue;
+    const int jn = jmap[(size_t)v * U.KC + j];
+    if (jn < 0) continue;
+    if (dd < U.D) S1T_out[((size_t)v * U.D + dd) * U.KC + jn] = S1T[((size_t)v * U.D + dd) * U.KC + j];
+    else S2_out[(size_t)v * U.KC + jn] = S2[(size_t)v * U.KC + j];
+  }
+}
+// one block per (incremental view, dish): walk the view's moved customers in
+// ascending order, subtract y from the old dish / add it to the new one
+// (thread dd < D owns S1[.][dd], thread dd == D owns S2)
+extern "C" __global__ __launch_bounds__(256) void mvc_par_stats_apply_kernel(
+    StatsUpd U, const int32_t *vlist, const double *y, const double *Y2, const int32_t *mlist,
+    const int32_t *dold, const int32_t *dnew, double *S1T, double *S2) {
+  __shared__ int s_i[256], s_o[256], s_w[256];
+  const int v = vlist[blockIdx.y];
+  const int j = blockIdx.x;
+  if (j >= U.Knew[v]) return;
+  const int tid = threadIdx.x;
+  const int D = U.D, n = U.n, KC = U.KC, M = U.M[v];
+  constexpr int Q = 4;                      // (D + 1) <= 4 * blockDim.x
+  double acc[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int dd = tid + q * 256;
+    acc[q] = dd < D ? S1T[((size_t)v * D + dd) * KC + j] : (dd == D ? S2[(size_t)v * KC + j] : 0.0);
+  }
+  const int32_t *ml = mlist + (size_t)v * n;
+  for (int m0 = 0; m0 < M; m0 += 256) {
+    const int cntm = min(256, M - m0);
+    __syncthreads();
+    if (tid < cntm) {
+      const int i = ml[m0 + tid];
+      s_i[tid] = i;
+      s_o[tid] = dold[(size_t)v * n + i];
+      s_w[tid] = dnew[(size_t)v * n + i];
+    }
+    __syncthreads();
+    for (int e = 0; e < cntm; ++e) {
+      const int o = s_o[e], w = s_w[e];
+      if (o != j && w != j) continue;                 // block-uniform
+      const int i = s_i[e];
+      const double *yr = y + ((size_t)v * n + i) * D;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int dd = tid + q * 256;
+        if (dd <= D) {
+          const double x = dd < D ? yr[dd] : Y2[(size_t)v * n + i];
+          acc[q] = (o == j) ? acc[q] - x : acc[q] + x;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int dd = tid + q * 256;
+    if (dd < D) S1T[((size_t)v * D + dd) * KC + j] = acc[q];
+    else if (dd == D) S2[(size_t)v * KC + j] = acc[q];
   }
 }
 
@@ -1239,11 +1347,11 @@ extern "C" __global__ void mvc_par_y2_kernel(int n, int V, int D, const double *
 // 8 loads in flight.  part1[c][Koff[v]+j][d], part2[c][Koff[v]+j].
 // ---------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(256) void mvc_par_stats_partial_kernel(
-    ParState P, const double *y, const double *Y2, const int32_t *Koff, int stride, int unused,
+    ParState P, const double *y, const double *Y2, const int32_t *Koff, int stride, uint64_t vmask,
     double *part1, double *part2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  (void)unused;
   const int c = blockIdx.x, v = blockIdx.y;
+  if (!((vmask >> v) & 1ull)) return;
   const int tid = threadIdx.x;
   const int n = P.n, D = P.D, TC = P.TC;
   const int K = P.Kact[v];
@@ -1306,7 +1414,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_stats_partial_kernel(
 // S1T[v][d][j] = sum_c part1[c][..] (ascending c, from 0.0); same for S2.
 // stride = dish-row stride of the partial buffers (>= Koff[V]).
 extern "C" __global__ void mvc_par_stats_combine_kernel(ParState P, const int32_t *Koff, int stride, int nchunk,
-                                                        const double *part1, const double *part2) {
+                                                        uint64_t vmask, const double *part1, const double *part2) {
   const int D = P.D, KC = P.KC, V = P.V;
   const size_t tot = (size_t)Koff[V] * (D + 1);
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < tot; e += (size_t)gridDim.x * blockDim.x) {
@@ -1314,6 +1422,7 @@ extern "C" __global__ void mvc_par_stats_combine_kernel(ParState P, const int32_
     const int d = (int)(e % (D + 1));
     int v = 0;
     while (v + 1 < V && Koff[v + 1] <= k) ++v;
+    if (!((vmask >> v) & 1ull)) continue;
     const int j = k - Koff[v];
     double s = 0.0;
     if (d < D) {
@@ -1674,6 +1783,13 @@ class ParallelSampler : public Sampler {
     double *mh_scratch = nullptr;
     size_t mh_half = 0;
     double *S1t = nullptr;         // MFMA B-fragment layout of S1 (K_v <= 64)
+    int32_t *dish_old = nullptr;   // [V*TC] table -> dish before the commit
+    int32_t *dold = nullptr, *dnew = nullptr, *mflag = nullptr, *mlist = nullptr;   // [V*n]
+    int32_t *nsel = nullptr, *vlist = nullptr;
+    double *S1T_alt = nullptr, *S2_alt = nullptr;   // ping-pong of P.S1T / P.S2
+    // host sources of async uploads: they outlive the copies (the next write
+    // happens after the next sweep's status synchronisation)
+    std::vector<int32_t> koff_h, vlist_h;
     bool s1t_ok = false;
     int T = 0;
     std::vector<int32_t> K;
@@ -1732,7 +1848,7 @@ class ParallelSampler : public Sampler {
                                           (int32_t *)nullptr, n, stream));
     cub_bytes = std::max(b1, b2);
     MVC_HIP(hipMalloc(&cub_tmp, cub_bytes));
-    st_host.assign(V + 4, 0);
+    st_host.assign(2 * V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
     {
@@ -1784,7 +1900,7 @@ class ParallelSampler : public Sampler {
     c.L2pt = own<double>(c, V);
     c.cnew = own<double>(c, V);
     c.Koff = own<int32_t>(c, V + 1);
-    c.status = own<int32_t>(c, V + 4);
+    c.status = own<int32_t>(c, 2 * V + 4);
     c.choice = own<int32_t>(c, n);
     c.flags = own<int32_t>(c, n);
     c.brank = own<int32_t>(c, n);
@@ -1804,6 +1920,15 @@ class ParallelSampler : public Sampler {
     c.tmp_nt = own<int32_t>(c, TC);
     c.lcnt = own<int32_t>(c, (size_t)V * KC);
     c.jmap = own<int32_t>(c, (size_t)V * KC);
+    c.dish_old = own<int32_t>(c, (size_t)V * TC);
+    c.dold = own<int32_t>(c, (size_t)V * n);
+    c.dnew = own<int32_t>(c, (size_t)V * n);
+    c.mflag = own<int32_t>(c, (size_t)V * n);
+    c.mlist = own<int32_t>(c, (size_t)V * n);
+    c.nsel = own<int32_t>(c, 1);
+    c.vlist = own<int32_t>(c, MVC_MAXV);
+    c.S1T_alt = own<double>(c, (size_t)V * D * KC);
+    c.S2_alt = own<double>(c, (size_t)V * KC);
     c.histT = own<int32_t>(c, (size_t)n + 2);
     c.histL = own<int32_t>(c, (size_t)V * (TC + 2));
     c.mh_half = (size_t)n / 64 + 128;
@@ -1851,7 +1976,7 @@ class ParallelSampler : public Sampler {
     up(P.Kact, c.K.data(), sizeof(int32_t) * V);
     up(P.next_id, next.data(), sizeof(int32_t) * V);
     up(P.hyper, hyp.data(), sizeof(double) * hyp.size());
-    std::vector<int32_t> st(V + 4, 0);
+    std::vector<int32_t> st(2 * V + 4, 0);
     st[0] = 4;
     up(c.status, st.data(), sizeof(int32_t) * st.size());
     MVC_HIP(hipStreamSynchronize(stream));
@@ -1866,15 +1991,14 @@ class ParallelSampler : public Sampler {
   }
 
   void upload_koff(Chain &c) {
-    std::vector<int32_t> ko(V + 1, 0);
-    for (int v = 0; v < V; ++v) ko[v + 1] = ko[v] + c.K[v];
-    MVC_HIP(hipMemcpyAsync(c.Koff, ko.data(), sizeof(int32_t) * ko.size(), hipMemcpyHostToDevice, stream));
-    // the copy source must outlive the async copy
-    MVC_HIP(hipStreamSynchronize(stream));
+    c.koff_h.assign(V + 1, 0);
+    for (int v = 0; v < V; ++v) c.koff_h[v + 1] = c.koff_h[v] + c.K[v];
+    MVC_HIP(hipMemcpyAsync(c.Koff, c.koff_h.data(), sizeof(int32_t) * (V + 1), hipMemcpyHostToDevice, stream));
   }
 
-  void rebuild_stats(Chain &c) {
-    upload_koff(c);
+
+  // Full chunked rebuild of the views in vmask.
+  void rebuild_views(Chain &c, uint64_t vmask) {
     const int sk = sumK(c);
     if ((size_t)sk > part_cap) {
       if (part1) hipFree(part1);
@@ -1886,17 +2010,19 @@ class ParallelSampler : public Sampler {
     int Kmax = 1;
     for (int k : c.K) Kmax = std::max(Kmax, k);
     const size_t lds = sizeof(int) * (2 * 4096 + (size_t)Kmax + 1);
-    const int dg = 0;
-    hipEvent_t ev = nullptr;
-    timers.begin("stats", &ev);
     hipLaunchKernelGGL(mvc_par_stats_partial_kernel, dim3(nchunk, V), dim3(256), lds, stream, c.P, (const double *)y,
-                       (const double *)Y2, (const int32_t *)c.Koff, (int)part_cap, dg, part1, part2);
+                       (const double *)Y2, (const int32_t *)c.Koff, (int)part_cap, vmask, part1, part2);
     MVC_HIP(hipGetLastError());
     const size_t tot = (size_t)sk * (D + 1);
     hipLaunchKernelGGL(mvc_par_stats_combine_kernel, dim3((unsigned)std::min<size_t>(4096, (tot + 255) / 256)), dim3(256),
-                       0, stream, c.P, (const int32_t *)c.Koff, (int)part_cap, nchunk, (const double *)part1,
+                       0, stream, c.P, (const int32_t *)c.Koff, (int)part_cap, nchunk, vmask, (const double *)part1,
                        (const double *)part2);
     MVC_HIP(hipGetLastError());
+  }
+
+  void tile_s1(Chain &c) {
+    int Kmax = 1;
+    for (int k : c.K) Kmax = std::max(Kmax, k);
     c.s1t_ok = false;
     if (SP > 0 && Kmax <= MVC_Z_KMAX) {
       if (!c.S1t) c.S1t = own<double>(c, (size_t)V * SP * 4 * 64);
@@ -1905,6 +2031,65 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipGetLastError());
       c.s1t_ok = true;
     }
+  }
+
+  // initial state / set_state: every view from scratch
+  void rebuild_stats(Chain &c) {
+    upload_koff(c);
+    hipEvent_t ev = nullptr;
+    timers.begin("stats", &ev);
+    rebuild_views(c, V >= 64 ? ~0ull : ((1ull << V) - 1));
+    tile_s1(c);
+    timers.end("stats", ev);
+  }
+
+  // After a commit: per view, a full rebuild if more than
+  // n/8 customers changed dish, else the surviving dishes' sums carried over
+  // through the compaction map plus the moves in ascending customer order.
+  void update_stats(Chain &c, const std::vector<int32_t> &Kold, const int32_t *moved) {
+    upload_koff(c);
+    hipEvent_t ev = nullptr;
+    timers.begin("stats", &ev);
+    StatsUpd U{};
+    U.V = V; U.D = D; U.KC = KC; U.n = n;
+    uint64_t full = 0;
+    std::vector<int32_t> inc;
+    for (int v = 0; v < V; ++v) {
+      U.Kold[v] = Kold[v];
+      U.Knew[v] = c.K[v];
+      U.M[v] = moved[v];
+      if ((int64_t)8 * moved[v] > (int64_t)n) full |= 1ull << v;
+      else inc.push_back(v);
+    }
+    // carry the sums over to the new dish numbering (all views; rebuilt views overwrite)
+    const size_t elems = (size_t)V * (D + 1) * KC;
+    const unsigned g = (unsigned)std::min<size_t>(4096, (elems + 255) / 256);
+    hipLaunchKernelGGL(mvc_par_stats_zero_kernel, dim3(g), dim3(256), 0, stream, U, c.S1T_alt, c.S2_alt);
+    hipLaunchKernelGGL(mvc_par_stats_scatter_kernel, dim3(g), dim3(256), 0, stream, U, (const int32_t *)c.jmap,
+                       (const double *)c.P.S1T, (const double *)c.P.S2, c.S1T_alt, c.S2_alt);
+    MVC_HIP(hipGetLastError());
+    std::swap(c.P.S1T, c.S1T_alt);
+    std::swap(c.P.S2, c.S2_alt);
+    if (!inc.empty()) {
+      int Kmax = 1;
+      for (int v : inc) {
+        Kmax = std::max(Kmax, c.K[v]);
+        if (moved[v] == 0) continue;
+        size_t bytes = cub_bytes;
+        hipcub::CountingInputIterator<int32_t> it(0);
+        MVC_HIP(hipcub::DeviceSelect::Flagged(cub_tmp, bytes, it, c.mflag + (size_t)v * n, c.mlist + (size_t)v * n,
+                                              c.nsel, n, stream));
+      }
+      c.vlist_h = inc;
+      MVC_HIP(hipMemcpyAsync(c.vlist, c.vlist_h.data(), sizeof(int32_t) * inc.size(), hipMemcpyHostToDevice,
+                             stream));
+      hipLaunchKernelGGL(mvc_par_stats_apply_kernel, dim3(Kmax, (unsigned)inc.size()), dim3(256), 0, stream, U,
+                         (const int32_t *)c.vlist, (const double *)y, (const double *)Y2, (const int32_t *)c.mlist,
+                         (const int32_t *)c.dold, (const int32_t *)c.dnew, c.P.S1T, c.P.S2);
+      MVC_HIP(hipGetLastError());
+    }
+    if (full) rebuild_views(c, full);
+    tile_s1(c);
     timers.end("stats", ev);
   }
 
@@ -1970,8 +2155,7 @@ class ParallelSampler : public Sampler {
   }
 
   void sweep_chain(Chain &c, uint32_t s) {
-    ensure_lp((size_t)sumK(c));
-    upload_koff(c);
+    ensure_lp((size_t)sumK(c));   // Koff is current: uploaded by the previous stats update
     Sweep A = make_sweep(c, s);
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     // phase 1 in customer batches: lp producer (MFMA or generic), then draw
@@ -2046,21 +2230,23 @@ class ParallelSampler : public Sampler {
     timers.begin("commit", &e1);
     hipLaunchKernelGGL(mvc_par_commit_kernel, dim3(1), dim3(256), 0, stream, c.P, c.T, (const int32_t *)c.cnt,
                        (const int32_t *)c.p2meta, (const int32_t *)c.p2_c, (const int32_t *)c.p2_tup, c.pos_new,
-                       c.tmp_dish, c.tmp_nt, c.lcnt, c.jmap, c.status);
+                       c.tmp_dish, c.tmp_nt, c.lcnt, c.jmap, c.status, c.dish_old);
     MVC_HIP(hipGetLastError());
     hipLaunchKernelGGL(mvc_par_relabel_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n, V,
-                       (const int32_t *)c.choice, (const int32_t *)c.pos_new, (const int32_t *)c.brank,
-                       (const int32_t *)c.btab, (const int32_t *)c.status, c.P.z);
+                       TC, KC, (const int32_t *)c.choice, (const int32_t *)c.pos_new, (const int32_t *)c.brank,
+                       (const int32_t *)c.btab, c.status, c.P.z, (const int32_t *)c.dish_old,
+                       (const int32_t *)c.jmap, (const int32_t *)c.P.dish, c.dold, c.dnew, c.mflag);
     MVC_HIP(hipGetLastError());
     timers.end("commit", e1);
     // the one host synchronisation of a sweep: new T and dish counts
-    MVC_HIP(hipMemcpyAsync(st_host.data(), c.status, sizeof(int32_t) * (V + 4), hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipMemcpyAsync(st_host.data(), c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
     MVC_HIP(hipStreamSynchronize(stream));
     if (st_host[V + 1] != 0)
       throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: table (4096) or dish (4095 per view) capacity exceeded");
+    const std::vector<int32_t> Kold = c.K;
     c.T = st_host[0];
     for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
-    rebuild_stats(c);
+    update_stats(c, Kold, st_host.data() + V + 4);
     launch_hyper(c, 1, s);
     (void)e2;
   }
@@ -2098,6 +2284,25 @@ class ParallelSampler : public Sampler {
   void get_dish_counts(int chain, int32_t *k_out) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
     for (int v = 0; v < V; ++v) k_out[v] = chains[chain].K[v];
+  }
+
+  void get_stats(int chain, int view, int32_t *K, double *S1, double *S2, int32_t *n_vk, int32_t cap) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    Chain &c = chains[chain];
+    MVC_HIP(hipStreamSynchronize(stream));
+    const int k = c.K[view];
+    if (K) *K = k;
+    const int m = std::min<int>(k, cap);
+    if (m <= 0) return;
+    if (S1) {
+      std::vector<double> row((size_t)D * KC);
+      MVC_HIP(hipMemcpy(row.data(), c.P.S1T + (size_t)view * D * KC, sizeof(double) * row.size(),
+                        hipMemcpyDeviceToHost));
+      for (int j = 0; j < m; ++j)
+        for (int d = 0; d < D; ++d) S1[(size_t)j * D + d] = row[(size_t)d * KC + j];
+    }
+    if (S2) MVC_HIP(hipMemcpy(S2, c.P.S2 + (size_t)view * KC, sizeof(double) * m, hipMemcpyDeviceToHost));
+    if (n_vk) MVC_HIP(hipMemcpy(n_vk, c.P.d_n + (size_t)view * KC, sizeof(int32_t) * m, hipMemcpyDeviceToHost));
   }
 
   void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of, const double *hyper) override {

@@ -85,6 +85,7 @@ def lib():
         "mvc_sampler_get_state": (i32, [vp, i32, ip, ip, ip, ctypes.c_int32, dp, cp, sz]),
         "mvc_sampler_get_dish_counts": (i32, [vp, i32, ip, cp, sz]),
         "mvc_sampler_set_state": (i32, [vp, i32, ip, ctypes.c_int32, ip, dp, cp, sz]),
+        "mvc_sampler_get_stats": (i32, [vp, i32, i32, ip, dp, dp, ip, ctypes.c_int32, cp, sz]),
         "mvc_sampler_kernel_time": (i32, [vp, cp, dp, lp]),
         "mvc_sampler_reset_timers": (None, [vp]),
         "mvc_sampler_zpath": (i32, [vp]),

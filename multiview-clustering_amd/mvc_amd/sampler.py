@@ -190,6 +190,23 @@ class Sampler:
                                                       buf, len(buf)), buf)
         return k
 
+    def stats(self, view, chain=0):
+        """Sufficient statistics of one view: dict S1 [K][D], S2 [K], n [K]
+        (live dishes in ascending raw id)."""
+        buf = L.errbuf()
+        K = ctypes.c_int32()
+        ip = ctypes.POINTER(ctypes.c_int32)
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.check(self._lib.mvc_sampler_get_stats(self._h, chain, view, ctypes.byref(K), None, None, None, 0, buf,
+                                                len(buf)), buf)
+        k = K.value
+        s1 = np.empty((max(k, 1), self.D))
+        s2 = np.empty(max(k, 1))
+        nk = np.empty(max(k, 1), dtype=np.int32)
+        L.check(self._lib.mvc_sampler_get_stats(self._h, chain, view, ctypes.byref(K), s1.ctypes.data_as(dp),
+                                                s2.ctypes.data_as(dp), nk.ctypes.data_as(ip), k, buf, len(buf)), buf)
+        return {"S1": s1[:k], "S2": s2[:k], "n": nk[:k]}
+
     def kernel_time(self, name):
         """(total_ms, launches) recorded with HIP events on the handle's stream."""
         ms = ctypes.c_double()

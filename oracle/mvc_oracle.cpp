@@ -88,6 +88,11 @@ struct Result {
   std::vector<double> alpha_g, sigma_g;    // S
   std::vector<int> trace_T;                // per sweep: T after the sweep
   std::vector<uint64_t> trace_draws;       // per sweep: sequential draws used so far
+  // final sufficient statistics (parallel sampler): per view, live dishes in
+  // ascending raw id; S1 [K][D], S2 [K], n_vk [K]
+  std::vector<std::vector<double>> fS1, fS2;
+  std::vector<std::vector<int>> fnk;
+  int D = 1;
   std::string error;
 };
 
@@ -723,7 +728,12 @@ struct ParallelSampler {
 
   // chunked ordered rebuild of n, S1, S2 from z/dish
   void rebuild_stats() {
-    for (int v = 0; v < V; ++v) {
+    for (int v = 0; v < V; ++v) rebuild_view(v);
+  }
+
+  // chunked ordered rebuild of one view
+  void rebuild_view(int v) {
+    {
       const int K = (int)ids[v].size();
       nk[v].assign(K, 0);
       S1[v].assign((size_t)K * D, 0.0);
@@ -1178,6 +1188,9 @@ struct ParallelSampler {
       for (int i = 0; i < n; ++i) z_new[i] = choice[i] >= 0 ? pos_new[choice[i]] : Tsurv + btab[b++];
     }
     (void)births;
+    const std::vector<int> z_old = z;
+    const std::vector<std::vector<int>> dish_old = dish;
+    std::vector<std::vector<int>> jmaps(V);
     for (int v = 0; v < V; ++v) {
       const int Kext = Kold[v] + nnew[v];
       std::vector<int> l(Kext, 0);
@@ -1194,12 +1207,62 @@ struct ParallelSampler {
       for (int p = 0; p < Tn; ++p) dext[v][p] = jmap[dext[v][p]];
       ids[v] = ids_new;
       lk[v] = l_new;
+      jmaps[v] = jmap;
     }
     T = Tn;
     n_t = nt_new;
     dish = dext;
     z = z_new;
-    rebuild_stats();
+    update_stats(z_old, dish_old, jmaps, Kold);
+  }
+
+  // Sufficient statistics after a commit.  Per view: the
+  // dishes that survive keep their sums (re-indexed by the compaction map),
+  // new dishes start at 0; then every customer whose dish changed moves its
+  // y from the old dish (if that dish survived) to the new one, in ascending
+  // customer order -- the reference's incremental remove/add updates
+  // (multiview_utils.cpp:155-157, 199-206).  If more than n/8 customers of
+  // the view changed dish, the view is rebuilt from scratch instead.
+  void update_stats(const std::vector<int> &z_old, const std::vector<std::vector<int>> &dish_old,
+                    const std::vector<std::vector<int>> &jmaps, const std::vector<int> &Kold) {
+    for (int v = 0; v < V; ++v) {
+      const int K = (int)ids[v].size();
+      const std::vector<int> &jmap = jmaps[v];
+      std::vector<int> dold(n), dnew(n);
+      int moved = 0;
+      for (int i = 0; i < n; ++i) {
+        dold[i] = jmap[dish_old[v][z_old[i]]];
+        dnew[i] = dish[v][z[i]];
+        if (dold[i] != dnew[i]) ++moved;
+      }
+#ifdef MVC_ORACLE_FORCE_REBUILD
+      if (true) {
+#else
+      if ((int64_t)8 * moved > (int64_t)n) {
+#endif
+        rebuild_view(v);
+        continue;
+      }
+      std::vector<double> s1((size_t)K * D, 0.0), s2(K, 0.0);
+      for (int j = 0; j < Kold[v]; ++j)
+        if (jmap[j] >= 0) {
+          for (int d = 0; d < D; ++d) s1[(size_t)jmap[j] * D + d] = S1[v][(size_t)j * D + d];
+          s2[jmap[j]] = S2[v][j];
+        }
+      for (int i = 0; i < n; ++i) {
+        if (dold[i] == dnew[i]) continue;
+        if (dold[i] >= 0) {
+          for (int d = 0; d < D; ++d) s1[(size_t)dold[i] * D + d] = s1[(size_t)dold[i] * D + d] - yv(v, i, d);
+          s2[dold[i]] = s2[dold[i]] - Y2[(size_t)v * n + i];
+        }
+        for (int d = 0; d < D; ++d) s1[(size_t)dnew[i] * D + d] = s1[(size_t)dnew[i] * D + d] + yv(v, i, d);
+        s2[dnew[i]] = s2[dnew[i]] + Y2[(size_t)v * n + i];
+      }
+      S1[v] = s1;
+      S2[v] = s2;
+      nk[v].assign(K, 0);
+      for (int i = 0; i < n; ++i) nk[v][dnew[i]]++;
+    }
   }
 
   // ---- parallel-mode hyperparameter MH ----
@@ -1409,6 +1472,7 @@ void *mvo_run(const double *y, int n, int V, int D, int M, int burn_in, int thin
       P.init_rng = SeqRng{seed, (uint32_t)chain, 0};
       P.initialize();
       P.run(M, burn_in, thin, *R);
+      R->fS1 = P.S1; R->fS2 = P.S2; R->fnk = P.nk; R->D = D;
     }
   } catch (const std::exception &e) {
     R->error = e.what();
@@ -1445,11 +1509,24 @@ void *mvo_run_from(const double *y, int n, int V, int D, int M, int burn_in, int
       P.init_rng = SeqRng{seed, (uint32_t)chain, 0};
       P.load_state(table_of, T, dish_of, hyper);
       P.run(M, burn_in, thin, *R);
+      R->fS1 = P.S1; R->fS2 = P.S2; R->fnk = P.nk; R->D = D;
     }
   } catch (const std::exception &e) {
     R->error = e.what();
   }
   return R;
+}
+
+int mvo_stats_K(void *h, int v) {
+  Result *R = (Result *)h;
+  return v < (int)R->fnk.size() ? (int)R->fnk[v].size() : 0;
+}
+void mvo_copy_stats(void *h, int v, double *S1, double *S2, int *nk) {
+  Result *R = (Result *)h;
+  const size_t K = R->fnk[v].size();
+  memcpy(S1, R->fS1[v].data(), sizeof(double) * K * R->D);
+  memcpy(S2, R->fS2[v].data(), sizeof(double) * K);
+  memcpy(nk, R->fnk[v].data(), sizeof(int) * K);
 }
 
 const char *mvo_error(void *h) {

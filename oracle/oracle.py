@@ -49,6 +49,9 @@ def lib():
         L.mvo_copy_hyper.argtypes = [vp, dp, dp, dp, dp, dp]
         L.mvo_copy_trace.argtypes = [vp, ip, ctypes.POINTER(ctypes.c_uint64)]
         L.mvo_free.argtypes = [vp]
+        L.mvo_stats_K.restype = i32
+        L.mvo_stats_K.argtypes = [vp, i32]
+        L.mvo_copy_stats.argtypes = [vp, i32, dp, dp, ip]
         for f in ("mvo_pm_exp", "mvo_pm_log", "mvo_pm_lgamma", "mvo_pm_qnorm"):
             getattr(L, f).argtypes = [dp, dp, i64]
         L.mvo_philox.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.c_uint32,
@@ -107,6 +110,13 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=Non
         av, sv, tv = (np.empty(S * V) for _ in range(3))
         ag, sg = np.empty(S), np.empty(S)
         L.mvo_copy_hyper(h, _dp(av), _dp(sv), _dp(tv), _dp(ag), _dp(sg))
+        stats = []
+        for v in range(V):
+            K = L.mvo_stats_K(h, v)
+            if K:
+                s1, s2, nk = np.empty((K, D)), np.empty(K), np.empty(K, dtype=np.int32)
+                L.mvo_copy_stats(h, v, _dp(s1), _dp(s2), nk.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+                stats.append({"S1": s1, "S2": s2, "n": nk})
         nsw = L.mvo_num_sweeps(h)
         tT = np.empty(nsw, dtype=np.int32)
         td = np.empty(nsw, dtype=np.uint64)
@@ -122,6 +132,7 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=Non
             "sigma_global": sg,
             "trace_T": tT,
             "trace_draws": td,
+            "stats": stats,            # parallel mode: final S1 [K][D], S2, n per view
         }
     finally:
         L.mvo_free(h)

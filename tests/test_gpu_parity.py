@@ -338,3 +338,28 @@ def test_c_abi_example_matches_python_path(tmp_path):
     assert np.array_equal(tab, ref["table_of"][-1])
     assert np.array_equal(dish, np.stack(ref["dish_of"][-1]))
     assert np.array_equal(ag, ref["alpha_global"])
+
+
+# ------------------------------------------ sufficient statistics
+@pytest.mark.parametrize("D,path", [(32, 2), (3, 0)])
+def test_parallel_stats_bitwise_vs_oracle(D, path, monkeypatch):
+    """S1, S2, n of every view after warm-started sweeps (incremental updates
+    at steady state, full rebuilds when more than n/8 customers move)."""
+    m = _mvc()
+    from mvc_amd import data
+    V, K = 3, 16
+    y, z = data.synthetic(4000, V, D, K, seed=40 + D)
+    st = _warm_state(z, V, K)
+    monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
+    s = m.Sampler(y, seed=13, mode="parallel")
+    s.set_state(*st)
+    s.sweep(6)
+    assert s.zpath() == path
+    ref = O.run(y, 6, 0, 1, 13, mode=O.PARALLEL, state=st)
+    for v in range(V):
+        g = s.stats(v)
+        r = ref["stats"][v]
+        assert np.array_equal(g["n"], r["n"]), v
+        assert np.array_equal(g["S1"], r["S1"]), v
+        assert np.array_equal(g["S2"], r["S2"]), v
+    s.close()
