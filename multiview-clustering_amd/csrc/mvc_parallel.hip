@@ -1446,69 +1446,32 @@ struct BlockCtx {
   size_t half;      // scratch half size
 };
 
-// tree64 over n leaves produced by leaf(e), executed by the whole block.
-// Level partials ping-pong between the two halves of ctx.scratch.
+// tree64 over n <= 4096 leaves produced by leaf(e), executed by the whole
+// block of 256; the 64-leaf chunk sums go through LDS (second level = one
+// butterfly over <= 64 partials).  Same association as oracle Tree64::build.
 template <class F>
-__device__ double block_tree64(const BlockCtx &ctx, int64_t n, F leaf) {
+__device__ double block_tree64(int64_t n, F leaf) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ double s_part[64];
   __shared__ double s_root;
   if (n <= 0) return 0.0;
-  double *src = nullptr;
-  double *dst = ctx.scratch;
-  int64_t m = (n + 63) / 64;
-  for (int64_t c = w; c < m; c += 4) {
-    const int64_t e = c * 64 + lane;
+  const int m = (int)((n + 63) / 64);
+  for (int c = w; c < m; c += 4) {
+    const int64_t e = (int64_t)c * 64 + lane;
     const double x = e < n ? leaf(e) : 0.0;
     const double s = wave_tree_sum(x);
-    if (lane == 0) dst[c] = s;
+    if (lane == 0) s_part[c] = s;
   }
   __syncthreads();
-  while (m > 1) {
-    src = dst;
-    dst = (src == ctx.scratch) ? ctx.scratch + ctx.half : ctx.scratch;
-    const int64_t m2 = (m + 63) / 64;
-    for (int64_t c = w; c < m2; c += 4) {
-      const int64_t e = c * 64 + lane;
-      const double x = e < m ? src[e] : 0.0;
-      const double s = wave_tree_sum(x);
-      if (lane == 0) dst[c] = s;
-    }
-    __syncthreads();
-    m = m2;
+  if (w == 0) {
+    const double x = lane < m ? s_part[lane] : 0.0;
+    const double r = (m == 1) ? x : wave_tree_sum(x);
+    if (lane == 0) s_root = (m == 1) ? s_part[0] : r;
   }
-  if (tid == 0) s_root = dst[0];
   __syncthreads();
   const double r = s_root;
   __syncthreads();
   return r;
-}
-
-// In-place exclusive SUFFIX scan of a[0..len) by the whole block:
-// a[m] <- sum_{s > m} a[s].  Integer, so any order gives the same result.
-__device__ void block_suffix_exclusive(int32_t *a, int len) {
-  __shared__ int sc[256];
-  __shared__ int carry;
-  const int tid = threadIdx.x;
-  if (tid == 0) carry = 0;
-  __syncthreads();
-  for (int top = len - 1; top >= 0; top -= 256) {
-    const int m = top - tid;              // descending within the chunk
-    const int x = m >= 0 ? a[m] : 0;
-    sc[tid] = x;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {
-      const int t = tid >= off ? sc[tid - off] : 0;
-      __syncthreads();
-      sc[tid] += t;
-      __syncthreads();
-    }
-    const int incl = sc[tid];
-    const int c0 = carry;
-    __syncthreads();
-    if (m >= 0) a[m] = c0 + incl - x;
-    if (tid == 255) carry = c0 + incl;
-    __syncthreads();
-  }
 }
 
 struct MHArgs {
@@ -1516,10 +1479,6 @@ struct MHArgs {
   int32_t *status;        // [V+3]: T, K[V], err, NB  -> we add T_ne at status[V+3]
   int32_t *Koff;          // [V+1] (output)
   double *L2pt, *cnew;    // [V] (output)
-  int32_t *histT;         // [n+2] scratch: c_m for tables
-  int32_t *histL;         // [V*(TC+2)] scratch: c_m for dishes
-  double *scratch;        // tree levels
-  size_t half;
   uint64_t seed;
   uint32_t chain, sweep;
   int do_mh;
@@ -1531,19 +1490,34 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
   ParState &P = A.P;
   const int tid = threadIdx.x;
   const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
-  __shared__ double s_red[8];
-  __shared__ double s_b[4];
   __shared__ int s_i[8];
-  BlockCtx ctx{s_red, A.scratch, A.half};
   const int T = A.status[0];
-  // ---- Q = ||S1||^2 per live dish, Ltot, Koff ----
-  for (int v = 0; v < V; ++v) {
-    const int K = P.Kact[v];
-    for (int j = tid; j < K; j += 256) {
+  // ---- Q = ||S1||^2 per live dish (fma chain in d order), all views at once;
+  //      the strided S1 loads are issued 16 ahead of the chain ----
+  {
+    __shared__ int s_koff[MVC_MAXV + 1];
+    if (tid == 0) {
+      s_koff[0] = 0;
+      for (int v = 0; v < V; ++v) s_koff[v + 1] = s_koff[v] + P.Kact[v];
+    }
+    __syncthreads();
+    for (int k = tid; k < s_koff[V]; k += 256) {
+      int v = 0;
+      while (k >= s_koff[v + 1]) ++v;
+      const int j = k - s_koff[v];
+      const double *col = P.S1T + (size_t)v * D * KC + j;
       double q = 0.0;
-      for (int d = 0; d < D; ++d) {
-        const double s = P.S1T[((size_t)v * D + d) * KC + j];
-        q = __builtin_fma(s, s, q);
+      int d = 0;
+      for (; d + 16 <= D; d += 16) {
+        double x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = col[(size_t)(d + u) * KC];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) q = __builtin_fma(x[u], x[u], q);
+      }
+      for (; d < D; ++d) {
+        const double x = col[(size_t)d * KC];
+        q = __builtin_fma(x, x, q);
       }
       P.Q[v * KC + j] = q;
     }
@@ -1554,56 +1528,18 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       for (int j = 0; j < P.Kact[v]; ++j) lt += P.d_l[v * KC + j];
       P.Ltot[v] = lt;
     }
-    int tne = 0, maxn = 0;
-    for (int p = 0; p < T; ++p) { if (P.n_t[p] > 0) ++tne; maxn = max(maxn, P.n_t[p]); }
+    int tne = 0;
+    for (int p = 0; p < T; ++p)
+      if (P.n_t[p] > 0) ++tne;
     s_i[0] = tne;
-    s_i[1] = maxn;
     A.status[V + 3] = tne;
   }
   __syncthreads();
-  const int maxn = s_i[1];
   double *hyp = P.hyper;
   if (A.do_mh) {
-    // c_m = #{tables with n_t > m}, m = 0..maxn
-    for (int m = tid; m <= maxn + 1; m += 256) A.histT[m] = 0;
-    __syncthreads();
-    for (int p = tid; p < T; p += 256) atomicAdd(&A.histT[P.n_t[p]], 1);
-    __syncthreads();
-    block_suffix_exclusive(A.histT, maxn + 1);   // c_m = sum_{s > m} hist[s]
-    for (int v = 0; v < V; ++v) {
-      int *hl = A.histL + (size_t)v * (TC + 2);
-      for (int m = tid; m < TC + 2; m += 256) hl[m] = 0;
-    }
-    __syncthreads();
-    int maxl_loc = 0;
-    for (int v = 0; v < V; ++v) {
-      int *hl = A.histL + (size_t)v * (TC + 2);
-      for (int j = tid; j < P.Kact[v]; j += 256) atomicAdd(&hl[P.d_l[v * KC + j]], 1);
-    }
-    __syncthreads();
-    for (int v = 0; v < V; ++v) {
-      int *hl = A.histL + (size_t)v * (TC + 2);
-      int mx = 0;
-      for (int j = tid; j < P.Kact[v]; j += 256) mx = max(mx, P.d_l[v * KC + j]);
-      for (int m = 32; m >= 1; m >>= 1) mx = max(mx, __shfl_xor(mx, m, 64));
-      if ((tid & 63) == 0) s_i[2 + (tid >> 6)] = mx;
-      __syncthreads();
-      mx = max(max(s_i[2], s_i[3]), max(s_i[4], s_i[5]));
-      __syncthreads();
-      block_suffix_exclusive(hl, mx + 1);
-      if (tid == 0) hl[TC + 1] = mx;   // stash max l
-      __syncthreads();
-    }
-    (void)maxl_loc;
-
     uint32_t kdraw = 0;
-    auto unif = [&]() -> double {   // block-uniform
-      if (tid == 0) s_b[0] = mvc_uniform(A.seed, kdraw, A.sweep, A.chain, MVC_TAG_MH);
-      __syncthreads();
-      const double u = s_b[0];
-      __syncthreads();
-      ++kdraw;
-      return u;
+    auto unif = [&]() -> double {   // block-uniform: every thread draws the same counter
+      return mvc_uniform(A.seed, kdraw++, A.sweep, A.chain, MVC_TAG_MH);
     };
     auto rnorm = [&](double mu, double sd) -> double {
       const double u1 = unif();
@@ -1626,36 +1562,34 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       }
       return p < kEps ? kEps : (p > 1.0 - kEps ? 1.0 - kEps : p);
     };
-    // EPPF of a partition: K blocks, total tot, counts c_m (exclusive suffix),
-    // max block size mx.
-    auto eppf = [&](int K, int tot, const int *cm, int mx, double a, double s) -> double {
+    // EPPF of a partition: K blocks of sizes size(j) >= 1, total tot
+    auto eppf = [&](int K, int tot, auto size, double a, double s) -> double {
       if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
       if (a <= -s) return -MVC_PM_INF;
       // any term a + j s <= 0 ?  (monotone in j for s > 0: check j = 0)
       if (K > 0 && !(a + 0.0 * s > 0.0)) return -MVC_PM_INF;
-      const double P1 = block_tree64(ctx, K, [&](int64_t j) { return mvc_log(a + (double)j * s); });
+      const double P1 = block_tree64(K, [&](int64_t j) { return mvc_log(a + (double)j * s); });
       const double P2 = mvc_lgamma_pos(a + (double)tot) - mvc_lgamma_pos(a + 1.0);
-      const double P3 = block_tree64(ctx, mx > 1 ? mx - 1 : 0,
-                                     [&](int64_t e) { const int m = (int)e + 1; return (double)cm[m] * mvc_log((double)m - s); });
+      const double lg1 = mvc_lgamma_pos(1.0 - s);
+      const double P3 = block_tree64(K, [&](int64_t j) { return mvc_lgamma_pos((double)size((int)j) - s) - lg1; });
       return (P1 - P2) + P3;
     };
     auto eppf_view = [&](int v, double a, double s) -> double {
       if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
       if (a <= -s) return -MVC_PM_INF;
       if (P.Ltot[v] == 0) return 0.0;
-      const int *hl = A.histL + (size_t)v * (TC + 2);
-      return eppf(P.Kact[v], P.Ltot[v], hl, hl[TC + 1], a, s);
+      return eppf(P.Kact[v], P.Ltot[v], [&](int j) { return P.d_l[v * KC + j]; }, a, s);
     };
     auto eppf_global = [&](double a, double s) -> double {
       if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
       if (a <= -s) return -MVC_PM_INF;
       if (T <= 0) return 0.0;
-      return eppf(T, n, A.histT, maxn, a, s);
+      return eppf(T, n, [&](int p) { return P.n_t[p]; }, a, s);
     };
     auto post_tau = [&](int v, double t) -> double {
       if (t <= 0.0) return -MVC_PM_INF;
       const double L = mvc_log((2.0 * MVC_PI) * t);
-      const double ll = block_tree64(ctx, P.Kact[v], [&](int64_t j) {
+      const double ll = block_tree64(P.Kact[v], [&](int64_t j) {
         const int nk = P.d_n[v * KC + j];
         if (nk == 0) return 0.0;
         double sse = P.S2[v * KC + j] - P.Q[v * KC + j] / (double)nk;
@@ -1779,9 +1713,7 @@ class ParallelSampler : public Sampler {
     int32_t *cnt = nullptr, *pos_new = nullptr, *tmp_dish = nullptr, *tmp_nt = nullptr;
     int32_t *p2meta = nullptr, *p2_c = nullptr, *p2_tup = nullptr, *n2 = nullptr, *l2 = nullptr, *btab = nullptr;
     double *S1_2T = nullptr, *lp2 = nullptr;
-    int32_t *lcnt = nullptr, *jmap = nullptr, *histT = nullptr, *histL = nullptr;
-    double *mh_scratch = nullptr;
-    size_t mh_half = 0;
+    int32_t *lcnt = nullptr, *jmap = nullptr;
     double *S1t = nullptr;         // MFMA B-fragment layout of S1 (K_v <= 64)
     int32_t *dish_old = nullptr;   // [V*TC] table -> dish before the commit
     int32_t *dold = nullptr, *dnew = nullptr, *mflag = nullptr, *mlist = nullptr;   // [V*n]
@@ -1929,10 +1861,6 @@ class ParallelSampler : public Sampler {
     c.vlist = own<int32_t>(c, MVC_MAXV);
     c.S1T_alt = own<double>(c, (size_t)V * D * KC);
     c.S2_alt = own<double>(c, (size_t)V * KC);
-    c.histT = own<int32_t>(c, (size_t)n + 2);
-    c.histL = own<int32_t>(c, (size_t)V * (TC + 2));
-    c.mh_half = (size_t)n / 64 + 128;
-    c.mh_scratch = own<double>(c, 2 * c.mh_half);
   }
 
   void init_chain(Chain &c, uint32_t gid, const double *yh) {
@@ -2100,10 +2028,6 @@ class ParallelSampler : public Sampler {
     A.Koff = c.Koff;
     A.L2pt = c.L2pt;
     A.cnew = c.cnew;
-    A.histT = c.histT;
-    A.histL = c.histL;
-    A.scratch = c.mh_scratch;
-    A.half = c.mh_half;
     A.seed = cfg.seed;
     A.chain = c.gid;
     A.sweep = sweep_ix;

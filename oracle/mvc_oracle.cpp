@@ -1296,14 +1296,11 @@ struct ParallelSampler {
     }
     const double P1 = tree64_sum(t1);
     const double P2 = mvc_lgamma_pos(a + (double)tot) - mvc_lgamma_pos(a + 1.0);
-    int mx = 0;
-    for (int c : sz) mx = std::max(mx, c);
-    std::vector<double> t3(mx > 1 ? mx - 1 : 0);
-    for (int m = 1; m < mx; ++m) {
-      int c = 0;
-      for (int b : sz) if (b > m) ++c;
-      t3[m - 1] = (double)c * mvc_log((double)m - s);
-    }
+    // sum_j sum_{m=1}^{sz_j - 1} log(m - s) (multiview_hyper.cpp:325-336) as
+    // sum_j [lgamma(sz_j - s) - lgamma(1 - s)], block order, tree64
+    const double lg1 = mvc_lgamma_pos(1.0 - s);
+    std::vector<double> t3(K);
+    for (int j = 0; j < K; ++j) t3[j] = mvc_lgamma_pos((double)sz[j] - s) - lg1;
     const double P3 = tree64_sum(t3);
     return (P1 - P2) + P3;
   }
