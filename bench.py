@@ -201,7 +201,8 @@ def main():
                 "mfma_tflops": round(tflops, 3), "mfma_frac": round(tflops / PEAK_F64_TFLOPS, 4),
                 "arith_intensity": round(flops_alg / bytes_alg, 3), "ridge": round(ridge, 3),
                 "bytes_per_launch": bytes_alg, "flops_per_launch": flops_alg, "pass_ms": round(k_avg_s * 1e3, 4),
-                "lp_producer": "mfma" if zpath == 2 else "generic"},
+                "lp_producer": "mfma" if (zpath & 3) == 2 else "generic",
+                "draw": "registers" if zpath & 4 else "lds-checkpoints"},
         "hyper_pooled_mean": {"chains": pooled_n, "alpha_global": round(float(pooled_mean[-2]), 6),
                               "sigma_global": round(float(pooled_mean[-1]), 6)},
         "nvk_sweeps_per_s": round(value * N * V * K, 1),

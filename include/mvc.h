@@ -137,10 +137,11 @@ int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms,
                             int64_t *launches);
 void mvc_sampler_reset_timers(mvc_sampler *s);
-/* z-resample kernel used by the last parallel sweep: 0 generic (one wave per
- * customer), 1 per-wave MFMA tiles, 2 block-lockstep MFMA tiles; -1 for the
- * exact schedule or before the first sweep.  (No reference counterpart:
- * diagnostics of this implementation.) */
+/* z-resample kernels used by the last parallel sweep: bits 0-1 the lp
+ * producer (0 generic, one lane per customer; 2 per-view MFMA tiles), bit 2
+ * set when the register-resident draw kernel ran (T <= 64, K_v <= 64);
+ * -1 for the exact schedule or before the first sweep.  (No reference
+ * counterpart: diagnostics of this implementation.) */
 int mvc_sampler_zpath(mvc_sampler *s);
 /* Opaque HIP stream the handle launches on (hipStream_t as void*). */
 void *mvc_sampler_stream(mvc_sampler *s);

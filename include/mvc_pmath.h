@@ -48,6 +48,41 @@ MVC_PM double mvc_u2d(uint64_t u) { double x; __builtin_memcpy(&x, &u, 8); retur
 #define MVC_PI 3.14159265358979323846          /* M_PI as used by the reference */
 
 MVC_PM double mvc_exp(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* Device: the same value without branches (divergence-free; 64 unrolled
+   * calls in the draw kernel would otherwise spill exec masks).  The three
+   * scalings below all equal the correctly rounded e * 2^k, which is what
+   * v_ldexp_f64 computes; the range checks become selects. */
+  {
+    const double shifter = 6755399441055744.0;
+    double kd = x * MVC_INVLN2;
+    kd = kd + shifter;
+    kd = kd - shifter;
+    kd = __builtin_fmin(__builtin_fmax(kd, -1100.0), 1100.0);
+    const int k = (int)kd;
+    double r = __builtin_fma(-kd, MVC_LN2_HI, x);
+    r = __builtin_fma(-kd, MVC_LN2_LO, r);
+    double p = 1.1470745597729725e-11;
+    p = __builtin_fma(p, r, 1.6059043836821613e-10);
+    p = __builtin_fma(p, r, 2.08767569878681e-09);
+    p = __builtin_fma(p, r, 2.505210838544172e-08);
+    p = __builtin_fma(p, r, 2.755731922398589e-07);
+    p = __builtin_fma(p, r, 2.7557319223985893e-06);
+    p = __builtin_fma(p, r, 2.48015873015873e-05);
+    p = __builtin_fma(p, r, 0.0001984126984126984);
+    p = __builtin_fma(p, r, 0.001388888888888889);
+    p = __builtin_fma(p, r, 0.008333333333333333);
+    p = __builtin_fma(p, r, 0.041666666666666664);
+    p = __builtin_fma(p, r, 0.16666666666666666);
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    const double e = __builtin_fma(p, r, 1.0);
+    double res = __builtin_amdgcn_ldexp(e, k);
+    res = (x > 709.782712893384) ? MVC_PM_INF : res;
+    res = (x < -745.1332191019412) ? 0.0 : res;
+    return (x == x) ? res : x + x;
+  }
+#endif
   if (!(x == x)) return x + x;
   if (x > 709.782712893384) return MVC_PM_INF;
   if (x < -745.1332191019412) return 0.0;

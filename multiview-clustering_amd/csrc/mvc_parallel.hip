@@ -949,6 +949,198 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
   }
 }
 
+// Register-resident draw for T <= TM tables and K_v <= 64 dishes (the common
+// case): same arithmetic, same order as mvc_par_zdraw_kernel, but each view's
+// lp row is loaded once into registers (the max and the sum both read them)
+// and the table scores live in registers, so the table phase is ONE gather
+// pass (V loads per table) instead of 2.25; the running cumulative weights
+// overwrite the scores and the pick is the first p with r < cum_p.  An
+// excluded table adds +0.0, which leaves the running sum bit-identical.
+template <int KB>
+__device__ __forceinline__ void zview_reg(const double *lpv, int K, int j0, int l0p, const int *dl, double lfn,
+                                          double sigma, double &m_out, double &S_out) {
+  double x[KB];
+#pragma unroll
+  for (int j = 0; j < KB; ++j) x[j] = lpv[(size_t)min(j, K - 1) * 16];
+  double m = -MVC_PM_INF;
+#pragma unroll
+  for (int j = 0; j < KB; ++j) {
+    if (j < K) {
+      const int l = (j == j0) ? l0p : dl[j];
+      if (l > 0 && x[j] > m) m = x[j];
+    }
+  }
+  if (lfn > m) m = lfn;
+  double S = 0.0;
+#pragma unroll
+  for (int j = 0; j < KB; ++j) {
+    if (j < K) {
+      const int l = (j == j0) ? l0p : dl[j];
+      double w = (double)l - sigma;
+      if (w < 0.0) w = 0.0;
+      double xe = x[j] - m;
+      asm volatile("" : "+v"(xe) : "v"(S));      // one exp in flight (register pressure)
+      const double t = l > 0 ? w * mvc_exp(xe) : -1.0;
+      if (t >= 0.0) S = S + t;
+    }
+  }
+  m_out = m;
+  S_out = S;
+}
+
+// Same reduction with the row streamed twice in batches of 8 (any K).
+__device__ __forceinline__ void zview_loop(const double *lpv, int K, int j0, int l0p, const int *dl, double lfn,
+                                           double sigma, double &m_out, double &S_out) {
+  double m = -MVC_PM_INF;
+  int j = 0;
+  for (; j + 8 <= K; j += 8) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int l = (j + u == j0) ? l0p : dl[j + u];
+      if (l > 0 && x[u] > m) m = x[u];
+    }
+  }
+  for (; j < K; ++j) {
+    const int l = (j == j0) ? l0p : dl[j];
+    const double x = lpv[(size_t)j * 16];
+    if (l > 0 && x > m) m = x;
+  }
+  if (lfn > m) m = lfn;
+  double S = 0.0;
+  j = 0;
+  for (; j + 8 <= K; j += 8) {
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int l = (j + u == j0) ? l0p : dl[j + u];
+      double w = (double)l - sigma;
+      if (w < 0.0) w = 0.0;
+      x[u] = l > 0 ? w * mvc_exp(x[u] - m) : -1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (x[u] >= 0.0) S = S + x[u];
+  }
+  for (; j < K; ++j) {
+    const int l = (j == j0) ? l0p : dl[j];
+    double w = (double)l - sigma;
+    if (w < 0.0) w = 0.0;
+    const double e = mvc_exp(l > 0 ? lpv[(size_t)j * 16] - m : 0.0);
+    if (l > 0) S = S + w * e;
+  }
+  m_out = m;
+  S_out = S;
+}
+
+template <int TM>
+__global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
+  const int T = __builtin_amdgcn_readfirstlane(A.T);
+  const int tid = threadIdx.x;
+  double *s_base = (double *)smem;                 // [T] log mass (or -inf)
+  int *s_tix = (int *)(s_base + TM);               // [T][V] Koff[v] + dish_v(p)
+  int *s_koff = s_tix + (size_t)TM * V;            // [V+1]
+  int *s_dl = s_koff + V + 1;                      // [sumK] l of each dish
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  if (tid <= V) s_koff[tid] = A.Koff[tid];
+  __syncthreads();
+  const int sumK = s_koff[V];
+  for (int p = tid; p < T; p += blockDim.x) {
+    const int np = P.n_t[p];
+    s_base[p] = (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
+    for (int v = 0; v < V; ++v) s_tix[p * V + v] = s_koff[v] + P.dish[v * TC + p];
+  }
+  for (int k = tid; k < sumK; k += blockDim.x) {
+    int v = 0;
+    while (v + 1 < V && s_koff[v + 1] <= k) ++v;
+    s_dl[k] = P.d_l[v * KC + (k - s_koff[v])];
+  }
+  __syncthreads();
+  const int T_ne = A.status[V + 3];
+  {
+    const int li = blockIdx.x * blockDim.x + tid;   // one customer per thread (no loop-invariant hoisting)
+    if (li >= nb) return;
+    const int i = b0 + li;
+    const int p0 = P.z[i];
+    const bool alive = (P.n_t[p0] - 1) > 0;
+    const double *lpi = lpb + lpb_index(li, 0, sumK);   // dish k at lpi[k * 16]
+    double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+    for (int v = 0; v < V; ++v) {
+      const int koff = __builtin_amdgcn_readfirstlane(s_koff[v]);
+      const int K = __builtin_amdgcn_readfirstlane(s_koff[v + 1]) - koff;
+      const int j0 = s_tix[p0 * V + v] - koff;
+      const double sigma = P.hyper[2 * V + v];
+      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+      const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
+      const int *dl = s_dl + koff;
+      const double *lpv = lpi + (size_t)koff * 16;
+      double m, S;
+      if (K <= 8) zview_reg<8>(lpv, K, j0, l0p, dl, lfn, sigma, m, S);          // row in registers
+      else if (K <= 16) zview_reg<16>(lpv, K, j0, l0p, dl, lfn, sigma, m, S);
+      else zview_loop(lpv, K, j0, l0p, dl, lfn, sigma, m, S);                    // streamed twice
+      const int Kact = K - ((l0p == 0) ? 1 : 0);
+      double wn = P.hyper[V + v] + (double)Kact * sigma;
+      if (wn < 0.0) wn = 0.0;
+      S = S + wn * mvc_exp(lfn - m);
+      const double denom = P.hyper[V + v] + (double)(P.Ltot[v] - (alive ? 0 : 1));
+      const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
+      s_new = s_new + lm;
+    }
+    const int np0 = P.n_t[p0] - 1;
+    const double m0 = (double)np0 - sg;
+    const double base_self = (np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
+    // table scores in view order, 16 tables' gathers in flight per step
+    double sp[TM];
+#pragma unroll
+    for (int p = 0; p < TM; ++p) {
+      const int pc = min(p, T - 1);
+      sp[p] = (pc == p0) ? base_self : s_base[pc];
+    }
+#pragma unroll
+    for (int c = 0; c < TM; c += 16) {
+      for (int v = 0; v < V; ++v) {
+        double x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = lpi[(size_t)s_tix[min(c + u, T - 1) * V + v] * 16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
+      }
+    }
+    double M = -MVC_PM_INF;
+#pragma unroll
+    for (int p = 0; p < TM; ++p)
+      if (p < T && sp[p] > M) M = sp[p];
+    if (s_new > M) M = s_new;
+    double cum = 0.0;
+#pragma unroll
+    for (int p = 0; p < TM; ++p) {
+      const bool in = p < T && sp[p] != -MVC_PM_INF;
+      double xe = in ? sp[p] - M : 0.0;
+      asm volatile("" : "+v"(xe) : "v"(cum));     // order: one exp in flight, not 64 live
+      const double e = mvc_exp(xe);
+      cum = cum + (in ? e : 0.0);
+      sp[p] = cum;                                 // running cumulative weight
+    }
+    const double W = mvc_exp(s_new - M) + cum;
+    const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+    int pick = -1;
+#pragma unroll
+    for (int p = 0; p < TM; ++p)
+      if (pick < 0 && p < T && r < sp[p]) pick = p;
+    A.choice[i] = pick;
+  }
+}
+__host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
+  return 8 * (size_t)TM + 4 * ((size_t)V * TM + (size_t)sumK + (size_t)V + 1) + 64;
+}
+
 // Phase 2: births resolved sequentially in ascending
 // customer order by ONE wavefront.  Each birth joins a table born earlier in
 // this sweep or opens one (dish per view from frozen + phase-2 + new dishes).
@@ -1739,6 +1931,7 @@ class ParallelSampler : public Sampler {
   size_t cub_bytes = 0;
   std::vector<int32_t> st_host;
   bool force_generic = false;
+  bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   int n_cu = 256;
 
   template <class Tp>
@@ -1783,6 +1976,8 @@ class ParallelSampler : public Sampler {
     st_host.assign(2 * V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
+    const char *zl = getenv("MVC_ZDRAW_LDS");
+    force_zdraw_lds = zl && zl[0] == '1';
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
@@ -2099,7 +2294,8 @@ class ParallelSampler : public Sampler {
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap);
     }
-    if (zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
+    const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
+    if (!use_zreg && zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
       throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: V x tables too large for the draw kernel's LDS tables");
     timers.begin("zresample", &e0);
     for (size_t b0 = 0; b0 < (size_t)n; b0 += nbatch_sz) {
@@ -2128,13 +2324,24 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipGetLastError());
       timers.end("lp", el);
       timers.begin("draw", &ed);
-      hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
-                         zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb);
+      const dim3 zg((nb + 255) / 256);   // the register kernel takes one customer per thread
+      if (use_zreg && c.T <= 16)
+        hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<16>, zg, dim3(256), zdraw_reg_shared_bytes(V, 16, sk), stream, A,
+                           (int)b0, nb, (const double *)lpb);
+      else if (use_zreg && c.T <= 32)
+        hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<32>, zg, dim3(256), zdraw_reg_shared_bytes(V, 32, sk), stream, A,
+                           (int)b0, nb, (const double *)lpb);
+      else if (use_zreg)
+        hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<64>, zg, dim3(256), zdraw_reg_shared_bytes(V, 64, sk), stream, A,
+                           (int)b0, nb, (const double *)lpb);
+      else
+        hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
+                           zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb);
       MVC_HIP(hipGetLastError());
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
-    zpath = use_mfma ? 2 : 0;
+    zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0);
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
     hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, n, c.T,

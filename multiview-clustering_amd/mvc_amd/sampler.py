@@ -217,8 +217,9 @@ class Sampler:
         return ms.value, cnt.value
 
     def zpath(self):
-        """z-resample kernel of the last parallel sweep (0 generic, 1 per-wave
-        MFMA, 2 block-lockstep MFMA; -1 exact schedule / no sweep yet)."""
+        """z-resample kernels of the last parallel sweep: bits 0-1 the lp
+        producer (0 generic, 2 MFMA), bit 2 the register-resident draw kernel;
+        -1 exact schedule / no sweep yet."""
         return int(self._lib.mvc_sampler_zpath(self._h))
 
     def reset_timers(self):

@@ -26,6 +26,7 @@ def test_device_exp_log_bitwise():
     m = _mvc()
     rng = np.random.default_rng(0)
     x = np.concatenate([rng.uniform(-745, 709.7, 200000), rng.uniform(-40, 40, 200000),
+                        rng.uniform(-745.2, -707.5, 100000), rng.uniform(709.0, 709.79, 20000),
                         [0.0, -0.0, 1e-310, -1e-310, 709.78, -745.2, np.inf, -np.inf, np.nan]])
     assert np.array_equal(m.device_math("exp", x), O.pm_exp(x), equal_nan=True)
     y = np.concatenate([np.exp(rng.uniform(-700, 700, 200000)), rng.uniform(0.5, 2.0, 200000),
@@ -235,17 +236,20 @@ def test_parallel_warm_start(D):
     s.close()
 
 
-def _run_path(m, y, st, seed, sweeps, path, monkeypatch):
+def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=None):
     """Run `sweeps` warm-started sweeps forcing the lp producer (0 generic,
-    2 MFMA); check the path on the first sweep."""
+    2 MFMA) and the draw kernel ("reg" registers, "lds" checkpoints); check
+    both on the first sweep."""
     monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
+    monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
     states = []
     for it in range(sweeps):
         s.sweep(1)
         if it == 0:          # later sweeps may leave the path's limits (births)
-            assert s.zpath() == path
+            assert s.zpath() & 3 == path
+            assert bool(s.zpath() & 4) == ((draw == "reg") if expect_reg is None else expect_reg)
         states.append(s.state())
     s.close()
     return states
@@ -267,9 +271,12 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
 
 # MFMA lp producer (path 2): ragged tiles (n % 16 != 0), fewer tiles than
 # waves, D not a multiple of 16 (zero-padded k-steps), T > 64, K_v of 64
+# draw kernel: registers (T <= 64, K_v <= 64) or LDS checkpoints (any T)
+@pytest.mark.parametrize("draw", ["reg", "lds"])
 @pytest.mark.parametrize("n,V,D,K,T", [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96),
-                                       (2500, 2, 128, 64, 64)])
-def test_zpath2_vs_oracle(n, V, D, K, T, monkeypatch):
+                                       (2500, 2, 128, 64, 64), (1500, 3, 16, 32, 40),
+                                       (2000, 2, 24, 8, 24)])
+def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     m = _mvc()
     from mvc_amd import data
     y, z = data.synthetic(n, V, D, T, seed=n + D)
@@ -279,7 +286,7 @@ def test_zpath2_vs_oracle(n, V, D, K, T, monkeypatch):
     dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
     hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
     st = (table_of, dish, hyper)
-    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch)
+    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw == "reg" and T <= 64))
     ref = O.run(y, 3, 0, 1, seed=31, mode=O.PARALLEL, state=st)
     for it in range(3):
         t, d, h = gpu[it]
@@ -354,7 +361,7 @@ def test_parallel_stats_bitwise_vs_oracle(D, path, monkeypatch):
     s = m.Sampler(y, seed=13, mode="parallel")
     s.set_state(*st)
     s.sweep(6)
-    assert s.zpath() == path
+    assert s.zpath() & 3 == path
     ref = O.run(y, 6, 0, 1, 13, mode=O.PARALLEL, state=st)
     for v in range(V):
         g = s.stats(v)
