@@ -62,7 +62,7 @@ struct Sweep {
   const int32_t *status;  // [V+4]; status[V+3] = tables with n_t > 0
   const double *yt;       // MFMA A-fragment layout of y (mvc_par_ytile_kernel)
   const double *S1t;      // MFMA B-fragment layout of S1 (mvc_par_s1tile_kernel)
-  int32_t SP;             // k-steps per view in yt/S1t (D/4 rounded up to MVC_Z_KS)
+  int32_t SP;             // k-steps per view in yt/S1t (D/4 rounded up to MVC_ZR)
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
@@ -228,32 +228,26 @@ typedef double mvc_d4 __attribute__((ext_vector_type(4)));
 //      dishes and tables (the spec of oracle eval_view_seq /
 //      resample_customer), no cross-lane traffic.
 // ---------------------------------------------------------------------------
-#define MVC_Z_NW 8            // wavefronts per block of the MFMA producer
-#define MVC_Z_KS 4            // k-steps per staged S1 chunk
-#define MVC_Z_PF 4            // L2 warm-up distance (chunks past the register prefetch)
 #define MVC_Z_KMAX 64
 #define MVC_Z_VMAX 8
-#define MVC_Z_BUFD (MVC_Z_KS * 4 * 64)   // doubles per S1 chunk buffer
 
 __host__ __device__ inline size_t lpb_index(int li, int k, int sumK) {
   return ((size_t)(li >> 4) * (size_t)sumK + (size_t)k) * 16 + (size_t)(li & 15);
 }
-__host__ __device__ inline size_t zlp_shared_bytes(int V, int sumK, int T) {
-  return 8 * (2 * (size_t)MVC_Z_BUFD + 3 * (size_t)sumK + 2 * (size_t)V +
-              (size_t)MVC_Z_NW * (16 + 16 * (size_t)V + 16 * ((size_t)sumK + 1))) +
-         4 * ((size_t)sumK + 3 * (size_t)V + 1 + (size_t)V * T + (size_t)MVC_Z_NW * 16) + 64;
-}
 
-// A-fragment layout: yt[((v*ntile + tile)*SP + s)*64 + lane] = y[v][16 tile +
-// (lane & 15)][4 s + (lane >> 4)], zero outside n x D.
+// A-fragment layout, k-steps in pairs (one 16 B load per lane covers two):
+// yt[((v*ntile + tile)*SP + 2*(s/2))*64 + 2*lane + (s & 1)] = y[v][16 tile +
+// (lane & 15)][4 s + (lane >> 4)], zero outside n x D (SP is even).
 extern "C" __global__ void mvc_par_ytile_kernel(int n, int V, int D, int SP, const double *y, double *yt) {
   const int ntile = (n + 15) >> 4;
   const size_t total = (size_t)V * ntile * SP * 64;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (size_t)gridDim.x * blockDim.x) {
-    const int ln = (int)(e & 63);
-    const size_t q = e >> 6;
-    const int s = (int)(q % SP);
-    const size_t vt = q / SP;
+    const size_t q = e >> 7;                       // (view, tile, pair)
+    const int r = (int)(e & 127);
+    const int ln = r >> 1;
+    const int SPP = SP >> 1;
+    const int s = 2 * (int)(q % SPP) + (r & 1);
+    const size_t vt = q / SPP;
     const int tile = (int)(vt % ntile);
     const int v = (int)(vt / ntile);
     const int row = tile * 16 + (ln & 15), d = 4 * s + (ln >> 4);
@@ -284,19 +278,6 @@ extern "C" __global__ void mvc_par_s1tile_kernel(ParState P, const int32_t *Koff
   }
 }
 
-template <int NT>
-__device__ __forceinline__ void z_mfma_chunk(const double (&a)[MVC_Z_KS], const double *__restrict__ buf,
-                                             mvc_d4 (&acc)[4]) {
-#pragma unroll
-  for (int s = 0; s < MVC_Z_KS; ++s) {
-    double b[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) b[t] = buf[(s * NT + t) * 64];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[s], b[t], acc[t], 0, 0, 0);
-  }
-}
-
 // LDS hand-off between lanes of one wavefront: a wave's LDS instructions
 // execute in order, so only the compiler must not reorder across this point
 // (a memory fence here would also wait for every outstanding global load,
@@ -312,322 +293,69 @@ __device__ __forceinline__ void block_lds_sync() {
 }
 
 typedef double mvc_d2 __attribute__((ext_vector_type(2)));
-struct ZStage {
-  mvc_d2 st;              // this thread's share (16 B) of the next S1 chunk
-  double an[MVC_Z_KS];    // next chunk's A fragments
-  int pz;                 // z of row (lane & 15) of the next tile
-  double y2[2];           // Y2[grp + 4q][row] of the next tile
-  double pf;              // L2 warm-up load (consumed one chunk later)
-};
-// tile0: first global 16-row tile of the batch; ntile: tiles in the batch
-struct ZGeom { int per_it, nCC, ntile, tile0, ntile_all, SP, n, V, nblk, blk, w, tid, lane, col, grp, nX; };
-
-__device__ __forceinline__ int z_tile(const ZGeom &g, int it) {
-  return min((it * g.nblk + g.blk) * MVC_Z_NW + g.w, g.ntile - 1);
-}
-__device__ __forceinline__ size_t z_aoff(const ZGeom &g, int X, int &rem) {
-  const int it = X / g.per_it;
-  rem = X - it * g.per_it;
-  const int v = rem / g.nCC, cc = rem - v * g.nCC;
-  const int tile = g.tile0 + z_tile(g, it);
-  return (((size_t)v * g.ntile_all + tile) * g.SP + (size_t)cc * MVC_Z_KS) * 64;
-}
-
-// issue the global loads of flat chunk X (tile iteration, view, k-chunk)
-__device__ __forceinline__ void z_issue(const Sweep &A, const ZGeom &g, const int *s_nct, const int *s_S1o, int X,
-                                        ZStage &o) {
-  int rem;
-  const size_t aoff = z_aoff(g, X, rem);
-  const int v = rem / g.nCC, cc = rem - v * g.nCC;
-  const int nct = s_nct[v];
-  const mvc_d2 *src = (const mvc_d2 *)(A.S1t + ((size_t)s_S1o[v] + (size_t)cc * MVC_Z_KS * nct) * 64);
-  const int units = MVC_Z_KS * nct * 32;          // <= MVC_Z_NW * 64
-  o.st = src[min(g.tid, units - 1)];               // unconditional: stays in registers
-  const double *ap = A.yt + aoff + g.lane;
-#pragma unroll
-  for (int s = 0; s < MVC_Z_KS; ++s) o.an[s] = ap[s * 64];
-  {   // one load per lane, 32 B apart, pulls chunk X + MVC_Z_PF (2 KB per wave) into L2
-    int rem2;
-    const size_t off2 = z_aoff(g, min(X + MVC_Z_PF, g.nX - 1), rem2);
-    o.pf = A.yt[off2 + (size_t)g.lane * 4];
-  }
-  {   // the tile's z and Y2, loaded on every chunk (a load count that
-      // depends on the path would make the compiler drain vmcnt)
-    const int it = X / g.per_it;
-    const int tile = g.tile0 + z_tile(g, it);
-    const int i = min(tile * 16 + g.col, g.n - 1);
-    o.pz = A.P.z[i];
-    o.y2[0] = A.Y2[(size_t)min(g.grp, g.V - 1) * g.n + i];
-    o.y2[1] = A.Y2[(size_t)min(g.grp + 4, g.V - 1) * g.n + i];
-  }
-}
-// write the staged S1 chunk X into its LDS buffer; block barrier
-__device__ __forceinline__ void z_commit(const ZGeom &g, const int *s_nct, double *sbuf, int X, const ZStage &o) {
-  const int it = X / g.per_it;
-  const int rem = X - it * g.per_it;
-  const int v = rem / g.nCC;
-  const int units = MVC_Z_KS * s_nct[v] * 32;
-  mvc_d2 *dst = (mvc_d2 *)(sbuf + (X & 1) * MVC_Z_BUFD);
-  if (g.tid < units) dst[g.tid] = o.st;
-  block_lds_sync();
-}
-
-// lp of one view's dishes for the wave's 16 customers: frozen-dish formula
-// from the accumulators (C layout: lane (grp, col) holds rows grp + 4r, dish
-// 16t + col), the own dish with the customer removed (coefficients once per
-// row), transposed through LDS (row stride MVC_Z_TS) and stored as one
-// contiguous K x 16 block of the customers' slab.
-// lp of one view's dishes for the wave's 16 customers into the wave's LDS
-// tile tl[row * (sumK + 1) + Koff[v] + j]: frozen-dish formula from the
-// accumulators (C layout: lane (grp, col) holds rows grp + 4r, dish 16t +
-// col), then the own dish with the customer removed (coefficients once per
-// row).  No global memory traffic here (see zlp_flush).
-template <int NT>
-__device__ __forceinline__ void zlp_store(const mvc_d4 (&acc)[4], const double *y2s, const int *zs, const int *t_dish,
-                                          int T, double tau, double L2pt, int D, int v, int K, int koff, int LSP,
-                                          int lane, int grp, int col, const double *d_c0, const double *d_cb,
-                                          const double *d_Q, const int *d_n, double *selfG, double *tl) {
-  double hy[4], hr[4];
-  int j0[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const double y2r = y2s[v * 16 + grp + 4 * r];
-    hy[r] = 0.5 * y2r;
-    hr[r] = (-0.5 * y2r) / tau;
-    j0[r] = t_dish[v * T + zs[grp + 4 * r]];
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {   // G of the own dish -> LDS
-    const int jt = j0[r] >> 4;
-    double g = acc[0][r];
-#pragma unroll
-    for (int t = 1; t < NT; ++t)
-      if (jt == t) g = acc[t][r];
-    if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int j = 16 * t + col;
-    const int k = koff + min(j, K - 1);
-    const double c0j = d_c0[k], cbj = d_cb[k];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (j < K) tl[(grp + 4 * r) * LSP + koff + j] = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
-  }
-  wave_lds_sync();
-  {   // own dish, one row per lane (row = lane & 15)
-    const double G = selfG[col];
-    const double y2 = y2s[v * 16 + col];
-    const int jj = t_dish[v * T + zs[col]];
-    const int k0 = koff + jj;
-    const double Gp = G - y2;
-    const double Qp = (d_Q[k0] - 2.0 * G) + y2;
-    const Coef cf = coef(d_n[k0] - 1, Qp, tau, L2pt, D);
-    const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
-    if (lane < 16) tl[col * LSP + k0] = sv;
-  }
-  wave_lds_sync();
-}
-
-// the tile's lp (all views) to its slab: sumK x 16 doubles, contiguous
-__device__ __forceinline__ void zlp_flush(const double *tl, int LSP, int sumK, int li0, int lane, double *lpb,
-                                          bool active, int nb) {
-  if (!active) return;
-  if (li0 + 16 <= nb) {
-    double *dst = lpb + lpb_index(li0, 0, sumK);
-    for (int e = 2 * lane; e < 16 * sumK; e += 128) {
-      const int k = e >> 4, row = e & 15;
-      mvc_d2 val;
-      val.x = tl[row * LSP + k];
-      val.y = tl[(row + 1) * LSP + k];
-      *(mvc_d2 *)(dst + e) = val;
-    }
-  } else {
-    for (int e = lane; e < 16 * sumK; e += 64) {
-      const int k = e >> 4, row = e & 15;
-      if (li0 + row < nb) lpb[lpb_index(li0 + row, k, sumK)] = tl[row * LSP + k];
-    }
-  }
-  wave_lds_sync();
-}
-
-struct ZShared {           // LDS carve of the MFMA producer
-  double *sbuf;
-  const double *d_c0, *d_cb, *d_Q, *s_tau, *s_L2pt;
-  double *selfG, *y2s, *tl;
-  const int *d_n, *s_nct, *s_S1o, *t_dish, *s_koff;
-  int *zs;
-};
-struct ZLoop {             // per-wave state carried across chunks
-  mvc_d4 acc[4];
-  int li0;
-  bool active;
-  double pf_sink;
-};
-
-// one flat chunk X: tile setup, next chunk's loads (into nxt), MFMAs from cur,
-// view epilogue, staging of the next S1 chunk
-__device__ __forceinline__ void zlp_chunk(const Sweep &A, const ZGeom &g, const ZShared &Z, int X, ZStage &cur,
-                                          ZStage &nxt, ZLoop &L, double *lpb, int b0, int nb) {
-  const int it = X / g.per_it;
-  const int rem = X - it * g.per_it;
-  const int v = rem / g.nCC, cc = rem - v * g.nCC;
-  const int NT = Z.s_nct[v];
-  const int V = g.V;
-  if (rem == 0) {   // tile setup: z and Y2 arrived with this chunk's loads
-    const int tl_ = (it * g.nblk + g.blk) * MVC_Z_NW + g.w;
-    L.active = tl_ < g.ntile;
-    L.li0 = min(tl_, g.ntile - 1) * 16;
-    if (g.grp == 0) Z.zs[g.col] = cur.pz;
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (g.grp + 4 * q < V) Z.y2s[(g.grp + 4 * q) * 16 + g.col] = cur.y2[q];
-    wave_lds_sync();
-  }
-  if (cc == 0) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) L.acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
-  }
-  L.pf_sink = L.pf_sink + cur.pf;   // that warm-up load has had a chunk to land
-  if (X + 1 < g.nX) z_issue(A, g, Z.s_nct, Z.s_S1o, X + 1, nxt);
-  const double *bufl = Z.sbuf + (X & 1) * MVC_Z_BUFD + g.lane;
-  switch (NT) {
-    case 1: z_mfma_chunk<1>(cur.an, bufl, L.acc); break;
-    case 2: z_mfma_chunk<2>(cur.an, bufl, L.acc); break;
-    case 3: z_mfma_chunk<3>(cur.an, bufl, L.acc); break;
-    default: z_mfma_chunk<4>(cur.an, bufl, L.acc); break;
-  }
-  if (cc == g.nCC - 1) {
-    const int K = Z.s_koff[v + 1] - Z.s_koff[v], koff = Z.s_koff[v];
-    const int sumK = Z.s_koff[V];
-    switch (NT) {
-#define MVC_ZLP(NTV) zlp_store<NTV>(L.acc, Z.y2s, Z.zs, Z.t_dish, A.T, Z.s_tau[v], Z.s_L2pt[v], A.P.D, v, K, koff, \
-                                    sumK + 1, g.lane, g.grp, g.col, Z.d_c0, Z.d_cb, Z.d_Q, Z.d_n, Z.selfG, Z.tl)
-      case 1: MVC_ZLP(1); break;
-      case 2: MVC_ZLP(2); break;
-      case 3: MVC_ZLP(3); break;
-      default: MVC_ZLP(4); break;
-#undef MVC_ZLP
-    }
-    if (v == V - 1) zlp_flush(Z.tl, sumK + 1, sumK, L.li0, g.lane, lpb, L.active, nb);
-  }
-  if (X + 1 < g.nX) z_commit(g, Z.s_nct, Z.sbuf, X + 1, nxt);
-}
-
-// MFMA lp producer.  A block of MVC_Z_NW waves walks MVC_Z_NW tiles of 16
-// customers at a time, all waves in step over (view, k-chunk); each chunk's
-// S1 B-fragments are staged once into double-buffered LDS for the block, each
-// wave's A-fragments are prefetched one chunk ahead into registers and
-// MVC_Z_PF chunks ahead into L2.
-extern "C" __global__ __launch_bounds__(MVC_Z_NW * 64) void mvc_par_lpmfma_kernel(Sweep A, int b0, int nb,
-                                                                                   double *lpb) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const ParState &P = A.P;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, w = tid >> 6;
-  const int col = lane & 15, grp = lane >> 4;
-  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
-  const int SP = A.SP;
-  const int sumK = A.Koff[V];
-  const int ntile = (nb + 15) >> 4;                 // tiles in this batch (b0 % 64 == 0)
-  double *dp = (double *)smem;
-  double *sbuf = dp; dp += 2 * MVC_Z_BUFD;          // first: 16-byte aligned
-  double *d_c0 = dp; dp += sumK;
-  double *d_cb = dp; dp += sumK;
-  double *d_Q = dp; dp += sumK;
-  double *s_tau = dp; dp += V;
-  double *s_L2pt = dp; dp += V;
-  const size_t wst = 16 + 16 * (size_t)V + 16 * ((size_t)sumK + 1);
-  double *selfG = dp + (size_t)w * wst;             // [16]
-  double *y2s = selfG + 16;                         // [V][16]
-  double *tl = y2s + 16 * V;                        // [16][sumK + 1] the tile's lp
-  dp += (size_t)MVC_Z_NW * wst;
-  int *ip = (int *)dp;
-  int *d_n = ip; ip += sumK;
-  int *s_nct = ip; ip += V;
-  int *s_S1o = ip; ip += V;                         // in units of 64 doubles
-  int *t_dish = ip; ip += V * A.T;                  // [V][T] dish of each table
-  int *s_koff = ip; ip += V + 1;                    // Koff
-  int *zs = ip + w * 16;                            // [16]
-  if (tid <= V) s_koff[tid] = A.Koff[tid];
-  // everything the epilogue reads lives in LDS: a global load there would
-  // wait (vmcnt is in order) for the y prefetch issued just before it
-  for (int e = tid; e < V * A.T; e += blockDim.x) {
-    const int v = e / A.T, p = e - v * A.T;
-    t_dish[e] = P.dish[v * P.TC + p];
-  }
-  if (tid < V) { s_tau[tid] = P.hyper[tid]; s_L2pt[tid] = A.L2pt[tid]; }
-  for (int k = tid; k < sumK; k += blockDim.x) {
-    int v = 0;
-    while (v + 1 < V && A.Koff[v + 1] <= k) ++v;
-    const int j = k - A.Koff[v];
-    d_c0[k] = P.c0[v * KC + j];
-    d_cb[k] = P.cb[v * KC + j];
-    d_Q[k] = P.Q[v * KC + j];
-    d_n[k] = P.d_n[v * KC + j];
-  }
-  if (tid == 0) {
-    int o = 0;
-    for (int v = 0; v < V; ++v) {
-      const int nct = (A.Koff[v + 1] - A.Koff[v] + 15) >> 4;
-      s_nct[v] = nct;
-      s_S1o[v] = o;
-      o += SP * nct;
-    }
-  }
-  __syncthreads();
-  const int nCC = SP / MVC_Z_KS;
-  const int per_it = V * nCC;
-  const int stride_t = gridDim.x * MVC_Z_NW;
-  const int nIt = (ntile - (int)blockIdx.x * MVC_Z_NW + stride_t - 1) / stride_t;
-  const int nX = nIt > 0 ? nIt * per_it : 0;
-  if (nX == 0) return;
-
-  const ZGeom geo{per_it, nCC, ntile, b0 >> 4, (n + 15) >> 4, SP, n, V, (int)gridDim.x, (int)blockIdx.x,
-                  w, tid, lane, col, grp, nX};
-  ZLoop L;
-  L.li0 = 0;
-  L.active = false;
-  L.pf_sink = 0.0;
-  ZStage s0, s1;
-  s0.pz = s1.pz = 0;
-  s0.y2[0] = s0.y2[1] = s1.y2[0] = s1.y2[1] = 0.0;
-  z_issue(A, geo, s_nct, s_S1o, 0, s0);
-  z_commit(geo, s_nct, sbuf, 0, s0);
-  const ZShared Z{sbuf, d_c0, d_cb, d_Q, s_tau, s_L2pt, selfG, y2s, tl, d_n, s_nct, s_S1o, t_dish, s_koff, zs};
-  // two stage register sets: chunk X computes from one while chunk X+1's
-  // loads land in the other (no register copy, so no early wait)
-  for (int X = 0; X < nX; X += 2) {
-    zlp_chunk(A, geo, Z, X, s0, s1, L, lpb, b0, nb);
-    if (X + 1 < nX) zlp_chunk(A, geo, Z, X + 1, s1, s0, L, lpb, b0, nb);
-  }
-  // keep the L2 warm-up loads alive (y is finite, so this never stores)
-  if (L.pf_sink != L.pf_sink) lpb[0] = 0.0;
-}
 
 // MFMA lp producer, one launch per view.  The view's S1
 // B-fragments for every k-step (S1t block, <= 64 KB at D = 128) are staged
 // in LDS once per block; waves then run independently over their 16-customer
-// tiles, streaming the A-fragments (yt, 512 B per k-step per wave) through a
-// ring of MVC_ZR registers: each k-step waits for the oldest load only and
-// issues the load MVC_ZR k-steps ahead (across tile boundaries), so HBM
-// latency hides behind MVC_ZR k-steps of every wave on the CU.  The tile's lp
-// goes straight from the accumulators to the lp buffer (a fixed number of
-// stores per tile).
-#define MVC_ZR 8
+// tiles, streaming the A-fragments from yt (paired layout: one 16 B load per
+// lane covers two k-steps, 1 KB per wave) through a ring of RP registers:
+// each k-step pair waits for the oldest load only and issues the load RP
+// pairs ahead (across tile boundaries), so HBM latency hides behind 2 RP
+// k-steps of every wave on the CU.  The tile's lp goes straight from the
+// accumulators to the lp buffer (a fixed number of stores per tile).
+#define MVC_ZR 8              // SP (k-steps per view) is padded to a multiple of this
 __host__ __device__ inline size_t lpview_shared_bytes(int SP, int NT, int K, int T) {
   return 8 * ((size_t)SP * NT * 64 + 3 * (size_t)K + 8 * 32) + 4 * ((size_t)K + (size_t)T + 8 * 16) + 64;
 }
 
-template <int NT>
-__global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int b0, int nb, double *lpb) {
+// k-step pairs of one 16-customer tile: SPPT > 0 fully unrolled (static ring
+// slots, so the compiler can count outstanding loads exactly and never drains
+// the ring), SPPT == 0 a runtime loop for other D.
+template <int NT, int SPPT, int RP>
+__device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2 *nxt, int SPP, const double *Bl,
+                                                 mvc_d2 (&ring)[RP], mvc_d4 (&acc)[4]) {
+  if constexpr (SPPT > 0) {
+#pragma unroll
+    for (int q = 0; q < SPPT; ++q) {
+      const int u = q % RP;
+      const mvc_d2 a = ring[u];
+      ring[u] = (q + RP < SPPT) ? cur[(q + RP) * 64] : nxt[(q + RP - SPPT) * 64];
+      const double *bk = Bl + (size_t)(2 * q) * NT * 64;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bk[t * 64], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bk[(NT + t) * 64], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
+    }
+  } else {
+    for (int s0 = 0; s0 < SPP; s0 += RP) {
+#pragma unroll
+      for (int u = 0; u < RP; ++u) {
+        const int q = s0 + u;
+        const mvc_d2 a = ring[u];
+        ring[u] = (q + RP < SPP) ? cur[(size_t)(q + RP) * 64] : nxt[(size_t)(q + RP - SPP) * 64];
+        const double *bk = Bl + (size_t)(2 * q) * NT * 64;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bk[t * 64], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bk[(NT + t) * 64], acc[t], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <int NT, int SPPT, int RP>
+__global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int b0, int nb, double *lpb,
+                                                             double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int tid = threadIdx.x;
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
   const int col = lane & 15, grp = lane >> 4;
   const int V = P.V, D = P.D, KC = P.KC, n = P.n, T = A.T;
-  const int SP = A.SP;
+  const int SP = A.SP, SPP = SPPT > 0 ? SPPT : (SP >> 1);   // k-steps, k-step pairs per tile
   const int koff = A.Koff[v], K = A.Koff[v + 1] - koff, sumK = A.Koff[V];
   const double tau = P.hyper[v], L2pt = A.L2pt[v];
   double *Bs = (double *)smem;                     // [SP][NT][64]
@@ -660,19 +388,20 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
   const int ntile = (nb + 15) >> 4;
   const int ntile_all = (n + 15) >> 4;
   const int tile0 = b0 >> 4;
-  const int gw = blockIdx.x * 8 + w, NWT = gridDim.x * 8;
+  const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
   if (gw >= ntile) return;                         // whole wave: no barriers below
   const int nmy = (ntile - gw + NWT - 1) / NWT;    // tiles of this wave
-  const int nq = nmy * SP;                         // k-steps of this wave
-  const double *ybase = A.yt + (size_t)v * ntile_all * SP * 64 + lane;
-  auto aptr = [&](int q) -> const double * {       // A-fragment of flat k-step q (clamped)
-    q = min(q, nq - 1);
-    const int m = q / SP, s = q - m * SP;
-    return ybase + ((size_t)(tile0 + gw + m * NWT) * SP + s) * 64;
+  const mvc_d2 *ybase = (const mvc_d2 *)(A.yt + (size_t)v * ntile_all * SP * 64) + lane;
+  auto tptr = [&](int m) -> const mvc_d2 * {       // A-fragments of the wave's m-th tile (clamped)
+    return ybase + (size_t)(tile0 + gw + min(m, nmy - 1) * NWT) * SPP * 64;
   };
-  double ring[MVC_ZR];
+  double *const dslot = discard + lane;            // stores of padding / out-of-batch lanes
+  mvc_d2 ring[RP];
+  {
+    const mvc_d2 *c0p = tptr(0), *c1p = tptr(1);
 #pragma unroll
-  for (int u = 0; u < MVC_ZR; ++u) ring[u] = *aptr(u);
+    for (int u = 0; u < RP; ++u) ring[u] = (u < SPP) ? c0p[u * 64] : c1p[(u - SPP) * 64];
+  }
   const double *Bl = Bs + lane;
   for (int m = 0; m < nmy; ++m) {
     const int tile = gw + m * NWT;                 // batch-local tile
@@ -684,17 +413,7 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
     mvc_d4 acc[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
-    const int qb = m * SP;
-    for (int s0 = 0; s0 < SP; s0 += MVC_ZR) {
-#pragma unroll
-      for (int u = 0; u < MVC_ZR; ++u) {
-        const double a = ring[u];
-        ring[u] = *aptr(qb + s0 + u + MVC_ZR);     // refill: MVC_ZR k-steps ahead
-        const double *bk = Bl + (size_t)(s0 + u) * NT * 64;
-#pragma unroll
-        for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bk[t * 64], acc[t], 0, 0, 0);
-      }
-    }
+    lpview_tile_mfma<NT, SPPT, RP>(tptr(m), tptr(m + 1), SPP, Bl, ring, acc);
     // ---- epilogue: lp of the tile's 16 customers for this view
     if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
     wave_lds_sync();
@@ -716,6 +435,9 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
         if (jt == t) g = acc[t][r];
       if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
     }
+    // frozen-dish lp for every (row, dish): a fixed number of unconditional
+    // stores (invalid lanes go to their discard slot; the own dish is
+    // overwritten below by this same wave, in program order)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int j = 16 * t + col;
@@ -725,7 +447,8 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
       for (int r = 0; r < 4; ++r) {
         const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
         const int li = li0 + grp + 4 * r;
-        if (j < K && j != j0[r] && li < nb) lpb[lpb_index(li, koff + j, sumK)] = val;
+        double *dst = (j < K && li < nb) ? lpb + lpb_index(li, koff + j, sumK) : dslot;
+        *dst = val;
       }
     }
     wave_lds_sync();
@@ -736,7 +459,8 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
       const double Qp = (d_Q[jj] - 2.0 * G) + y2;
       const Coef cf = coef(d_n[jj] - 1, Qp, tau, L2pt, D);
       const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
-      if (lane < 16 && li0 + col < nb) lpb[lpb_index(li0 + col, koff + jj, sumK)] = sv;
+      double *dst = (lane < 16 && li0 + col < nb) ? lpb + lpb_index(li0 + col, koff + jj, sumK) : dslot;
+      *dst = sv;
     }
     wave_lds_sync();
   }
@@ -1931,6 +1655,7 @@ class ParallelSampler : public Sampler {
   size_t cub_bytes = 0;
   std::vector<int32_t> st_host;
   bool force_generic = false;
+  int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   int n_cu = 256;
 
@@ -1976,6 +1701,8 @@ class ParallelSampler : public Sampler {
     st_host.assign(2 * V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
+    if (const char *e = getenv("MVC_LPV_WAVES")) lpv_waves = std::max(0, std::min(8, atoi(e)));
+    if (const char *e = getenv("MVC_LPV_BPC")) lpv_bpc = std::max(0, std::min(8, atoi(e)));
     const char *zl = getenv("MVC_ZDRAW_LDS");
     force_zdraw_lds = zl && zl[0] == '1';
     {
@@ -1985,9 +1712,10 @@ class ParallelSampler : public Sampler {
     }
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zdraw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024));
-    for (const void *f : {(const void *)mvc_par_lpview_kernel<1>, (const void *)mvc_par_lpview_kernel<2>,
-                          (const void *)mvc_par_lpview_kernel<3>, (const void *)mvc_par_lpview_kernel<4>})
-      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    lpview_attr<4, 4>();
+    lpview_attr<8, 8>();
+    lpview_attr<16, 8>();
+    lpview_attr<0, 4>();
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_stats_partial_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     chains.resize(cf.n_chains);
@@ -2273,6 +2001,37 @@ class ParallelSampler : public Sampler {
     return A;
   }
 
+  // waves per block of the MFMA producer: 4, two blocks per CU = 2 waves per
+  // SIMD.  Measured (scripts/lpv_sweep.py, D = 128, K = 64/32/16/8): more
+  // waves per SIMD only contend for the f64 MFMA pipe and the load queue
+  // (lp 1.11 ms at 4x2, 1.12 at 4x3 / 4x4, 1.22 at 6x2, 1.36 at 2x4).
+  int lpview_waves(int) const { return lpv_waves > 0 ? lpv_waves : 4; }
+  template <int SPPT, int RP>
+  void launch_lpview_nt(int NT, dim3 grid, dim3 block, size_t lds, const Sweep &A, int v, int b0, int nb) {
+    double *disc = lpb + lpb_cap;
+    switch (NT) {
+      case 1: hipLaunchKernelGGL((mvc_par_lpview_kernel<1, SPPT, RP>), grid, block, lds, stream, A, v, b0, nb, lpb, disc); break;
+      case 2: hipLaunchKernelGGL((mvc_par_lpview_kernel<2, SPPT, RP>), grid, block, lds, stream, A, v, b0, nb, lpb, disc); break;
+      case 3: hipLaunchKernelGGL((mvc_par_lpview_kernel<3, SPPT, RP>), grid, block, lds, stream, A, v, b0, nb, lpb, disc); break;
+      default: hipLaunchKernelGGL((mvc_par_lpview_kernel<4, SPPT, RP>), grid, block, lds, stream, A, v, b0, nb, lpb, disc); break;
+    }
+  }
+  // SP (k-steps per tile) is a multiple of 8: pairs per tile SPP = SP / 2
+  void launch_lpview(int NT, dim3 grid, dim3 block, size_t lds, const Sweep &A, int v, int b0, int nb) {
+    switch (SP / 2) {
+      case 4: launch_lpview_nt<4, 4>(NT, grid, block, lds, A, v, b0, nb); break;
+      case 8: launch_lpview_nt<8, 8>(NT, grid, block, lds, A, v, b0, nb); break;
+      case 16: launch_lpview_nt<16, 8>(NT, grid, block, lds, A, v, b0, nb); break;
+      default: launch_lpview_nt<0, 4>(NT, grid, block, lds, A, v, b0, nb); break;
+    }
+  }
+  template <int SPPT, int RP>
+  static void lpview_attr() {
+    for (const void *f : {(const void *)mvc_par_lpview_kernel<1, SPPT, RP>, (const void *)mvc_par_lpview_kernel<2, SPPT, RP>,
+                          (const void *)mvc_par_lpview_kernel<3, SPPT, RP>, (const void *)mvc_par_lpview_kernel<4, SPPT, RP>})
+      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  }
+
   void sweep_chain(Chain &c, uint32_t s) {
     ensure_lp((size_t)sumK(c));   // Koff is current: uploaded by the previous stats update
     Sweep A = make_sweep(c, s);
@@ -2292,7 +2051,7 @@ class ParallelSampler : public Sampler {
     if (need > lpb_cap) {
       if (lpb) hipFree(lpb);
       lpb_cap = need;
-      lpb = dmalloc<double>(lpb_cap);
+      lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
     }
     const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
     if (!use_zreg && zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
@@ -2307,14 +2066,10 @@ class ParallelSampler : public Sampler {
         for (int v = 0; v < V; ++v) {
           const int NT = (c.K[v] + 15) / 16;
           const size_t lds = lpview_shared_bytes(SP, NT, c.K[v], c.T);
-          const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / std::max<size_t>(lds, 1)));
-          const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + 7) / 8));
-          switch (NT) {
-            case 1: hipLaunchKernelGGL(mvc_par_lpview_kernel<1>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
-            case 2: hipLaunchKernelGGL(mvc_par_lpview_kernel<2>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
-            case 3: hipLaunchKernelGGL(mvc_par_lpview_kernel<3>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
-            default: hipLaunchKernelGGL(mvc_par_lpview_kernel<4>, dim3(grid), dim3(512), lds, stream, A, v, (int)b0, nb, lpb); break;
-          }
+          const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(lpv_bpc > 0 ? lpv_bpc : 2, (160 * 1024) / std::max<size_t>(lds, 1)));
+          const int bw = lpview_waves(NT);
+          const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + bw - 1) / bw));
+          launch_lpview(NT, dim3(grid), dim3(64 * bw), lds, A, v, (int)b0, nb);
           MVC_HIP(hipGetLastError());
         }
       } else {
