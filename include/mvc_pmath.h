@@ -62,18 +62,27 @@ MVC_PM double mvc_exp(double x) {
     const int k = (int)kd;
     double r = __builtin_fma(-kd, MVC_LN2_HI, x);
     r = __builtin_fma(-kd, MVC_LN2_LO, r);
+    /* Horner steps as one three-operand v_fma_f64 each (coefficients in
+     * VGPRs, hoisted by the compiler); left to itself the compiler emits
+     * v_mov_b64 + v_fmac_f64, two instructions per step. */
+#if !defined(MVC_PM_NO_ASM_FMA)
+#define MVC_DFMA_S(p, r, c) asm("v_fma_f64 %0, %1, %2, %3" : "=v"(p) : "v"(p), "v"(r), "v"((double)(c)))
+#else
+#define MVC_DFMA_S(p, r, c) p = __builtin_fma(p, r, c)
+#endif
     double p = 1.1470745597729725e-11;
-    p = __builtin_fma(p, r, 1.6059043836821613e-10);
-    p = __builtin_fma(p, r, 2.08767569878681e-09);
-    p = __builtin_fma(p, r, 2.505210838544172e-08);
-    p = __builtin_fma(p, r, 2.755731922398589e-07);
-    p = __builtin_fma(p, r, 2.7557319223985893e-06);
-    p = __builtin_fma(p, r, 2.48015873015873e-05);
-    p = __builtin_fma(p, r, 0.0001984126984126984);
-    p = __builtin_fma(p, r, 0.001388888888888889);
-    p = __builtin_fma(p, r, 0.008333333333333333);
-    p = __builtin_fma(p, r, 0.041666666666666664);
-    p = __builtin_fma(p, r, 0.16666666666666666);
+    MVC_DFMA_S(p, r, 1.6059043836821613e-10);
+    MVC_DFMA_S(p, r, 2.08767569878681e-09);
+    MVC_DFMA_S(p, r, 2.505210838544172e-08);
+    MVC_DFMA_S(p, r, 2.755731922398589e-07);
+    MVC_DFMA_S(p, r, 2.7557319223985893e-06);
+    MVC_DFMA_S(p, r, 2.48015873015873e-05);
+    MVC_DFMA_S(p, r, 0.0001984126984126984);
+    MVC_DFMA_S(p, r, 0.001388888888888889);
+    MVC_DFMA_S(p, r, 0.008333333333333333);
+    MVC_DFMA_S(p, r, 0.041666666666666664);
+    MVC_DFMA_S(p, r, 0.16666666666666666);
+#undef MVC_DFMA_S
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     const double e = __builtin_fma(p, r, 1.0);

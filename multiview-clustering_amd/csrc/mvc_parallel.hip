@@ -680,31 +680,91 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
 // pass (V loads per table) instead of 2.25; the running cumulative weights
 // overwrite the scores and the pick is the first p with r < cum_p.  An
 // excluded table adds +0.0, which leaves the running sum bit-identical.
-template <int KB>
-__device__ __forceinline__ void zview_reg(const double *lpv, int K, int j0, int l0p, const int *dl, double lfn,
-                                          double sigma, double &m_out, double &S_out) {
-  double x[KB];
-#pragma unroll
-  for (int j = 0; j < KB; ++j) x[j] = lpv[(size_t)min(j, K - 1) * 16];
-  double m = -MVC_PM_INF;
-#pragma unroll
-  for (int j = 0; j < KB; ++j) {
-    if (j < K) {
-      const int l = (j == j0) ? l0p : dl[j];
-      if (l > 0 && x[j] > m) m = x[j];
-    }
+// One customer's lp row in the lp buffer: dish k's value at a uniform base
+// (lpb + 16 k, scalar registers) plus the customer's 32-bit byte offset, so
+// every gather is a saddr load with no per-lane address arithmetic.
+typedef int mvc_i4 __attribute__((ext_vector_type(4)));
+extern "C" __device__ double mvc_raw_buffer_load_f64(mvc_i4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.load.f64");
+struct LpRow {
+  mvc_i4 rsrc;       // buffer resource over the lp buffer (scalar registers)
+  int boff;          // this customer's byte offset in its slab (< 2^31: kLpbBudget)
+  __device__ __forceinline__ LpRow(const double *lpb, int boff_) : boff(boff_) {
+    const uint64_t a = (uint64_t)lpb;
+    rsrc = (mvc_i4){(int)(uint32_t)a, (int)(uint32_t)(a >> 32), -1, 0x00020000};   // raw, no range limit
   }
-  if (lfn > m) m = lfn;
-  double S = 0.0;
+  // k must be wave-uniform (it becomes the SGPR soffset)
+  __device__ __forceinline__ double operator()(int k) const { return mvc_raw_buffer_load_f64(rsrc, boff, k * 128, 0); }
+};
+
+// View reduction of the draw (oracle eval_view_seq): max, then the sum of
+// w_j exp(lp_j - m) in dish order.  w_j = max(l_j - sigma, 0) for l_j > 0 and
+// -1 (excluded) otherwise: uniform per dish (s_w, staged once per block)
+// except the customer's own dish (w0).  KB > 0: row held in registers (one
+// load pass); KB == 0: streamed twice in batches of 8.
+template <int KB>
+__device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int j0, double w0, const double *sw,
+                                          double lfn, double &m_out, double &S_out) {
+  double m = -MVC_PM_INF, S = 0.0;
+  if constexpr (KB > 0) {
+    double x[KB];
 #pragma unroll
-  for (int j = 0; j < KB; ++j) {
-    if (j < K) {
-      const int l = (j == j0) ? l0p : dl[j];
-      double w = (double)l - sigma;
-      if (w < 0.0) w = 0.0;
-      double xe = x[j] - m;
-      asm volatile("" : "+v"(xe) : "v"(S));      // one exp in flight (register pressure)
-      const double t = l > 0 ? w * mvc_exp(xe) : -1.0;
+    for (int j = 0; j < KB; ++j) x[j] = row(koff + min(j, K - 1));
+    // every frozen dish other than the customer's own has l >= 1 (the
+    // caller takes this path only then), so validity is a question at j0 only
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      if (j < K) {
+        const bool ok = (j != j0) || (w0 >= 0.0);
+        if (ok && x[j] > m) m = x[j];
+      }
+    }
+    if (lfn > m) m = lfn;
+#pragma unroll
+    for (int j = 0; j < KB; ++j) {
+      if (j < K) {
+        const double w = (j == j0) ? w0 : sw[j];
+        double xe = x[j] - m;
+        asm volatile("" : "+v"(xe) : "v"(S));    // one exp in flight (register pressure)
+        const double t = w >= 0.0 ? w * mvc_exp(xe) : -1.0;
+        if (t >= 0.0) S = S + t;
+      }
+    }
+  } else {
+    int j = 0;
+    for (; j + 8 <= K; j += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = row(koff + j + u);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double w = (j + u == j0) ? w0 : sw[j + u];
+        if (w >= 0.0 && x[u] > m) m = x[u];
+      }
+    }
+    for (; j < K; ++j) {
+      const double w = (j == j0) ? w0 : sw[j];
+      const double x = row(koff + j);
+      if (w >= 0.0 && x > m) m = x;
+    }
+    if (lfn > m) m = lfn;
+    j = 0;
+    for (; j + 8 <= K; j += 8) {
+      double x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[u] = row(koff + j + u);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double w = (j + u == j0) ? w0 : sw[j + u];
+        x[u] = w >= 0.0 ? w * mvc_exp(x[u] - m) : -1.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (x[u] >= 0.0) S = S + x[u];
+    }
+    for (; j < K; ++j) {
+      const double w = (j == j0) ? w0 : sw[j];
+      const double t = w >= 0.0 ? w * mvc_exp(row(koff + j) - m) : -1.0;
       if (t >= 0.0) S = S + t;
     }
   }
@@ -712,66 +772,22 @@ __device__ __forceinline__ void zview_reg(const double *lpv, int K, int j0, int 
   S_out = S;
 }
 
-// Same reduction with the row streamed twice in batches of 8 (any K).
-__device__ __forceinline__ void zview_loop(const double *lpv, int K, int j0, int l0p, const int *dl, double lfn,
-                                           double sigma, double &m_out, double &S_out) {
-  double m = -MVC_PM_INF;
-  int j = 0;
-  for (; j + 8 <= K; j += 8) {
-    double x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int l = (j + u == j0) ? l0p : dl[j + u];
-      if (l > 0 && x[u] > m) m = x[u];
-    }
-  }
-  for (; j < K; ++j) {
-    const int l = (j == j0) ? l0p : dl[j];
-    const double x = lpv[(size_t)j * 16];
-    if (l > 0 && x > m) m = x;
-  }
-  if (lfn > m) m = lfn;
-  double S = 0.0;
-  j = 0;
-  for (; j + 8 <= K; j += 8) {
-    double x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int l = (j + u == j0) ? l0p : dl[j + u];
-      double w = (double)l - sigma;
-      if (w < 0.0) w = 0.0;
-      x[u] = l > 0 ? w * mvc_exp(x[u] - m) : -1.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (x[u] >= 0.0) S = S + x[u];
-  }
-  for (; j < K; ++j) {
-    const int l = (j == j0) ? l0p : dl[j];
-    double w = (double)l - sigma;
-    if (w < 0.0) w = 0.0;
-    const double e = mvc_exp(l > 0 ? lpv[(size_t)j * 16] - m : 0.0);
-    if (l > 0) S = S + w * e;
-  }
-  m_out = m;
-  S_out = S;
-}
-
 template <int TM>
-__global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
+#ifndef MVC_ZDRAW_MINB
+#define MVC_ZDRAW_MINB 3      // blocks of 4 waves per CU the register budget must allow
+#endif
+__global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
   const int T = __builtin_amdgcn_readfirstlane(A.T);
   const int tid = threadIdx.x;
-  double *s_base = (double *)smem;                 // [T] log mass (or -inf)
-  int *s_tix = (int *)(s_base + TM);               // [T][V] Koff[v] + dish_v(p)
+  double *s_base = (double *)smem;                 // [TM] log mass (or -inf)
+  double *s_w = s_base + TM;                       // [sumK] dish weights max(l - sigma, 0) / -1
+  int *s_tix = (int *)(s_w + MVC_Z_VMAX * 64);     // [TM][V] Koff[v] + dish_v(p)
   int *s_koff = s_tix + (size_t)TM * V;            // [V+1]
-  int *s_dl = s_koff + V + 1;                      // [sumK] l of each dish
+  int *s_lmin = s_koff + V + 1;                    // [VMAX] 1: every dish of view v has l >= 1
+  int *s_dl = s_lmin + MVC_Z_VMAX;                 // [sumK] l of each dish
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
   if (tid <= V) s_koff[tid] = A.Koff[tid];
   __syncthreads();
@@ -781,10 +797,17 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0,
     s_base[p] = (np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
     for (int v = 0; v < V; ++v) s_tix[p * V + v] = s_koff[v] + P.dish[v * TC + p];
   }
+  if (tid < MVC_Z_VMAX) s_lmin[tid] = 1;
+  __syncthreads();
   for (int k = tid; k < sumK; k += blockDim.x) {
     int v = 0;
     while (v + 1 < V && s_koff[v + 1] <= k) ++v;
-    s_dl[k] = P.d_l[v * KC + (k - s_koff[v])];
+    const int l = P.d_l[v * KC + (k - s_koff[v])];
+    double w = (double)l - P.hyper[2 * V + v];
+    if (w < 0.0) w = 0.0;
+    s_dl[k] = l;
+    s_w[k] = l > 0 ? w : -1.0;
+    if (l < 1) s_lmin[v] = 0;                    // benign race: every writer stores 0
   }
   __syncthreads();
   const int T_ne = A.status[V + 3];
@@ -794,7 +817,7 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0,
     const int i = b0 + li;
     const int p0 = P.z[i];
     const bool alive = (P.n_t[p0] - 1) > 0;
-    const double *lpi = lpb + lpb_index(li, 0, sumK);   // dish k at lpi[k * 16]
+    const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
     double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
     for (int v = 0; v < V; ++v) {
       const int koff = __builtin_amdgcn_readfirstlane(s_koff[v]);
@@ -803,12 +826,21 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0,
       const double sigma = P.hyper[2 * V + v];
       const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
       const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
-      const int *dl = s_dl + koff;
-      const double *lpv = lpi + (size_t)koff * 16;
+      double w0 = (double)l0p - sigma;
+      if (w0 < 0.0) w0 = 0.0;
+      if (!(l0p > 0)) w0 = -1.0;
+      const double *sw = s_w + koff;
       double m, S;
-      if (K <= 8) zview_reg<8>(lpv, K, j0, l0p, dl, lfn, sigma, m, S);          // row in registers
-      else if (K <= 16) zview_reg<16>(lpv, K, j0, l0p, dl, lfn, sigma, m, S);
-      else zview_loop(lpv, K, j0, l0p, dl, lfn, sigma, m, S);                    // streamed twice
+      const bool allv = __builtin_amdgcn_readfirstlane(s_lmin[v]) != 0;
+      if (!allv) zview_red<0>(row, koff, K, j0, w0, sw, lfn, m, S);           // general: streamed twice
+      else if (K <= 8) zview_red<8>(row, koff, K, j0, w0, sw, lfn, m, S);     // row in registers
+      else if (K <= 16) zview_red<16>(row, koff, K, j0, w0, sw, lfn, m, S);
+#ifdef MVC_ZREG_WIDE
+      else if (K <= 32) zview_red<32>(row, koff, K, j0, w0, sw, lfn, m, S);
+      else zview_red<64>(row, koff, K, j0, w0, sw, lfn, m, S);
+#else
+      else zview_red<0>(row, koff, K, j0, w0, sw, lfn, m, S);
+#endif
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = P.hyper[V + v] + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
@@ -832,7 +864,7 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0,
       for (int v = 0; v < V; ++v) {
         double x[16];
 #pragma unroll
-        for (int u = 0; u < 16; ++u) x[u] = lpi[(size_t)s_tix[min(c + u, T - 1) * V + v] * 16];
+        for (int u = 0; u < 16; ++u) x[u] = row(__builtin_amdgcn_readfirstlane(s_tix[min(c + u, T - 1) * V + v]));
 #pragma unroll
         for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
       }
@@ -862,7 +894,7 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_reg_kernel(Sweep A, int b0,
   }
 }
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
-  return 8 * (size_t)TM + 4 * ((size_t)V * TM + (size_t)sumK + (size_t)V + 1) + 64;
+  return 8 * ((size_t)TM + MVC_Z_VMAX * 64) + 4 * ((size_t)V * TM + (size_t)sumK + (size_t)V + 1 + MVC_Z_VMAX) + 64;
 }
 
 // Phase 2: births resolved sequentially in ascending
@@ -2053,7 +2085,8 @@ class ParallelSampler : public Sampler {
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
     }
-    const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
+    const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && sk <= MVC_Z_VMAX * 64 &&
+                          zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
     if (!use_zreg && zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
       throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: V x tables too large for the draw kernel's LDS tables");
     timers.begin("zresample", &e0);

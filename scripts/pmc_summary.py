@@ -26,22 +26,16 @@ def per_kernel(counter):
 
 fetch = per_kernel("FETCH_SIZE")
 write = per_kernel("WRITE_SIZE")
+# one z pass = V producer launches + one draw launch; count passes by the draw
+passes = max(1, sum(len(v) for k, v in fetch.items() if "zdraw" in k))
 # calibration: every lpview launch streams N*D*8 bytes of y plus small tables
 lp_fetch = [b for k, v in fetch.items() if "lpview" in k for b in v]
 factor = (N * D * 8) / (sum(lp_fetch) / len(lp_fetch)) if lp_fetch else 1.0
-# lpview<NT> templates: average per template name, the pass has V launches in total
-lp_templates = [k for k in fetch if "lpview" in k]
-fetch_pass = 0.0
-for k, v in fetch.items():
-    per = sum(v) / len(v)
-    fetch_pass += factor * per * (V / max(1, len(lp_templates)) if "lpview" in k else 1)
-write_pass = 0.0
-for k, v in write.items():
-    per = sum(v) / len(v)
-    write_pass += per * (V / max(1, len(lp_templates)) if "lpview" in k else 1)
+fetch_pass = factor * sum(sum(v) for v in fetch.values()) / passes
+write_pass = sum(sum(v) for v in write.values()) / passes
 out = {cfg: {"bytes_per_pass": int(fetch_pass + write_pass), "fetch_bytes": int(fetch_pass),
              "write_bytes": int(write_pass), "fetch_factor": round(factor, 4),
              "algorithmic_bytes": N * (8 * V * D + 8), "source": f"profiles/pmcz_{tag}_*",
-             "per_kernel_fetch_raw": {k: sum(v) / len(v) for k, v in fetch.items()},
+             "per_kernel_fetch": {k: factor * sum(v) / len(v) for k, v in fetch.items()},
              "per_kernel_write": {k: sum(v) / len(v) for k, v in write.items()}}}
 print(json.dumps(out, indent=1))
