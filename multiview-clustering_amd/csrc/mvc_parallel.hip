@@ -1689,6 +1689,7 @@ class ParallelSampler : public Sampler {
   bool force_generic = false;
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
+  size_t lpb_batch = 0;           // MVC_LPB_BATCH: customers per phase-1 batch (0: kLpbBudget)
   int n_cu = 256;
 
   template <class Tp>
@@ -1737,6 +1738,7 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_LPV_BPC")) lpv_bpc = std::max(0, std::min(8, atoi(e)));
     const char *zl = getenv("MVC_ZDRAW_LDS");
     force_zdraw_lds = zl && zl[0] == '1';
+    if (const char *e = getenv("MVC_LPB_BATCH")) lpb_batch = (size_t)std::max(0L, atol(e)) / 64 * 64;
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
@@ -2076,7 +2078,8 @@ class ParallelSampler : public Sampler {
                           lpview_shared_bytes(SP, (Kmax + 15) / 16, Kmax, c.T) <= 160 * 1024;
     // batch: multiple of 64 customers, lp buffer <= kLpbBudget doubles
     const size_t per64 = (size_t)std::max(1, sk) * 64;
-    const size_t nb_max = std::max<size_t>(64, (kLpbBudget / per64) * 64);
+    size_t nb_max = std::max<size_t>(64, (kLpbBudget / per64) * 64);
+    if (lpb_batch) nb_max = std::min(nb_max, lpb_batch);
     const size_t nb_full = ((size_t)n + 63) / 64 * 64;
     const size_t nbatch_sz = std::min(nb_max, nb_full);
     const size_t need = (nbatch_sz / 64) * per64;
