@@ -123,6 +123,60 @@ MVC_PM double mvc_exp(double x) {
   return (e * mvc_u2d((uint64_t)(k + 54 + 1023) << 52)) * 5.551115123125783e-17; /* 2^-54 */
 }
 
+#if defined(__HIPCC__)
+/* mvc_exp with the Horner coefficients as SGPR operands: the same
+ * instructions on the same values (bitwise equal to mvc_exp); for kernels
+ * whose VGPR budget cannot hold 22 registers of hoisted constants. */
+static __device__ __forceinline__ double mvc_exp_sk(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  /* Device: the same value without branches (divergence-free; 64 unrolled
+   * calls in the draw kernel would otherwise spill exec masks).  The three
+   * scalings below all equal the correctly rounded e * 2^k, which is what
+   * v_ldexp_f64 computes; the range checks become selects. */
+  {
+    const double shifter = 6755399441055744.0;
+    double kd = x * MVC_INVLN2;
+    kd = kd + shifter;
+    kd = kd - shifter;
+    kd = __builtin_fmin(__builtin_fmax(kd, -1100.0), 1100.0);
+    const int k = (int)kd;
+    double r = __builtin_fma(-kd, MVC_LN2_HI, x);
+    r = __builtin_fma(-kd, MVC_LN2_LO, r);
+    /* Horner steps as one three-operand v_fma_f64 each (coefficients in
+     * VGPRs, hoisted by the compiler); left to itself the compiler emits
+     * v_mov_b64 + v_fmac_f64, two instructions per step. */
+#if !defined(MVC_PM_NO_ASM_FMA)
+#define MVC_DFMA_S(p, r, c) asm("v_fma_f64 %0, %1, %2, %3" : "=v"(p) : "v"(p), "v"(r), "s"((double)(c)))
+#else
+#define MVC_DFMA_S(p, r, c) p = __builtin_fma(p, r, c)
+#endif
+    double p = 1.1470745597729725e-11;
+    MVC_DFMA_S(p, r, 1.6059043836821613e-10);
+    MVC_DFMA_S(p, r, 2.08767569878681e-09);
+    MVC_DFMA_S(p, r, 2.505210838544172e-08);
+    MVC_DFMA_S(p, r, 2.755731922398589e-07);
+    MVC_DFMA_S(p, r, 2.7557319223985893e-06);
+    MVC_DFMA_S(p, r, 2.48015873015873e-05);
+    MVC_DFMA_S(p, r, 0.0001984126984126984);
+    MVC_DFMA_S(p, r, 0.001388888888888889);
+    MVC_DFMA_S(p, r, 0.008333333333333333);
+    MVC_DFMA_S(p, r, 0.041666666666666664);
+    MVC_DFMA_S(p, r, 0.16666666666666666);
+#undef MVC_DFMA_S
+    p = __builtin_fma(p, r, 0.5);
+    p = __builtin_fma(p, r, 1.0);
+    const double e = __builtin_fma(p, r, 1.0);
+    double res = __builtin_amdgcn_ldexp(e, k);
+    res = (x > 709.782712893384) ? MVC_PM_INF : res;
+    res = (x < -745.1332191019412) ? 0.0 : res;
+    return (x == x) ? res : x + x;
+  }
+#else
+  return mvc_exp(x);
+#endif
+}
+#endif
+
 MVC_PM double mvc_log(double x) {
   if (!(x == x)) return x + x;
   if (x < 0.0) return MVC_PM_NAN;

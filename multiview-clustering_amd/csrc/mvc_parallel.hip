@@ -321,11 +321,17 @@ __device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2
       const mvc_d2 a = ring[u];
       ring[u] = (q + RP < SPPT) ? cur[(q + RP) * 64] : nxt[(q + RP - SPPT) * 64];
       const double *bk = Bl + (size_t)(2 * q) * NT * 64;
+#ifdef FZ_ABL_MFMA
+      asm volatile("" :: "v"(a));
+      if (false)
+#endif
+      {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bk[t * 64], acc[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bk[(NT + t) * 64], acc[t], 0, 0, 0);
+      }
       __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
     }
   } else {
@@ -504,6 +510,45 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_lpgen_kernel(Sweep A, 
 // every BS tables so the pick re-walks one block only.  Every uniform
 // per-table / per-dish quantity is staged in LDS first (a gather whose index
 // comes from global memory would pay two dependent memory round trips).
+// pw16 (oracle pw16): pairwise tree over 16 values, pairs (c, c + h) for
+// h = 1, 2, 4, 8; in-lane form of the 16-lane xor butterfly.
+__device__ __forceinline__ double pw16(const double (&a)[16]) {
+  double b[8], c[4];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = a[2 * k] + a[2 * k + 1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c[k] = b[2 * k] + b[2 * k + 1];
+  return (c[0] + c[1]) + (c[2] + c[3]);
+}
+// pw16 descent (oracle pw16_select): at a node with halves (L, R) go left iff
+// R == 0 || r < L, else r -= L.
+__device__ __forceinline__ int pw16_select(const double (&a)[16], double r) {
+  double b[8], c[4], d[2];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) b[k] = a[2 * k] + a[2 * k + 1];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c[k] = b[2 * k] + b[2 * k + 1];
+  d[0] = c[0] + c[1];
+  d[1] = c[2] + c[3];
+  // selects, not dynamic indexing (private arrays stay in registers)
+  auto pick2 = [](const double *x, int n2, int idx, double &L, double &R) {
+    L = x[0]; R = x[1];
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+      if (k < n2 && k == idx) { L = x[2 * k]; R = x[2 * k + 1]; }
+  };
+  int lo = 0;
+  double L, R;
+  auto step = [&](int h) {
+    if (!(R == 0.0 || r < L)) { r = r - L; lo += h; }
+  };
+  L = d[0]; R = d[1]; step(8);
+  pick2(c, 2, lo >> 3, L, R); step(4);
+  pick2(b, 4, lo >> 2, L, R); step(2);
+  pick2(a, 8, lo >> 1, L, R); step(1);
+  return lo;
+}
+
 #define MVC_ZD_NCP 16
 __host__ __device__ inline size_t zdraw_shared_bytes(int V, int T, int sumK) {
   return 8 * ((size_t)MVC_ZD_NCP * 256 + (size_t)T) + 4 * ((size_t)V * T + (size_t)sumK + (size_t)V + 1) + 64;
@@ -535,7 +580,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
   }
   __syncthreads();
   const int T_ne = A.status[V + 3];
-  const int BS = max(16, ((T + MVC_ZD_NCP - 1) / MVC_ZD_NCP + 3) & ~3);   // multiple of 4
+  const int BS = max(16, ((T + MVC_ZD_NCP - 1) / MVC_ZD_NCP + 15) & ~15);   // multiple of 16
   const int nblk = (T + BS - 1) / BS;
   for (int li = blockIdx.x * blockDim.x + tid; li < nb; li += gridDim.x * blockDim.x) {
     const int i = b0 + li;
@@ -571,30 +616,25 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
         if (l > 0 && x > m) m = x;
       }
       if (lfn > m) m = lfn;
-      double S = 0.0;
-      j = 0;
-      for (; j + 8 <= K; j += 8) {
-        double x[8];
+      // 16 column partials (dish j -> column j & 15, ascending j), then pw16
+      double col[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
+      for (int c = 0; c < 16; ++c) col[c] = 0.0;
+      for (j = 0; j < K; j += 16) {
+        double x[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int l = (j + u == j0) ? l0p : dl[j + u];
+        for (int u = 0; u < 16; ++u) x[u] = lpv[(size_t)min(j + u, K - 1) * 16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int l = (j + u == j0) ? l0p : dl[min(j + u, K - 1)];
           double w = (double)l - sigma;
           if (w < 0.0) w = 0.0;
-          x[u] = l > 0 ? w * mvc_exp(x[u] - m) : -1.0;
+          const bool in = j + u < K && l > 0;
+          const double t = w * mvc_exp(in ? x[u] - m : 0.0);
+          if (in) col[u] = col[u] + t;
         }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (x[u] >= 0.0) S = S + x[u];
       }
-      for (; j < K; ++j) {
-        const int l = (j == j0) ? l0p : dl[j];
-        double w = (double)l - sigma;
-        if (w < 0.0) w = 0.0;
-        const double e = mvc_exp(l > 0 ? lpv[(size_t)j * 16] - m : 0.0);
-        if (l > 0) S = S + w * e;
-      }
+      double S = pw16(col);
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = alpha + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
@@ -632,41 +672,45 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
         if (p + u < T && sp[u] > M) M = sp[u];
     }
     if (s_new > M) M = s_new;
-    // cumulative weights; a checkpoint before every block of BS tables
-    double cum = 0.0;
-    for (int b = 0; b < nblk; ++b) {
-      cp_s[b * 256 + tid] = cum;
-      const int pe = min(T, (b + 1) * BS);
-      for (int p = b * BS; p < pe; p += 4) {
-        double sp[4], e[4];
-        score4(p, sp);
+    // weights in blocks of 16 positions: block sums pw16, running totals
+    // C_b = C_{b-1} + B_b; a checkpoint (C before the segment) every BS tables
+    auto block_e = [&](int b, double (&e)[16]) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = mvc_exp(sp[u] != -MVC_PM_INF ? sp[u] - M : 0.0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (p + u < pe && sp[u] != -MVC_PM_INF) cum = cum + e[u];
-      }
-    }
-    const double W = mvc_exp(s_new - M) + cum;
-    const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-    int pick = -1;
-    if (r < cum) {
-      int b = 0;
-      while (b + 1 < nblk && !(r < cp_s[(b + 1) * 256 + tid])) ++b;
-      double c = cp_s[b * 256 + tid];
-      const int pe = min(T, (b + 1) * BS);
-      for (int p = b * BS; p < pe && pick < 0; p += 4) {
-        double sp[4], e[4];
-        score4(p, sp);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = mvc_exp(sp[u] != -MVC_PM_INF ? sp[u] - M : 0.0);
+      for (int q = 0; q < 16; q += 4) {
+        double sp[4];
+        score4(16 * b + q, sp);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          if (pick < 0 && p + u < pe) {
-            if (sp[u] != -MVC_PM_INF) c = c + e[u];
-            if (r < c) pick = p + u;
-          }
+          const bool in = 16 * b + q + u < T && sp[u] != -MVC_PM_INF;
+          const double x = mvc_exp(in ? sp[u] - M : 0.0);
+          e[q + u] = in ? x : 0.0;
         }
+      }
+    };
+    const int TB = (T + 15) >> 4, BSB = BS >> 4;   // blocks, blocks per segment
+    double tot = 0.0;
+    for (int b = 0; b < TB; ++b) {
+      if (b % BSB == 0) cp_s[(b / BSB) * 256 + tid] = tot;
+      double e[16];
+      block_e(b, e);
+      tot = tot + pw16(e);
+    }
+    const double W = mvc_exp(s_new - M) + tot;
+    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+    int pick = -1;
+    if (r < tot) {
+      int g = 0;
+      while (g + 1 < nblk && !(r < cp_s[(g + 1) * 256 + tid])) ++g;
+      double c = cp_s[g * 256 + tid];
+      for (int b = g * BSB; b < TB; ++b) {
+        double e[16];
+        block_e(b, e);
+        const double cn = c + pw16(e);
+        if (r < cn) {
+          pick = 16 * b + pw16_select(e, r - c);
+          break;
+        }
+        c = cn;
       }
     }
     A.choice[i] = pick;
@@ -698,14 +742,18 @@ struct LpRow {
 };
 
 // View reduction of the draw (oracle eval_view_seq): max, then the sum of
-// w_j exp(lp_j - m) in dish order.  w_j = max(l_j - sigma, 0) for l_j > 0 and
-// -1 (excluded) otherwise: uniform per dish (s_w, staged once per block)
-// except the customer's own dish (w0).  KB > 0: row held in registers (one
-// load pass); KB == 0: streamed twice in batches of 8.
+// w_j exp(lp_j - m) as 16 column partials (dish j -> column j & 15, ascending
+// j) folded by pw16.  w_j = max(l_j - sigma, 0) for l_j > 0 and -1 (excluded)
+// otherwise: uniform per dish (s_w, staged once per block) except the
+// customer's own dish (w0).  KB > 0: row held in registers (one load pass);
+// KB == 0: streamed twice in batches of 16.
 template <int KB>
 __device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int j0, double w0, const double *sw,
                                           double lfn, double &m_out, double &S_out) {
-  double m = -MVC_PM_INF, S = 0.0;
+  double m = -MVC_PM_INF;
+  double col[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) col[c] = 0.0;
   if constexpr (KB > 0) {
     double x[KB];
 #pragma unroll
@@ -725,19 +773,19 @@ __device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int
       if (j < K) {
         const double w = (j == j0) ? w0 : sw[j];
         double xe = x[j] - m;
-        asm volatile("" : "+v"(xe) : "v"(S));    // one exp in flight (register pressure)
+        asm volatile("" : "+v"(xe) : "v"(col[(j + 15) & 15]));    // one exp in flight (register pressure)
         const double t = w >= 0.0 ? w * mvc_exp(xe) : -1.0;
-        if (t >= 0.0) S = S + t;
+        if (t >= 0.0) col[j & 15] = col[j & 15] + t;
       }
     }
   } else {
     int j = 0;
-    for (; j + 8 <= K; j += 8) {
-      double x[8];
+    for (; j + 16 <= K; j += 16) {
+      double x[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = row(koff + j + u);
+      for (int u = 0; u < 16; ++u) x[u] = row(koff + j + u);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
         if (w >= 0.0 && x[u] > m) m = x[u];
       }
@@ -749,27 +797,30 @@ __device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int
     }
     if (lfn > m) m = lfn;
     j = 0;
-    for (; j + 8 <= K; j += 8) {
-      double x[8];
+    for (; j + 16 <= K; j += 16) {
+      double x[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[u] = row(koff + j + u);
+      for (int u = 0; u < 16; ++u) x[u] = row(koff + j + u);
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        x[u] = w >= 0.0 ? w * mvc_exp(x[u] - m) : -1.0;
+        double xe = x[u] - m;
+        asm volatile("" : "+v"(xe) : "v"(col[(u + 15) & 15]));
+        const double t = w >= 0.0 ? w * mvc_exp(xe) : -1.0;
+        if (t >= 0.0) col[u] = col[u] + t;
       }
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (x[u] >= 0.0) S = S + x[u];
     }
-    for (; j < K; ++j) {
-      const double w = (j == j0) ? w0 : sw[j];
-      const double t = w >= 0.0 ? w * mvc_exp(row(koff + j) - m) : -1.0;
-      if (t >= 0.0) S = S + t;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (j + u < K) {
+        const double w = (j + u == j0) ? w0 : sw[j + u];
+        const double t = w >= 0.0 ? w * mvc_exp(row(koff + j + u) - m) : -1.0;
+        if (t >= 0.0) col[u] = col[u] + t;
+      }
     }
   }
   m_out = m;
-  S_out = S;
+  S_out = pw16(col);
 }
 
 template <int TM>
@@ -874,27 +925,471 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     for (int p = 0; p < TM; ++p)
       if (p < T && sp[p] > M) M = sp[p];
     if (s_new > M) M = s_new;
-    double cum = 0.0;
+    // weights e_p in place; block sums pw16, running block totals C_b
+    double C[TM / 16];
+    double tot = 0.0;
 #pragma unroll
-    for (int p = 0; p < TM; ++p) {
-      const bool in = p < T && sp[p] != -MVC_PM_INF;
-      double xe = in ? sp[p] - M : 0.0;
-      asm volatile("" : "+v"(xe) : "v"(cum));     // order: one exp in flight, not 64 live
-      const double e = mvc_exp(xe);
-      cum = cum + (in ? e : 0.0);
-      sp[p] = cum;                                 // running cumulative weight
+    for (int b = 0; b < TM / 16; ++b) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int p = 16 * b + c;
+        const bool in = p < T && sp[p] != -MVC_PM_INF;
+        double xe = in ? sp[p] - M : 0.0;
+        asm volatile("" : "+v"(xe) : "v"(sp[(p + TM - 1) % TM]));   // one exp in flight, not TM live
+        const double e = mvc_exp(xe);
+        sp[p] = in ? e : 0.0;
+      }
+      double blk[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) blk[c] = sp[16 * b + c];
+      tot = tot + pw16(blk);
+      C[b] = tot;
     }
-    const double W = mvc_exp(s_new - M) + cum;
-    const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+    const double W = mvc_exp(s_new - M) + tot;
+    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
     int pick = -1;
+    if (r < tot) {
+      int bsel = TM / 16 - 1;
+      double prev = 0.0;
 #pragma unroll
-    for (int p = 0; p < TM; ++p)
-      if (pick < 0 && p < T && r < sp[p]) pick = p;
+      for (int b = TM / 16 - 1; b >= 0; --b)
+        if (r < C[b]) { bsel = b; prev = b > 0 ? C[b - 1] : 0.0; }
+      r = r - prev;
+      double blk[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        double x = sp[c];
+#pragma unroll
+        for (int b = 1; b < TM / 16; ++b)
+          if (bsel == b) x = sp[16 * b + c];
+        blk[c] = x;
+      }
+      pick = 16 * bsel + pw16_select(blk, r);
+    }
     A.choice[i] = pick;
   }
 }
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
   return 8 * ((size_t)TM + MVC_Z_VMAX * 64) + 4 * ((size_t)V * TM + (size_t)sumK + (size_t)V + 1 + MVC_Z_VMAX) + 64;
+}
+
+// ---------------------------------------------------------------------------
+// Fused phase 1: lp producer and draw in ONE kernel, no lp
+// buffer.  Applies when T <= 64, every K_v <= 64, V <= MVC_Z_VMAX and every
+// view's S1 B-fragments fit in LDS together (one block per CU, persistent).
+// Each wave owns 16-customer tiles.  Per tile and view: the MFMA tile of
+// lpview_tile_mfma (A-fragments streamed from yt through the register ring,
+// which runs ahead across view and tile boundaries), then the epilogue works
+// in the accumulator layout: customer row = grp + 4 r sits in the 16 lanes
+// of DPP row grp (dish column = lane & 15, dish block t in-register).  So the
+// oracle's per-customer reductions are in-lane over dish blocks plus a 16-lane
+// xor butterfly (row16 max; the pw16 tree of the column partials), and the
+// table scores sp[p] (lane column = table position within a block of 16)
+// gather lp of dish_v(p) from the row's lanes with ds_bpermute.  The draw
+// (block sums pw16, running block totals, pw16 descent) ends with one lane per
+// row set; choices are stored unconditionally (inactive lanes hit a discard
+// slot).  Same arithmetic as oracle eval_view_seq / resample_customer.
+// ---------------------------------------------------------------------------
+#define MVC_FZ_TB 4               // table blocks of 16 (T <= 64)
+#ifndef MVC_FZ_THREADS
+#define MVC_FZ_THREADS 256        // one wave per SIMD: the fused tile needs more than 256 VGPRs
+#endif
+#ifndef MVC_FZ_RP16
+#define MVC_FZ_RP16 8             // A-fragment ring depth (k-step pairs) at D = 128
+#endif
+__host__ __device__ inline size_t fused_shared_bytes(size_t s1t_doubles, int V, int sumK, int waves) {
+  return ((4 * (4 * (size_t)V + 2) + 15) & ~(size_t)15) + 8 * 2 * (size_t)V +
+         8 * (s1t_doubles + 7 * (size_t)sumK + 2 * 16 * MVC_FZ_TB + (size_t)waves * ((V + 1) * 16 + 8)) +
+         4 * ((size_t)sumK + (size_t)16 * MVC_FZ_TB * V + 16 * MVC_FZ_TB) + 64;
+}
+// View patterns with a fused kernel instance (fz_pat_v / fz_pat_nt below):
+// the bench's K_v = 64, 32, 16, 8 and configs[1]'s 16, 8 shapes, every view
+// count <= 4 with a common dish-block count of 1 or 2, and up to two views of
+// 4 blocks (more spill at this register budget).
+#define MVC_FZ_PAT(V, n0, n1, n2, n3) ((V) | (((n0) - 1) << 4) | (((n1) - 1) << 6) | (((n2) - 1) << 8) | (((n3) - 1) << 10))
+#define MVC_FZ_PATS(X)                                                                                     \
+  X(MVC_FZ_PAT(4, 4, 2, 1, 1)) X(MVC_FZ_PAT(3, 4, 2, 1, 1)) X(MVC_FZ_PAT(2, 4, 2, 1, 1))                  \
+  X(MVC_FZ_PAT(2, 2, 1, 1, 1)) X(MVC_FZ_PAT(1, 1, 1, 1, 1)) X(MVC_FZ_PAT(2, 1, 1, 1, 1))                  \
+  X(MVC_FZ_PAT(3, 1, 1, 1, 1)) X(MVC_FZ_PAT(4, 1, 1, 1, 1)) X(MVC_FZ_PAT(1, 2, 2, 2, 2))                  \
+  X(MVC_FZ_PAT(2, 2, 2, 2, 2)) X(MVC_FZ_PAT(3, 2, 2, 2, 2)) X(MVC_FZ_PAT(4, 2, 2, 2, 2))                  \
+  X(MVC_FZ_PAT(1, 4, 4, 4, 4)) X(MVC_FZ_PAT(2, 4, 4, 4, 4)) X(MVC_FZ_PAT(3, 2, 1, 1, 1))
+
+// 16-lane xor butterfly steps on fp64 (DPP within each row): after the steps
+// with masks 1, 2 the 4-groups are uniform, so row_half_mirror / row_mirror
+// deliver the sibling 4- / 8-group exactly as xor 4 / xor 8 would.
+__device__ __forceinline__ double x1_d(double x) { return dpp_d<0xB1>(x); }    // quad_perm [1,0,3,2]
+__device__ __forceinline__ double x2_d(double x) { return dpp_d<0x4E>(x); }    // quad_perm [2,3,0,1]
+__device__ __forceinline__ double x4_d(double x) { return dpp_d<0x141>(x); }   // row_half_mirror
+__device__ __forceinline__ double x8_d(double x) { return dpp_d<0x140>(x); }   // row_mirror
+// pw16 over the row's 16 lanes (lane = column), result in every lane
+__device__ __forceinline__ double row_pw16(double x) {
+  x = x + x1_d(x);
+  x = x + x2_d(x);
+  x = x + x4_d(x);
+  x = x + x8_d(x);
+  return x;
+}
+__device__ __forceinline__ double row_max16(double x) {
+  x = dmax(x, x1_d(x));
+  x = dmax(x, x2_d(x));
+  x = dmax(x, x4_d(x));
+  x = dmax(x, x8_d(x));
+  return x;
+}
+__device__ __forceinline__ int row_max16_i(int x) {
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, true));
+  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, true));
+  return x;
+}
+__device__ __forceinline__ double bperm_d(int addr, double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+struct FzLds {
+  const double *Bs, *c0, *cb, *Q, *w, *sd0, *sden, *scb, *base, *bself, *lden;
+  const int *dl, *tix, *nt, *koff, *boff, *dpos;
+};
+
+// Per-wave row data of the current tile in LDS (row = customer within the
+// tile): Y2 per view, table, uniform.  Lanes read rows grp + 4 r by broadcast.
+struct FzRows {
+  double *y2;     // [V][16]
+  double *u;      // [16]
+  int *p0;        // [16]
+};
+
+// View v of one tile: MFMA, then lp in registers (in place of the
+// accumulators), the view's marginal into s_new and its table contributions
+// into sp.  The row loop is not unrolled: each pass works on component 0 of
+// the row vectors and rotates them (4 passes restore the order), so one row's
+// temporaries are live at a time.  The own dish's coefficients with the
+// customer removed come from per-dish LDS tables (coef() split into its
+// customer-independent parts, same operations), log(denominator) per view
+// likewise, leaving one log, NT + 1 exps and one division per row.
+__device__ __forceinline__ mvc_d4 rot4(mvc_d4 x) { return (mvc_d4){x[1], x[2], x[3], x[0]}; }
+template <int NT, int SPPT, int RP>
+__device__ __forceinline__ void fz_view(const Sweep &A, const FzLds &L, const FzRows &R, int v, int T,
+                                        const mvc_d2 *cur, const mvc_d2 *nxt, mvc_d2 (&ring)[RP], int alive4,
+                                        mvc_d4 &s_new, mvc_d4 (&sp)[MVC_FZ_TB], int oz) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
+  const int V = P.V;
+  mvc_d4 acc[4];                                   // blocks t >= NT unused
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+  lpview_tile_mfma<NT, SPPT, RP>(cur, nxt, SPPT, L.Bs + L.boff[v] + lane, ring, acc);
+  const int koff = L.koff[v], K = L.koff[v + 1] - koff;
+  const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+  const double cnew = A.cnew[v];
+  // per-dish / per-table LDS reads through an opaque per-tile zero: they are
+  // tile-invariant, and hoisted out of the tile loop they would pin ~80 VGPRs
+  const double *Lc0 = L.c0 + oz, *Lcb = L.cb + oz, *Lw = L.w + oz;
+  const int *Ltix = L.tix + oz;
+#ifdef FZ_ABL_EPI
+#pragma unroll
+  for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(acc[t]));
+  if (false)
+#endif
+#pragma unroll 1
+  for (int r = 0; r < 4; ++r) {
+    const int alive = (alive4 >> r) & 1;
+    const int row = grp + 4 * r;
+    const double y2 = R.y2[v * 16 + row];
+    const int p0 = R.p0[row];
+    const double hy = 0.5 * y2;
+    const double hr = (-0.5 * y2) / tau;
+    const int k0 = L.tix[p0 * V + v];              // Koff[v] + own dish
+    const int j0 = k0 - koff;
+    const int l0p = L.dl[k0] - (alive ? 0 : 1);
+    double w0 = (double)l0p - sigma;
+    if (w0 < 0.0) w0 = 0.0;
+    if (!(l0p > 0)) w0 = -1.0;
+    // the own dish with the customer removed (computed in every lane; kept
+    // by the lane whose column and block hold j0)
+    double Gs = acc[0][0];
+#pragma unroll
+    for (int t = 1; t < NT; ++t)
+      if ((j0 >> 4) == t) Gs = acc[t][0];
+    const double Gp = Gs - y2;
+    const double Qp = (L.Q[k0] - 2.0 * Gs) + y2;
+    const double c0s = L.sd0[k0] - (0.5 * Qp) / L.sden[k0];
+    const double sv = __builtin_fma(Gp + hy, L.scb[k0], c0s) + hr;
+    double m = -MVC_PM_INF;
+    double wt[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int j = 16 * t + col;
+      const int kc = koff + min(j, K - 1);
+      const double fr = __builtin_fma(acc[t][0] + hy, Lcb[kc], Lc0[kc]) + hr;
+      acc[t][0] = (j == j0) ? sv : fr;             // lp
+      wt[t] = (j == j0) ? w0 : (j < K ? Lw[kc] : -1.0);
+      if (wt[t] >= 0.0 && acc[t][0] > m) m = acc[t][0];
+    }
+    m = row_max16(m);
+    const double lfn = cnew + hr;
+    if (lfn > m) m = lfn;
+    double cs = 0.0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const double e = mvc_exp_sk(wt[t] >= 0.0 ? acc[t][0] - m : 0.0);
+      if (wt[t] >= 0.0) cs = cs + wt[t] * e;
+    }
+    double S = row_pw16(cs);
+    const int Kact = K - ((l0p == 0) ? 1 : 0);
+    double wn = alpha + (double)Kact * sigma;
+    if (wn < 0.0) wn = 0.0;
+    S = S + wn * mvc_exp_sk(lfn - m);
+    const int di = 2 * v + (alive ? 0 : 1);
+    const double lm = L.dpos[di] ? (m + mvc_log(S)) - L.lden[di] : lfn;
+    s_new[0] = s_new[0] + lm;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = rot4(acc[t]);
+    s_new = rot4(s_new);
+  }
+  // table scores: sp[tb][r] += lp[row][dish_v(16 tb + col)] (row lanes only).
+  // Branch-free over all MVC_FZ_TB blocks: padding positions p >= T hold
+  // -inf, which the (finite) lp leaves at -inf.
+#ifdef FZ_ABL_GATHER
+#pragma unroll
+  for (int t = 0; t < NT; ++t) asm volatile("" :: "v"(acc[t]));
+  if (false)
+#endif
+#pragma unroll
+  for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
+    const int p = min(16 * tb + col, T - 1);
+    const int jj = Ltix[p * V + v] - koff;
+    const int addr = ((lane & 48) | (jj & 15)) << 2;
+    const int ts = jj >> 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double val = bperm_d(addr, acc[0][r]);
+#pragma unroll
+      for (int t = 1; t < NT; ++t) {
+        const double x = bperm_d(addr, acc[t][r]);
+        if (ts == t) val = x;
+      }
+      sp[tb][r] = sp[tb][r] + val;
+    }
+  }
+}
+
+// View pattern of a fused kernel instance: bits 0-3 = V, bits 4 + 2 v .. =
+// NT_v - 1 (dish blocks of 16 in view v).  Views run in order, unrolled at
+// compile time, so the tile is straight-line code (no joins between views
+// with different NT, which cost the register allocator ~60 VGPRs).
+__host__ __device__ constexpr int fz_pat_v(uint32_t pat) { return (int)(pat & 15u); }
+__host__ __device__ constexpr int fz_pat_nt(uint32_t pat, int v) { return (int)((pat >> (4 + 2 * v)) & 3u) + 1; }
+template <int SPPT, int RP, uint32_t PAT, int VI>
+__device__ __forceinline__ void fz_views(const Sweep &A, const FzLds &L, const FzRows &R, int T,
+                                         const mvc_d2 *ybase, size_t vstride, size_t tcur, size_t tnext,
+                                         mvc_d2 (&ring)[RP], int alive4, mvc_d4 &s_new, mvc_d4 (&sp)[MVC_FZ_TB],
+                                         int oz) {
+  if constexpr (VI < fz_pat_v(PAT)) {
+    const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
+    const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
+    fz_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, R, VI, T, cur, nxt, ring, alive4, s_new, sp, oz);
+    fz_views<SPPT, RP, PAT, VI + 1>(A, L, R, T, ybase, vstride, tcur, tnext, ring, alive4, s_new, sp, oz);
+  }
+}
+
+template <int SPPT, int RP, uint32_t PAT>
+__global__ __launch_bounds__(MVC_FZ_THREADS, 1) void mvc_par_zfused_kernel(Sweep A, int *discard) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  constexpr int V = fz_pat_v(PAT);
+  const int KC = P.KC, TC = P.TC, n = P.n, D = P.D;
+  const int T = __builtin_amdgcn_readfirstlane(A.T);
+  constexpr int SP = 2 * SPPT;
+  // ---- LDS: S1 B-fragments of every view, per-dish and per-table tables,
+  // per-wave row data
+  int *s_koff = (int *)smem;                                   // [V+1]
+  int *s_boff = s_koff + V + 1;                                // [V+1] (doubles)
+  int *s_dpos = s_boff + V + 1;                                // [2V]
+  double *s_lden = (double *)(smem + ((4 * (4 * (size_t)V + 2) + 15) & ~(size_t)15));   // [2V]
+  if (tid <= V) {
+    s_koff[tid] = A.Koff[tid];
+    int acc = 0;
+    for (int u = 0; u < tid; ++u) acc += SP * 64 * fz_pat_nt(PAT, u);
+    s_boff[tid] = acc;
+  }
+  if (tid < 2 * V) {
+    const int v = tid >> 1, dead = tid & 1;
+    const double denom = P.hyper[V + v] + (double)(P.Ltot[v] - dead);
+    s_dpos[tid] = !(denom <= 0.0);
+    s_lden[tid] = !(denom <= 0.0) ? mvc_log(denom) : 0.0;
+  }
+  __syncthreads();
+  const int sumK = s_koff[V];
+  const int nB = s_boff[V];
+  double *Bs = s_lden + 2 * V;                                  // 16 B aligned
+  double *f_c0 = Bs + nB, *f_cb = f_c0 + sumK, *f_Q = f_cb + sumK, *f_w = f_Q + sumK;
+  double *f_sd0 = f_w + sumK, *f_sden = f_sd0 + sumK, *f_scb = f_sden + sumK;
+  double *f_base = f_scb + sumK, *f_bself = f_base + 16 * MVC_FZ_TB;
+  double *f_rows = f_bself + 16 * MVC_FZ_TB;                   // per wave [(V + 1) * 16] doubles + [16] ints
+  constexpr int rows_d = (V + 1) * 16 + 8;
+  int *f_dl = (int *)(f_rows + (size_t)BW * rows_d);
+  int *f_tix = f_dl + sumK, *f_nt = f_tix + 16 * MVC_FZ_TB * V;
+  {
+    const mvc_d2 *src = (const mvc_d2 *)A.S1t;
+    mvc_d2 *dst = (mvc_d2 *)Bs;
+    for (int e = tid; e < nB / 2; e += blockDim.x) dst[e] = src[e];
+  }
+  const double sg = P.hyper[3 * V + 1], ag = P.hyper[3 * V];
+  for (int k = tid; k < sumK; k += blockDim.x) {
+    int v = 0;
+    while (v + 1 < V && s_koff[v + 1] <= k) ++v;
+    const int j = k - s_koff[v];
+    const double tau = P.hyper[v];
+    f_c0[k] = P.c0[v * KC + j];
+    f_cb[k] = P.cb[v * KC + j];
+    f_Q[k] = P.Q[v * KC + j];
+    const int l = P.d_l[v * KC + j];
+    double wl = (double)l - P.hyper[2 * V + v];
+    if (wl < 0.0) wl = 0.0;
+    f_w[k] = l > 0 ? wl : -1.0;
+    f_dl[k] = l;
+    // coef(d_n - 1, Q', tau, L2pt, D) = sd0 - (0.5 Q') / sden, cb = scb
+    const int n_ = P.d_n[v * KC + j] - 1;
+    const double a = tau + (double)n_;
+    const double b = tau + (double)(n_ + 1);
+    f_sd0[k] = (double)D * ((-0.5 * A.L2pt[v]) - 0.5 * mvc_log(b / a));
+    f_sden[k] = (tau * a) * b;
+    f_scb[k] = 1.0 / (tau * b);
+  }
+  for (int p = tid; p < 16 * MVC_FZ_TB; p += blockDim.x) {
+    const int np = p < T ? P.n_t[p] : 0;
+    f_nt[p] = np;
+    f_base[p] = (p < T && np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
+    const int np0 = np - 1;
+    const double m0 = (double)np0 - sg;
+    f_bself[p] = (p < T && np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
+    for (int v = 0; v < V; ++v) f_tix[p * V + v] = s_koff[v] + (p < T ? P.dish[v * TC + p] : 0);
+  }
+  __syncthreads();
+  const FzLds L{Bs, f_c0, f_cb, f_Q, f_w, f_sd0, f_sden, f_scb, f_base, f_bself, s_lden,
+                f_dl, f_tix, f_nt, s_koff, s_boff, s_dpos};
+  double *wrows = f_rows + (size_t)w * rows_d;
+  const FzRows R{wrows, wrows + V * 16, (int *)(wrows + (V + 1) * 16)};
+  const int T_ne = A.status[V + 3];
+  const double snew_alive = mvc_log(ag + sg * (double)T_ne);
+  const double snew_dead = mvc_log(ag + sg * (double)(T_ne - 1));
+
+  const int ntile = (n + 15) >> 4;
+  const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
+  if (gw >= ntile) return;                         // whole wave: no barriers below
+  const int nmy = (ntile - gw + NWT - 1) / NWT;
+  const size_t vstride = (size_t)ntile * SPPT * 64;  // mvc_d2 per view in yt
+  const mvc_d2 *ybase = (const mvc_d2 *)A.yt + lane;
+  auto toff = [&](int m) -> size_t {               // offset of my m-th tile (clamped) within a view
+    return (size_t)(gw + min(m, nmy - 1) * NWT) * SPPT * 64;
+  };
+  mvc_d2 ring[RP];
+  {
+    const mvc_d2 *c0p = ybase + toff(0);
+#pragma unroll
+    for (int u = 0; u < RP; ++u) ring[u] = c0p[u * 64];
+  }
+  int *const dslot = discard + lane;
+  for (int m = 0; m < nmy; ++m) {
+    const int li0 = (gw + m * NWT) * 16;
+    // row data of the tile: lane (grp, col) fills view grp, grp + 4, ... of row col
+    {
+      const int ic = min(li0 + col, n - 1);
+#pragma unroll
+      for (int v = 0; v < V; v += 4)
+        if (v + grp < V) R.y2[(v + grp) * 16 + col] = A.Y2[(size_t)(v + grp) * n + ic];
+      if (grp == 0) R.p0[col] = P.z[ic];
+      if (grp == 1) R.u[col] = mvc_uniform(A.seed, (uint32_t)ic, A.sweep, A.chain, MVC_TAG_Z);
+    }
+    wave_lds_sync();
+    int alive4 = 0;
+    mvc_d4 s_new, sp[MVC_FZ_TB];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int p0 = R.p0[grp + 4 * r];
+      const bool alive = (f_nt[p0] - 1) > 0;
+      alive4 |= alive ? (1 << r) : 0;
+      s_new[r] = alive ? snew_alive : snew_dead;
+#pragma unroll
+      for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
+        const int p = 16 * tb + col;
+        sp[tb][r] = (p == p0) ? f_bself[p] : f_base[p];
+      }
+    }
+    int oz = 0;
+    asm volatile("" : "+v"(oz));
+    fz_views<SPPT, RP, PAT, 0>(A, L, R, T, ybase, vstride, toff(m), toff(m + 1), ring, alive4, s_new, sp, oz);
+    // ---- draw (oracle resample_customer), one row per pass (rotating)
+    int pv = -1;
+#ifdef FZ_ABL_DRAW
+#pragma unroll
+    for (int tb = 0; tb < MVC_FZ_TB; ++tb) asm volatile("" :: "v"(sp[tb]), "v"(s_new));
+    pv = R.p0[grp + 4 * col];
+    if (false)
+#endif
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r) {
+      double M = -MVC_PM_INF;
+#pragma unroll
+      for (int tb = 0; tb < MVC_FZ_TB; ++tb)
+        if (16 * tb + col < T && sp[tb][0] > M) M = sp[tb][0];
+      M = row_max16(M);
+      if (s_new[0] > M) M = s_new[0];
+      double ev[MVC_FZ_TB], C[MVC_FZ_TB];
+      double tot = 0.0;
+#pragma unroll
+      for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
+        const bool in = 16 * tb + col < T && sp[tb][0] != -MVC_PM_INF;
+        const double e = mvc_exp_sk(in ? sp[tb][0] - M : 0.0);
+        ev[tb] = in ? e : 0.0;
+        tot = tot + row_pw16(ev[tb]);              // blocks past T add +0.0: exact
+        C[tb] = tot;
+      }
+      const double W = mvc_exp_sk(s_new[0] - M) + tot;
+      double rr = R.u[grp + 4 * r] * W;
+      const bool birth = !(rr < tot);
+      int bsel = 0;
+      double prev = 0.0, x = ev[0];
+#pragma unroll
+      for (int tb = MVC_FZ_TB - 1; tb >= 0; --tb)
+        if (rr < C[tb]) { bsel = tb; prev = tb > 0 ? C[tb - 1] : 0.0; x = ev[tb]; }
+      rr = rr - prev;
+      // pw16 descent: every lane follows the path towards its own column
+      const double t1 = x1_d(x), l1 = x + t1;
+      const double t2 = x2_d(l1), l2 = l1 + t2;
+      const double t4 = x4_d(l2), l4 = l2 + t4;
+      const double t8 = x8_d(l4);
+      bool on = !birth;
+      auto step = [&](double own, double other, int h) {
+        const bool hi = (col & h) != 0;
+        const double Lh = hi ? other : own, Rh = hi ? own : other;
+        const bool right = !(Rh == 0.0 || rr < Lh);
+        if (right != hi) on = false;
+        if (right) rr = rr - Lh;
+      };
+      step(l4, t8, 8);
+      step(l2, t4, 4);
+      step(l1, t2, 2);
+      step(x, t1, 1);
+      const int pk = row_max16_i(on ? 16 * bsel + col : -1);
+      if (col == r) pv = pk;                       // lane (col = r, grp) stores row grp + 4 r
+#pragma unroll
+      for (int tb = 0; tb < MVC_FZ_TB; ++tb) sp[tb] = rot4(sp[tb]);
+      s_new = rot4(s_new);
+    }
+    const int li = li0 + grp + 4 * col;
+    int *dst = (col < 4 && li < n) ? A.choice + li : dslot;
+    *dst = pv;
+    wave_lds_sync();                               // row data reused by the next tile
+  }
 }
 
 // Phase 2: births resolved sequentially in ascending
@@ -1690,6 +2185,9 @@ class ParallelSampler : public Sampler {
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   size_t lpb_batch = 0;           // MVC_LPB_BATCH: customers per phase-1 batch (0: kLpbBudget)
+  bool no_fused = true;           // MVC_FUSED=1: the fused phase-1 kernel where it applies (experimental: slower today)
+  int fz_waves = MVC_FZ_THREADS / 64;   // waves per block of the fused kernel (MVC_FZ_WAVES: fewer)
+  int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
   int n_cu = 256;
 
   template <class Tp>
@@ -1739,6 +2237,9 @@ class ParallelSampler : public Sampler {
     const char *zl = getenv("MVC_ZDRAW_LDS");
     force_zdraw_lds = zl && zl[0] == '1';
     if (const char *e = getenv("MVC_LPB_BATCH")) lpb_batch = (size_t)std::max(0L, atol(e)) / 64 * 64;
+    if (const char *e = getenv("MVC_FUSED")) no_fused = e[0] != '1';
+    if (const char *e = getenv("MVC_FZ_WAVES")) fz_waves = std::max(1, std::min(MVC_FZ_THREADS / 64, atoi(e)));
+    fz_discard = dmalloc<int>(64);
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
@@ -1752,6 +2253,9 @@ class ParallelSampler : public Sampler {
     lpview_attr<0, 4>();
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_stats_partial_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    fused_attr<4, 4>();
+    fused_attr<8, 8>();
+    fused_attr<16, MVC_FZ_RP16>();
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh.data());
     MVC_HIP(hipStreamSynchronize(stream));
@@ -1762,7 +2266,7 @@ class ParallelSampler : public Sampler {
     for (auto &c : chains)
       for (void *p : c.owned) hipFree(p);
     for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)lpb, (void *)part1, (void *)part2,
-                    cub_tmp})
+                    cub_tmp, (void *)fz_discard})
       if (p) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -2066,6 +2570,27 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   }
 
+  template <int SPPT, int RP>
+  void launch_fused(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A) {
+    switch (pat) {
+#define X(p)                                                                                             \
+  case p:                                                                                                \
+    hipLaunchKernelGGL((mvc_par_zfused_kernel<SPPT, RP, p>), grid, block, lds, stream, A, fz_discard); \
+    break;
+      MVC_FZ_PATS(X)
+#undef X
+      default: throw Error(MVC_ERR_STATE, "fused kernel: no instance for this view pattern");
+    }
+  }
+  template <int SPPT, int RP>
+  static void fused_attr() {
+#define X(p)                                                                                              \
+  MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zfused_kernel<SPPT, RP, p>,                           \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MVC_FZ_PATS(X)
+#undef X
+  }
+
   void sweep_chain(Chain &c, uint32_t s) {
     ensure_lp((size_t)sumK(c));   // Koff is current: uploaded by the previous stats update
     Sweep A = make_sweep(c, s);
@@ -2083,17 +2608,47 @@ class ParallelSampler : public Sampler {
     const size_t nb_full = ((size_t)n + 63) / 64 * 64;
     const size_t nbatch_sz = std::min(nb_max, nb_full);
     const size_t need = (nbatch_sz / 64) * per64;
-    if (need > lpb_cap) {
-      if (lpb) hipFree(lpb);
-      lpb_cap = need;
-      lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
-    }
     const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && sk <= MVC_Z_VMAX * 64 &&
                           zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
     if (!use_zreg && zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
       throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: V x tables too large for the draw kernel's LDS tables");
+    // fused phase 1 (lp never leaves registers): T <= 64, K_v <= 64, every
+    // view's S1 B-fragments in LDS at once, fully unrolled k-step pairs
+    size_t s1t_d = 0;
+    for (int v = 0; v < V; ++v) s1t_d += (size_t)SP * 64 * ((c.K[v] + 15) / 16);
+    const size_t fz_lds = fused_shared_bytes(s1t_d, V, sk, fz_waves);
+    const int spp = SP / 2;
+    uint32_t fz_pat = (uint32_t)V;
+    for (int v = 0; v < V && v < 4; ++v) fz_pat |= (uint32_t)(std::min(4, (c.K[v] + 15) / 16) - 1) << (4 + 2 * v);
+    bool pat_ok = V <= 4 && Kmax <= 64;
+    switch (pat_ok ? fz_pat : 0u) {
+#define X(p) case p:
+      MVC_FZ_PATS(X)
+#undef X
+      break;
+      default: pat_ok = false;
+    }
+    const bool use_fused = !no_fused && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
+                           (spp == 4 || spp == 8 || spp == 16) && fz_lds <= 160 * 1024;
+    if (!use_fused && need > lpb_cap) {   // the lp buffer only exists for the two-kernel path
+      if (lpb) hipFree(lpb);
+      lpb_cap = need;
+      lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
+    }
     timers.begin("zresample", &e0);
-    for (size_t b0 = 0; b0 < (size_t)n; b0 += nbatch_sz) {
+    if (use_fused) {
+      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / fz_lds));
+      const int ntile = (n + 15) / 16;
+      const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + fz_waves - 1) / fz_waves));
+      const dim3 blk(64 * fz_waves);
+      switch (spp) {
+        case 4: launch_fused<4, 4>(fz_pat, dim3(grid), blk, fz_lds, A); break;
+        case 8: launch_fused<8, 8>(fz_pat, dim3(grid), blk, fz_lds, A); break;
+        default: launch_fused<16, MVC_FZ_RP16>(fz_pat, dim3(grid), blk, fz_lds, A); break;
+      }
+      MVC_HIP(hipGetLastError());
+    }
+    for (size_t b0 = 0; !use_fused && b0 < (size_t)n; b0 += nbatch_sz) {
       const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
       hipEvent_t el = nullptr, ed = nullptr;
       timers.begin("lp", &el);
@@ -2132,7 +2687,7 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
-    zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0);
+    zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0);
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
     hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, n, c.T,

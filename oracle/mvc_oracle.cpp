@@ -690,6 +690,34 @@ struct Tree64 {
   }
 };
 
+// pw16: pairwise tree over 16 slots, pairs (c, c + h) for h = 1, 2, 4, 8 (the
+// wavefront's xor butterfly across one 16-lane DPP row)
+static double pw16(const double *x) {
+  double a[16];
+  for (int c = 0; c < 16; ++c) a[c] = x[c];
+  for (int h = 1; h < 16; h <<= 1)
+    for (int c = 0; c < 16; c += 2 * h) a[c] = a[c] + a[c + h];
+  return a[0];
+}
+
+// Descent through the pw16 tree: at a node with halves (L, R) go left iff
+// R == 0 || r < L, else r -= L.  The half sums are the tree's own partials.
+static int pw16_select(const double *x, double r) {
+  double lv[5][16];
+  for (int c = 0; c < 16; ++c) lv[0][c] = x[c];
+  for (int k = 0, h = 1; k < 4; ++k, h <<= 1)
+    for (int c = 0; c < 16; c += 2 * h) lv[k + 1][c] = lv[k][c] + lv[k][c + h];
+  int lo = 0;
+  for (int k = 3, h = 8; k >= 0; --k, h >>= 1) {
+    const double L = lv[k][lo], R = lv[k][lo + h];
+    if (!(R == 0.0 || r < L)) {
+      r = r - L;
+      lo += h;
+    }
+  }
+  return lo;
+}
+
 static double tree64_sum(const std::vector<double> &x) {
   Tree64 t;
   return t.build(x);
@@ -1012,16 +1040,19 @@ struct ParallelSampler {
       if (l > 0 && lp_out[j] > m) m = lp_out[j];
     }
     if (lfn > m) m = lfn;
-    // sequential sum of w * exp(lp - m) in dish order, then the new dish
-    double S = 0.0;
+    // sum of w * exp(lp - m): column partials (dish j -> column j mod 16,
+    // sequential in ascending j), then the pairwise tree over the 16 columns
+    // (pw16), then the new dish
+    double col[16] = {0.0};
     for (int j = 0; j < K; ++j) {
       const int l = (j == j0) ? l0p : lk[v][j];
       if (l > 0) {
         double w = (double)l - sigma[v];
         if (w < 0.0) w = 0.0;
-        S = S + w * mvc_exp(lp_out[j] - m);
+        col[j & 15] = col[j & 15] + w * mvc_exp(lp_out[j] - m);
       }
     }
+    double S = pw16(col);
     const int Kact = K - ((l0p == 0) ? 1 : 0);
     double wn = alpha[v] + (double)Kact * sigma[v];
     if (wn < 0.0) wn = 0.0;
@@ -1032,9 +1063,12 @@ struct ParallelSampler {
   }
 
   // Phase 1: table against the frozen state; -1 = birth.
-  // Table weights e_p = exp(sp_p - M) accumulate in position order
-  // (cum_p = cum_{p-1} + e_p); W = exp(s_new - M) + cum_{T-1}; r = u W picks
-  // the first p with r < cum_p, or a birth when r >= cum_{T-1}.
+  // Table weights e_p = exp(sp_p - M) (0 for excluded tables and for the
+  // padding p >= T) in blocks of 16 positions; block sums B_b = pw16, running
+  // block totals C_b = C_{b-1} + B_b (C_{-1} = 0); Tot = C_last,
+  // W = exp(s_new - M) + Tot, r = u W.  r >= Tot is a birth; otherwise the
+  // first block with r < C_b is entered with r - C_{b-1} and the leaf is the
+  // pw16 descent (pw16_select) inside it.
   int resample_customer(int i, int s) const {
     const int p0 = z[i];
     const bool alive = (n_t[p0] - 1) > 0;
@@ -1045,7 +1079,8 @@ struct ParallelSampler {
       lp[v].resize(ids[v].size());
       s_new = s_new + eval_view_seq(i, v, alive, dish[v][p0], lp[v].data());
     }
-    std::vector<double> sc(T, -MVC_PM_INF);
+    const int TB = (T + 15) / 16;
+    std::vector<double> sc((size_t)TB * 16, -MVC_PM_INF);
     double M = -MVC_PM_INF;
     for (int p = 0; p < T; ++p) {
       const int np = n_t[p] - (p == p0 ? 1 : 0);
@@ -1057,18 +1092,23 @@ struct ParallelSampler {
       if (sp > M) M = sp;
     }
     if (s_new > M) M = s_new;
-    double cum = 0.0;
-    std::vector<double> cums(T);
-    for (int p = 0; p < T; ++p) {
-      if (sc[p] != -MVC_PM_INF) cum = cum + mvc_exp(sc[p] - M);
-      cums[p] = cum;
+    std::vector<double> e((size_t)TB * 16), C(TB);
+    double tot = 0.0;
+    for (int b = 0; b < TB; ++b) {
+      for (int c = 0; c < 16; ++c) {
+        const double x = sc[(size_t)b * 16 + c];
+        e[(size_t)b * 16 + c] = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
+      }
+      tot = tot + pw16(&e[(size_t)b * 16]);
+      C[b] = tot;
     }
-    const double W = mvc_exp(s_new - M) + cum;
-    const double r = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_Z) * W;
-    if (r < cum)
-      for (int p = 0; p < T; ++p)
-        if (r < cums[p]) return p;
-    return -1;
+    const double W = mvc_exp(s_new - M) + tot;
+    double r = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_Z) * W;
+    if (!(r < tot)) return -1;
+    int b = 0;
+    while (!(r < C[b])) ++b;
+    r = r - (b > 0 ? C[b - 1] : 0.0);
+    return b * 16 + pw16_select(&e[(size_t)b * 16], r);
   }
 
   // Phase 2: births in ascending customer order either join

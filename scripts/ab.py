@@ -21,7 +21,7 @@ s.set_state(*bench.warm_state(z, V, K))
 s.sweep(2); s.synchronize(); s.reset_timers()
 s.sweep(10); s.synchronize()
 out = [sys.argv[1]]
-for k in ("lp", "draw", "commit", "stats", "hyper", "sweep"):
+for k in ("zresample", "lp", "draw", "commit", "stats", "hyper", "sweep"):
     ms, cnt = s.kernel_time(k)
     out.append(f"{{k}}={{ms / 10:.3f}}")
 print(" ".join(out), flush=True)

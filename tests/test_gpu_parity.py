@@ -236,20 +236,27 @@ def test_parallel_warm_start(D):
     s.close()
 
 
-def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=None):
+def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=None, expect_fused=None):
     """Run `sweeps` warm-started sweeps forcing the lp producer (0 generic,
-    2 MFMA) and the draw kernel ("reg" registers, "lds" checkpoints); check
-    both on the first sweep."""
+    2 MFMA) and the phase-1 kernels ("fused" the one-pass MFMA + draw kernel,
+    "reg" lp buffer + register draw, "lds" lp buffer + checkpoint draw); check
+    the path taken on the first sweep."""
     monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
     monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
+    monkeypatch.setenv("MVC_FUSED", "1" if draw == "fused" else "0")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
     states = []
     for it in range(sweeps):
         s.sweep(1)
         if it == 0:          # later sweeps may leave the path's limits (births)
-            assert s.zpath() & 3 == path
-            assert bool(s.zpath() & 4) == ((draw == "reg") if expect_reg is None else expect_reg)
+            zp = s.zpath()
+            assert zp & 3 == path
+            if draw == "fused":
+                assert bool(zp & 8) == (True if expect_fused is None else expect_fused)
+            else:
+                assert not zp & 8
+                assert bool(zp & 4) == ((draw == "reg") if expect_reg is None else expect_reg)
         states.append(s.state())
     s.close()
     return states
@@ -262,6 +269,7 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
     y, z = data.synthetic(2000, V, D, K, seed=5)
     st = _warm_state(z, V, K)
     out = [_run_path(m, y, st, 9, 3, p, monkeypatch) for p in (0, 2)]
+    out.append(_run_path(m, y, st, 9, 3, 2, monkeypatch, draw="fused"))
     for a in out[1:]:
         for sa, sb in zip(out[0], a):
             assert np.array_equal(sa[0], sb[0])
@@ -270,15 +278,21 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
 
 
 # MFMA lp producer (path 2): ragged tiles (n % 16 != 0), fewer tiles than
-# waves, D not a multiple of 16 (zero-padded k-steps), T > 64, K_v of 64
-# draw kernel: registers (T <= 64, K_v <= 64) or LDS checkpoints (any T)
-@pytest.mark.parametrize("draw", ["reg", "lds"])
-@pytest.mark.parametrize("n,V,D,K,T", [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96),
-                                       (2500, 2, 128, 64, 64), (1500, 3, 16, 32, 40),
-                                       (2000, 2, 24, 8, 24)])
+# waves, D not a multiple of 16 (zero-padded k-steps), T > 64, K_v of 64;
+# phase 1 as the fused kernel (T <= 64 and an instantiated view pattern,
+# else the two-kernel path), or lp buffer + register draw (T <= 64, K_v <= 64)
+# or lp buffer + LDS checkpoint draw (any T)
+FUSED_SHAPES = {(3001, 4, 64, 16, 16): True, (50, 2, 20, 4, 4): True, (4000, 3, 32, 64, 96): False,
+                (2500, 2, 128, 64, 64): True, (1500, 3, 16, 32, 40): True, (2000, 2, 24, 8, 24): True,
+                (4100, 4, 128, 64, 64): True, (777, 1, 32, 16, 16): True}
+
+
+@pytest.mark.parametrize("draw", ["fused", "reg", "lds"])
+@pytest.mark.parametrize("n,V,D,K,T", list(FUSED_SHAPES))
 def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     m = _mvc()
     from mvc_amd import data
+    T_gen = T
     y, z = data.synthetic(n, V, D, T, seed=n + D)
     uniq, table_of = np.unique(z, return_inverse=True)   # generating partition
     table_of = table_of.astype(np.int32)
@@ -286,7 +300,8 @@ def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
     hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
     st = (table_of, dish, hyper)
-    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw == "reg" and T <= 64))
+    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw == "reg" and T <= 64),
+                    expect_fused=FUSED_SHAPES[(n, V, D, K, T_gen)])
     ref = O.run(y, 3, 0, 1, seed=31, mode=O.PARALLEL, state=st)
     for it in range(3):
         t, d, h = gpu[it]
