@@ -219,6 +219,48 @@ MVC_PM double mvc_log(double x) {
   return dk * MVC_LN2_HI - ((hfsq - (s * (hfsq + R) + dk * MVC_LN2_LO)) - f);
 }
 
+#if defined(__HIPCC__)
+/* mvc_log without branches (device): every path of mvc_log computed with the
+ * same operations, the result picked by selects, so it is bitwise equal to
+ * mvc_log for every input and keeps a wavefront converged. */
+static __device__ __forceinline__ double mvc_log_nb(double x) {
+  const uint64_t u0 = mvc_d2u(x);
+  const bool sub = u0 < 0x0010000000000000ull;           /* +0 and subnormals (x >= 0) */
+  const double xs = sub ? x * 18014398509481984.0 : x;   /* 2^54 */
+  const uint64_t u = mvc_d2u(xs);
+  int e = (sub ? -54 : 0) + (int)((u >> 52) & 0x7FF) - 1023;
+  const uint64_t mant = u & 0x000FFFFFFFFFFFFFull;
+  const bool big = mant > 0x6A09E667F3BCDull;
+  const uint64_t ebits = big ? 0x3FE0000000000000ull : 0x3FF0000000000000ull;
+  e += big ? 1 : 0;
+  const double m = mvc_u2d(mant | ebits);
+  const double f = m - 1.0;
+  const double s = f / (2.0 + f);
+  const double z = s * s;
+  double R = 0.08;
+  R = __builtin_fma(R, z, 0.08695652173913043);
+  R = __builtin_fma(R, z, 0.09523809523809523);
+  R = __builtin_fma(R, z, 0.10526315789473684);
+  R = __builtin_fma(R, z, 0.11764705882352941);
+  R = __builtin_fma(R, z, 0.13333333333333333);
+  R = __builtin_fma(R, z, 0.15384615384615385);
+  R = __builtin_fma(R, z, 0.18181818181818182);
+  R = __builtin_fma(R, z, 0.2222222222222222);
+  R = __builtin_fma(R, z, 0.2857142857142857);
+  R = __builtin_fma(R, z, 0.4);
+  R = __builtin_fma(R, z, 0.6666666666666666);
+  R = R * z;
+  const double hfsq = 0.5 * f * f;
+  const double dk = (double)e;
+  double res = (e == 0) ? f - (hfsq - s * (hfsq + R))
+                        : dk * MVC_LN2_HI - ((hfsq - (s * (hfsq + R) + dk * MVC_LN2_LO)) - f);
+  res = (u0 == 0x7FF0000000000000ull) ? x : res;
+  res = (x == 0.0) ? -MVC_PM_INF : res;
+  res = (x < 0.0) ? MVC_PM_NAN : res;
+  return (x == x) ? res : x + x;
+}
+#endif
+
 /* log Gamma(x) for x > 0 (used only by the parallel-mode EPPF). */
 MVC_PM double mvc_lgamma_pos(double x) {
   if (!(x > 0.0)) return MVC_PM_NAN;

@@ -1065,9 +1065,8 @@ struct FzRows {
 
 // View v of one tile: MFMA, then lp in registers (in place of the
 // accumulators), the view's marginal into s_new and its table contributions
-// into sp.  The row loop is not unrolled: each pass works on component 0 of
-// the row vectors and rotates them (4 passes restore the order), so one row's
-// temporaries are live at a time.  The own dish's coefficients with the
+// into sp.  The four rows a lane holds are processed together (independent
+// chains for the one wave on its SIMD to overlap).  The own dish's coefficients with the
 // customer removed come from per-dish LDS tables (coef() split into its
 // customer-independent parts, same operations), log(denominator) per view
 // likewise, leaving one log, NT + 1 exps and one division per row.
@@ -1087,7 +1086,7 @@ __device__ __forceinline__ void fz_view(const Sweep &A, const FzLds &L, const Fz
   const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
   const double cnew = A.cnew[v];
   // per-dish / per-table LDS reads through an opaque per-tile zero: they are
-  // tile-invariant, and hoisted out of the tile loop they would pin ~80 VGPRs
+  // tile-invariant, and hoisted out of the tile loop they would pin registers
   const double *Lc0 = L.c0 + oz, *Lcb = L.cb + oz, *Lw = L.w + oz;
   const int *Ltix = L.tix + oz;
 #ifdef FZ_ABL_EPI
@@ -1095,61 +1094,78 @@ __device__ __forceinline__ void fz_view(const Sweep &A, const FzLds &L, const Fz
   for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(acc[t]));
   if (false)
 #endif
-#pragma unroll 1
+  {
+  // the four rows of this lane are independent: every step below runs on all
+  // four at once (instruction-level parallelism at one wave per SIMD)
+  double hy[4], hr[4], w0[4], sv[4];
+  int j0[4], l0p[4];
+#pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int alive = (alive4 >> r) & 1;
     const int row = grp + 4 * r;
     const double y2 = R.y2[v * 16 + row];
-    const int p0 = R.p0[row];
-    const double hy = 0.5 * y2;
-    const double hr = (-0.5 * y2) / tau;
-    const int k0 = L.tix[p0 * V + v];              // Koff[v] + own dish
-    const int j0 = k0 - koff;
-    const int l0p = L.dl[k0] - (alive ? 0 : 1);
-    double w0 = (double)l0p - sigma;
-    if (w0 < 0.0) w0 = 0.0;
-    if (!(l0p > 0)) w0 = -1.0;
+    const int k0 = Ltix[R.p0[row] * V + v];        // Koff[v] + own dish
+    const bool alive = (alive4 >> r) & 1;
+    hy[r] = 0.5 * y2;
+    hr[r] = (-0.5 * y2) / tau;
+    j0[r] = k0 - koff;
+    l0p[r] = L.dl[k0] - (alive ? 0 : 1);
+    double w = (double)l0p[r] - sigma;
+    if (w < 0.0) w = 0.0;
+    w0[r] = (l0p[r] > 0) ? w : -1.0;
     // the own dish with the customer removed (computed in every lane; kept
     // by the lane whose column and block hold j0)
-    double Gs = acc[0][0];
+    double Gs = acc[0][r];
 #pragma unroll
     for (int t = 1; t < NT; ++t)
-      if ((j0 >> 4) == t) Gs = acc[t][0];
+      if ((j0[r] >> 4) == t) Gs = acc[t][r];
     const double Gp = Gs - y2;
     const double Qp = (L.Q[k0] - 2.0 * Gs) + y2;
     const double c0s = L.sd0[k0] - (0.5 * Qp) / L.sden[k0];
-    const double sv = __builtin_fma(Gp + hy, L.scb[k0], c0s) + hr;
-    double m = -MVC_PM_INF;
-    double wt[NT];
+    sv[r] = __builtin_fma(Gp + hy[r], L.scb[k0], c0s) + hr[r];
+  }
+  double wt[NT][4], m[4];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int j = 16 * t + col;
-      const int kc = koff + min(j, K - 1);
-      const double fr = __builtin_fma(acc[t][0] + hy, Lcb[kc], Lc0[kc]) + hr;
-      acc[t][0] = (j == j0) ? sv : fr;             // lp
-      wt[t] = (j == j0) ? w0 : (j < K ? Lw[kc] : -1.0);
-      if (wt[t] >= 0.0 && acc[t][0] > m) m = acc[t][0];
-    }
-    m = row_max16(m);
-    const double lfn = cnew + hr;
-    if (lfn > m) m = lfn;
-    double cs = 0.0;
+  for (int r = 0; r < 4; ++r) m[r] = -MVC_PM_INF;
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const double e = mvc_exp_sk(wt[t] >= 0.0 ? acc[t][0] - m : 0.0);
-      if (wt[t] >= 0.0) cs = cs + wt[t] * e;
+  for (int t = 0; t < NT; ++t) {
+    const int j = 16 * t + col;
+    const int kc = koff + min(j, K - 1);
+    const double cbj = Lcb[kc], c0j = Lc0[kc], wj = j < K ? Lw[kc] : -1.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double fr = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+      acc[t][r] = (j == j0[r]) ? sv[r] : fr;       // lp
+      wt[t][r] = (j == j0[r]) ? w0[r] : wj;
+      if (wt[t][r] >= 0.0 && acc[t][r] > m[r]) m[r] = acc[t][r];
     }
-    double S = row_pw16(cs);
-    const int Kact = K - ((l0p == 0) ? 1 : 0);
+  }
+  double lfn[4], cs[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = row_max16(m[r]);
+    lfn[r] = cnew + hr[r];
+    if (lfn[r] > m[r]) m[r] = lfn[r];
+    cs[r] = 0.0;
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double e = mvc_exp_sk(wt[t][r] >= 0.0 ? acc[t][r] - m[r] : 0.0);
+      if (wt[t][r] >= 0.0) cs[r] = cs[r] + wt[t][r] * e;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double S = row_pw16(cs[r]);
+    const int Kact = K - ((l0p[r] == 0) ? 1 : 0);
     double wn = alpha + (double)Kact * sigma;
     if (wn < 0.0) wn = 0.0;
-    S = S + wn * mvc_exp_sk(lfn - m);
-    const int di = 2 * v + (alive ? 0 : 1);
-    const double lm = L.dpos[di] ? (m + mvc_log(S)) - L.lden[di] : lfn;
-    s_new[0] = s_new[0] + lm;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = rot4(acc[t]);
-    s_new = rot4(s_new);
+    S = S + wn * mvc_exp_sk(lfn[r] - m[r]);
+    const int di = 2 * v + (((alive4 >> r) & 1) ? 0 : 1);
+    const double lm = L.dpos[di] ? (m[r] + mvc_log_nb(S)) - L.lden[di] : lfn[r];
+    s_new[r] = s_new[r] + lm;
+  }
   }
   // table scores: sp[tb][r] += lp[row][dish_v(16 tb + col)] (row lanes only).
   // Branch-free over all MVC_FZ_TB blocks: padding positions p >= T hold
@@ -1297,17 +1313,33 @@ __global__ __launch_bounds__(MVC_FZ_THREADS, 1) void mvc_par_zfused_kernel(Sweep
 #pragma unroll
     for (int u = 0; u < RP; ++u) ring[u] = c0p[u * 64];
   }
+  // row data (table, Y2 per view) of the tiles, loaded one tile ahead and
+  // unconditionally: a load under a lane-dependent branch makes hipcc wait
+  // vmcnt(0), which would drain the A-fragment ring every tile
+  constexpr int NQ = (V + 3) / 4;
+  auto row_load = [&](int m, int &pz, double (&y2v)[NQ]) {
+    const int ic = min((gw + min(m, nmy - 1) * NWT) * 16 + col, n - 1);
+    pz = P.z[ic];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) y2v[q] = A.Y2[(size_t)min(4 * q + grp, V - 1) * n + ic];
+  };
+  int pz_n;
+  double y2v_n[NQ];
+  row_load(0, pz_n, y2v_n);
   int *const dslot = discard + lane;
   for (int m = 0; m < nmy; ++m) {
     const int li0 = (gw + m * NWT) * 16;
-    // row data of the tile: lane (grp, col) fills view grp, grp + 4, ... of row col
     {
-      const int ic = min(li0 + col, n - 1);
+      const int pz = pz_n;
+      double y2v[NQ];
 #pragma unroll
-      for (int v = 0; v < V; v += 4)
-        if (v + grp < V) R.y2[(v + grp) * 16 + col] = A.Y2[(size_t)(v + grp) * n + ic];
-      if (grp == 0) R.p0[col] = P.z[ic];
-      if (grp == 1) R.u[col] = mvc_uniform(A.seed, (uint32_t)ic, A.sweep, A.chain, MVC_TAG_Z);
+      for (int q = 0; q < NQ; ++q) y2v[q] = y2v_n[q];
+      row_load(m + 1, pz_n, y2v_n);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q)
+        if (4 * q + grp < V) R.y2[(4 * q + grp) * 16 + col] = y2v[q];
+      if (grp == 0) R.p0[col] = pz;
+      if (grp == 1) R.u[col] = mvc_uniform(A.seed, (uint32_t)min(li0 + col, n - 1), A.sweep, A.chain, MVC_TAG_Z);
     }
     wave_lds_sync();
     int alive4 = 0;
@@ -1327,7 +1359,7 @@ __global__ __launch_bounds__(MVC_FZ_THREADS, 1) void mvc_par_zfused_kernel(Sweep
     int oz = 0;
     asm volatile("" : "+v"(oz));
     fz_views<SPPT, RP, PAT, 0>(A, L, R, T, ybase, vstride, toff(m), toff(m + 1), ring, alive4, s_new, sp, oz);
-    // ---- draw (oracle resample_customer), one row per pass (rotating)
+    // ---- draw (oracle resample_customer), the four rows at once
     int pv = -1;
 #ifdef FZ_ABL_DRAW
 #pragma unroll
@@ -1335,55 +1367,66 @@ __global__ __launch_bounds__(MVC_FZ_THREADS, 1) void mvc_par_zfused_kernel(Sweep
     pv = R.p0[grp + 4 * col];
     if (false)
 #endif
-#pragma unroll 1
-    for (int r = 0; r < 4; ++r) {
-      double M = -MVC_PM_INF;
+    {
+      double M[4], tot[4], C[MVC_FZ_TB][4];
 #pragma unroll
-      for (int tb = 0; tb < MVC_FZ_TB; ++tb)
-        if (16 * tb + col < T && sp[tb][0] > M) M = sp[tb][0];
-      M = row_max16(M);
-      if (s_new[0] > M) M = s_new[0];
-      double ev[MVC_FZ_TB], C[MVC_FZ_TB];
-      double tot = 0.0;
+      for (int r = 0; r < 4; ++r) {
+        double mx = -MVC_PM_INF;
+#pragma unroll
+        for (int tb = 0; tb < MVC_FZ_TB; ++tb)
+          if (16 * tb + col < T && sp[tb][r] > mx) mx = sp[tb][r];
+        M[r] = row_max16(mx);
+        if (s_new[r] > M[r]) M[r] = s_new[r];
+        tot[r] = 0.0;
+      }
 #pragma unroll
       for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
-        const bool in = 16 * tb + col < T && sp[tb][0] != -MVC_PM_INF;
-        const double e = mvc_exp_sk(in ? sp[tb][0] - M : 0.0);
-        ev[tb] = in ? e : 0.0;
-        tot = tot + row_pw16(ev[tb]);              // blocks past T add +0.0: exact
-        C[tb] = tot;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool in = 16 * tb + col < T && sp[tb][r] != -MVC_PM_INF;
+          const double e = mvc_exp_sk(in ? sp[tb][r] - M[r] : 0.0);
+          sp[tb][r] = in ? e : 0.0;                  // weights in place
+        }
       }
-      const double W = mvc_exp_sk(s_new[0] - M) + tot;
-      double rr = R.u[grp + 4 * r] * W;
-      const bool birth = !(rr < tot);
-      int bsel = 0;
-      double prev = 0.0, x = ev[0];
 #pragma unroll
-      for (int tb = MVC_FZ_TB - 1; tb >= 0; --tb)
-        if (rr < C[tb]) { bsel = tb; prev = tb > 0 ? C[tb - 1] : 0.0; x = ev[tb]; }
-      rr = rr - prev;
-      // pw16 descent: every lane follows the path towards its own column
-      const double t1 = x1_d(x), l1 = x + t1;
-      const double t2 = x2_d(l1), l2 = l1 + t2;
-      const double t4 = x4_d(l2), l4 = l2 + t4;
-      const double t8 = x8_d(l4);
-      bool on = !birth;
-      auto step = [&](double own, double other, int h) {
-        const bool hi = (col & h) != 0;
-        const double Lh = hi ? other : own, Rh = hi ? own : other;
-        const bool right = !(Rh == 0.0 || rr < Lh);
-        if (right != hi) on = false;
-        if (right) rr = rr - Lh;
-      };
-      step(l4, t8, 8);
-      step(l2, t4, 4);
-      step(l1, t2, 2);
-      step(x, t1, 1);
-      const int pk = row_max16_i(on ? 16 * bsel + col : -1);
-      if (col == r) pv = pk;                       // lane (col = r, grp) stores row grp + 4 r
+      for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
 #pragma unroll
-      for (int tb = 0; tb < MVC_FZ_TB; ++tb) sp[tb] = rot4(sp[tb]);
-      s_new = rot4(s_new);
+        for (int r = 0; r < 4; ++r) {
+          tot[r] = tot[r] + row_pw16(sp[tb][r]);     // blocks past T add +0.0: exact
+          C[tb][r] = tot[r];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double W = mvc_exp_sk(s_new[r] - M[r]) + tot[r];
+        double rr = R.u[grp + 4 * r] * W;
+        const bool birth = !(rr < tot[r]);
+        int bsel = 0;
+        double prev = 0.0, x = sp[0][r];
+#pragma unroll
+        for (int tb = MVC_FZ_TB - 1; tb >= 0; --tb)
+          if (rr < C[tb][r]) { bsel = tb; prev = tb > 0 ? C[tb - 1][r] : 0.0; x = sp[tb][r]; }
+        rr = rr - prev;
+        // pw16 descent: every lane follows the path towards its own column
+        const double t1 = x1_d(x), l1 = x + t1;
+        const double t2 = x2_d(l1), l2 = l1 + t2;
+        const double t4 = x4_d(l2), l4 = l2 + t4;
+        const double t8 = x8_d(l4);
+        bool on = !birth;
+        auto step = [&](double own, double other, int h) {
+          const bool hi = (col & h) != 0;
+          const double Lh = hi ? other : own, Rh = hi ? own : other;
+          const bool right = !(Rh == 0.0 || rr < Lh);
+          if (right != hi) on = false;
+          if (right) rr = rr - Lh;
+        };
+        step(l4, t8, 8);
+        step(l2, t4, 4);
+        step(l1, t2, 2);
+        step(x, t1, 1);
+        const int pk = row_max16_i(on ? 16 * bsel + col : -1);
+        if (col == r) pv = pk;                       // lane (col = r, grp) stores row grp + 4 r
+      }
     }
     const int li = li0 + grp + 4 * col;
     int *dst = (col < 4 && li < n) ? A.choice + li : dslot;
@@ -1980,13 +2023,15 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
   __syncthreads();
   double *hyp = P.hyper;
   if (A.do_mh) {
-    uint32_t kdraw = 0;
-    auto unif = [&]() -> double {   // block-uniform: every thread draws the same counter
-      return mvc_uniform(A.seed, kdraw++, A.sweep, A.chain, MVC_TAG_MH);
-    };
-    auto rnorm = [&](double mu, double sd) -> double {
-      const double u1 = unif();
-      const double u2 = unif();
+    // Every MH step draws from its own window of the MH counter (oracle
+    // update_hyper): tau of view v at 3v, alpha/sigma of view v at 3V + 6v,
+    // the global pair at 9V.  The per-view steps are independent, so wave w
+    // runs views w, w + 4, ... with wavefront-level tree64 sums (same
+    // association as block_tree64); the global pair then runs on the block.
+    auto unif_at = [&](uint32_t k) -> double { return mvc_uniform(A.seed, k, A.sweep, A.chain, MVC_TAG_MH); };
+    auto rnorm_at = [&](uint32_t k, double mu, double sd) -> double {
+      const double u1 = unif_at(k);
+      const double u2 = unif_at(k + 1);
       return mu + sd * mvc_norm_from_uniforms(u1, u2);
     };
     auto prior_alpha = [](double a) -> double {
@@ -2005,100 +2050,130 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       }
       return p < kEps ? kEps : (p > 1.0 - kEps ? 1.0 - kEps : p);
     };
-    // EPPF of a partition: K blocks of sizes size(j) >= 1, total tot
-    auto eppf = [&](int K, int tot, auto size, double a, double s) -> double {
+    // EPPF of a partition: K blocks of sizes size(j) >= 1, total tot; tree is
+    // the wave- or block-level tree64
+    auto eppf = [&](int K, int tot, auto size, double a, double s, auto tree) -> double {
       if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
       if (a <= -s) return -MVC_PM_INF;
       // any term a + j s <= 0 ?  (monotone in j for s > 0: check j = 0)
       if (K > 0 && !(a + 0.0 * s > 0.0)) return -MVC_PM_INF;
-      const double P1 = block_tree64(K, [&](int64_t j) { return mvc_log(a + (double)j * s); });
+      const double P1 = tree(K, [&](int64_t j) { return mvc_log(a + (double)j * s); });
       const double P2 = mvc_lgamma_pos(a + (double)tot) - mvc_lgamma_pos(a + 1.0);
       const double lg1 = mvc_lgamma_pos(1.0 - s);
-      const double P3 = block_tree64(K, [&](int64_t j) { return mvc_lgamma_pos((double)size((int)j) - s) - lg1; });
+      const double P3 = tree(K, [&](int64_t j) { return mvc_lgamma_pos((double)size((int)j) - s) - lg1; });
       return (P1 - P2) + P3;
     };
-    auto eppf_view = [&](int v, double a, double s) -> double {
-      if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
-      if (a <= -s) return -MVC_PM_INF;
-      if (P.Ltot[v] == 0) return 0.0;
-      return eppf(P.Kact[v], P.Ltot[v], [&](int j) { return P.d_l[v * KC + j]; }, a, s);
-    };
+    // ---- per-view steps, one wavefront per view (multiview_hyper.cpp:211-266)
+    {
+      __shared__ double s_wpart[4][64];
+      const int lane = tid & 63, wv = tid >> 6;
+      auto wtree = [&](int64_t nn, auto leaf) -> double {   // tree64 by one wavefront (nn <= 4096)
+        if (nn <= 0) return 0.0;
+        const int mch = (int)((nn + 63) / 64);
+        double root = 0.0;
+        for (int c = 0; c < mch; ++c) {
+          const int64_t e = (int64_t)c * 64 + lane;
+          const double x = e < nn ? leaf(e) : 0.0;
+          const double cs = wave_tree_sum(x);
+          if (mch == 1) root = cs;
+          else if (lane == 0) s_wpart[wv][c] = cs;
+        }
+        if (mch > 1) {
+          wave_lds_sync();
+          root = wave_tree_sum(lane < mch ? s_wpart[wv][lane] : 0.0);
+          wave_lds_sync();
+        }
+        return root;
+      };
+      for (int v = wv; v < V; v += 4) {
+        const int Kv = P.Kact[v], Lv = P.Ltot[v];
+        auto eppf_view = [&](double a, double s) -> double {
+          if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
+          if (a <= -s) return -MVC_PM_INF;
+          if (Lv == 0) return 0.0;
+          return eppf(Kv, Lv, [&](int j) { return P.d_l[v * KC + j]; }, a, s, wtree);
+        };
+        auto post_tau = [&](double t) -> double {
+          if (t <= 0.0) return -MVC_PM_INF;
+          const double L = mvc_log((2.0 * MVC_PI) * t);
+          const double ll = wtree(Kv, [&](int64_t j) {
+            const int nk = P.d_n[v * KC + j];
+            if (nk == 0) return 0.0;
+            double sse = P.S2[v * KC + j] - P.Q[v * KC + j] / (double)nk;
+            if (sse < 0.0) sse = 0.0;
+            return ((-0.5 * (double)nk) * (double)D) * L - 0.5 * (sse / t);
+          });
+          const double prior = (-3.0 * mvc_log(t)) - 1.0 / t;
+          return ll + prior;
+        };
+        // tau (multiview_hyper.cpp:211-231), counters 3v ..
+        double tau_v = hyp[v];
+        {
+          const uint32_t k0 = 3u * (uint32_t)v;
+          double t_old = tau_v;
+          if (t_old <= 0.0) t_old = kEps;
+          const double l_old = post_tau(t_old);
+          const double t_prop = mvc_exp(mvc_log(t_old) + rnorm_at(k0, 0.0, 0.3));
+          if (t_prop > 0.0) {
+            const double l_new = post_tau(t_prop);
+            const double acc = (l_new - l_old) + (mvc_log(t_prop) - mvc_log(t_old));
+            if (mvc_log(unif_at(k0 + 2)) < acc) tau_v = t_prop;
+          }
+        }
+        // alpha_v, sigma_v (:239-266), counters 3V + 6v ..
+        double a_v = hyp[V + v], s_v = hyp[2 * V + v];
+        {
+          const uint32_t k0 = 3u * (uint32_t)V + 6u * (uint32_t)v;
+          double a_old = a_v;
+          if (a_old <= 0.0) a_old = kEps;
+          const double la = mvc_log(a_old > kEps ? a_old : kEps) + rnorm_at(k0, 0.0, 0.1);
+          double a_prop = mvc_exp(la);
+          if (!(a_prop > kEps)) a_prop = kEps;
+          const double lo = (a_old <= 0.0) ? -MVC_PM_INF : eppf_view(a_old, s_v) + prior_alpha(a_old);
+          const double ln = (a_prop <= 0.0) ? -MVC_PM_INF : eppf_view(a_prop, s_v) + prior_alpha(a_prop);
+          const double lq = mvc_log(a_prop) - mvc_log(a_old);
+          if (mvc_log(unif_at(k0 + 2)) < (ln - lo) + lq) a_v = a_prop;
+          const double s_old = s_v;
+          const double s_prop = reflect_unit(s_old + rnorm_at(k0 + 3, 0.0, 0.05));
+          const double u2 = unif_at(k0 + 5);
+          const double pn = (s_prop <= kEps || s_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(a_v, s_prop) + prior_sigma(s_prop);
+          const double po = (s_old <= kEps || s_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(a_v, s_old) + prior_sigma(s_old);
+          if (mvc_log(u2) < pn - po) s_v = s_prop;
+        }
+        if (lane == 0) { hyp[v] = tau_v; hyp[V + v] = a_v; hyp[2 * V + v] = s_v; }
+      }
+    }
+    __syncthreads();
+    // ---- global pair (:268-291), counters 9V .., the whole block
+    auto btree = [&](int64_t nn, auto leaf) -> double { return block_tree64(nn, leaf); };
     auto eppf_global = [&](double a, double s) -> double {
       if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
       if (a <= -s) return -MVC_PM_INF;
       if (T <= 0) return 0.0;
-      return eppf(T, n, [&](int p) { return P.n_t[p]; }, a, s);
+      return eppf(T, n, [&](int p) { return P.n_t[p]; }, a, s, btree);
     };
-    auto post_tau = [&](int v, double t) -> double {
-      if (t <= 0.0) return -MVC_PM_INF;
-      const double L = mvc_log((2.0 * MVC_PI) * t);
-      const double ll = block_tree64(P.Kact[v], [&](int64_t j) {
-        const int nk = P.d_n[v * KC + j];
-        if (nk == 0) return 0.0;
-        double sse = P.S2[v * KC + j] - P.Q[v * KC + j] / (double)nk;
-        if (sse < 0.0) sse = 0.0;
-        return ((-0.5 * (double)nk) * (double)D) * L - 0.5 * (sse / t);
-      });
-      const double prior = (-3.0 * mvc_log(t)) - 1.0 / t;
-      return ll + prior;
-    };
-    // ---- multiview_hyper.cpp:211-231 ----
-    for (int v = 0; v < V; ++v) {
-      double t_old = hyp[v];
-      if (t_old <= 0.0) t_old = kEps;
-      const double l_old = post_tau(v, t_old);
-      const double t_prop = mvc_exp(mvc_log(t_old) + rnorm(0.0, 0.3));
-      if (t_prop <= 0.0) continue;
-      const double l_new = post_tau(v, t_prop);
-      const double acc = (l_new - l_old) + (mvc_log(t_prop) - mvc_log(t_old));
-      const double u = unif();
-      if (mvc_log(u) < acc) { if (tid == 0) hyp[v] = t_prop; }
-      __syncthreads();
-    }
-    // ---- :239-266 ----
-    for (int v = 0; v < V; ++v) {
-      double a_old = hyp[V + v];
-      if (a_old <= 0.0) a_old = kEps;
-      const double la = mvc_log(a_old > kEps ? a_old : kEps) + rnorm(0.0, 0.1);
-      double a_prop = mvc_exp(la);
-      if (!(a_prop > kEps)) a_prop = kEps;
-      const double sv = hyp[2 * V + v];
-      const double lo = (a_old <= 0.0) ? -MVC_PM_INF : eppf_view(v, a_old, sv) + prior_alpha(a_old);
-      const double ln = (a_prop <= 0.0) ? -MVC_PM_INF : eppf_view(v, a_prop, sv) + prior_alpha(a_prop);
-      const double lq = mvc_log(a_prop) - mvc_log(a_old);
-      const double u = unif();
-      if (mvc_log(u) < (ln - lo) + lq) { if (tid == 0) hyp[V + v] = a_prop; }
-      __syncthreads();
-      const double s_old = hyp[2 * V + v];
-      const double s_prop = reflect_unit(s_old + rnorm(0.0, 0.05));
-      const double u2 = unif();
-      const double av = hyp[V + v];
-      const double pn = (s_prop <= kEps || s_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(v, av, s_prop) + prior_sigma(s_prop);
-      const double po = (s_old <= kEps || s_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(v, av, s_old) + prior_sigma(s_old);
-      if (mvc_log(u2) < pn - po) { if (tid == 0) hyp[2 * V + v] = s_prop; }
-      __syncthreads();
-    }
-    // ---- :268-291 ----
     {
+      const uint32_t k0 = 9u * (uint32_t)V;
       double ag_old = hyp[3 * V];
       if (ag_old <= 0.0) ag_old = kEps;
-      const double la = mvc_log(ag_old > kEps ? ag_old : kEps) + rnorm(0.0, 0.1);
+      const double la = mvc_log(ag_old > kEps ? ag_old : kEps) + rnorm_at(k0, 0.0, 0.1);
       double ag_prop = mvc_exp(la);
       if (!(ag_prop > kEps)) ag_prop = kEps;
       const double sg0 = hyp[3 * V + 1];
       const double lo = eppf_global(ag_old, sg0) + prior_alpha(ag_old);
       const double ln = eppf_global(ag_prop, sg0) + prior_alpha(ag_prop);
       const double lq = mvc_log(ag_prop) - mvc_log(ag_old);
-      const double u = unif();
-      if (mvc_log(u) < (ln - lo) + lq) { if (tid == 0) hyp[3 * V] = ag_prop; }
-      __syncthreads();
-      const double sg_old = hyp[3 * V + 1];
-      const double sg_prop = reflect_unit(sg_old + rnorm(0.0, 0.05));
-      const double u2 = unif();
-      const double a_g = hyp[3 * V];
+      double a_g = hyp[3 * V];
+      if (mvc_log(unif_at(k0 + 2)) < (ln - lo) + lq) a_g = ag_prop;
+      const double sg_old = sg0;
+      const double sg_prop = reflect_unit(sg_old + rnorm_at(k0 + 3, 0.0, 0.05));
+      const double u2 = unif_at(k0 + 5);
       const double pn = (sg_prop <= kEps || sg_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_prop) + prior_sigma(sg_prop);
       const double po = (sg_old <= kEps || sg_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_old) + prior_sigma(sg_old);
-      if (mvc_log(u2) < pn - po) { if (tid == 0) hyp[3 * V + 1] = sg_prop; }
+      double s_g = sg_old;
+      if (mvc_log(u2) < pn - po) s_g = sg_prop;
+      __syncthreads();
+      if (tid == 0) { hyp[3 * V] = a_g; hyp[3 * V + 1] = s_g; }
       __syncthreads();
     }
   }

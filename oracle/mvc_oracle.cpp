@@ -1383,9 +1383,14 @@ struct ParallelSampler {
     }
     return std::clamp(p, kEps, 1.0 - kEps);
   }
+  // Each MH step draws from its own fixed window of the MH counter (tau of
+  // view v: 3v..3v+2; alpha/sigma of view v: 3V+6v..+5; global: 9V..9V+5),
+  // so the per-view steps are independent and run on separate GPU wavefronts
+  // (DESIGN.md §4.7).  The step order within a window is the reference's
+  // (multiview_hyper.cpp:233-292).
   void update_hyper(int s) {
-    MHRng R{seed, chain, (uint32_t)s, 0};
     for (int v = 0; v < V; ++v) {
+      MHRng R{seed, chain, (uint32_t)s, (uint32_t)(3 * v)};
       double t_old = tau[v];
       if (t_old <= 0.0) t_old = kEps;
       const double l_old = post_tau(v, t_old);
@@ -1396,6 +1401,7 @@ struct ParallelSampler {
       if (mvc_log(R.unif()) < acc) tau[v] = t_prop;
     }
     for (int v = 0; v < V; ++v) {
+      MHRng R{seed, chain, (uint32_t)s, (uint32_t)(3 * V + 6 * v)};
       double a_old = alpha[v];
       if (a_old <= 0.0) a_old = kEps;
       double la = mvc_log(std::max(a_old, kEps)) + R.rnorm(0.0, 0.1);
@@ -1414,6 +1420,7 @@ struct ParallelSampler {
       };
       if (mvc_log(u) < ps(s_prop) - ps(s_old)) sigma[v] = s_prop;
     }
+    MHRng R{seed, chain, (uint32_t)s, (uint32_t)(9 * V)};
     double ag_old = ag;
     if (ag_old <= 0.0) ag_old = kEps;
     double la = mvc_log(std::max(ag_old, kEps)) + R.rnorm(0.0, 0.1);
