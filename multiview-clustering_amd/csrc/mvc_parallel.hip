@@ -63,6 +63,7 @@ struct Sweep {
   const double *yt;       // MFMA A-fragment layout of y (mvc_par_ytile_kernel)
   const double *S1t;      // MFMA B-fragment layout of S1 (mvc_par_s1tile_kernel)
   int32_t SP;             // k-steps per view in yt/S1t (D/4 rounded up to MVC_ZR)
+  double *vmax;           // [V][n] the view maximum m_v of each customer (producer -> draw)
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
@@ -305,7 +306,7 @@ typedef double mvc_d2 __attribute__((ext_vector_type(2)));
 // accumulators to the lp buffer (a fixed number of stores per tile).
 #define MVC_ZR 8              // SP (k-steps per view) is padded to a multiple of this
 __host__ __device__ inline size_t lpview_shared_bytes(int SP, int NT, int K, int T) {
-  return 8 * ((size_t)SP * NT * 64 + 3 * (size_t)K + 8 * 32) + 4 * ((size_t)K + (size_t)T + 8 * 16) + 64;
+  return 8 * ((size_t)SP * NT * 64 + 3 * (size_t)K + 8 * 48) + 4 * (2 * (size_t)K + 2 * (size_t)T + 8 * 16) + 64;
 }
 
 // k-step pairs of one 16-customer tile: SPPT > 0 fully unrolled (static ring
@@ -368,13 +369,16 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
   double *d_c0 = Bs + (size_t)SP * NT * 64;        // [K]
   double *d_cb = d_c0 + K;
   double *d_Q = d_cb + K;
-  double *wsp = d_Q + K;                           // per wave: y2s[16], selfG[16]
-  double *y2s = wsp + w * 32;
+  double *wsp = d_Q + K;                           // per wave: y2s[16], selfG[16], mrest[16]
+  double *y2s = wsp + w * 48;
   double *selfG = y2s + 16;
-  int *ip = (int *)(wsp + 8 * 32);
+  double *mrest = selfG + 16;
+  int *ip = (int *)(wsp + 8 * 48);
   int *d_n = ip;                                   // [K]
-  int *t_dish = d_n + K;                           // [T]
-  int *zs = t_dish + T + w * 16;                   // per wave [16]
+  int *d_l = d_n + K;                              // [K]
+  int *t_dish = d_l + K;                           // [T]
+  int *t_n = t_dish + T;                           // [T]
+  int *zs = t_n + T + w * 16;                      // per wave [16]
   {
     size_t off = 0;
     for (int u = 0; u < v; ++u) off += (size_t)SP * 64 * ((A.Koff[u + 1] - A.Koff[u] + 15) >> 4);
@@ -387,9 +391,14 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
     d_cb[j] = P.cb[v * KC + j];
     d_Q[j] = P.Q[v * KC + j];
     d_n[j] = P.d_n[v * KC + j];
+    d_l[j] = P.d_l[v * KC + j];
   }
-  for (int p = tid; p < T; p += blockDim.x) t_dish[p] = P.dish[v * P.TC + p];
+  for (int p = tid; p < T; p += blockDim.x) {
+    t_dish[p] = P.dish[v * P.TC + p];
+    t_n[p] = P.n_t[p];
+  }
   __syncthreads();
+  const double cnew = A.cnew[v];
 
   const int ntile = (nb + 15) >> 4;
   const int ntile_all = (n + 15) >> 4;
@@ -444,18 +453,32 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
     // frozen-dish lp for every (row, dish): a fixed number of unconditional
     // stores (invalid lanes go to their discard slot; the own dish is
     // overwritten below by this same wave, in program order)
+    // The view maximum of the draw (oracle eval_view_seq: max over included
+    // dishes, then the new dish) is formed here: the frozen dishes other than
+    // the own one by a 16-lane max per row, the own dish and the new dish by
+    // the row's lane below; m_v goes to vmax, so the draw reads each lp row once.
+    double mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[r] = -MVC_PM_INF;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int j = 16 * t + col;
       const int jc = min(j, K - 1);
       const double c0j = d_c0[jc], cbj = d_cb[jc];
+      const bool inc = j < K && d_l[jc] > 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
         const int li = li0 + grp + 4 * r;
         double *dst = (j < K && li < nb) ? lpb + lpb_index(li, koff + j, sumK) : dslot;
         *dst = val;
+        if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
       }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double mr = row16_max(mx[r]);
+      if (col == 0) mrest[grp + 4 * r] = mr;
     }
     wave_lds_sync();
     {   // own dish, one row per lane
@@ -464,9 +487,18 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
       const double Gp = G - y2;
       const double Qp = (d_Q[jj] - 2.0 * G) + y2;
       const Coef cf = coef(d_n[jj] - 1, Qp, tau, L2pt, D);
-      const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + (-0.5 * y2) / tau;
-      double *dst = (lane < 16 && li0 + col < nb) ? lpb + lpb_index(li0 + col, koff + jj, sumK) : dslot;
+      const double hself = (-0.5 * y2) / tau;
+      const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
+      const bool ok = lane < 16 && li0 + col < nb;
+      double *dst = ok ? lpb + lpb_index(li0 + col, koff + jj, sumK) : dslot;
       *dst = sv;
+      const int l0p = d_l[jj] - ((t_n[pz] - 1) > 0 ? 0 : 1);
+      double m = mrest[col];
+      if (l0p > 0 && sv > m) m = sv;
+      const double lfn = cnew + hself;
+      if (lfn > m) m = lfn;
+      double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
+      *dm = m;
     }
     wave_lds_sync();
   }
@@ -488,18 +520,27 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_lpgen_kernel(Sweep A, 
       const double hy = 0.5 * Y2i, h = (-0.5 * Y2i) / tau;
       const double *yrow = A.y + ((size_t)v * n + i) * D;
       const double *S1v = P.S1T + (size_t)v * D * KC;
-      double G0 = 0.0;
+      double G0 = 0.0, mx = -MVC_PM_INF;
       for (int j = 0; j < K; ++j) {
         double G = 0.0;
         for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S1v[(size_t)d * KC + j], G);
         if (j == j0) G0 = G;
-        lpb[lpb_index(li, koff + j, sumK)] = __builtin_fma(G + hy, P.cb[v * KC + j], P.c0[v * KC + j]) + h;
+        const double val = __builtin_fma(G + hy, P.cb[v * KC + j], P.c0[v * KC + j]) + h;
+        lpb[lpb_index(li, koff + j, sumK)] = val;
+        if (j != j0 && P.d_l[v * KC + j] > 0 && val > mx) mx = val;
       }
       // own dish: reduced statistics (same thread, stored after the loop)
       const double Gp = G0 - Y2i;
       const double Qp = (P.Q[v * KC + j0] - 2.0 * G0) + Y2i;
       const Coef c = coef(P.d_n[v * KC + j0] - 1, Qp, tau, A.L2pt[v], D);
-      lpb[lpb_index(li, koff + j0, sumK)] = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
+      const double sv = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
+      lpb[lpb_index(li, koff + j0, sumK)] = sv;
+      // the view maximum of the draw (see mvc_par_lpview_kernel)
+      const int l0p = P.d_l[v * KC + j0] - ((P.n_t[p0] - 1) > 0 ? 0 : 1);
+      if (l0p > 0 && sv > mx) mx = sv;
+      const double lfn = A.cnew[v] + h;
+      if (lfn > mx) mx = lfn;
+      A.vmax[(size_t)v * n + i] = mx;
     }
   }
 }
@@ -741,16 +782,16 @@ struct LpRow {
   __device__ __forceinline__ double operator()(int k) const { return mvc_raw_buffer_load_f64(rsrc, boff, k * 128, 0); }
 };
 
-// View reduction of the draw (oracle eval_view_seq): max, then the sum of
+// View reduction of the draw (oracle eval_view_seq): the sum of
 // w_j exp(lp_j - m) as 16 column partials (dish j -> column j & 15, ascending
-// j) folded by pw16.  w_j = max(l_j - sigma, 0) for l_j > 0 and -1 (excluded)
-// otherwise: uniform per dish (s_w, staged once per block) except the
-// customer's own dish (w0).  KB > 0: row held in registers (one load pass);
-// KB == 0: streamed twice in batches of 16.
+// j) folded by pw16; m (the max over included dishes and the new dish) comes
+// from the producer (vmax), so every row is read once.  w_j = max(l_j - sigma,
+// 0) for l_j > 0 and -1 (excluded) otherwise: uniform per dish (s_w, staged
+// once per block) except the customer's own dish (w0).  KB > 0: row loaded
+// into registers at once; KB == 0: streamed in batches of 16.
 template <int KB>
-__device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int j0, double w0, const double *sw,
-                                          double lfn, double &m_out, double &S_out) {
-  double m = -MVC_PM_INF;
+__device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, int j0, double w0, const double *sw,
+                                            double m, double *stg = nullptr) {
   double col[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) col[c] = 0.0;
@@ -758,16 +799,11 @@ __device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int
     double x[KB];
 #pragma unroll
     for (int j = 0; j < KB; ++j) x[j] = row(koff + min(j, K - 1));
-    // every frozen dish other than the customer's own has l >= 1 (the
-    // caller takes this path only then), so validity is a question at j0 only
+    if (stg) {                                     // wave-uniform: keep the row in LDS for the table gathers
 #pragma unroll
-    for (int j = 0; j < KB; ++j) {
-      if (j < K) {
-        const bool ok = (j != j0) || (w0 >= 0.0);
-        if (ok && x[j] > m) m = x[j];
-      }
+      for (int j = 0; j < KB; ++j)
+        if (j < K) stg[j * 64] = x[j];
     }
-    if (lfn > m) m = lfn;
 #pragma unroll
     for (int j = 0; j < KB; ++j) {
       if (j < K) {
@@ -780,23 +816,6 @@ __device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int
     }
   } else {
     int j = 0;
-    for (; j + 16 <= K; j += 16) {
-      double x[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) x[u] = row(koff + j + u);
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const double w = (j + u == j0) ? w0 : sw[j + u];
-        if (w >= 0.0 && x[u] > m) m = x[u];
-      }
-    }
-    for (; j < K; ++j) {
-      const double w = (j == j0) ? w0 : sw[j];
-      const double x = row(koff + j);
-      if (w >= 0.0 && x > m) m = x;
-    }
-    if (lfn > m) m = lfn;
-    j = 0;
     for (; j + 16 <= K; j += 16) {
       double x[16];
 #pragma unroll
@@ -819,10 +838,10 @@ __device__ __forceinline__ void zview_red(const LpRow &row, int koff, int K, int
       }
     }
   }
-  m_out = m;
-  S_out = pw16(col);
+  return pw16(col);
 }
 
+#define MVC_ZSTAGE 24          // dishes per wave whose lp rows the register draw keeps in LDS (3 blocks/CU)
 template <int TM>
 #ifndef MVC_ZDRAW_MINB
 #define MVC_ZDRAW_MINB 3      // blocks of 4 waves per CU the register budget must allow
@@ -833,12 +852,16 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
   const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
   const int T = __builtin_amdgcn_readfirstlane(A.T);
   const int tid = threadIdx.x;
+  const int sumK0 = __builtin_amdgcn_readfirstlane(A.Koff[V]);
   double *s_base = (double *)smem;                 // [TM] log mass (or -inf)
   double *s_w = s_base + TM;                       // [sumK] dish weights max(l - sigma, 0) / -1
-  int *s_tix = (int *)(s_w + MVC_Z_VMAX * 64);     // [TM][V] Koff[v] + dish_v(p)
+  double *s_stage = s_w + sumK0;                   // [4 waves][MVC_ZSTAGE][64] staged lp rows
+  int *s_tix = (int *)(s_stage + 4 * MVC_ZSTAGE * 64);   // [TM][V] Koff[v] + dish_v(p)
   int *s_koff = s_tix + (size_t)TM * V;            // [V+1]
   int *s_lmin = s_koff + V + 1;                    // [VMAX] 1: every dish of view v has l >= 1
-  int *s_dl = s_lmin + MVC_Z_VMAX;                 // [sumK] l of each dish
+  int *s_soff = s_lmin + MVC_Z_VMAX;               // [VMAX] staging offset of view v (dishes), -1: not staged
+  int *s_dl = s_soff + MVC_Z_VMAX;                 // [sumK] l of each dish
+  s_stage += (size_t)(threadIdx.x >> 6) * MVC_ZSTAGE * 64;
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
   if (tid <= V) s_koff[tid] = A.Koff[tid];
   __syncthreads();
@@ -861,6 +884,16 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     if (l < 1) s_lmin[v] = 0;                    // benign race: every writer stores 0
   }
   __syncthreads();
+  if (tid == 0) {   // views whose rows the draw holds in registers (K <= 16) also go to LDS, budget permitting
+    int tot = 0;
+    for (int v = 0; v < V; ++v) {
+      const int K = s_koff[v + 1] - s_koff[v];
+      const bool st = s_lmin[v] != 0 && K <= 16 && tot + K <= MVC_ZSTAGE;
+      s_soff[v] = st ? tot : -1;
+      tot += st ? K : 0;
+    }
+  }
+  __syncthreads();
   const int T_ne = A.status[V + 3];
   {
     const int li = blockIdx.x * blockDim.x + tid;   // one customer per thread (no loop-invariant hoisting)
@@ -881,17 +914,15 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
       if (w0 < 0.0) w0 = 0.0;
       if (!(l0p > 0)) w0 = -1.0;
       const double *sw = s_w + koff;
-      double m, S;
+      const double m = A.vmax[(size_t)v * n + i];
+      double S;
       const bool allv = __builtin_amdgcn_readfirstlane(s_lmin[v]) != 0;
-      if (!allv) zview_red<0>(row, koff, K, j0, w0, sw, lfn, m, S);           // general: streamed twice
-      else if (K <= 8) zview_red<8>(row, koff, K, j0, w0, sw, lfn, m, S);     // row in registers
-      else if (K <= 16) zview_red<16>(row, koff, K, j0, w0, sw, lfn, m, S);
-#ifdef MVC_ZREG_WIDE
-      else if (K <= 32) zview_red<32>(row, koff, K, j0, w0, sw, lfn, m, S);
-      else zview_red<64>(row, koff, K, j0, w0, sw, lfn, m, S);
-#else
-      else zview_red<0>(row, koff, K, j0, w0, sw, lfn, m, S);
-#endif
+      const int so = __builtin_amdgcn_readfirstlane(s_soff[v]);
+      double *stg = so >= 0 ? s_stage + (size_t)so * 64 + (tid & 63) : nullptr;
+      if (!allv) S = zview_sum<0>(row, koff, K, j0, w0, sw, m);           // general: streamed
+      else if (K <= 8) S = zview_sum<8>(row, koff, K, j0, w0, sw, m, stg);     // row in registers
+      else if (K <= 16) S = zview_sum<16>(row, koff, K, j0, w0, sw, m, stg);
+      else S = zview_sum<0>(row, koff, K, j0, w0, sw, m);
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = P.hyper[V + v] + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
@@ -914,8 +945,15 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     for (int c = 0; c < TM; c += 16) {
       for (int v = 0; v < V; ++v) {
         double x[16];
+        const int so = __builtin_amdgcn_readfirstlane(s_soff[v]);
+        if (so >= 0) {                             // staged row: LDS [dish][lane], conflict-free
+          const double *st = s_stage + (size_t)(so - s_koff[v]) * 64 + (tid & 63);
 #pragma unroll
-        for (int u = 0; u < 16; ++u) x[u] = row(__builtin_amdgcn_readfirstlane(s_tix[min(c + u, T - 1) * V + v]));
+          for (int u = 0; u < 16; ++u) x[u] = st[(size_t)__builtin_amdgcn_readfirstlane(s_tix[min(c + u, T - 1) * V + v]) * 64];
+        } else {
+#pragma unroll
+          for (int u = 0; u < 16; ++u) x[u] = row(__builtin_amdgcn_readfirstlane(s_tix[min(c + u, T - 1) * V + v]));
+        }
 #pragma unroll
         for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
       }
@@ -970,7 +1008,8 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
   }
 }
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
-  return 8 * ((size_t)TM + MVC_Z_VMAX * 64) + 4 * ((size_t)V * TM + (size_t)sumK + (size_t)V + 1 + MVC_Z_VMAX) + 64;
+  return 8 * ((size_t)TM + (size_t)sumK + (size_t)4 * MVC_ZSTAGE * 64) +
+         4 * ((size_t)V * TM + (size_t)V + 1 + 2 * MVC_Z_VMAX + (size_t)sumK) + 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -2249,6 +2288,7 @@ class ParallelSampler : public Sampler {
   std::vector<Chain> chains;
   double *lp_scratch = nullptr;   // births kernel (one wave)
   double *lpb = nullptr;          // phase-1 lp buffer (lpb_index layout)
+  double *vmax = nullptr;         // [V][n] view maxima of the draw (producer -> draw)
   size_t lpb_cap = 0;             // doubles
   size_t lp_cap = 0;               // doubles per wave
   double *part1 = nullptr, *part2 = nullptr;
@@ -2286,6 +2326,7 @@ class ParallelSampler : public Sampler {
     for (int v = 0; v < V; ++v) std::memcpy(&yh[(size_t)v * n * D], views[v], sizeof(double) * (size_t)n * D);
     y = dmalloc<double>(yh.size());
     Y2 = dmalloc<double>((size_t)V * n);
+    vmax = dmalloc<double>((size_t)V * n);
     MVC_HIP(hipMemcpyAsync(y, yh.data(), sizeof(double) * yh.size(), hipMemcpyHostToDevice, stream));
     hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
     MVC_HIP(hipGetLastError());
@@ -2341,7 +2382,7 @@ class ParallelSampler : public Sampler {
     for (auto &c : chains)
       for (void *p : c.owned) hipFree(p);
     for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)lpb, (void *)part1, (void *)part2,
-                    cub_tmp, (void *)fz_discard})
+                    cub_tmp, (void *)fz_discard, (void *)vmax})
       if (p) hipFree(p);
     if (stream) hipStreamDestroy(stream);
   }
@@ -2606,6 +2647,7 @@ class ParallelSampler : public Sampler {
     A.yt = yt;
     A.S1t = c.S1t;
     A.SP = SP;
+    A.vmax = vmax;
     A.T = c.T;
     A.sumK = (int32_t)lp_cap;
     A.seed = cfg.seed;

@@ -18,6 +18,8 @@ extern "C" __global__ void mvc_spec_math_kernel(int op, const double *x, double 
       case 1: r = mvc_log(a); break;
       case 2: r = mvc_lgamma_pos(a); break;
       case 3: r = mvc_qnorm(a); break;
+      case 5: r = mvc_exp_sk(a); break;            // the fused kernel's variants
+      case 6: r = mvc_log_nb(a); break;
       default: r = __builtin_sqrt(a); break;
     }
     o[i] = r;

@@ -29,9 +29,12 @@ def test_device_exp_log_bitwise():
                         rng.uniform(-745.2, -707.5, 100000), rng.uniform(709.0, 709.79, 20000),
                         [0.0, -0.0, 1e-310, -1e-310, 709.78, -745.2, np.inf, -np.inf, np.nan]])
     assert np.array_equal(m.device_math("exp", x), O.pm_exp(x), equal_nan=True)
+    assert np.array_equal(m.device_math("exp_sk", x), O.pm_exp(x), equal_nan=True)
     y = np.concatenate([np.exp(rng.uniform(-700, 700, 200000)), rng.uniform(0.5, 2.0, 200000),
                         [0.0, 1.0, 2.0, 1e-320, np.inf, -1.0, np.nan]])
     assert np.array_equal(m.device_math("log", y), O.pm_log(y), equal_nan=True)
+    y = np.concatenate([y, [-0.0, 5e-324, 2.2250738585072014e-308, 1.4142135623730951, 0.7071067811865476]])
+    assert np.array_equal(m.device_math("log_nb", y), O.pm_log(y), equal_nan=True)
 
 
 def test_device_lgamma_qnorm_sqrt_bitwise():
