@@ -1610,18 +1610,74 @@ extern "C" __global__ __launch_bounds__(64) void mvc_par_births_kernel(Sweep A) 
 // (per-block LDS histogram, then one global add per touched table: integer
 // counts, so the result is independent of the order)
 extern "C" __global__ __launch_bounds__(256) void mvc_par_count_kernel(int n, int T, const int32_t *choice,
-                                                                      int32_t *cnt, int32_t *flag) {
+                                                                      int32_t *cnt, int32_t *bcnt) {
+  // block b owns the contiguous customers [b C, (b + 1) C): table counts by an
+  // LDS histogram (one global add per table and block: few blocks, because
+  // adds to one address serialise in L2), births counted per block
   __shared__ int h[4096];
+  __shared__ int nb;
   for (int p = threadIdx.x; p < T; p += blockDim.x) h[p] = 0;
+  if (threadIdx.x == 0) nb = 0;
   __syncthreads();
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const int C = (n + gridDim.x - 1) / gridDim.x;
+  const int i0 = blockIdx.x * C, i1 = min(n, i0 + C);
+  int mine = 0;
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int c = choice[i];
-    flag[i] = c < 0 ? 1 : 0;
     if (c >= 0) atomicAdd(&h[c], 1);
+    else ++mine;
   }
+  if (mine) atomicAdd(&nb, mine);
   __syncthreads();
   for (int p = threadIdx.x; p < T; p += blockDim.x)
     if (h[p]) atomicAdd(&cnt[p], h[p]);
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = nb;
+}
+
+// Births in ascending customer order (the spec's phase-2 order): block b
+// writes its births at the offset sum_{b' < b} bcnt[b'] (same contiguous
+// ranges as the count kernel), in customer order within the block by wave
+// ballots; brank[i] = position of birth i in the list; nbirth = total.
+extern "C" __global__ __launch_bounds__(256) void mvc_par_blist_kernel(int n, const int32_t *choice,
+                                                                      const int32_t *bcnt, int32_t *blist,
+                                                                      int32_t *brank, int32_t *nbirth) {
+  __shared__ int s_off, s_tot, s_w[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) { s_off = 0; s_tot = 0; }
+  __syncthreads();
+  {
+    int a = 0, t = 0;
+    for (int b = tid; b < (int)gridDim.x; b += blockDim.x) {
+      const int c = bcnt[b];
+      t += c;
+      if (b < (int)blockIdx.x) a += c;
+    }
+    if (a) atomicAdd(&s_off, a);
+    if (t) atomicAdd(&s_tot, t);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid == 0) *nbirth = s_tot;
+  int base = s_off;
+  if (s_tot == 0) return;
+  const int C = (n + gridDim.x - 1) / gridDim.x;
+  const int i0 = blockIdx.x * C, i1 = min(n, i0 + C);
+  for (int c0 = i0; c0 < i1; c0 += blockDim.x) {
+    const int i = c0 + tid;
+    const bool is_b = i < i1 && choice[i] < 0;
+    const unsigned long long bal = __ballot(is_b);
+    const int below = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) s_w[w] = __popcll(bal);
+    __syncthreads();
+    int woff = 0;
+    for (int u = 0; u < w; ++u) woff += s_w[u];
+    const int tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    if (is_b) {
+      blist[base + woff + below] = i;
+      brank[i] = base + woff + below;
+    }
+    base += tot;
+    __syncthreads();
+  }
 }
 
 // commit step 2 (one workgroup of 256): new tables, dish lists, counts.
@@ -2247,6 +2303,7 @@ namespace {
 constexpr int kParTC = 4096;   // table capacity (two-level tree64)
 constexpr int kParKC = 4095;   // live dishes per view (+1 new element <= 4096)
 constexpr size_t kLpbBudget = (size_t)1 << 28;   // phase-1 lp buffer: 2 GiB of doubles per batch
+constexpr int kCountBlocks = 256;  // count / birth-list kernels (c.flags holds the per-block birth counts)
 
 template <class Tp>
 Tp *dmalloc(size_t count) {
@@ -2807,14 +2864,12 @@ class ParallelSampler : public Sampler {
     zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0);
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
-    hipLaunchKernelGGL(mvc_par_count_kernel, dim3(std::min(1024, (n + 255) / 256)), dim3(256), 0, stream, n, c.T,
+    hipLaunchKernelGGL(mvc_par_count_kernel, dim3(kCountBlocks), dim3(256), 0, stream, n, c.T,
                        (const int32_t *)c.choice, c.cnt, c.flags);
     MVC_HIP(hipGetLastError());
-    size_t bytes = cub_bytes;
-    MVC_HIP(hipcub::DeviceScan::ExclusiveSum(cub_tmp, bytes, c.flags, c.brank, n, stream));
-    bytes = cub_bytes;
-    hipcub::CountingInputIterator<int32_t> it(0);
-    MVC_HIP(hipcub::DeviceSelect::Flagged(cub_tmp, bytes, it, c.flags, c.blist, c.nbirth, n, stream));
+    hipLaunchKernelGGL(mvc_par_blist_kernel, dim3(kCountBlocks), dim3(256), 0, stream, n, (const int32_t *)c.choice,
+                       (const int32_t *)c.flags, c.blist, c.brank, c.nbirth);
+    MVC_HIP(hipGetLastError());
     timers.end("commit", e1);
     hipEvent_t eb = nullptr;
     timers.begin("births", &eb);
