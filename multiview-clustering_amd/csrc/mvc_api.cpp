@@ -335,12 +335,19 @@ int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out,
     std::vector<std::vector<std::vector<double>>> hv(C);   // [chain][s] hyper vectors
     std::vector<double> hyper(3 * V + 2);
     const bool quiet = (cfg->flags & MVC_FLAG_QUIET) != 0;
+    const mvc::Sampler::SampleFn save_fn = [&](int c, int T, const int32_t *t, const int32_t *d, const double *h) {
+      R->table_of[c].emplace_back(t, t + n);
+      R->dish_of[c].emplace_back(d, d + (size_t)V * T);
+      R->T[c].push_back(T);
+      hv[c].emplace_back(h, h + 3 * V + 2);
+    };
     for (int iter = 0; iter < cfg->n_iter; ++iter) {
       if (!quiet && (iter + 1) % 100 == 0)                          // gibbs.cpp:152-155
         std::fprintf(stderr, "Iteration %d / %d\n", iter + 1, cfg->n_iter);
       S->sweep(1);
       if (iter >= cfg->burn_in && ((iter - cfg->burn_in) % cfg->thin == 0)) {   // gibbs.cpp:205
         for (int c = 0; c < C; ++c) {
+          if (S->save_async(c, save_fn)) continue;        // device snapshot + async D2H (f3)
           std::vector<int32_t> t(n);
           int32_t T = 0;
           // first query T, then fetch dish_of with an exact capacity
@@ -356,6 +363,7 @@ int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out,
         R->S++;
       }
     }
+    S->flush_saves();
     S->synchronize();
     const int Sn = R->S;
     for (int c = 0; c < C; ++c) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <map>
 #include <stdexcept>
 #include <string>
@@ -63,6 +64,16 @@ class Sampler {
                          int32_t dish_cap) = 0;
   virtual void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of,
                          const double *hyper) = 0;
+  // Asynchronous sample output: the chain state is
+  // snapshotted on the device (a D2D copy into a ring slot, ordered after the
+  // sweep on the sampler's stream) and copied to pinned host memory on a
+  // second stream, so saving a sample does not stall the sweeps.  fn is called
+  // on the host thread, in sample order, once the copy has landed (from a
+  // later save_async or from flush_saves).  dish_of is [V][T] raw dish ids.
+  using SampleFn = std::function<void(int chain, int T, const int32_t *table_of, const int32_t *dish_of,
+                                      const double *hyper)>;
+  virtual bool save_async(int chain, const SampleFn &fn) { (void)chain; (void)fn; return false; }
+  virtual void flush_saves() {}
   mvc_config cfg;
   int sweeps_done = 0;
   int zpath = -1;                        // mvc_sampler_zpath

@@ -2434,8 +2434,90 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipStreamSynchronize(stream));
   }
 
+  // ---- asynchronous sample output (Sampler::save_async) ----
+  static constexpr int kSaveSlots = 4;
+  struct SaveSlot {
+    int32_t *dz = nullptr, *ddish = nullptr, *ddid = nullptr;   // device snapshot
+    double *dhyp = nullptr;
+    int32_t *hz = nullptr, *hdish = nullptr, *hdid = nullptr;   // pinned host copy
+    double *hhyp = nullptr;
+    hipEvent_t snap = nullptr, done = nullptr;
+    bool busy = false;
+    int chain = 0, T = 0;
+    SampleFn fn;
+  };
+  SaveSlot saves[kSaveSlots];
+  int save_next = 0, save_pending = 0;
+  hipStream_t cstream = nullptr;
+
+  void finish_slot(SaveSlot &q) {
+    MVC_HIP(hipEventSynchronize(q.done));
+    std::vector<int32_t> dish_raw((size_t)V * std::max(q.T, 1));
+    for (int v = 0; v < V; ++v)
+      for (int p = 0; p < q.T; ++p) dish_raw[(size_t)v * q.T + p] = q.hdid[(size_t)v * KC + q.hdish[(size_t)v * TC + p]];
+    q.busy = false;
+    --save_pending;
+    q.fn(q.chain, q.T, q.hz, dish_raw.data(), q.hhyp);
+  }
+
+  bool save_async(int chain, const SampleFn &fn) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    Chain &c = chains[chain];
+    if (!cstream) MVC_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    // slots are reused in order, so finishing the oldest keeps samples in order
+    SaveSlot &q = saves[save_next];
+    if (q.busy) finish_slot(q);
+    if (!q.dz) {
+      q.dz = dmalloc<int32_t>(n);
+      q.ddish = dmalloc<int32_t>((size_t)V * TC);
+      q.ddid = dmalloc<int32_t>((size_t)V * KC);
+      q.dhyp = dmalloc<double>(3 * V + 2);
+      MVC_HIP(hipHostMalloc((void **)&q.hz, sizeof(int32_t) * std::max(n, 1), hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hdish, sizeof(int32_t) * (size_t)V * TC, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hdid, sizeof(int32_t) * (size_t)V * KC, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hhyp, sizeof(double) * (3 * V + 2), hipHostMallocDefault));
+      MVC_HIP(hipEventCreateWithFlags(&q.snap, hipEventDisableTiming));
+      MVC_HIP(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+    }
+    MVC_HIP(hipMemcpyAsync(q.dz, c.P.z, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, stream));
+    MVC_HIP(hipMemcpyAsync(q.ddish, c.P.dish, sizeof(int32_t) * (size_t)V * TC, hipMemcpyDeviceToDevice, stream));
+    MVC_HIP(hipMemcpyAsync(q.ddid, c.P.d_id, sizeof(int32_t) * (size_t)V * KC, hipMemcpyDeviceToDevice, stream));
+    MVC_HIP(hipMemcpyAsync(q.dhyp, c.P.hyper, sizeof(double) * (3 * V + 2), hipMemcpyDeviceToDevice, stream));
+    MVC_HIP(hipEventRecord(q.snap, stream));
+    MVC_HIP(hipStreamWaitEvent(cstream, q.snap, 0));
+    MVC_HIP(hipMemcpyAsync(q.hz, q.dz, sizeof(int32_t) * n, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipMemcpyAsync(q.hdish, q.ddish, sizeof(int32_t) * (size_t)V * TC, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipMemcpyAsync(q.hdid, q.ddid, sizeof(int32_t) * (size_t)V * KC, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipMemcpyAsync(q.hhyp, q.dhyp, sizeof(double) * (3 * V + 2), hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipEventRecord(q.done, cstream));
+    q.busy = true;
+    q.chain = chain;
+    q.T = c.T;
+    q.fn = fn;
+    ++save_pending;
+    save_next = (save_next + 1) % kSaveSlots;
+    return true;
+  }
+
+  void flush_saves() override {
+    for (int k = 0; k < kSaveSlots && save_pending > 0; ++k) {
+      SaveSlot &q = saves[(save_next + k) % kSaveSlots];   // oldest first
+      if (q.busy) finish_slot(q);
+    }
+  }
+
   ~ParallelSampler() override {
     if (stream) hipStreamSynchronize(stream);
+    if (cstream) hipStreamSynchronize(cstream);
+    for (SaveSlot &q : saves) {
+      for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp})
+        if (p) hipFree(p);
+      for (void *p : {(void *)q.hz, (void *)q.hdish, (void *)q.hdid, (void *)q.hhyp})
+        if (p) hipHostFree(p);
+      if (q.snap) hipEventDestroy(q.snap);
+      if (q.done) hipEventDestroy(q.done);
+    }
+    if (cstream) hipStreamDestroy(cstream);
     for (auto &c : chains)
       for (void *p : c.owned) hipFree(p);
     for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)lpb, (void *)part1, (void *)part2,

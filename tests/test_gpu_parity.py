@@ -388,3 +388,29 @@ def test_parallel_stats_bitwise_vs_oracle(D, path, monkeypatch):
         assert np.array_equal(g["S1"], r["S1"]), v
         assert np.array_equal(g["S2"], r["S2"]), v
     s.close()
+
+
+# ---------------------------------------------------------------- sample output
+def test_async_sample_output_two_chains_vs_handle():
+    """mvc_run saves samples through the device snapshot ring + async D2H; with
+    two chains, burn-in and thinning, every saved sample must equal the state
+    read synchronously from a Sampler handle after the same sweep."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.synthetic(20000, 2, 64, 16, seed=4)
+    M, burn, thin = 13, 2, 3
+    res = m.run_gibbs_cpp(y, M, burn, thin, seed=17, mode="parallel", n_chains=2, quiet=True)
+    saved = [it for it in range(M) if it >= burn and (it - burn) % thin == 0]
+    for c in range(2):
+        s = m.Sampler(y, seed=17, mode="parallel", first_chain=c)
+        k = 0
+        for it in range(M):
+            s.sweep(1)
+            if it in saved:
+                t, d, h = s.state()
+                assert np.array_equal(res[c]["table_of"][k], t), (c, it)
+                assert np.array_equal(np.stack(res[c]["dish_of"][k]), d), (c, it)
+                assert res[c]["alpha_global"][k] == h["alpha_global"]
+                k += 1
+        assert k == len(res[c]["table_of"])
+        s.close()
