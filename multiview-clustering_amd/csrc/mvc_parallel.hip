@@ -316,6 +316,31 @@ template <int NT, int SPPT, int RP>
 __device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2 *nxt, int SPP, const double *Bl,
                                                  mvc_d2 (&ring)[RP], mvc_d4 (&acc)[4]) {
   if constexpr (SPPT > 0) {
+#ifndef MVC_BPIPE_OFF
+    // B-fragments one k-step pair ahead (LDS latency off the MFMA issue path)
+    double bc[2 * NT], bn[2 * NT];
+#pragma unroll
+    for (int t = 0; t < 2 * NT; ++t) bc[t] = Bl[t * 64];
+#pragma unroll
+    for (int q = 0; q < SPPT; ++q) {
+      const int u = q % RP;
+      const mvc_d2 a = ring[u];
+      ring[u] = (q + RP < SPPT) ? cur[(q + RP) * 64] : nxt[(q + RP - SPPT) * 64];
+      if (q + 1 < SPPT) {
+        const double *bk = Bl + (size_t)(2 * (q + 1)) * NT * 64;
+#pragma unroll
+        for (int t = 0; t < 2 * NT; ++t) bn[t] = bk[t * 64];
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bc[t], acc[t], 0, 0, 0);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bc[NT + t], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
+#pragma unroll
+      for (int t = 0; t < 2 * NT; ++t) bc[t] = bn[t];
+    }
+    if (false)
+#endif
 #pragma unroll
     for (int q = 0; q < SPPT; ++q) {
       const int u = q % RP;
