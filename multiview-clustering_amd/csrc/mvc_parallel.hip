@@ -2412,7 +2412,20 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipMemcpyAsync(y, yh.data(), sizeof(double) * yh.size(), hipMemcpyHostToDevice, stream));
     hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
     MVC_HIP(hipGetLastError());
+    // the MFMA tiling yt is a second copy of y: build it only when it fits
+    // beside y with room for the lp buffer and the chains' state (at N = 10M,
+    // D = 256 the two copies would not fit in 288 GB; the generic producer
+    // then runs on y alone)
+    size_t yt_bytes = 0;
     if (D % 4 == 0 && D >= 16 && V <= MVC_Z_VMAX) {
+      const int sp = ((D / 4 + MVC_ZR - 1) / MVC_ZR) * MVC_ZR;
+      yt_bytes = sizeof(double) * (size_t)V * (((size_t)n + 15) / 16) * sp * 64;
+      size_t mfree = 0, mtotal = 0;
+      MVC_HIP(hipMemGetInfo(&mfree, &mtotal));
+      const size_t reserve = sizeof(double) * kLpbBudget + (size_t)cf.n_chains * ((size_t)V * n * 32 + ((size_t)1 << 30));
+      if (yt_bytes + reserve > mfree) yt_bytes = 0;
+    }
+    if (yt_bytes) {
       SP = ((D / 4 + MVC_ZR - 1) / MVC_ZR) * MVC_ZR;
       const size_t ntile = ((size_t)n + 15) / 16;
       yt = dmalloc<double>((size_t)V * ntile * SP * 64);
