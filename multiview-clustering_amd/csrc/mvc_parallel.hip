@@ -1499,6 +1499,196 @@ __global__ __launch_bounds__(MVC_FZ_THREADS, 1) void mvc_par_zfused_kernel(Sweep
   }
 }
 
+// ---------------------------------------------------------------------------
+// All-views lp producer: the per-view producers' work in ONE launch.  Every
+// view's S1 B-fragments sit in LDS (one block per CU); each wave takes a
+// 16-customer tile through all views in order (view pattern PAT fixed at
+// compile time, as the fused kernel), so MFMA-heavy views (K_v = 64) and
+// stream-heavy ones (K_v <= 16) alternate inside each wave and the two waves
+// of a SIMD overlap them; one launch instead of V removes V - 1 prologues and
+// tails.  Same outputs and arithmetic as mvc_par_lpview_kernel (lp rows and
+// the view maxima vmax).
+// ---------------------------------------------------------------------------
+struct LpaLds {
+  const double *Bs, *c0, *cb, *Q;
+  const int *dn, *dl, *tix, *nt, *koff, *boff;
+};
+__host__ __device__ inline size_t lpall_shared_bytes(size_t s1t_doubles, int V, int sumK, int waves) {
+  return 16 * 4 + 8 * (s1t_doubles + 3 * (size_t)sumK + (size_t)waves * 48) +
+         4 * (2 * (size_t)sumK + (size_t)MVC_FZ_TB * 16 * V + MVC_FZ_TB * 16 + (size_t)waves * 16) + 64;
+}
+
+template <int NT, int SPPT, int RP>
+__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int li0, int nb, int pz, double y2,
+                                         const mvc_d2 *cur, const mvc_d2 *nxt, mvc_d2 (&ring)[RP], double *lpb,
+                                         double *dslot, double *y2s, double *selfG, double *mrest, int *zs) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
+  const int V = P.V, D = P.D, n = P.n;
+  const int koff = L.koff[v], K = L.koff[v + 1] - koff, sumK = L.koff[V];
+  const double tau = P.hyper[v], L2pt = A.L2pt[v], cnew = A.cnew[v];
+  mvc_d4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+  lpview_tile_mfma<NT, SPPT, RP>(cur, nxt, SPPT, L.Bs + L.boff[v] + lane, ring, acc);
+  if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
+  wave_lds_sync();
+  double hy[4], hr[4];
+  int j0[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double y2r = y2s[grp + 4 * r];
+    hy[r] = 0.5 * y2r;
+    hr[r] = (-0.5 * y2r) / tau;
+    j0[r] = L.tix[zs[grp + 4 * r] * V + v] - koff;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {   // G of the own dish -> LDS
+    const int jt = j0[r] >> 4;
+    double g = acc[0][r];
+#pragma unroll
+    for (int t = 1; t < NT; ++t)
+      if (jt == t) g = acc[t][r];
+    if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
+  }
+  double mx[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mx[r] = -MVC_PM_INF;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int j = 16 * t + col;
+    const int kc = koff + min(j, K - 1);
+    const double c0j = L.c0[kc], cbj = L.cb[kc];
+    const bool inc = j < K && L.dl[kc] > 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+      const int li = li0 + grp + 4 * r;
+      double *dst = (j < K && li < nb) ? lpb + lpb_index(li, koff + j, sumK) : dslot;
+      *dst = val;
+      if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const double mr = row16_max(mx[r]);
+    if (col == 0) mrest[grp + 4 * r] = mr;
+  }
+  wave_lds_sync();
+  {   // own dish, one row per lane
+    const double G = selfG[col];
+    const int kk = L.tix[pz * V + v];
+    const double Gp = G - y2;
+    const double Qp = (L.Q[kk] - 2.0 * G) + y2;
+    const Coef cf = coef(L.dn[kk] - 1, Qp, tau, L2pt, D);
+    const double hself = (-0.5 * y2) / tau;
+    const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
+    const bool ok = lane < 16 && li0 + col < nb;
+    double *dst = ok ? lpb + lpb_index(li0 + col, kk, sumK) : dslot;
+    *dst = sv;
+    const int l0p = L.dl[kk] - ((L.nt[pz] - 1) > 0 ? 0 : 1);
+    double m = mrest[col];
+    if (l0p > 0 && sv > m) m = sv;
+    const double lfn = cnew + hself;
+    if (lfn > m) m = lfn;
+    double *dm = ok ? A.vmax + (size_t)v * n + li0 + col : dslot;
+    *dm = m;
+  }
+  wave_lds_sync();
+}
+
+template <int SPPT, int RP, uint32_t PAT, int VI>
+__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int li0, int nb, int pz,
+                                          const double (&y2v)[MVC_Z_VMAX], const mvc_d2 *ybase, size_t vstride,
+                                          size_t tcur, size_t tnext, mvc_d2 (&ring)[RP], double *lpb, double *dslot,
+                                          double *y2s, double *selfG, double *mrest, int *zs) {
+  if constexpr (VI < fz_pat_v(PAT)) {
+    const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
+    const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
+    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, li0, nb, pz, y2v[VI], cur, nxt, ring, lpb, dslot, y2s, selfG,
+                                           mrest, zs);
+    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, li0, nb, pz, y2v, ybase, vstride, tcur, tnext, ring, lpb, dslot, y2s,
+                                     selfG, mrest, zs);
+  }
+}
+
+template <int SPPT, int RP, uint32_t PAT>
+__global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, double *lpb, double *discard) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
+  const int col = lane & 15;
+  constexpr int V = fz_pat_v(PAT);
+  const int KC = P.KC, TC = P.TC, n = P.n;
+  const int T = __builtin_amdgcn_readfirstlane(A.T);
+  constexpr int SP = 2 * SPPT;
+  int *s_koff = (int *)smem;                                   // [V+1]
+  int *s_boff = s_koff + V + 1;                                // [V+1] (doubles)
+  if (tid <= V) {
+    s_koff[tid] = A.Koff[tid];
+    int acc = 0;
+    for (int u = 0; u < tid; ++u) acc += SP * 64 * fz_pat_nt(PAT, u);
+    s_boff[tid] = acc;
+  }
+  __syncthreads();
+  const int sumK = s_koff[V];
+  const int nB = s_boff[V];
+  double *Bs = (double *)(smem + 16 * 4);
+  double *f_c0 = Bs + nB, *f_cb = f_c0 + sumK, *f_Q = f_cb + sumK;
+  double *wsp = f_Q + sumK + (size_t)w * 48;                   // per wave: y2s, selfG, mrest
+  int *f_dn = (int *)(f_Q + sumK + (size_t)BW * 48), *f_dl = f_dn + sumK;
+  int *f_tix = f_dl + sumK, *f_nt = f_tix + MVC_FZ_TB * 16 * V;
+  int *zs = f_nt + MVC_FZ_TB * 16 + w * 16;
+  {
+    const mvc_d2 *src = (const mvc_d2 *)A.S1t;
+    mvc_d2 *dst = (mvc_d2 *)Bs;
+    for (int e = tid; e < nB / 2; e += blockDim.x) dst[e] = src[e];
+  }
+  for (int k = tid; k < sumK; k += blockDim.x) {
+    int v = 0;
+    while (v + 1 < V && s_koff[v + 1] <= k) ++v;
+    const int j = k - s_koff[v];
+    f_c0[k] = P.c0[v * KC + j];
+    f_cb[k] = P.cb[v * KC + j];
+    f_Q[k] = P.Q[v * KC + j];
+    f_dn[k] = P.d_n[v * KC + j];
+    f_dl[k] = P.d_l[v * KC + j];
+  }
+  for (int p = tid; p < MVC_FZ_TB * 16; p += blockDim.x) {
+    f_nt[p] = p < T ? P.n_t[p] : 0;
+    for (int v = 0; v < V; ++v) f_tix[p * V + v] = s_koff[v] + (p < T ? P.dish[v * TC + p] : 0);
+  }
+  __syncthreads();
+  const LpaLds L{Bs, f_c0, f_cb, f_Q, f_dn, f_dl, f_tix, f_nt, s_koff, s_boff};
+  double *y2s = wsp, *selfG = wsp + 16, *mrest = wsp + 32;
+
+  const int ntile = (n + 15) >> 4;
+  const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
+  if (gw >= ntile) return;                         // whole wave: no barriers below
+  const int nmy = (ntile - gw + NWT - 1) / NWT;
+  const size_t vstride = (size_t)ntile * SPPT * 64;
+  const mvc_d2 *ybase = (const mvc_d2 *)A.yt + lane;
+  auto toff = [&](int m) -> size_t { return (size_t)(gw + min(m, nmy - 1) * NWT) * SPPT * 64; };
+  mvc_d2 ring[RP];
+  {
+    const mvc_d2 *c0p = ybase + toff(0);
+#pragma unroll
+    for (int u = 0; u < RP; ++u) ring[u] = c0p[u * 64];
+  }
+  double *const dslot = discard + lane;
+  for (int m = 0; m < nmy; ++m) {
+    const int li0 = (gw + m * NWT) * 16;
+    const int li_row = min(li0 + col, n - 1);
+    const int pz = P.z[li_row];
+    double y2v[MVC_Z_VMAX];
+#pragma unroll
+    for (int v = 0; v < MVC_Z_VMAX; ++v) y2v[v] = v < V ? A.Y2[(size_t)v * n + li_row] : 0.0;
+    lpa_views<SPPT, RP, PAT, 0>(A, L, li0, n, pz, y2v, ybase, vstride, toff(m), toff(m + 1), ring, lpb, dslot, y2s,
+                                selfG, mrest, zs);
+  }
+}
+
 // Phase 2: births resolved sequentially in ascending
 // customer order by ONE wavefront.  Each birth joins a table born earlier in
 // this sweep or opens one (dish per view from frozen + phase-2 + new dishes).
@@ -2383,6 +2573,7 @@ class ParallelSampler : public Sampler {
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   size_t lpb_batch = 0;           // MVC_LPB_BATCH: customers per phase-1 batch (0: kLpbBudget)
   bool no_fused = true;           // MVC_FUSED=1: the fused phase-1 kernel where it applies (experimental: slower today)
+  bool no_lpall = false;          // MVC_LPALL=0: per-view producer launches even where the all-views producer applies
   int fz_waves = MVC_FZ_THREADS / 64;   // waves per block of the fused kernel (MVC_FZ_WAVES: fewer)
   int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
   int n_cu = 256;
@@ -2449,6 +2640,7 @@ class ParallelSampler : public Sampler {
     force_zdraw_lds = zl && zl[0] == '1';
     if (const char *e = getenv("MVC_LPB_BATCH")) lpb_batch = (size_t)std::max(0L, atol(e)) / 64 * 64;
     if (const char *e = getenv("MVC_FUSED")) no_fused = e[0] != '1';
+    if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
     if (const char *e = getenv("MVC_FZ_WAVES")) fz_waves = std::max(1, std::min(MVC_FZ_THREADS / 64, atoi(e)));
     fz_discard = dmalloc<int>(64);
     {
@@ -2464,6 +2656,9 @@ class ParallelSampler : public Sampler {
     lpview_attr<0, 4>();
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_stats_partial_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    lpall_attr<4, 4>();
+    lpall_attr<8, 8>();
+    lpall_attr<16, 8>();
     fused_attr<4, 4>();
     fused_attr<8, 8>();
     fused_attr<16, MVC_FZ_RP16>();
@@ -2877,6 +3072,27 @@ class ParallelSampler : public Sampler {
     }
   }
   template <int SPPT, int RP>
+  void launch_lpall(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A) {
+    double *disc = lpb + lpb_cap;
+    switch (pat) {
+#define X(p)                                                                                       \
+  case p:                                                                                          \
+    hipLaunchKernelGGL((mvc_par_lpall_kernel<SPPT, RP, p>), grid, block, lds, stream, A, lpb, disc); \
+    break;
+      MVC_FZ_PATS(X)
+#undef X
+      default: throw Error(MVC_ERR_STATE, "all-views producer: no instance for this view pattern");
+    }
+  }
+  template <int SPPT, int RP>
+  static void lpall_attr() {
+#define X(p)                                                                                            \
+  MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_lpall_kernel<SPPT, RP, p>,                          \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MVC_FZ_PATS(X)
+#undef X
+  }
+  template <int SPPT, int RP>
   static void fused_attr() {
 #define X(p)                                                                                              \
   MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zfused_kernel<SPPT, RP, p>,                           \
@@ -2929,6 +3145,7 @@ class ParallelSampler : public Sampler {
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
     }
+    bool zpath_lpall = false;
     timers.begin("zresample", &e0);
     if (use_fused) {
       const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / fz_lds));
@@ -2946,7 +3163,19 @@ class ParallelSampler : public Sampler {
       const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
       hipEvent_t el = nullptr, ed = nullptr;
       timers.begin("lp", &el);
-      if (use_mfma) {
+      const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, 8);
+      const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB && b0 == 0 && nb == n &&
+                             (spp == 4 || spp == 8 || spp == 16) && lpa_lds <= 160 * 1024;
+      if (use_lpall) {
+        const int ntile = (n + 15) / 16;
+        const int grid = std::max(1, std::min(n_cu, (ntile + 7) / 8));
+        switch (spp) {
+          case 4: launch_lpall<4, 4>(fz_pat, dim3(grid), dim3(512), lpa_lds, A); break;
+          case 8: launch_lpall<8, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A); break;
+          default: launch_lpall<16, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A); break;
+        }
+        zpath_lpall = true;
+      } else if (use_mfma) {
         const int ntile = (nb + 15) / 16;
         for (int v = 0; v < V; ++v) {
           const int NT = (c.K[v] + 15) / 16;
@@ -2981,7 +3210,7 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
-    zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0);
+    zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0);
     timers.begin("commit", &e1);
     MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
     hipLaunchKernelGGL(mvc_par_count_kernel, dim3(kCountBlocks), dim3(256), 0, stream, n, c.T,

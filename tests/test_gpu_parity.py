@@ -247,6 +247,8 @@ def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=
     monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
     monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
     monkeypatch.setenv("MVC_FUSED", "1" if draw == "fused" else "0")
+    monkeypatch.setenv("MVC_LPALL", "0" if draw.endswith("-perview") else "1")
+    draw = draw.replace("-perview", "")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
     states = []
@@ -290,7 +292,7 @@ FUSED_SHAPES = {(3001, 4, 64, 16, 16): True, (50, 2, 20, 4, 4): True, (4000, 3, 
                 (4100, 4, 128, 64, 64): True, (777, 1, 32, 16, 16): True}
 
 
-@pytest.mark.parametrize("draw", ["fused", "reg", "lds"])
+@pytest.mark.parametrize("draw", ["fused", "reg", "lds", "reg-perview"])
 @pytest.mark.parametrize("n,V,D,K,T", list(FUSED_SHAPES))
 def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     m = _mvc()
@@ -303,7 +305,7 @@ def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
     hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
     st = (table_of, dish, hyper)
-    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw == "reg" and T <= 64),
+    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw.startswith("reg") and T <= 64),
                     expect_fused=FUSED_SHAPES[(n, V, D, K, T_gen)])
     ref = O.run(y, 3, 0, 1, seed=31, mode=O.PARALLEL, state=st)
     for it in range(3):
