@@ -196,13 +196,14 @@ def main():
                    "schedule": "parallel z-resample (DESIGN.md §4)", "parallelism": f"chains{world}",
                    "tables_at_end": int(T), "dishes_at_end": kdish.tolist()},
         "roofline": roof,
-        "hbm": {"pass": "z-resample (lp producer x V + draw, DESIGN.md §5)", "achieved_gbs": round(hbm_gbs, 1),
+        "hbm": {"pass": "z-resample (lp producer + draw, DESIGN.md §5)", "achieved_gbs": round(hbm_gbs, 1),
                 "peak_gbs": PEAK_HBM_GBS, "frac": round(hbm_gbs / PEAK_HBM_GBS, 4),
                 "mfma_tflops": round(tflops, 3), "mfma_frac": round(tflops / PEAK_F64_TFLOPS, 4),
                 "arith_intensity": round(flops_alg / bytes_alg, 3), "ridge": round(ridge, 3),
                 "bytes_per_launch": bytes_alg, "flops_per_launch": flops_alg, "pass_ms": round(k_avg_s * 1e3, 4),
-                "lp_producer": "mfma" if (zpath & 3) == 2 else "generic",
-                "draw": "registers" if zpath & 4 else "lds-checkpoints"},
+                "lp_producer": ("fused" if zpath & 8 else "mfma-all-views" if zpath & 16
+                                else "mfma" if (zpath & 3) == 2 else "generic"),
+                "draw": "fused" if zpath & 8 else "registers" if zpath & 4 else "lds-checkpoints"},
         "hyper_pooled_mean": {"chains": pooled_n, "alpha_global": round(float(pooled_mean[-2]), 6),
                               "sigma_global": round(float(pooled_mean[-1]), 6)},
         "nvk_sweeps_per_s": round(value * N * V * K, 1),

@@ -30,7 +30,11 @@ write = per_kernel("WRITE_SIZE")
 passes = max(1, sum(len(v) for k, v in fetch.items() if "zdraw" in k))
 # calibration: every lpview launch streams N*D*8 bytes of y plus small tables
 lp_fetch = [b for k, v in fetch.items() if "lpview" in k for b in v]
-factor = (N * D * 8) / (sum(lp_fetch) / len(lp_fetch)) if lp_fetch else 1.0
+la_fetch = [b for k, v in fetch.items() if "lpall" in k for b in v]   # all-views producer: V views per launch
+if la_fetch:
+    factor = (N * D * 8 * V) / (sum(la_fetch) / len(la_fetch))
+else:
+    factor = (N * D * 8) / (sum(lp_fetch) / len(lp_fetch)) if lp_fetch else 1.0
 fetch_pass = factor * sum(sum(v) for v in fetch.values()) / passes
 write_pass = sum(sum(v) for v in write.values()) / passes
 out = {cfg: {"bytes_per_pass": int(fetch_pass + write_pass), "fetch_bytes": int(fetch_pass),
