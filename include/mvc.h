@@ -71,6 +71,9 @@ typedef struct mvc_config {
 
 #define MVC_FLAG_TIMING 1   /* record per-kernel HIP-event times (mvc_sampler_kernel_time) */
 #define MVC_FLAG_QUIET  2   /* no progress lines on stderr                                 */
+#define MVC_FLAG_TIMING_COARSE 4   /* with MVC_FLAG_TIMING: only "zresample", "sweep" and
+                                      "exact_sweep" (two events per timer; the per-phase
+                                      events cost ~5 us of idle GPU each per sweep)       */
 
 void mvc_config_init(mvc_config *cfg);   /* fills defaults: thin=1, n_chains=1, ... */
 int mvc_abi_version(void);
@@ -137,6 +140,10 @@ int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms,
                             int64_t *launches);
 void mvc_sampler_reset_timers(mvc_sampler *s);
+/* Switch timing at run time: flags = 0 (off), MVC_FLAG_TIMING (every
+ * phase) or MVC_FLAG_TIMING | MVC_FLAG_TIMING_COARSE (whole passes only).
+ * Synchronises the handle's stream; accumulated times are kept. */
+int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags);
 /* z-resample kernels used by the last parallel sweep: bits 0-1 the lp
  * producer (0 generic, one lane per customer; 2 per-view MFMA tiles), bit 2
  * set when the register-resident draw kernel ran (T <= 64, K_v <= 64);

@@ -103,16 +103,31 @@ UserState check_user_state(int n, int V, const int32_t *table_of, int32_t T, con
   return U;
 }
 
-void Timers::begin(const char *, hipEvent_t *ev) {
+hipEvent_t Timers::get() {
+  hipEvent_t e;
+  if (!pool.empty()) {
+    e = pool.back();
+    pool.pop_back();
+  } else {
+    MVC_HIP(hipEventCreate(&e));
+  }
+  return e;
+}
+bool Timers::wanted(const char *name) const {
+  if (!on) return false;
+  if (!coarse) return true;
+  const std::string s(name);
+  return s == "zresample" || s == "sweep" || s == "exact_sweep";
+}
+void Timers::begin(const char *name, hipEvent_t *ev) {
   *ev = nullptr;
-  if (!on) return;
-  MVC_HIP(hipEventCreate(ev));
+  if (!wanted(name)) return;
+  *ev = get();
   MVC_HIP(hipEventRecord(*ev, stream));
 }
 void Timers::end(const char *name, hipEvent_t a) {
   if (!on || !a) return;
-  hipEvent_t b;
-  MVC_HIP(hipEventCreate(&b));
+  hipEvent_t b = get();
   MVC_HIP(hipEventRecord(b, stream));
   pending.push_back({a, b, name});
   if (pending.size() > 4096) {
@@ -128,8 +143,8 @@ void Timers::collect() {
     auto &e = acc[r.name];
     e.first += ms;
     e.second += 1;
-    hipEventDestroy(r.a);
-    hipEventDestroy(r.b);
+    pool.push_back(r.a);
+    pool.push_back(r.b);
   }
   pending.clear();
 }
@@ -143,6 +158,7 @@ Timers::~Timers() {
     hipEventDestroy(r.a);
     hipEventDestroy(r.b);
   }
+  for (hipEvent_t e : pool) hipEventDestroy(e);
 }
 
 }  // namespace mvc
@@ -308,6 +324,18 @@ int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms
 
 void mvc_sampler_reset_timers(mvc_sampler *s) {
   if (s && s->impl) s->impl->timers.reset();
+}
+
+int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags) {
+  if (!s || !s->impl) return MVC_ERR_ARG;
+  try {
+    s->impl->synchronize();
+  } catch (...) {
+    return MVC_ERR_HIP;
+  }
+  s->impl->timers.on = (flags & MVC_FLAG_TIMING) != 0;
+  s->impl->timers.coarse = (flags & MVC_FLAG_TIMING_COARSE) != 0;
+  return MVC_OK;
 }
 
 int mvc_sampler_zpath(mvc_sampler *s) { return (s && s->impl) ? s->impl->zpath : -1; }

@@ -795,6 +795,7 @@ class ExactSampler : public Sampler {
     MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     timers.stream = stream;
     timers.on = (c.flags & MVC_FLAG_TIMING) != 0;
+    timers.coarse = (c.flags & MVC_FLAG_TIMING_COARSE) != 0;
     std::vector<double> y((size_t)V * n);
     for (int v = 0; v < V; ++v) std::memcpy(&y[(size_t)v * n], views[v], sizeof(double) * n);
     MVC_HIP(hipMalloc(&y_dev, sizeof(double) * y.size()));

@@ -41,7 +41,11 @@ InitState draw_initial_state(const double *y /*[V][n][D]*/, int n, int V, int D,
 // Per-kernel HIP-event timers (MVC_FLAG_TIMING).
 struct Timers {
   bool on = false;
+  bool coarse = false;                 // MVC_FLAG_TIMING_COARSE: the whole-pass timers only
   hipStream_t stream = nullptr;
+  std::vector<hipEvent_t> pool;        // recycled events (no create/destroy per record)
+  hipEvent_t get();
+  bool wanted(const char *name) const;
   struct Rec { hipEvent_t a, b; std::string name; };
   std::vector<Rec> pending;
   std::map<std::string, std::pair<double, int64_t>> acc;

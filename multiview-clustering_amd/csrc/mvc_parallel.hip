@@ -2548,9 +2548,11 @@ class ParallelSampler : public Sampler {
     int32_t *dold = nullptr, *dnew = nullptr, *mflag = nullptr, *mlist = nullptr;   // [V*n]
     int32_t *nsel = nullptr, *vlist = nullptr;
     double *S1T_alt = nullptr, *S2_alt = nullptr;   // ping-pong of P.S1T / P.S2
-    // host sources of async uploads: they outlive the copies (the next write
-    // happens after the next sweep's status synchronisation)
-    std::vector<int32_t> koff_h, vlist_h;
+    // pinned host sources of the async uploads ([V+1] Koff, then [MAXV] view
+    // list): pageable sources would make each copy a blocking staged copy that
+    // waits for the stream.  The next write to them happens after the next
+    // sweep's status synchronisation, so they outlive the copies.
+    int32_t *hpin = nullptr;
     bool s1t_ok = false;
     int T = 0;
     std::vector<int32_t> K;
@@ -2567,7 +2569,7 @@ class ParallelSampler : public Sampler {
   size_t part_cap = 0;             // sumK capacity of partials
   void *cub_tmp = nullptr;
   size_t cub_bytes = 0;
-  std::vector<int32_t> st_host;
+  int32_t *st_host = nullptr;   // pinned [2V+4]: the per-sweep status readback
   bool force_generic = false;
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
@@ -2591,10 +2593,18 @@ class ParallelSampler : public Sampler {
     TC = kParTC; KC = kParKC;
     nchunk = (n + 4095) / 4096;
     if (V > MVC_MAXV) throw Error(MVC_ERR_UNSUPPORTED, "at most 64 views");
+    {   // the sweep loop waits on the device once per sweep (new T, K): spin
+        // instead of yielding so the GPU idles as briefly as possible.  Only
+        // possible before the device's context exists; otherwise left as is.
+      const char *e = getenv("MVC_SPIN");
+      if (!(e && e[0] == '0')) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+      (void)hipGetLastError();
+    }
     MVC_HIP(hipSetDevice(cf.device));
     MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     timers.stream = stream;
     timers.on = (cf.flags & MVC_FLAG_TIMING) != 0;
+    timers.coarse = (cf.flags & MVC_FLAG_TIMING_COARSE) != 0;
     std::vector<double> yh((size_t)V * n * D);
     for (int v = 0; v < V; ++v) std::memcpy(&yh[(size_t)v * n * D], views[v], sizeof(double) * (size_t)n * D);
     y = dmalloc<double>(yh.size());
@@ -2631,7 +2641,8 @@ class ParallelSampler : public Sampler {
                                           (int32_t *)nullptr, n, stream));
     cub_bytes = std::max(b1, b2);
     MVC_HIP(hipMalloc(&cub_tmp, cub_bytes));
-    st_host.assign(2 * V + 4, 0);
+    MVC_HIP(hipHostMalloc((void **)&st_host, sizeof(int32_t) * (2 * V + 4), hipHostMallocDefault));
+    std::fill(st_host, st_host + 2 * V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
     if (const char *e = getenv("MVC_LPV_WAVES")) lpv_waves = std::max(0, std::min(8, atoi(e)));
@@ -2751,11 +2762,14 @@ class ParallelSampler : public Sampler {
       if (q.done) hipEventDestroy(q.done);
     }
     if (cstream) hipStreamDestroy(cstream);
-    for (auto &c : chains)
+    for (auto &c : chains) {
       for (void *p : c.owned) hipFree(p);
+      if (c.hpin) hipHostFree(c.hpin);
+    }
     for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)lpb, (void *)part1, (void *)part2,
                     cub_tmp, (void *)fz_discard, (void *)vmax})
       if (p) hipFree(p);
+    if (st_host) hipHostFree(st_host);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -2808,6 +2822,7 @@ class ParallelSampler : public Sampler {
     c.mlist = own<int32_t>(c, (size_t)V * n);
     c.nsel = own<int32_t>(c, 1);
     c.vlist = own<int32_t>(c, MVC_MAXV);
+    MVC_HIP(hipHostMalloc((void **)&c.hpin, sizeof(int32_t) * (V + 1 + MVC_MAXV), hipHostMallocDefault));
     c.S1T_alt = own<double>(c, (size_t)V * D * KC);
     c.S2_alt = own<double>(c, (size_t)V * KC);
   }
@@ -2868,9 +2883,10 @@ class ParallelSampler : public Sampler {
   }
 
   void upload_koff(Chain &c) {
-    c.koff_h.assign(V + 1, 0);
-    for (int v = 0; v < V; ++v) c.koff_h[v + 1] = c.koff_h[v] + c.K[v];
-    MVC_HIP(hipMemcpyAsync(c.Koff, c.koff_h.data(), sizeof(int32_t) * (V + 1), hipMemcpyHostToDevice, stream));
+    int32_t *koff = c.hpin;
+    koff[0] = 0;
+    for (int v = 0; v < V; ++v) koff[v + 1] = koff[v] + c.K[v];
+    MVC_HIP(hipMemcpyAsync(c.Koff, koff, sizeof(int32_t) * (V + 1), hipMemcpyHostToDevice, stream));
   }
 
 
@@ -2957,9 +2973,8 @@ class ParallelSampler : public Sampler {
         MVC_HIP(hipcub::DeviceSelect::Flagged(cub_tmp, bytes, it, c.mflag + (size_t)v * n, c.mlist + (size_t)v * n,
                                               c.nsel, n, stream));
       }
-      c.vlist_h = inc;
-      MVC_HIP(hipMemcpyAsync(c.vlist, c.vlist_h.data(), sizeof(int32_t) * inc.size(), hipMemcpyHostToDevice,
-                             stream));
+      std::copy(inc.begin(), inc.end(), c.hpin + V + 1);
+      MVC_HIP(hipMemcpyAsync(c.vlist, c.hpin + V + 1, sizeof(int32_t) * inc.size(), hipMemcpyHostToDevice, stream));
       hipLaunchKernelGGL(mvc_par_stats_apply_kernel, dim3(Kmax, (unsigned)inc.size()), dim3(256), 0, stream, U,
                          (const int32_t *)c.vlist, (const double *)y, (const double *)Y2, (const int32_t *)c.mlist,
                          (const int32_t *)c.dold, (const int32_t *)c.dnew, c.P.S1T, c.P.S2);
@@ -3237,14 +3252,14 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipGetLastError());
     timers.end("commit", e1);
     // the one host synchronisation of a sweep: new T and dish counts
-    MVC_HIP(hipMemcpyAsync(st_host.data(), c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
+    MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
     MVC_HIP(hipStreamSynchronize(stream));
     if (st_host[V + 1] != 0)
       throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: table (4096) or dish (4095 per view) capacity exceeded");
     const std::vector<int32_t> Kold = c.K;
     c.T = st_host[0];
     for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
-    update_stats(c, Kold, st_host.data() + V + 4);
+    update_stats(c, Kold, st_host + V + 4);
     launch_hyper(c, 1, s);
     (void)e2;
   }

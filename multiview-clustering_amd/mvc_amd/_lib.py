@@ -16,6 +16,7 @@ MODE_EXACT = 0
 MODE_PARALLEL = 1
 FLAG_TIMING = 1
 FLAG_QUIET = 2
+FLAG_TIMING_COARSE = 4
 TRACE_ALPHA_V, TRACE_SIGMA_V, TRACE_TAU_V, TRACE_ALPHA_GLOBAL, TRACE_SIGMA_GLOBAL = range(5)
 
 
@@ -89,6 +90,7 @@ def lib():
         "mvc_sampler_kernel_time": (i32, [vp, cp, dp, lp]),
         "mvc_sampler_reset_timers": (None, [vp]),
         "mvc_sampler_zpath": (i32, [vp]),
+        "mvc_sampler_set_timing": (i32, [vp, i32]),
         "mvc_sampler_stream": (vp, [vp]),
         "mvc_sampler_destroy": (None, [vp]),
         "mvc_device_math": (i32, [i32, i32, dp, dp, i64, cp, sz]),

@@ -44,6 +44,13 @@ def _views_to_array(data_views):
     return np.ascontiguousarray(np.stack(out))
 
 
+def _timing_flags(timing):
+    """timing: False / True (every phase) / "coarse" (z-resample and whole sweeps only)."""
+    if timing == "coarse":
+        return L.FLAG_TIMING | L.FLAG_TIMING_COARSE
+    return L.FLAG_TIMING if timing else 0
+
+
 def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_chain=0, device=0,
                 mode="exact", table_cap=0, dish_cap=0, timing=False, quiet=True):
     cfg = L.Config()
@@ -54,7 +61,7 @@ def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_ch
     cfg.n_chains, cfg.first_chain, cfg.device = n_chains, first_chain, device
     cfg.mode = {"exact": L.MODE_EXACT, "parallel": L.MODE_PARALLEL}[mode]
     cfg.table_cap, cfg.dish_cap = table_cap, dish_cap
-    cfg.flags = (L.FLAG_TIMING if timing else 0) | (L.FLAG_QUIET if quiet else 0)
+    cfg.flags = _timing_flags(timing) | (L.FLAG_QUIET if quiet else 0)
     return cfg
 
 
@@ -221,6 +228,12 @@ class Sampler:
         producer (0 generic, 2 MFMA), bit 2 the register-resident draw kernel;
         -1 exact schedule / no sweep yet."""
         return int(self._lib.mvc_sampler_zpath(self._h))
+
+    def set_timing(self, timing):
+        """Switch HIP-event timing: False, True (every phase) or "coarse"."""
+        st = self._lib.mvc_sampler_set_timing(self._h, _timing_flags(timing))
+        if st != 0:
+            raise RuntimeError(f"mvc_sampler_set_timing failed ({st})")
 
     def reset_timers(self):
         self._lib.mvc_sampler_reset_timers(self._h)

@@ -416,3 +416,28 @@ def test_async_sample_output_two_chains_vs_handle():
                 k += 1
         assert k == len(res[c]["table_of"])
         s.close()
+
+
+def test_timing_levels_do_not_change_the_chain():
+    """Coarse timing records only the whole-pass timers; switching to full
+    timing at run time adds the per-phase ones.  Timing never changes the
+    chain: the state equals an untimed handle's after the same sweeps."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.synthetic(20000, 2, 64, 16, seed=5)
+    s = m.Sampler(y, seed=23, mode="parallel", timing="coarse")
+    s.sweep(3)
+    assert s.kernel_time("zresample")[1] == 3 and s.kernel_time("sweep")[1] == 3
+    assert s.kernel_time("lp")[1] == 0 and s.kernel_time("hyper")[1] == 0
+    s.set_timing(True)
+    s.sweep(2)
+    assert s.kernel_time("zresample")[1] == 5 and s.kernel_time("hyper")[1] == 2
+    s.set_timing(False)
+    s.sweep(1)
+    assert s.kernel_time("sweep")[1] == 5
+    ref = m.Sampler(y, seed=23, mode="parallel")
+    ref.sweep(6)
+    for a, b in zip(s.state()[:2], ref.state()[:2]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    s.close()
+    ref.close()
