@@ -2247,12 +2247,12 @@ struct BlockCtx {
 // butterfly over <= 64 partials).  Same association as oracle Tree64::build.
 template <class F>
 __device__ double block_tree64(int64_t n, F leaf) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   __shared__ double s_part[64];
   __shared__ double s_root;
   if (n <= 0) return 0.0;
   const int m = (int)((n + 63) / 64);
-  for (int c = w; c < m; c += 4) {
+  for (int c = w; c < m; c += nw) {
     const int64_t e = (int64_t)c * 64 + lane;
     const double x = e < n ? leaf(e) : 0.0;
     const double s = wave_tree_sum(x);
@@ -2282,7 +2282,11 @@ struct MHArgs {
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A) {
+// 5 waves: waves 0-3 run the per-view MH steps (views w, w + 4, ...); wave 4
+// runs the global pair at the same time when T is small (one-wave tree64 =
+// the block tree64's association), else the whole block runs it afterwards.
+constexpr int kHypWaves = 5, kHypThreads = 64 * kHypWaves, kHypGlobalWaveT = 512;
+extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(MHArgs A) {
   ParState &P = A.P;
   const int tid = threadIdx.x;
   const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
@@ -2297,7 +2301,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       for (int v = 0; v < V; ++v) s_koff[v + 1] = s_koff[v] + P.Kact[v];
     }
     __syncthreads();
-    for (int k = tid; k < s_koff[V]; k += 256) {
+    for (int k = tid; k < s_koff[V]; k += kHypThreads) {
       int v = 0;
       while (k >= s_koff[v + 1]) ++v;
       const int j = k - s_koff[v];
@@ -2318,17 +2322,18 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       P.Q[v * KC + j] = q;
     }
   }
-  if (tid == 0) {
-    for (int v = 0; v < V; ++v) {
-      int lt = 0;
-      for (int j = 0; j < P.Kact[v]; ++j) lt += P.d_l[v * KC + j];
-      P.Ltot[v] = lt;
+  {   // integer sums (order-free): L_v = sum of the view's table counts, tables non-empty
+    const int lane = tid & 63, w = tid >> 6;
+    for (int v = w; v <= V; v += kHypWaves) {
+      const int m = v < V ? P.Kact[v] : T;
+      int acc = 0;
+      for (int j = lane; j < m; j += 64) acc += v < V ? P.d_l[v * KC + j] : (P.n_t[j] > 0 ? 1 : 0);
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+      if (lane == 0) {
+        if (v < V) P.Ltot[v] = acc;
+        else { s_i[0] = acc; A.status[V + 3] = acc; }
+      }
     }
-    int tne = 0;
-    for (int p = 0; p < T; ++p)
-      if (P.n_t[p] > 0) ++tne;
-    s_i[0] = tne;
-    A.status[V + 3] = tne;
   }
   __syncthreads();
   double *hyp = P.hyper;
@@ -2374,8 +2379,37 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       return (P1 - P2) + P3;
     };
     // ---- per-view steps, one wavefront per view (multiview_hyper.cpp:211-266)
+    const bool global_on_wave = T <= kHypGlobalWaveT;
+    auto global_pair = [&](auto tree) {   // (:268-291), counters 9V ..
+      auto eppf_global = [&](double a, double s) -> double {
+        if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
+        if (a <= -s) return -MVC_PM_INF;
+        if (T <= 0) return 0.0;
+        return eppf(T, n, [&](int p) { return P.n_t[p]; }, a, s, tree);
+      };
+      const uint32_t k0 = 9u * (uint32_t)V;
+      double ag_old = hyp[3 * V];
+      if (ag_old <= 0.0) ag_old = kEps;
+      const double la = mvc_log(ag_old > kEps ? ag_old : kEps) + rnorm_at(k0, 0.0, 0.1);
+      double ag_prop = mvc_exp(la);
+      if (!(ag_prop > kEps)) ag_prop = kEps;
+      const double sg0 = hyp[3 * V + 1];
+      const double lo = eppf_global(ag_old, sg0) + prior_alpha(ag_old);
+      const double ln = eppf_global(ag_prop, sg0) + prior_alpha(ag_prop);
+      const double lq = mvc_log(ag_prop) - mvc_log(ag_old);
+      double a_g = hyp[3 * V];
+      if (mvc_log(unif_at(k0 + 2)) < (ln - lo) + lq) a_g = ag_prop;
+      const double sg_old = sg0;
+      const double sg_prop = reflect_unit(sg_old + rnorm_at(k0 + 3, 0.0, 0.05));
+      const double u2 = unif_at(k0 + 5);
+      const double pn = (sg_prop <= kEps || sg_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_prop) + prior_sigma(sg_prop);
+      const double po = (sg_old <= kEps || sg_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_old) + prior_sigma(sg_old);
+      double s_g = sg_old;
+      if (mvc_log(u2) < pn - po) s_g = sg_prop;
+      return std::make_pair(a_g, s_g);
+    };
     {
-      __shared__ double s_wpart[4][64];
+      __shared__ double s_wpart[kHypWaves][64];
       const int lane = tid & 63, wv = tid >> 6;
       auto wtree = [&](int64_t nn, auto leaf) -> double {   // tree64 by one wavefront (nn <= 4096)
         if (nn <= 0) return 0.0;
@@ -2395,7 +2429,11 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
         }
         return root;
       };
-      for (int v = wv; v < V; v += 4) {
+      if (wv == 4 && global_on_wave) {
+        const auto g = global_pair(wtree);
+        if (lane == 0) { hyp[3 * V] = g.first; hyp[3 * V + 1] = g.second; }
+      }
+      for (int v = wv; v < V && wv < 4; v += 4) {
         const int Kv = P.Kact[v], Lv = P.Ltot[v];
         auto eppf_view = [&](double a, double s) -> double {
           if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
@@ -2454,52 +2492,28 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_hyper_kernel(MHArgs A)
       }
     }
     __syncthreads();
-    // ---- global pair (:268-291), counters 9V .., the whole block
-    auto btree = [&](int64_t nn, auto leaf) -> double { return block_tree64(nn, leaf); };
-    auto eppf_global = [&](double a, double s) -> double {
-      if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
-      if (a <= -s) return -MVC_PM_INF;
-      if (T <= 0) return 0.0;
-      return eppf(T, n, [&](int p) { return P.n_t[p]; }, a, s, btree);
-    };
-    {
-      const uint32_t k0 = 9u * (uint32_t)V;
-      double ag_old = hyp[3 * V];
-      if (ag_old <= 0.0) ag_old = kEps;
-      const double la = mvc_log(ag_old > kEps ? ag_old : kEps) + rnorm_at(k0, 0.0, 0.1);
-      double ag_prop = mvc_exp(la);
-      if (!(ag_prop > kEps)) ag_prop = kEps;
-      const double sg0 = hyp[3 * V + 1];
-      const double lo = eppf_global(ag_old, sg0) + prior_alpha(ag_old);
-      const double ln = eppf_global(ag_prop, sg0) + prior_alpha(ag_prop);
-      const double lq = mvc_log(ag_prop) - mvc_log(ag_old);
-      double a_g = hyp[3 * V];
-      if (mvc_log(unif_at(k0 + 2)) < (ln - lo) + lq) a_g = ag_prop;
-      const double sg_old = sg0;
-      const double sg_prop = reflect_unit(sg_old + rnorm_at(k0 + 3, 0.0, 0.05));
-      const double u2 = unif_at(k0 + 5);
-      const double pn = (sg_prop <= kEps || sg_prop >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_prop) + prior_sigma(sg_prop);
-      const double po = (sg_old <= kEps || sg_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_global(a_g, sg_old) + prior_sigma(sg_old);
-      double s_g = sg_old;
-      if (mvc_log(u2) < pn - po) s_g = sg_prop;
+    // ---- global pair (:268-291) on the whole block when T is large
+    if (!global_on_wave) {
+      auto btree = [&](int64_t nn, auto leaf) -> double { return block_tree64(nn, leaf); };
+      const auto g = global_pair(btree);
       __syncthreads();
-      if (tid == 0) { hyp[3 * V] = a_g; hyp[3 * V + 1] = s_g; }
-      __syncthreads();
+      if (tid == 0) { hyp[3 * V] = g.first; hyp[3 * V + 1] = g.second; }
     }
+    __syncthreads();
   }
   // ---- coefficients of the next sweep (frozen state) ----
   for (int v = 0; v < V; ++v) {
     const double tau = hyp[v];
     const double L = mvc_log((2.0 * MVC_PI) * tau);
     if (tid == 0) { A.L2pt[v] = L; A.cnew[v] = (double)D * (-0.5 * L); }
-    for (int j = tid; j < P.Kact[v]; j += 256) {
+    for (int j = tid; j < P.Kact[v]; j += kHypThreads) {
       const Coef c = coef(P.d_n[v * KC + j], P.Q[v * KC + j], tau, L, D);
       P.c0[v * KC + j] = c.c0;
       P.cb[v * KC + j] = c.cb;
     }
   }
   const double sg = hyp[3 * V + 1];
-  for (int p = tid; p < T; p += 256) P.lmass[p] = mvc_log((double)P.n_t[p] - sg);
+  for (int p = tid; p < T; p += kHypThreads) P.lmass[p] = mvc_log((double)P.n_t[p] - sg);
 }
 
 // ===========================================================================
@@ -2998,7 +3012,7 @@ class ParallelSampler : public Sampler {
     A.do_mh = do_mh;
     hipEvent_t ev = nullptr;
     timers.begin("hyper", &ev);
-    hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(256), 0, stream, A);
+    hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(kHypThreads), 0, stream, A);
     MVC_HIP(hipGetLastError());
     timers.end("hyper", ev);
   }
