@@ -158,7 +158,8 @@ void mvc_sampler_destroy(mvc_sampler *s);
 /* Spec primitives on the device (parity tests of RNG / math / reductions).   */
 /* x, out are HOST arrays; computed on the device.                             */
 /* op: 0 exp, 1 log, 2 lgamma, 3 qnorm, 4 sqrt, 5 exp (SGPR-coefficient form),  */
-/*     6 log (branch-free form): 5 and 6 are bitwise equal to 0 and 1           */
+/*     6 log (branch-free form): 5 and 6 are bitwise equal to 0 and 1;         */
+/*     7 exp for x <= 709.78, not NaN (equal to 0 there)                        */
 /* ------------------------------------------------------------------------ */
 int mvc_device_math(int device, int op, const double *x, double *out, int64_t n,
                     char *err, size_t errlen);

@@ -175,6 +175,48 @@ static __device__ __forceinline__ double mvc_exp_sk(double x) {
   return mvc_exp(x);
 #endif
 }
+
+/* mvc_exp for arguments x <= 709.78 that are not NaN (the draw's a - max
+ * forms): the overflow and NaN selects are dropped, nothing else changes, so
+ * it is bitwise equal to mvc_exp on that domain (the underflow select stays:
+ * the clamped reduction is garbage below -745).  6 of ~28 instructions. */
+static __device__ __forceinline__ double mvc_exp_le0(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double shifter = 6755399441055744.0;
+  double kd = x * MVC_INVLN2;
+  kd = kd + shifter;
+  kd = kd - shifter;
+  kd = __builtin_fmin(__builtin_fmax(kd, -1100.0), 1100.0);
+  const int k = (int)kd;
+  double r = __builtin_fma(-kd, MVC_LN2_HI, x);
+  r = __builtin_fma(-kd, MVC_LN2_LO, r);
+#if !defined(MVC_PM_NO_ASM_FMA)
+#define MVC_DFMA_S(p, r, c) asm("v_fma_f64 %0, %1, %2, %3" : "=v"(p) : "v"(p), "v"(r), "v"((double)(c)))
+#else
+#define MVC_DFMA_S(p, r, c) p = __builtin_fma(p, r, c)
+#endif
+  double p = 1.1470745597729725e-11;
+  MVC_DFMA_S(p, r, 1.6059043836821613e-10);
+  MVC_DFMA_S(p, r, 2.08767569878681e-09);
+  MVC_DFMA_S(p, r, 2.505210838544172e-08);
+  MVC_DFMA_S(p, r, 2.755731922398589e-07);
+  MVC_DFMA_S(p, r, 2.7557319223985893e-06);
+  MVC_DFMA_S(p, r, 2.48015873015873e-05);
+  MVC_DFMA_S(p, r, 0.0001984126984126984);
+  MVC_DFMA_S(p, r, 0.001388888888888889);
+  MVC_DFMA_S(p, r, 0.008333333333333333);
+  MVC_DFMA_S(p, r, 0.041666666666666664);
+  MVC_DFMA_S(p, r, 0.16666666666666666);
+#undef MVC_DFMA_S
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  const double e = __builtin_fma(p, r, 1.0);
+  const double res = __builtin_amdgcn_ldexp(e, k);
+  return (x < -745.1332191019412) ? 0.0 : res;
+#else
+  return mvc_exp(x);
+#endif
+}
 #endif
 
 MVC_PM double mvc_log(double x) {

@@ -814,6 +814,9 @@ struct LpRow {
 // 0) for l_j > 0 and -1 (excluded) otherwise: uniform per dish (s_w, staged
 // once per block) except the customer's own dish (w0).  KB > 0: row loaded
 // into registers at once; KB == 0: streamed in batches of 16.
+#ifndef MVC_ZEXP_LAG
+#define MVC_ZEXP_LAG 1   // exps in flight per lane in the register draw (register pressure vs ILP)
+#endif
 template <int KB>
 __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, int j0, double w0, const double *sw,
                                             double m, double *stg = nullptr) {
@@ -834,8 +837,8 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
       if (j < K) {
         const double w = (j == j0) ? w0 : sw[j];
         double xe = x[j] - m;
-        asm volatile("" : "+v"(xe) : "v"(col[(j + 15) & 15]));    // one exp in flight (register pressure)
-        const double t = w >= 0.0 ? w * mvc_exp(xe) : -1.0;
+        asm volatile("" : "+v"(xe) : "v"(col[(j + 16 - MVC_ZEXP_LAG) & 15]));    // MVC_ZEXP_LAG exps in flight (register pressure)
+        const double t = w >= 0.0 ? w * mvc_exp_le0(xe) : -1.0;
         if (t >= 0.0) col[j & 15] = col[j & 15] + t;
       }
     }
@@ -849,8 +852,8 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
       for (int u = 0; u < 16; ++u) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
         double xe = x[u] - m;
-        asm volatile("" : "+v"(xe) : "v"(col[(u + 15) & 15]));
-        const double t = w >= 0.0 ? w * mvc_exp(xe) : -1.0;
+        asm volatile("" : "+v"(xe) : "v"(col[(u + 16 - MVC_ZEXP_LAG) & 15]));
+        const double t = w >= 0.0 ? w * mvc_exp_le0(xe) : -1.0;
         if (t >= 0.0) col[u] = col[u] + t;
       }
     }
@@ -858,7 +861,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
     for (int u = 0; u < 16; ++u) {
       if (j + u < K) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        const double t = w >= 0.0 ? w * mvc_exp(row(koff + j + u) - m) : -1.0;
+        const double t = w >= 0.0 ? w * mvc_exp_le0(row(koff + j + u) - m) : -1.0;
         if (t >= 0.0) col[u] = col[u] + t;
       }
     }
@@ -951,7 +954,7 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = P.hyper[V + v] + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
-      S = S + wn * mvc_exp(lfn - m);
+      S = S + wn * mvc_exp_le0(lfn - m);
       const double denom = P.hyper[V + v] + (double)(P.Ltot[v] - (alive ? 0 : 1));
       const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
       s_new = s_new + lm;
@@ -998,8 +1001,8 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
         const int p = 16 * b + c;
         const bool in = p < T && sp[p] != -MVC_PM_INF;
         double xe = in ? sp[p] - M : 0.0;
-        asm volatile("" : "+v"(xe) : "v"(sp[(p + TM - 1) % TM]));   // one exp in flight, not TM live
-        const double e = mvc_exp(xe);
+        asm volatile("" : "+v"(xe) : "v"(sp[(p + TM - MVC_ZEXP_LAG) % TM]));   // MVC_ZEXP_LAG exps in flight, not TM live
+        const double e = mvc_exp_le0(xe);
         sp[p] = in ? e : 0.0;
       }
       double blk[16];
@@ -1008,7 +1011,7 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
       tot = tot + pw16(blk);
       C[b] = tot;
     }
-    const double W = mvc_exp(s_new - M) + tot;
+    const double W = mvc_exp_le0(s_new - M) + tot;
     double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
     int pick = -1;
     if (r < tot) {
@@ -2291,6 +2294,12 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
   const int tid = threadIdx.x;
   const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
   __shared__ int s_i[8];
+#ifdef MVC_HYP_PROF
+  const uint64_t t0 = wall_clock64();
+#define HYP_MARK(name) if (tid == 0 && A.sweep == 5) printf("hyp %s %llu\n", name, (unsigned long long)(wall_clock64() - t0))
+#else
+#define HYP_MARK(name)
+#endif
   const int T = A.status[0];
   // ---- Q = ||S1||^2 per live dish (fma chain in d order), all views at once;
   //      the strided S1 loads are issued 16 ahead of the chain ----
@@ -2336,6 +2345,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     }
   }
   __syncthreads();
+  HYP_MARK("q+sums");
   double *hyp = P.hyper;
   if (A.do_mh) {
     // Every MH step draws from its own window of the MH counter (oracle
@@ -2492,6 +2502,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
       }
     }
     __syncthreads();
+    HYP_MARK("views");
     // ---- global pair (:268-291) on the whole block when T is large
     if (!global_on_wave) {
       auto btree = [&](int64_t nn, auto leaf) -> double { return block_tree64(nn, leaf); };
@@ -2501,6 +2512,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     }
     __syncthreads();
   }
+  HYP_MARK("mh");
   // ---- coefficients of the next sweep (frozen state) ----
   for (int v = 0; v < V; ++v) {
     const double tau = hyp[v];
@@ -2514,6 +2526,8 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
   }
   const double sg = hyp[3 * V + 1];
   for (int p = tid; p < T; p += kHypThreads) P.lmass[p] = mvc_log((double)P.n_t[p] - sg);
+  HYP_MARK("coef");
+#undef HYP_MARK
 }
 
 // ===========================================================================

@@ -252,7 +252,7 @@ class Sampler:
 
 # ---- spec primitives on the device (parity tests) ----
 def device_math(op, x, device=0):
-    ops = {"exp": 0, "log": 1, "lgamma": 2, "qnorm": 3, "sqrt": 4, "exp_sk": 5, "log_nb": 6}
+    ops = {"exp": 0, "log": 1, "lgamma": 2, "qnorm": 3, "sqrt": 4, "exp_sk": 5, "log_nb": 6, "exp_le0": 7}
     x = np.ascontiguousarray(x, dtype=np.float64)
     o = np.empty_like(x)
     buf = L.errbuf()

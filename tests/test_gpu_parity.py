@@ -30,6 +30,10 @@ def test_device_exp_log_bitwise():
                         [0.0, -0.0, 1e-310, -1e-310, 709.78, -745.2, np.inf, -np.inf, np.nan]])
     assert np.array_equal(m.device_math("exp", x), O.pm_exp(x), equal_nan=True)
     assert np.array_equal(m.device_math("exp_sk", x), O.pm_exp(x), equal_nan=True)
+    # the draw's exp: arguments of the form a - max (<= 0), never NaN
+    xl = np.concatenate([x[(x <= 709.78) & ~np.isnan(x)], -rng.exponential(50.0, 200000),
+                         rng.uniform(-746.0, -744.0, 100000), [-1e300, -5e5, -1100 * np.log(2)]])
+    assert np.array_equal(m.device_math("exp_le0", xl), O.pm_exp(xl))
     y = np.concatenate([np.exp(rng.uniform(-700, 700, 200000)), rng.uniform(0.5, 2.0, 200000),
                         [0.0, 1.0, 2.0, 1e-320, np.inf, -1.0, np.nan]])
     assert np.array_equal(m.device_math("log", y), O.pm_log(y), equal_nan=True)
