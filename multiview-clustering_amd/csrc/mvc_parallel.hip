@@ -838,8 +838,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
         const double w = (j == j0) ? w0 : sw[j];
         double xe = x[j] - m;
         asm volatile("" : "+v"(xe) : "v"(col[(j + 16 - MVC_ZEXP_LAG) & 15]));    // MVC_ZEXP_LAG exps in flight (register pressure)
-        const double t = w >= 0.0 ? w * mvc_exp_le0(xe) : -1.0;
-        if (t >= 0.0) col[j & 15] = col[j & 15] + t;
+        col[j & 15] = col[j & 15] + __builtin_fmax(w, 0.0) * mvc_exp_le0(xe);   // dead dish (w = -1): + 0, exact
       }
     }
   } else {
@@ -853,16 +852,14 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
         const double w = (j + u == j0) ? w0 : sw[j + u];
         double xe = x[u] - m;
         asm volatile("" : "+v"(xe) : "v"(col[(u + 16 - MVC_ZEXP_LAG) & 15]));
-        const double t = w >= 0.0 ? w * mvc_exp_le0(xe) : -1.0;
-        if (t >= 0.0) col[u] = col[u] + t;
+        col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(xe);
       }
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       if (j + u < K) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        const double t = w >= 0.0 ? w * mvc_exp_le0(row(koff + j + u) - m) : -1.0;
-        if (t >= 0.0) col[u] = col[u] + t;
+        col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(row(koff + j + u) - m);
       }
     }
   }
@@ -965,9 +962,9 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     // table scores in view order, 16 tables' gathers in flight per step
     double sp[TM];
 #pragma unroll
-    for (int p = 0; p < TM; ++p) {
+    for (int p = 0; p < TM; ++p) {   // p >= T: -inf, so its weight below is exp(-inf) = 0 like a dead table's
       const int pc = min(p, T - 1);
-      sp[p] = (pc == p0) ? base_self : s_base[pc];
+      sp[p] = p < T ? ((pc == p0) ? base_self : s_base[pc]) : -MVC_PM_INF;
     }
 #pragma unroll
     for (int c = 0; c < TM; c += 16) {
@@ -999,11 +996,10 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
         const int p = 16 * b + c;
-        const bool in = p < T && sp[p] != -MVC_PM_INF;
-        double xe = in ? sp[p] - M : 0.0;
+        // a dead table or p >= T has sp = -inf: exp_le0(-inf) = +0, the spec's 0 weight
+        double xe = sp[p] - M;
         asm volatile("" : "+v"(xe) : "v"(sp[(p + TM - MVC_ZEXP_LAG) % TM]));   // MVC_ZEXP_LAG exps in flight, not TM live
-        const double e = mvc_exp_le0(xe);
-        sp[p] = in ? e : 0.0;
+        sp[p] = mvc_exp_le0(xe);
       }
       double blk[16];
 #pragma unroll
