@@ -140,6 +140,12 @@ int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms,
                             int64_t *launches);
 void mvc_sampler_reset_timers(mvc_sampler *s);
+/* Adjusted Rand index of the chain's current table labels against truth[n]
+ * (host array, any int32 labels), computed on the device from exact pair
+ * counts in mclust::adjustedRandIndex's operation order (the ARI of
+ * New_Simulation.R:189).  MVC_ERR_UNSUPPORTED when range(labels) x
+ * range(truth) > 2^26 contingency cells. */
+int mvc_sampler_ari(mvc_sampler *s, int chain, const int32_t *truth, double *ari, char *err, size_t errlen);
 /* Switch timing at run time: flags = 0 (off), MVC_FLAG_TIMING (every
  * phase) or MVC_FLAG_TIMING | MVC_FLAG_TIMING_COARSE (whole passes only).
  * Synchronises the handle's stream; accumulated times are kept. */
@@ -161,6 +167,9 @@ void mvc_sampler_destroy(mvc_sampler *s);
 /*     6 log (branch-free form): 5 and 6 are bitwise equal to 0 and 1;         */
 /*     7 exp for x <= 709.78, not NaN (equal to 0 there)                        */
 /* ------------------------------------------------------------------------ */
+/* Adjusted Rand index of two host label arrays a[n], b[n] on the device
+ * (same computation as mvc_sampler_ari). */
+int mvc_ari(int device, const int32_t *a, const int32_t *b, int64_t n, double *ari, char *err, size_t errlen);
 int mvc_device_math(int device, int op, const double *x, double *out, int64_t n,
                     char *err, size_t errlen);
 int mvc_device_seq_uniforms(int device, uint64_t seed, uint32_t chain, uint64_t start,

@@ -291,6 +291,53 @@ int mvc_sampler_set_state(mvc_sampler *s, int chain, const int32_t *table_of, in
   });
 }
 
+int mvc_ari(int device, const int32_t *a, const int32_t *b, int64_t n, double *ari, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!a || !b || !ari) throw mvc::Error(MVC_ERR_ARG, "NULL argument");
+    if (n < 1) throw mvc::Error(MVC_ERR_ARG, "n must be >= 1");
+    MVC_HIP(hipSetDevice(device));
+    int32_t *d = nullptr;
+    MVC_HIP(hipMalloc(&d, sizeof(int32_t) * 2 * (size_t)n));
+    try {
+      MVC_HIP(hipMemcpy(d, a, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+      MVC_HIP(hipMemcpy(d + n, b, sizeof(int32_t) * n, hipMemcpyHostToDevice));
+      *ari = mvc::ari_device(d, d + n, n, nullptr);
+    } catch (...) {
+      hipFree(d);
+      throw;
+    }
+    hipFree(d);
+  });
+}
+
+int mvc_sampler_ari(mvc_sampler *s, int chain, const int32_t *truth, double *ari, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl || !truth || !ari) throw mvc::Error(MVC_ERR_ARG, "NULL argument");
+    mvc::Sampler &S = *s->impl;
+    const int64_t n = S.cfg.n;
+    MVC_HIP(hipSetDevice(S.cfg.device));
+    int32_t *d = nullptr;
+    MVC_HIP(hipMalloc(&d, sizeof(int32_t) * 2 * (size_t)n));
+    try {
+      MVC_HIP(hipMemcpyAsync(d + n, truth, sizeof(int32_t) * n, hipMemcpyHostToDevice, S.stream));
+      const int32_t *z = S.device_labels(chain);
+      if (!z) {   // labels on the host (exact schedule): one upload
+        std::vector<int32_t> h((size_t)n);
+        int32_t T = 0;
+        S.get_state(chain, h.data(), &T, nullptr, 0, nullptr);
+        MVC_HIP(hipMemcpyAsync(d, h.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, S.stream));
+        MVC_HIP(hipStreamSynchronize(S.stream));
+        z = d;
+      }
+      *ari = mvc::ari_device(z, d + n, n, S.stream);
+    } catch (...) {
+      hipFree(d);
+      throw;
+    }
+    hipFree(d);
+  });
+}
+
 int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char *err, size_t errlen) {
   return guarded(err, errlen, [&] {
     if (!s || !s->impl || !k_out) throw mvc::Error(MVC_ERR_ARG, "NULL argument");

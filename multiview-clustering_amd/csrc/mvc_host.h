@@ -78,12 +78,20 @@ class Sampler {
                                       const double *hyper)>;
   virtual bool save_async(int chain, const SampleFn &fn) { (void)chain; (void)fn; return false; }
   virtual void flush_saves() {}
+  // Device pointer to the chain's table labels [n] (valid until the next
+  // sweep; the stream is synchronised), or nullptr when they live on the host.
+  virtual const int32_t *device_labels(int chain) { (void)chain; return nullptr; }
   mvc_config cfg;
   int sweeps_done = 0;
   int zpath = -1;                        // mvc_sampler_zpath
   hipStream_t stream = nullptr;
   Timers timers;
 };
+
+// Adjusted Rand index (mvc_ari.hip): exact pair counts on the device, combined
+// in mclust::adjustedRandIndex's operation order.
+double ari_device(const int32_t *da, const int32_t *db, int64_t n, hipStream_t stream);
+double ari_from_pairs(uint64_t a, uint64_t sa, uint64_t sb, int64_t n, bool one_by_one);
 
 // Validated host view of a user-supplied state (warm start / resume).
 struct UserState {

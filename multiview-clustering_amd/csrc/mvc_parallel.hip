@@ -3300,6 +3300,12 @@ class ParallelSampler : public Sampler {
 
   void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
 
+  const int32_t *device_labels(int chain) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    MVC_HIP(hipStreamSynchronize(stream));
+    return chains[chain].P.z;
+  }
+
   void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of, int32_t dish_cap,
                  double *hyper) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");

@@ -91,6 +91,8 @@ def lib():
         "mvc_sampler_reset_timers": (None, [vp]),
         "mvc_sampler_zpath": (i32, [vp]),
         "mvc_sampler_set_timing": (i32, [vp, i32]),
+        "mvc_sampler_ari": (i32, [vp, i32, ip, dp, cp, sz]),
+        "mvc_ari": (i32, [i32, ip, ip, i64, dp, cp, sz]),
         "mvc_sampler_stream": (vp, [vp]),
         "mvc_sampler_destroy": (None, [vp]),
         "mvc_device_math": (i32, [i32, i32, dp, dp, i64, cp, sz]),

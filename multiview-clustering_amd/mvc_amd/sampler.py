@@ -156,6 +156,18 @@ class Sampler:
     def sweeps_done(self):
         return self._lib.mvc_sampler_sweeps_done(self._h)
 
+    def ari(self, truth, chain=0):
+        """Adjusted Rand index of the chain's current table labels against
+        truth[n] (mclust::adjustedRandIndex, New_Simulation.R:189), on the device."""
+        t = np.ascontiguousarray(truth, dtype=np.int32)
+        if t.shape != (self.n,):
+            raise ValueError(f"truth must have shape ({self.n},)")
+        out = ctypes.c_double()
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_ari(self._h, chain, t.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                          ctypes.byref(out), buf, len(buf)), buf)
+        return out.value
+
     def state(self, chain=0):
         """(table_of[n], dish_of[V][T], hyper dict) of one chain."""
         buf = L.errbuf()
@@ -251,6 +263,21 @@ class Sampler:
 
 
 # ---- spec primitives on the device (parity tests) ----
+def ari(a, b, device=0):
+    """Adjusted Rand index of two int32 labelings (mclust::adjustedRandIndex,
+    the ARI of New_Simulation.R:189), computed on the device."""
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    b = np.ascontiguousarray(b, dtype=np.int32)
+    if a.shape != b.shape or a.ndim != 1:
+        raise ValueError("a and b must be 1-D arrays of the same length")
+    out = ctypes.c_double()
+    buf = L.errbuf()
+    ip = ctypes.POINTER(ctypes.c_int32)
+    L.check(L.lib().mvc_ari(device, a.ctypes.data_as(ip), b.ctypes.data_as(ip), a.size, ctypes.byref(out), buf,
+                            len(buf)), buf)
+    return out.value
+
+
 def device_math(op, x, device=0):
     ops = {"exp": 0, "log": 1, "lgamma": 2, "qnorm": 3, "sqrt": 4, "exp_sk": 5, "log_nb": 6, "exp_le0": 7}
     x = np.ascontiguousarray(x, dtype=np.float64)

@@ -182,3 +182,31 @@ def tree64_sum(x):
 def tree64_select(x, r):
     x = np.ascontiguousarray(x, dtype=np.float64)
     return int(lib().mvo_tree64_select(_dp(x), x.size, r))
+
+
+def ari(a, b):
+    """Adjusted Rand index, restating mclust::adjustedRandIndex (the ARI of
+    New_Simulation.R:6,189; mclust is an R package absent here): exact pair
+    counts a, b, c, d from the contingency table, then its fp64 expression in
+    R's left-to-right operation order.  Pinned against scikit-learn's
+    adjusted_rand_score (the same Hubert-Arabie index) in tests/test_ari.py."""
+    from collections import Counter
+    a = np.asarray(a).ravel()
+    b = np.asarray(b).ravel()
+    assert a.shape == b.shape
+    n = int(a.size)
+    tab = Counter(zip(a.tolist(), b.tolist()))
+    rows = Counter(a.tolist())
+    cols = Counter(b.tolist())
+    if len(rows) == 1 and len(cols) == 1:
+        return 1.0
+    ch2 = lambda k: k * (k - 1) // 2  # noqa: E731
+    A = sum(ch2(v) for v in tab.values())
+    B = sum(ch2(v) for v in rows.values()) - A
+    C = sum(ch2(v) for v in cols.values()) - A
+    Dd = ch2(n) - A - B - C
+    a_, b_, c_ = float(A), float(B), float(C)
+    d_ = ((float(ch2(n)) - a_) - b_) - c_
+    assert d_ == float(Dd)
+    e = (a_ + b_) * (a_ + c_) / (((a_ + b_) + c_) + d_)
+    return (a_ - e) / ((((a_ + b_) + a_) + c_) / 2.0 - e)
