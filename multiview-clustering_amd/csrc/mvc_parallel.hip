@@ -2043,25 +2043,26 @@ struct StatsUpd {
   int V, D, KC, n;
   int Kold[MVC_MAXV], Knew[MVC_MAXV], M[MVC_MAXV];
 };
-// surviving dishes keep their sums under the compaction map; new dishes 0
-extern "C" __global__ void mvc_par_stats_zero_kernel(StatsUpd U, double *S1T, double *S2) {
-  const size_t per = (size_t)(U.D + 1) * U.KC;
+// surviving dishes keep their sums under the compaction map; new dishes 0.
+// Both walk only the live columns: W = max over views of K (new / old).
+extern "C" __global__ void mvc_par_stats_zero_kernel(StatsUpd U, int W, double *S1T, double *S2) {
+  const size_t per = (size_t)(U.D + 1) * W;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < per * U.V; e += (size_t)gridDim.x * blockDim.x) {
     const int v = (int)(e / per);
     const size_t r = e - (size_t)v * per;
-    const int dd = (int)(r / U.KC), j = (int)(r % U.KC);
+    const int dd = (int)(r / W), j = (int)(r % W);
     if (j >= U.Knew[v]) continue;
     if (dd < U.D) S1T[((size_t)v * U.D + dd) * U.KC + j] = 0.0;
     else S2[(size_t)v * U.KC + j] = 0.0;
   }
 }
-extern "C" __global__ void mvc_par_stats_scatter_kernel(StatsUpd U, const int32_t *jmap, const double *S1T,
+extern "C" __global__ void mvc_par_stats_scatter_kernel(StatsUpd U, int W, const int32_t *jmap, const double *S1T,
                                                         const double *S2, double *S1T_out, double *S2_out) {
-  const size_t per = (size_t)(U.D + 1) * U.KC;
+  const size_t per = (size_t)(U.D + 1) * W;
   for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < per * U.V; e += (size_t)gridDim.x * blockDim.x) {
     const int v = (int)(e / per);
     const size_t r = e - (size_t)v * per;
-    const int dd = (int)(r / U.KC), j = (int)(r % U.KC);
+    const int dd = (int)(r / W), j = (int)(r % W);
     if (j >= U.Kold[v]) continue;
     const int jn = jmap[(size_t)v * U.KC + j];
     if (jn < 0) continue;
@@ -2979,10 +2980,12 @@ class ParallelSampler : public Sampler {
       else inc.push_back(v);
     }
     // carry the sums over to the new dish numbering (all views; rebuilt views overwrite)
-    const size_t elems = (size_t)V * (D + 1) * KC;
-    const unsigned g = (unsigned)std::min<size_t>(4096, (elems + 255) / 256);
-    hipLaunchKernelGGL(mvc_par_stats_zero_kernel, dim3(g), dim3(256), 0, stream, U, c.S1T_alt, c.S2_alt);
-    hipLaunchKernelGGL(mvc_par_stats_scatter_kernel, dim3(g), dim3(256), 0, stream, U, (const int32_t *)c.jmap,
+    int Wn = 1, Wo = 1;
+    for (int v = 0; v < V; ++v) { Wn = std::max(Wn, c.K[v]); Wo = std::max(Wo, Kold[v]); }
+    const unsigned gz = (unsigned)std::min<size_t>(4096, ((size_t)V * (D + 1) * Wn + 255) / 256);
+    const unsigned gs = (unsigned)std::min<size_t>(4096, ((size_t)V * (D + 1) * Wo + 255) / 256);
+    hipLaunchKernelGGL(mvc_par_stats_zero_kernel, dim3(gz), dim3(256), 0, stream, U, Wn, c.S1T_alt, c.S2_alt);
+    hipLaunchKernelGGL(mvc_par_stats_scatter_kernel, dim3(gs), dim3(256), 0, stream, U, Wo, (const int32_t *)c.jmap,
                        (const double *)c.P.S1T, (const double *)c.P.S2, c.S1T_alt, c.S2_alt);
     MVC_HIP(hipGetLastError());
     std::swap(c.P.S1T, c.S1T_alt);
