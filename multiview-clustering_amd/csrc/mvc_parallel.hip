@@ -2027,10 +2027,12 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_relabel_kernel(
       const int o = jmap[v * KC + dish_old[v * TC + zo]];
       const int w = dish_new[v * TC + zn];
       const int m = o != w ? 1 : 0;
-      dold[(size_t)v * n + i] = o;
-      dnew[(size_t)v * n + i] = w;
       mflag[(size_t)v * n + i] = m;
-      if (m) atomicAdd(&s_cnt[v], 1);
+      if (m) {   // dold / dnew are read only at the moved customers (stats_apply via mlist)
+        dold[(size_t)v * n + i] = o;
+        dnew[(size_t)v * n + i] = w;
+        atomicAdd(&s_cnt[v], 1);
+      }
     }
   }
   __syncthreads();
