@@ -153,7 +153,8 @@ def main():
     s.sweep(n_detail)
     s.synchronize()
     parts = {k: s.kernel_time(k)[0] / n_detail
-             for k in ("zresample", "lp", "draw", "births", "commit", "stats", "hyper")}
+             for k in ("zresample", "lp", "draw", "repair", "hyper")}
+    repair = s.repair_stats()
     kdish = s.dish_counts()
     _, dish_now, hyper_now = s.state()
     T = dish_now.shape[1]
@@ -201,7 +202,7 @@ def main():
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": desc, "N": N, "V": V, "D": D, "K": K, "chains": world,
-                   "schedule": "parallel z-resample (DESIGN.md §4)", "parallelism": f"chains{world}",
+                   "schedule": "sequential (reference) schedule, data-parallel pass + in-order repair (DESIGN.md §4.8)", "parallelism": f"chains{world}",
                    "tables_at_end": int(T), "dishes_at_end": kdish.tolist()},
         "roofline": roof,
         "hbm": {"pass": "z-resample (lp producer + draw, DESIGN.md §5)", "achieved_gbs": round(hbm_gbs, 1),
@@ -216,6 +217,7 @@ def main():
                               "sigma_global": round(float(pooled_mean[-1]), 6)},
         "nvk_sweeps_per_s": round(value * N * V * K, 1),
         "kernel_ms_per_sweep": {k: round(v, 4) for k, v in parts.items()},
+        "repair_last_sweep": repair,
         "kernel_ms_note": "per-phase HIP-event times from 3 sweeps after the timed region",
         "data_gen_s": round(t_gen, 2),
     }

@@ -50,7 +50,8 @@ extern "C" {
 
 /* schedules */
 #define MVC_MODE_EXACT 0     /* reference schedule, bit-exact vs. the CPU oracle  */
-#define MVC_MODE_PARALLEL 1  /* parallel z-resample sweep          */
+#define MVC_MODE_PARALLEL 1  /* the same sequential schedule, executed data-parallel
+                                (speculative pass + in-order repair) */
 
 typedef struct mvc_config {
   int32_t n;            /* customers (observations)                              */
@@ -136,7 +137,7 @@ int mvc_sampler_get_dish_counts(mvc_sampler *s, int chain, int32_t *k_out, char 
 int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes, double *S1, double *S2,
                           int32_t *n_vk, int32_t dish_cap, char *err, size_t errlen);
 /* HIP-event kernel timing (needs MVC_FLAG_TIMING): kernel = "zresample",
- * "commit", "stats", "hyper", "exact_sweep", or "sweep" (whole sweep). */
+ * "repair", "stats", "hyper", "exact_sweep", or "sweep" (whole sweep). */
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms,
                             int64_t *launches);
 void mvc_sampler_reset_timers(mvc_sampler *s);
@@ -156,6 +157,11 @@ int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags);
  * -1 for the exact schedule or before the first sweep.  (No reference
  * counterpart: diagnostics of this implementation.) */
 int mvc_sampler_zpath(mvc_sampler *s);
+/* Counters of the chain's last parallel sweep: out[0]
+ * customers that changed table, out[1] births, out[2] in-order repair rounds,
+ * out[3] dishes opened.  MVC_ERR_UNSUPPORTED for the exact schedule.  (No
+ * reference counterpart: diagnostics of this implementation.) */
+int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out);
 /* Opaque HIP stream the handle launches on (hipStream_t as void*). */
 void *mvc_sampler_stream(mvc_sampler *s);
 void mvc_sampler_destroy(mvc_sampler *s);

@@ -387,6 +387,15 @@ int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags) {
 
 int mvc_sampler_zpath(mvc_sampler *s) { return (s && s->impl) ? s->impl->zpath : -1; }
 
+int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out) {
+  if (!s || !s->impl || !out) return MVC_ERR_ARG;
+  try {
+    return s->impl->repair_stats(chain, out) ? MVC_OK : MVC_ERR_UNSUPPORTED;
+  } catch (const mvc::Error &e) {
+    return e.code;
+  }
+}
+
 void *mvc_sampler_stream(mvc_sampler *s) { return (s && s->impl) ? (void *)s->impl->stream : nullptr; }
 
 void mvc_sampler_destroy(mvc_sampler *s) { delete s; }

@@ -81,6 +81,10 @@ class Sampler {
   // Device pointer to the chain's table labels [n] (valid until the next
   // sweep; the stream is synchronised), or nullptr when they live on the host.
   virtual const int32_t *device_labels(int chain) { (void)chain; return nullptr; }
+  // Repair counters of the chain's last parallel sweep:
+  // out[0] customers that moved, out[1] births, out[2] repair rounds,
+  // out[3] dishes opened.  False for the exact schedule.
+  virtual bool repair_stats(int chain, int32_t *out) { (void)chain; (void)out; return false; }
   mvc_config cfg;
   int sweeps_done = 0;
   int zpath = -1;                        // mvc_sampler_zpath

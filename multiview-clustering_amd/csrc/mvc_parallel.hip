@@ -47,18 +47,7 @@ struct Sweep {
   const double *L2pt;     // [V]  log(2 pi tau)
   const double *cnew;     // [V]  D * (-0.5 L2pt)
   const int32_t *Koff;    // [V+1] prefix of Kact
-  double *scratch;        // per wave: [sumK]
   int32_t *choice;        // [n] position or -1 (birth)
-  const int32_t *blist;   // [NB] birth customers, ascending
-  // birth resolution (phase 2) state
-  int32_t *p2meta;        // [V+2]: T2, K2[V], error
-  int32_t *p2_c;          // [TC] customers of phase-2 table t
-  int32_t *p2_tup;        // [TC*V] extended dish index (frozen j or K_v + q)
-  int32_t *n2, *l2;       // [V*KC]
-  double *S1_2T;          // [(v*D + d)*KC + q]
-  double *lp2;            // [V*KC] lp of phase-2 dishes for the current birth
-  int32_t *btab;          // [NB] phase-2 table of each birth
-  const int32_t *nbirth;  // [1]
   const int32_t *status;  // [V+4]; status[V+3] = tables with n_t > 0
   const double *yt;       // MFMA A-fragment layout of y (mvc_par_ytile_kernel)
   const double *S1t;      // MFMA B-fragment layout of S1 (mvc_par_s1tile_kernel)
@@ -68,148 +57,6 @@ struct Sweep {
   uint64_t seed;
   uint32_t chain, sweep;
 };
-
-// Per-view mixture of the new-table marginal for customer i.
-// Writes lp of every live dish into lp[0..K); returns lmarg; outputs the max
-// m, the tree sum S and (lane c) the level-0 chunk partial of chunk c.
-struct ViewOut { double lmarg, m, S, part; int nc; double lf_new, w_new; };
-
-__device__ __forceinline__ ViewOut view_eval(const Sweep &A, int i, int v, int p0, bool alive, double *lp,
-                                            bool with_p2 = false) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
-  const int K = P.Kact[v];
-  const int K2 = with_p2 ? A.p2meta[1 + v] : 0;
-  const int j0 = P.dish[v * P.TC + p0];
-  const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-  const double Y2i = A.Y2[(size_t)v * n + i];
-  const double hy = 0.5 * Y2i;
-  const double h = (-0.5 * Y2i) / tau;
-  const double *yrow = A.y + ((size_t)v * n + i) * D;
-  const double *S1v = P.S1T + (size_t)v * D * KC;
-  const int l0 = P.d_l[v * KC + j0];
-  const int l0p = alive ? l0 : l0 - 1;
-  double mx = -MVC_PM_INF;
-  for (int base = 0; base < K; base += 64) {
-    const int j = base + lane;
-    if (j < K) {
-      double G = 0.0;
-      for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S1v[(size_t)d * KC + j], G);
-      double val;
-      int l;
-      if (j == j0) {
-        l = l0p;
-        const double Gp = G - Y2i;
-        const double Qp = (P.Q[v * KC + j] - 2.0 * G) + Y2i;
-        const Coef c = coef(P.d_n[v * KC + j] - 1, Qp, tau, A.L2pt[v], D);
-        val = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
-      } else {
-        l = P.d_l[v * KC + j];
-        val = __builtin_fma(G + hy, P.cb[v * KC + j], P.c0[v * KC + j]) + h;
-      }
-      lp[j] = val;
-      if (l > 0 && val > mx) mx = val;
-    }
-  }
-  int L2sum = 0;
-  if (with_p2) {
-    const double *S2v = A.S1_2T + (size_t)v * D * KC;
-    for (int base = 0; base < K2; base += 64) {
-      const int q = base + lane;
-      if (q < K2) {
-        double G = 0.0, Q = 0.0;
-        for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S2v[(size_t)d * KC + q], G);
-        for (int d = 0; d < D; ++d) {
-          const double sq = S2v[(size_t)d * KC + q];
-          Q = __builtin_fma(sq, sq, Q);
-        }
-        const Coef c = coef(A.n2[v * KC + q], Q, tau, A.L2pt[v], D);
-        const double val = __builtin_fma(G + hy, c.cb, c.c0) + h;
-        A.lp2[v * KC + q] = val;
-        if (val > mx) mx = val;
-      }
-    }
-    for (int q = 0; q < K2; ++q) L2sum += A.l2[v * KC + q];
-  }
-  ViewOut o;
-  o.lf_new = A.cnew[v] + h;
-  const int Kact_i = K - ((l0p == 0) ? 1 : 0) + K2;
-  double wn = alpha + (double)Kact_i * sigma;
-  if (wn < 0.0) wn = 0.0;
-  o.w_new = wn;
-  mx = wave_max(mx);
-  if (o.lf_new > mx) mx = o.lf_new;
-  o.m = mx;
-  const int NE = K + K2;
-  o.nc = (NE + 1 + 63) >> 6;
-  double part = 0.0;
-  for (int c = 0; c < o.nc; ++c) {
-    const int e = c * 64 + lane;
-    double leaf = 0.0;
-    if (e < K) {
-      const int l = (e == j0) ? l0p : P.d_l[v * KC + e];
-      if (l > 0) {
-        double w = (double)l - sigma;
-        if (w < 0.0) w = 0.0;
-        leaf = w * mvc_exp(lp[e] - mx);
-      }
-    } else if (e < NE) {
-      double w = (double)A.l2[v * KC + (e - K)] - sigma;
-      if (w < 0.0) w = 0.0;
-      leaf = w * mvc_exp(A.lp2[v * KC + (e - K)] - mx);
-    } else if (e == NE) {
-      leaf = wn * mvc_exp(o.lf_new - mx);
-    }
-    const double cs = wave_tree_sum(leaf);
-    if (lane == c) part = cs;
-  }
-  o.part = part;
-  o.S = (o.nc == 1) ? __shfl(part, 0, 64) : wave_tree_sum(lane < o.nc ? part : 0.0);
-  const double denom = alpha + (double)((P.Ltot[v] - (alive ? 0 : 1)) + L2sum);
-  o.lmarg = (denom <= 0.0) ? o.lf_new : (mx + mvc_log(o.S)) - mvc_log(denom);
-  return o;
-}
-
-__device__ __forceinline__ int view_select(const Sweep &A, int v, int p0, bool alive, const double *lp,
-                                           const ViewOut &o, double r, bool with_p2) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int V = P.V, KC = P.KC;
-  const int K = P.Kact[v];
-  const int K2 = with_p2 ? A.p2meta[1 + v] : 0;
-  const int NE = K + K2;
-  const int j0 = P.dish[v * P.TC + p0];
-  const double sigma = P.hyper[2 * V + v];
-  const int l0p = alive ? P.d_l[v * KC + j0] : P.d_l[v * KC + j0] - 1;
-  int c = 0;
-  if (o.nc > 1) {
-    Tree64Levels L;
-    const double pv = lane < o.nc ? o.part : 0.0;
-    wave_tree_sum_levels(pv, L);
-    c = wave_tree_select(L, pv, r);
-  }
-  const int e = c * 64 + lane;
-  double leaf = 0.0;
-  if (e < K) {
-    const int l = (e == j0) ? l0p : P.d_l[v * KC + e];
-    if (l > 0) {
-      double w = (double)l - sigma;
-      if (w < 0.0) w = 0.0;
-      leaf = w * mvc_exp(lp[e] - o.m);
-    }
-  } else if (e < NE) {
-    double w = (double)A.l2[v * KC + (e - K)] - sigma;
-    if (w < 0.0) w = 0.0;
-    leaf = w * mvc_exp(A.lp2[v * KC + (e - K)] - o.m);
-  } else if (e == NE) {
-    leaf = o.w_new * mvc_exp(o.lf_new - o.m);
-  }
-  Tree64Levels L2;
-  wave_tree_sum_levels(leaf, L2);
-  const int l = wave_tree_select(L2, leaf, r);
-  return c * 64 + l;
-}
 
 }  // namespace
 
@@ -1688,442 +1535,7 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, double *lpb
   }
 }
 
-// Phase 2: births resolved sequentially in ascending
-// customer order by ONE wavefront.  Each birth joins a table born earlier in
-// this sweep or opens one (dish per view from frozen + phase-2 + new dishes).
-extern "C" __global__ __launch_bounds__(64) void mvc_par_births_kernel(Sweep A) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x;
-  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC;
-  double *lpall = A.scratch;
-  const int NB = *A.nbirth;
-  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
-  const int T_ne = A.status[V + 3];
-  if (lane == 0) {
-    A.p2meta[0] = 0;
-    for (int v = 0; v < V; ++v) A.p2meta[1 + v] = 0;
-    A.p2meta[V + 1] = 0;
-  }
-  __syncthreads();
-  for (int b = 0; b < NB; ++b) {
-    const int i = A.blist[b];
-    const int p0 = P.z[i];
-    const bool alive = (P.n_t[p0] - 1) > 0;
-    const int T2 = A.p2meta[0];
-    // capacity: one more table and one more dish per view
-    int bad = (A.T + T2 + 1 > TC) ? 1 : 0;
-    for (int v = 0; v < V; ++v) bad |= (P.Kact[v] + A.p2meta[1 + v] + 1 > KC) ? 1 : 0;
-    if (bad) {
-      if (lane == 0) A.p2meta[V + 1] = 1;
-      return;
-    }
-    double s_new = mvc_log(ag + sg * (double)((T_ne - (alive ? 0 : 1)) + T2));
-    for (int v = 0; v < V; ++v) {
-      const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v], true);
-      s_new = s_new + o.lmarg;
-    }
-    __syncthreads();
-    auto lpx = [&](int v, int ex) -> double {
-      const int K = P.Kact[v];
-      return ex < K ? lpall[A.Koff[v] + ex] : A.lp2[v * KC + (ex - K)];
-    };
-    auto score = [&](int t) -> double {
-      double st = mvc_log((double)A.p2_c[t] - sg);
-      for (int v = 0; v < V; ++v) st = st + lpx(v, A.p2_tup[t * V + v]);
-      return st;
-    };
-    double M = s_new;
-    for (int base = 0; base < T2; base += 64) {
-      const int t = base + lane;
-      if (t < T2) { const double st = score(t); if (st > M) M = st; }
-    }
-    M = wave_max(M);
-    const int nc = (T2 + 63) >> 6;
-    double part = 0.0;
-    for (int c = 0; c < nc; ++c) {
-      const int t = c * 64 + lane;
-      const double leaf = t < T2 ? mvc_exp(score(t) - M) : 0.0;
-      const double cs = wave_tree_sum(leaf);
-      if (lane == c) part = cs;
-    }
-    double B;
-    if (nc == 0) B = 0.0;
-    else if (nc == 1) B = __shfl(part, 0, 64);
-    else B = wave_tree_sum(lane < nc ? part : 0.0);
-    const double W = mvc_exp(s_new - M) + B;
-    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z2) * W;
-    int t_pick;
-    if (r < B) {
-      int c = 0;
-      if (nc > 1) {
-        Tree64Levels L;
-        const double pv = lane < nc ? part : 0.0;
-        wave_tree_sum_levels(pv, L);
-        c = wave_tree_select(L, pv, r);
-      }
-      const int t = c * 64 + lane;
-      const double leaf = t < T2 ? mvc_exp(score(t) - M) : 0.0;
-      Tree64Levels L2;
-      wave_tree_sum_levels(leaf, L2);
-      t_pick = c * 64 + wave_tree_select(L2, leaf, r);
-      __syncthreads();
-      if (lane == 0) A.p2_c[t_pick] += 1;
-      for (int v = 0; v < V; ++v) {
-        const int K = P.Kact[v];
-        const int ex = A.p2_tup[t_pick * V + v];
-        if (ex >= K) {
-          const int q = ex - K;
-          if (lane == 0) A.n2[v * KC + q] += 1;
-          const double *yrow = A.y + ((size_t)v * P.n + i) * D;
-          for (int d = lane; d < D; d += 64) {
-            double *cell = A.S1_2T + ((size_t)v * D + d) * KC + q;
-            *cell = *cell + yrow[d];
-          }
-        }
-      }
-    } else {
-      t_pick = T2;
-      for (int v = 0; v < V; ++v) {
-        const int K = P.Kact[v];
-        const int K2 = A.p2meta[1 + v];
-        int ex;
-        // recompute this view's mixture (identical arithmetic) for the draw
-        const ViewOut o = view_eval(A, i, v, p0, alive, lpall + A.Koff[v], true);
-        if (!(o.S > 0.0)) {
-          ex = K + K2;
-        } else {
-          const double rv = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_DISH + 1u + (uint32_t)v) * o.S;
-          ex = view_select(A, v, p0, alive, lpall + A.Koff[v], o, rv, true);
-        }
-        __syncthreads();
-        const double *yrow = A.y + ((size_t)v * P.n + i) * D;
-        if (ex == K + K2) {     // brand-new phase-2 dish
-          if (lane == 0) { A.n2[v * KC + K2] = 0; A.l2[v * KC + K2] = 0; A.p2meta[1 + v] = K2 + 1; }
-          for (int d = lane; d < D; d += 64) A.S1_2T[((size_t)v * D + d) * KC + K2] = 0.0;
-          __syncthreads();
-        }
-        if (ex >= K) {
-          const int q = ex - K;
-          if (lane == 0) { A.l2[v * KC + q] += 1; A.n2[v * KC + q] += 1; }
-          for (int d = lane; d < D; d += 64) {
-            double *cell = A.S1_2T + ((size_t)v * D + d) * KC + q;
-            *cell = *cell + yrow[d];
-          }
-        }
-        if (lane == 0) A.p2_tup[T2 * V + v] = ex;
-        __syncthreads();
-      }
-      if (lane == 0) { A.p2_c[T2] = 1; A.p2meta[0] = T2 + 1; }
-    }
-    if (lane == 0) A.btab[b] = t_pick;
-    __syncthreads();
-  }
-}
-
-// commit step 1: table counts and birth flags
-// (per-block LDS histogram, then one global add per touched table: integer
-// counts, so the result is independent of the order)
-extern "C" __global__ __launch_bounds__(256) void mvc_par_count_kernel(int n, int T, const int32_t *choice,
-                                                                      int32_t *cnt, int32_t *bcnt) {
-  // block b owns the contiguous customers [b C, (b + 1) C): table counts by an
-  // LDS histogram (one global add per table and block: few blocks, because
-  // adds to one address serialise in L2), births counted per block
-  __shared__ int h[4096];
-  __shared__ int nb;
-  for (int p = threadIdx.x; p < T; p += blockDim.x) h[p] = 0;
-  if (threadIdx.x == 0) nb = 0;
-  __syncthreads();
-  const int C = (n + gridDim.x - 1) / gridDim.x;
-  const int i0 = blockIdx.x * C, i1 = min(n, i0 + C);
-  int mine = 0;
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    const int c = choice[i];
-    if (c >= 0) atomicAdd(&h[c], 1);
-    else ++mine;
-  }
-  if (mine) atomicAdd(&nb, mine);
-  __syncthreads();
-  for (int p = threadIdx.x; p < T; p += blockDim.x)
-    if (h[p]) atomicAdd(&cnt[p], h[p]);
-  if (threadIdx.x == 0) bcnt[blockIdx.x] = nb;
-}
-
-// Births in ascending customer order (the spec's phase-2 order): block b
-// writes its births at the offset sum_{b' < b} bcnt[b'] (same contiguous
-// ranges as the count kernel), in customer order within the block by wave
-// ballots; brank[i] = position of birth i in the list; nbirth = total.
-extern "C" __global__ __launch_bounds__(256) void mvc_par_blist_kernel(int n, const int32_t *choice,
-                                                                      const int32_t *bcnt, int32_t *blist,
-                                                                      int32_t *brank, int32_t *nbirth) {
-  __shared__ int s_off, s_tot, s_w[4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) { s_off = 0; s_tot = 0; }
-  __syncthreads();
-  {
-    int a = 0, t = 0;
-    for (int b = tid; b < (int)gridDim.x; b += blockDim.x) {
-      const int c = bcnt[b];
-      t += c;
-      if (b < (int)blockIdx.x) a += c;
-    }
-    if (a) atomicAdd(&s_off, a);
-    if (t) atomicAdd(&s_tot, t);
-  }
-  __syncthreads();
-  if (blockIdx.x == 0 && tid == 0) *nbirth = s_tot;
-  int base = s_off;
-  if (s_tot == 0) return;
-  const int C = (n + gridDim.x - 1) / gridDim.x;
-  const int i0 = blockIdx.x * C, i1 = min(n, i0 + C);
-  for (int c0 = i0; c0 < i1; c0 += blockDim.x) {
-    const int i = c0 + tid;
-    const bool is_b = i < i1 && choice[i] < 0;
-    const unsigned long long bal = __ballot(is_b);
-    const int below = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) s_w[w] = __popcll(bal);
-    __syncthreads();
-    int woff = 0;
-    for (int u = 0; u < w; ++u) woff += s_w[u];
-    const int tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    if (is_b) {
-      blist[base + woff + below] = i;
-      brank[i] = base + woff + below;
-    }
-    base += tot;
-    __syncthreads();
-  }
-}
-
-// commit step 2 (one workgroup of 256): new tables, dish lists, counts.
-// status[0] = T_new, status[1..V] = K_new, status[V+1] = error flag,
-// status[V+2] = tables opened by the birth resolution.
-extern "C" __global__ __launch_bounds__(256) void mvc_par_commit_kernel(
-    ParState P, int T, const int32_t *cnt, const int32_t *p2meta, const int32_t *p2_c, const int32_t *p2_tup,
-    int32_t *pos_new, int32_t *tmp_dish /*[V*TC]*/, int32_t *tmp_nt /*[TC]*/, int32_t *lcnt /*[V*KC]*/,
-    int32_t *jmap /*[V*KC]*/, int32_t *status, int32_t *dish_old /*[V*TC]*/) {
-  __shared__ int s_scan[256];
-  const int tid = threadIdx.x;
-  const int V = P.V, TC = P.TC, KC = P.KC;
-  const int T2 = p2meta[0];
-  auto block_scan = [&](int x, int &total) {   // exclusive scan of x over the block
-    s_scan[tid] = x;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {
-      const int t = tid >= off ? s_scan[tid - off] : 0;
-      __syncthreads();
-      s_scan[tid] += t;
-      __syncthreads();
-    }
-    const int incl = s_scan[tid];
-    total = s_scan[255];
-    __syncthreads();
-    return incl - x;
-  };
-  if (p2meta[V + 1] != 0) {
-    if (tid == 0) status[V + 1] = 1;
-    return;
-  }
-  // survivors in ascending position
-  int run = 0;
-  for (int base = 0; base < T; base += 256) {
-    const int p = base + tid;
-    const int alive = (p < T && cnt[p] > 0) ? 1 : 0;
-    int tot;
-    const int ex = block_scan(alive, tot);
-    if (p < T) pos_new[p] = alive ? run + ex : -1;
-    run += tot;
-  }
-  const int Tsurv = run;
-  const int Tn = Tsurv + T2;
-  if (tid == 0) { status[0] = Tn; status[V + 1] = 0; status[V + 2] = T2; }
-  if (Tn > TC) { if (tid == 0) status[V + 1] = 1; return; }
-  __syncthreads();
-  for (int v = 0; v < V; ++v) {
-    const int Kold = P.Kact[v];
-    const int nnew = p2meta[1 + v];
-    // old table -> dish map, for the incremental statistics (relabel kernel)
-    for (int p = tid; p < T; p += 256) dish_old[v * TC + p] = P.dish[v * TC + p];
-    if (tid == 0) status[V + 4 + v] = 0;
-    for (int t = tid; t < T2; t += 256) tmp_dish[v * TC + Tsurv + t] = p2_tup[t * V + v];
-    for (int p = tid; p < T; p += 256)
-      if (pos_new[p] >= 0) tmp_dish[v * TC + pos_new[p]] = P.dish[v * TC + p];
-    for (int j = tid; j < Kold + nnew; j += 256) lcnt[v * KC + j] = 0;
-    __syncthreads();
-    for (int p = tid; p < Tn; p += 256) atomicAdd(&lcnt[v * KC + tmp_dish[v * TC + p]], 1);
-    __syncthreads();
-    // compact surviving dishes (ascending extended index == ascending raw id)
-    const int Kext = Kold + nnew;
-    int kr = 0;
-    for (int base = 0; base < Kext; base += 256) {
-      const int j = base + tid;
-      const int live = (j < Kext && lcnt[v * KC + j] > 0) ? 1 : 0;
-      int tot;
-      const int ex = block_scan(live, tot);
-      if (j < Kext) jmap[v * KC + j] = live ? kr + ex : -1;
-      kr += tot;
-    }
-    __syncthreads();
-    // in-place left compaction, one 256-chunk at a time (writes never reach
-    // entries of a later chunk)
-    const int next = P.next_id[v];
-    for (int base = 0; base < Kext; base += 256) {
-      const int j = base + tid;
-      int id = 0, l = 0, keep = 0;
-      if (j < Kext) {
-        keep = jmap[v * KC + j] >= 0;
-        id = j < Kold ? P.d_id[v * KC + j] : next + (j - Kold);
-        l = lcnt[v * KC + j];
-      }
-      __syncthreads();
-      if (keep) {
-        const int jn = jmap[v * KC + j];
-        P.d_id[v * KC + jn] = id;
-        P.d_l[v * KC + jn] = l;
-        P.d_n[v * KC + jn] = 0;
-      }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      P.next_id[v] = next + nnew;
-      P.Kact[v] = kr;
-      status[1 + v] = kr;
-    }
-    __syncthreads();
-    for (int p = tid; p < Tn; p += 256) P.dish[v * TC + p] = jmap[v * KC + tmp_dish[v * TC + p]];
-    __syncthreads();
-  }
-  // table counts, n_vk
-  for (int p = tid; p < T; p += 256)
-    if (pos_new[p] >= 0) tmp_nt[pos_new[p]] = cnt[p];
-  for (int t = tid; t < T2; t += 256) tmp_nt[Tsurv + t] = p2_c[t];
-  __syncthreads();
-  for (int p = tid; p < Tn; p += 256) {
-    const int c = tmp_nt[p];
-    P.n_t[p] = c;
-    for (int v = 0; v < V; ++v) atomicAdd(&P.d_n[v * KC + P.dish[v * TC + p]], c);
-  }
-}
-
-// commit step 3: relabel customers (births -> Tsurv + their phase-2 table);
-// per view, the customer's old dish (through the compaction map; -1 if the
-// dish died) and new dish, and the per-view count of customers whose dish
-// changed (status[V + 4 + v]) for the incremental statistics
-extern "C" __global__ __launch_bounds__(256) void mvc_par_relabel_kernel(
-    int n, int V, int TC, int KC, const int32_t *choice, const int32_t *pos_new, const int32_t *brank,
-    const int32_t *btab, int32_t *status, int32_t *z, const int32_t *dish_old, const int32_t *jmap,
-    const int32_t *dish_new, int32_t *dold, int32_t *dnew, int32_t *mflag) {
-  __shared__ int s_cnt[MVC_MAXV];
-  for (int v = threadIdx.x; v < V; v += blockDim.x) s_cnt[v] = 0;
-  __syncthreads();
-  const int32_t Tn = status[0];
-  const int32_t T2 = status[V + 2];
-  const int32_t Tsurv = Tn - T2;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const int c = choice[i];
-    const int zo = z[i];
-    const int zn = c >= 0 ? pos_new[c] : Tsurv + btab[brank[i]];
-    z[i] = zn;
-    for (int v = 0; v < V; ++v) {
-      const int o = jmap[v * KC + dish_old[v * TC + zo]];
-      const int w = dish_new[v * TC + zn];
-      const int m = o != w ? 1 : 0;
-      mflag[(size_t)v * n + i] = m;
-      if (m) {   // dold / dnew are read only at the moved customers (stats_apply via mlist)
-        dold[(size_t)v * n + i] = o;
-        dnew[(size_t)v * n + i] = w;
-        atomicAdd(&s_cnt[v], 1);
-      }
-    }
-  }
-  __syncthreads();
-  for (int v = threadIdx.x; v < V; v += blockDim.x)
-    if (s_cnt[v]) atomicAdd(&status[V + 4 + v], s_cnt[v]);
-}
-
-// Incremental statistics.  U carries per-view sizes.
-struct StatsUpd {
-  int V, D, KC, n;
-  int Kold[MVC_MAXV], Knew[MVC_MAXV], M[MVC_MAXV];
-};
-// surviving dishes keep their sums under the compaction map; new dishes 0.
-// Both walk only the live columns: W = max over views of K (new / old).
-extern "C" __global__ void mvc_par_stats_zero_kernel(StatsUpd U, int W, double *S1T, double *S2) {
-  const size_t per = (size_t)(U.D + 1) * W;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < per * U.V; e += (size_t)gridDim.x * blockDim.x) {
-    const int v = (int)(e / per);
-    const size_t r = e - (size_t)v * per;
-    const int dd = (int)(r / W), j = (int)(r % W);
-    if (j >= U.Knew[v]) continue;
-    if (dd < U.D) S1T[((size_t)v * U.D + dd) * U.KC + j] = 0.0;
-    else S2[(size_t)v * U.KC + j] = 0.0;
-  }
-}
-extern "C" __global__ void mvc_par_stats_scatter_kernel(StatsUpd U, int W, const int32_t *jmap, const double *S1T,
-                                                        const double *S2, double *S1T_out, double *S2_out) {
-  const size_t per = (size_t)(U.D + 1) * W;
-  for (size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x; e < per * U.V; e += (size_t)gridDim.x * blockDim.x) {
-    const int v = (int)(e / per);
-    const size_t r = e - (size_t)v * per;
-    const int dd = (int)(r / W), j = (int)(r % W);
-    if (j >= U.Kold[v]) continue;
-    const int jn = jmap[(size_t)v * U.KC + j];
-    if (jn < 0) continue;
-    if (dd < U.D) S1T_out[((size_t)v * U.D + dd) * U.KC + jn] = S1T[((size_t)v * U.D + dd) * U.KC + j];
-    else S2_out[(size_t)v * U.KC + jn] = S2[(size_t)v * U.KC + j];
-  }
-}
-// one block per (incremental view, dish): walk the view's moved customers in
-// ascending order, subtract y from the old dish / add it to the new one
-// (thread dd < D owns S1[.][dd], thread dd == D owns S2)
-extern "C" __global__ __launch_bounds__(256) void mvc_par_stats_apply_kernel(
-    StatsUpd U, const int32_t *vlist, const double *y, const double *Y2, const int32_t *mlist,
-    const int32_t *dold, const int32_t *dnew, double *S1T, double *S2) {
-  __shared__ int s_i[256], s_o[256], s_w[256];
-  const int v = vlist[blockIdx.y];
-  const int j = blockIdx.x;
-  if (j >= U.Knew[v]) return;
-  const int tid = threadIdx.x;
-  const int D = U.D, n = U.n, KC = U.KC, M = U.M[v];
-  constexpr int Q = 4;                      // (D + 1) <= 4 * blockDim.x
-  double acc[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int dd = tid + q * 256;
-    acc[q] = dd < D ? S1T[((size_t)v * D + dd) * KC + j] : (dd == D ? S2[(size_t)v * KC + j] : 0.0);
-  }
-  const int32_t *ml = mlist + (size_t)v * n;
-  for (int m0 = 0; m0 < M; m0 += 256) {
-    const int cntm = min(256, M - m0);
-    __syncthreads();
-    if (tid < cntm) {
-      const int i = ml[m0 + tid];
-      s_i[tid] = i;
-      s_o[tid] = dold[(size_t)v * n + i];
-      s_w[tid] = dnew[(size_t)v * n + i];
-    }
-    __syncthreads();
-    for (int e = 0; e < cntm; ++e) {
-      const int o = s_o[e], w = s_w[e];
-      if (o != j && w != j) continue;                 // block-uniform
-      const int i = s_i[e];
-      const double *yr = y + ((size_t)v * n + i) * D;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const int dd = tid + q * 256;
-        if (dd <= D) {
-          const double x = dd < D ? yr[dd] : Y2[(size_t)v * n + i];
-          acc[q] = (o == j) ? acc[q] - x : acc[q] + x;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int dd = tid + q * 256;
-    if (dd < D) S1T[((size_t)v * D + dd) * KC + j] = acc[q];
-    else if (dd == D) S2[(size_t)v * KC + j] = acc[q];
-  }
-}
+#include "mvc_repair.h"
 
 // Y2[v][i] = sum_d y^2, fma chain in d order (oracle ParallelSampler::fma_dot)
 extern "C" __global__ void mvc_par_y2_kernel(int n, int V, int D, const double *y, double *Y2) {
@@ -2275,11 +1687,12 @@ __device__ double block_tree64(int64_t n, F leaf) {
 struct MHArgs {
   ParState P;
   int32_t *status;        // [V+3]: T, K[V], err, NB  -> we add T_ne at status[V+3]
-  int32_t *Koff;          // [V+1] (output)
+  int32_t *Koff;          // [V+1] (prefix of Kact, maintained by the host / the repair's compaction)
   double *L2pt, *cnew;    // [V] (output)
   uint64_t seed;
   uint32_t chain, sweep;
   int do_mh;
+  const Repair *gate;     // non-null: run only once the sweep's repair is done
 };
 
 }  // namespace
@@ -2299,6 +1712,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
 #else
 #define HYP_MARK(name)
 #endif
+  if (A.gate && !A.gate->done) return;
   const int T = A.status[0];
   // ---- Q = ||S1||^2 per live dish (fma chain in d order), all views at once;
   //      the strided S1 loads are issued 16 ahead of the chain ----
@@ -2545,7 +1959,9 @@ namespace {
 constexpr int kParTC = 4096;   // table capacity (two-level tree64)
 constexpr int kParKC = 4095;   // live dishes per view (+1 new element <= 4096)
 constexpr size_t kLpbBudget = (size_t)1 << 28;   // phase-1 lp buffer: 2 GiB of doubles per batch
-constexpr int kCountBlocks = 256;  // count / birth-list kernels (c.flags holds the per-block birth counts)
+constexpr int kSeqWaves = 1024;    // waves of the repair eval grid (SeqArgs.G)
+constexpr int kSeqWmin = 1024;     // repair window after a mover
+constexpr int kSeqWmax = 1 << 16;  // cap of the window doubling over mover-free stretches
 
 template <class Tp>
 Tp *dmalloc(size_t count) {
@@ -2565,16 +1981,11 @@ class ParallelSampler : public Sampler {
     ParState P{};
     double *L2pt = nullptr, *cnew = nullptr;
     int32_t *Koff = nullptr, *status = nullptr;
-    int32_t *choice = nullptr, *flags = nullptr, *brank = nullptr, *blist = nullptr, *nbirth = nullptr;
-    int32_t *cnt = nullptr, *pos_new = nullptr, *tmp_dish = nullptr, *tmp_nt = nullptr;
-    int32_t *p2meta = nullptr, *p2_c = nullptr, *p2_tup = nullptr, *n2 = nullptr, *l2 = nullptr, *btab = nullptr;
-    double *S1_2T = nullptr, *lp2 = nullptr;
-    int32_t *lcnt = nullptr, *jmap = nullptr;
+    int32_t *choice = nullptr;
+    int32_t *pos_new = nullptr, *jmap = nullptr;   // compaction maps [TC], [V*KC]
+    Repair *R = nullptr;                           // repair state (mvc_repair.h), device
+    int32_t last[4] = {0, 0, 0, 0};                // repair counters of the last sweep (repair_stats)
     double *S1t = nullptr;         // MFMA B-fragment layout of S1 (K_v <= 64)
-    int32_t *dish_old = nullptr;   // [V*TC] table -> dish before the commit
-    int32_t *dold = nullptr, *dnew = nullptr, *mflag = nullptr, *mlist = nullptr;   // [V*n]
-    int32_t *nsel = nullptr, *vlist = nullptr;
-    double *S1T_alt = nullptr, *S2_alt = nullptr;   // ping-pong of P.S1T / P.S2
     // pinned host sources of the async uploads ([V+1] Koff, then [MAXV] view
     // list): pageable sources would make each copy a blocking staged copy that
     // waits for the stream.  The next write to them happens after the next
@@ -2587,15 +1998,15 @@ class ParallelSampler : public Sampler {
     std::vector<void *> owned;
   };
   std::vector<Chain> chains;
-  double *lp_scratch = nullptr;   // births kernel (one wave)
+  double *seq_scr = nullptr;      // repair eval scratch (SeqScratch), kSeqWaves waves
+  int64_t seq_stride = 0;
+  Repair *rs_host = nullptr;      // pinned copy of a chain's Repair after each batch
   double *lpb = nullptr;          // phase-1 lp buffer (lpb_index layout)
   double *vmax = nullptr;         // [V][n] view maxima of the draw (producer -> draw)
   size_t lpb_cap = 0;             // doubles
   size_t lp_cap = 0;               // doubles per wave
   double *part1 = nullptr, *part2 = nullptr;
   size_t part_cap = 0;             // sumK capacity of partials
-  void *cub_tmp = nullptr;
-  size_t cub_bytes = 0;
   int32_t *st_host = nullptr;   // pinned [2V+4]: the per-sweep status readback
   bool force_generic = false;
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
@@ -2617,7 +2028,10 @@ class ParallelSampler : public Sampler {
   ParallelSampler(const mvc_config &cf, const double *const *views) {
     cfg = cf;
     n = cf.n; V = cf.n_views; D = cf.dim;
-    TC = kParTC; KC = kParKC;
+    // initial capacities (mvc_config.table_cap / dish_cap); a birth beyond
+    // them grows every chain (grow_capacity), up to kParTC / kParKC
+    TC = std::min(kParTC, std::max(16, cf.table_cap > 0 ? cf.table_cap : 1024));
+    KC = std::min(kParKC, std::max(15, cf.dish_cap > 0 ? cf.dish_cap : 1023));
     nchunk = (n + 4095) / 4096;
     if (V > MVC_MAXV) throw Error(MVC_ERR_UNSUPPORTED, "at most 64 views");
     {   // the sweep loop waits on the device once per sweep (new T, K): spin
@@ -2660,15 +2074,9 @@ class ParallelSampler : public Sampler {
       hipLaunchKernelGGL(mvc_par_ytile_kernel, dim3(4096), dim3(256), 0, stream, n, V, D, SP, (const double *)y, yt);
       MVC_HIP(hipGetLastError());
     }
-    // hipcub temp storage (scan + select over n)
-    size_t b1 = 0, b2 = 0;
-    MVC_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (int32_t *)nullptr, (int32_t *)nullptr, n, stream));
-    hipcub::CountingInputIterator<int32_t> it(0);
-    MVC_HIP(hipcub::DeviceSelect::Flagged(nullptr, b2, it, (int32_t *)nullptr, (int32_t *)nullptr,
-                                          (int32_t *)nullptr, n, stream));
-    cub_bytes = std::max(b1, b2);
-    MVC_HIP(hipMalloc(&cub_tmp, cub_bytes));
     MVC_HIP(hipHostMalloc((void **)&st_host, sizeof(int32_t) * (2 * V + 4), hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&rs_host, sizeof(Repair), hipHostMallocDefault));
+    alloc_seq_scratch();
     std::fill(st_host, st_host + 2 * V + 4, 0);
     const char *fg = getenv("MVC_FORCE_GENERIC");
     force_generic = fg && fg[0] == '1';
@@ -2793,17 +2201,18 @@ class ParallelSampler : public Sampler {
       for (void *p : c.owned) hipFree(p);
       if (c.hpin) hipHostFree(c.hpin);
     }
-    for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)lp_scratch, (void *)lpb, (void *)part1, (void *)part2,
-                    cub_tmp, (void *)fz_discard, (void *)vmax})
+    for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2,
+                    (void *)fz_discard, (void *)vmax})
       if (p) hipFree(p);
     if (st_host) hipHostFree(st_host);
+    if (rs_host) hipHostFree(rs_host);
     if (stream) hipStreamDestroy(stream);
   }
 
-  void alloc_chain(Chain &c) {
+  // capacity-sized arrays of a chain (TC tables, KC dishes per view)
+  void alloc_cap(Chain &c) {
     ParState &P = c.P;
-    P.n = n; P.V = V; P.D = D; P.TC = TC; P.KC = KC;
-    P.z = own<int32_t>(c, n);
+    P.TC = TC; P.KC = KC;
     P.n_t = own<int32_t>(c, TC);
     P.dish = own<int32_t>(c, (size_t)V * TC);
     P.d_id = own<int32_t>(c, (size_t)V * KC);
@@ -2815,6 +2224,15 @@ class ParallelSampler : public Sampler {
     P.c0 = own<double>(c, (size_t)V * KC);
     P.cb = own<double>(c, (size_t)V * KC);
     P.lmass = own<double>(c, TC);
+    c.pos_new = own<int32_t>(c, TC);
+    c.jmap = own<int32_t>(c, (size_t)V * KC);
+  }
+
+  void alloc_chain(Chain &c) {
+    ParState &P = c.P;
+    P.n = n; P.V = V; P.D = D;
+    P.z = own<int32_t>(c, n);
+    alloc_cap(c);
     P.hyper = own<double>(c, 3 * V + 2);
     P.Kact = own<int32_t>(c, V);
     P.next_id = own<int32_t>(c, V);
@@ -2824,34 +2242,8 @@ class ParallelSampler : public Sampler {
     c.Koff = own<int32_t>(c, V + 1);
     c.status = own<int32_t>(c, 2 * V + 4);
     c.choice = own<int32_t>(c, n);
-    c.flags = own<int32_t>(c, n);
-    c.brank = own<int32_t>(c, n);
-    c.blist = own<int32_t>(c, n);
-    c.nbirth = own<int32_t>(c, 1);
-    c.p2meta = own<int32_t>(c, V + 2);
-    c.p2_c = own<int32_t>(c, TC);
-    c.p2_tup = own<int32_t>(c, (size_t)TC * V);
-    c.n2 = own<int32_t>(c, (size_t)V * KC);
-    c.l2 = own<int32_t>(c, (size_t)V * KC);
-    c.S1_2T = own<double>(c, (size_t)V * D * KC);
-    c.lp2 = own<double>(c, (size_t)V * KC);
-    c.btab = own<int32_t>(c, n);
-    c.cnt = own<int32_t>(c, TC);
-    c.pos_new = own<int32_t>(c, TC);
-    c.tmp_dish = own<int32_t>(c, (size_t)V * TC);
-    c.tmp_nt = own<int32_t>(c, TC);
-    c.lcnt = own<int32_t>(c, (size_t)V * KC);
-    c.jmap = own<int32_t>(c, (size_t)V * KC);
-    c.dish_old = own<int32_t>(c, (size_t)V * TC);
-    c.dold = own<int32_t>(c, (size_t)V * n);
-    c.dnew = own<int32_t>(c, (size_t)V * n);
-    c.mflag = own<int32_t>(c, (size_t)V * n);
-    c.mlist = own<int32_t>(c, (size_t)V * n);
-    c.nsel = own<int32_t>(c, 1);
-    c.vlist = own<int32_t>(c, MVC_MAXV);
+    c.R = own<Repair>(c, 1);
     MVC_HIP(hipHostMalloc((void **)&c.hpin, sizeof(int32_t) * (V + 1 + MVC_MAXV), hipHostMallocDefault));
-    c.S1T_alt = own<double>(c, (size_t)V * D * KC);
-    c.S2_alt = own<double>(c, (size_t)V * KC);
   }
 
   void init_chain(Chain &c, uint32_t gid, const double *yh) {
@@ -2895,8 +2287,9 @@ class ParallelSampler : public Sampler {
     up(P.Kact, c.K.data(), sizeof(int32_t) * V);
     up(P.next_id, next.data(), sizeof(int32_t) * V);
     up(P.hyper, hyp.data(), sizeof(double) * hyp.size());
-    std::vector<int32_t> st(2 * V + 4, 0);
+    std::vector<int32_t> st(2 * V + 4, 0);   // status: T, K[V], -, -, T_ne (set by the hyper kernel)
     st[0] = 4;
+    for (int v = 0; v < V; ++v) st[1 + v] = c.K[v];
     up(c.status, st.data(), sizeof(int32_t) * st.size());
     MVC_HIP(hipStreamSynchronize(stream));
     rebuild_stats(c);
@@ -2963,58 +2356,7 @@ class ParallelSampler : public Sampler {
     timers.end("stats", ev);
   }
 
-  // After a commit: per view, a full rebuild if more than
-  // n/8 customers changed dish, else the surviving dishes' sums carried over
-  // through the compaction map plus the moves in ascending customer order.
-  void update_stats(Chain &c, const std::vector<int32_t> &Kold, const int32_t *moved) {
-    upload_koff(c);
-    hipEvent_t ev = nullptr;
-    timers.begin("stats", &ev);
-    StatsUpd U{};
-    U.V = V; U.D = D; U.KC = KC; U.n = n;
-    uint64_t full = 0;
-    std::vector<int32_t> inc;
-    for (int v = 0; v < V; ++v) {
-      U.Kold[v] = Kold[v];
-      U.Knew[v] = c.K[v];
-      U.M[v] = moved[v];
-      if ((int64_t)8 * moved[v] > (int64_t)n) full |= 1ull << v;
-      else inc.push_back(v);
-    }
-    // carry the sums over to the new dish numbering (all views; rebuilt views overwrite)
-    int Wn = 1, Wo = 1;
-    for (int v = 0; v < V; ++v) { Wn = std::max(Wn, c.K[v]); Wo = std::max(Wo, Kold[v]); }
-    const unsigned gz = (unsigned)std::min<size_t>(4096, ((size_t)V * (D + 1) * Wn + 255) / 256);
-    const unsigned gs = (unsigned)std::min<size_t>(4096, ((size_t)V * (D + 1) * Wo + 255) / 256);
-    hipLaunchKernelGGL(mvc_par_stats_zero_kernel, dim3(gz), dim3(256), 0, stream, U, Wn, c.S1T_alt, c.S2_alt);
-    hipLaunchKernelGGL(mvc_par_stats_scatter_kernel, dim3(gs), dim3(256), 0, stream, U, Wo, (const int32_t *)c.jmap,
-                       (const double *)c.P.S1T, (const double *)c.P.S2, c.S1T_alt, c.S2_alt);
-    MVC_HIP(hipGetLastError());
-    std::swap(c.P.S1T, c.S1T_alt);
-    std::swap(c.P.S2, c.S2_alt);
-    if (!inc.empty()) {
-      int Kmax = 1;
-      for (int v : inc) {
-        Kmax = std::max(Kmax, c.K[v]);
-        if (moved[v] == 0) continue;
-        size_t bytes = cub_bytes;
-        hipcub::CountingInputIterator<int32_t> it(0);
-        MVC_HIP(hipcub::DeviceSelect::Flagged(cub_tmp, bytes, it, c.mflag + (size_t)v * n, c.mlist + (size_t)v * n,
-                                              c.nsel, n, stream));
-      }
-      std::copy(inc.begin(), inc.end(), c.hpin + V + 1);
-      MVC_HIP(hipMemcpyAsync(c.vlist, c.hpin + V + 1, sizeof(int32_t) * inc.size(), hipMemcpyHostToDevice, stream));
-      hipLaunchKernelGGL(mvc_par_stats_apply_kernel, dim3(Kmax, (unsigned)inc.size()), dim3(256), 0, stream, U,
-                         (const int32_t *)c.vlist, (const double *)y, (const double *)Y2, (const int32_t *)c.mlist,
-                         (const int32_t *)c.dold, (const int32_t *)c.dnew, c.P.S1T, c.P.S2);
-      MVC_HIP(hipGetLastError());
-    }
-    if (full) rebuild_views(c, full);
-    tile_s1(c);
-    timers.end("stats", ev);
-  }
-
-  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix) {
+  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr) {
     MHArgs A;
     A.P = c.P;
     A.status = c.status;
@@ -3025,6 +2367,7 @@ class ParallelSampler : public Sampler {
     A.chain = c.gid;
     A.sweep = sweep_ix;
     A.do_mh = do_mh;
+    A.gate = gate;
     hipEvent_t ev = nullptr;
     timers.begin("hyper", &ev);
     hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(kHypThreads), 0, stream, A);
@@ -3032,11 +2375,32 @@ class ParallelSampler : public Sampler {
     timers.end("hyper", ev);
   }
 
-  void ensure_lp(size_t per_wave) {
-    if (per_wave <= lp_cap) return;
-    if (lp_scratch) hipFree(lp_scratch);
-    lp_cap = per_wave + 64;
-    lp_scratch = dmalloc<double>(lp_cap);   // the births kernel's one wavefront
+  void alloc_seq_scratch() {
+    if (seq_scr) hipFree(seq_scr);
+    seq_stride = seq_scratch_stride(V, TC, KC);
+    seq_scr = dmalloc<double>((size_t)kSeqWaves * seq_stride);
+  }
+
+  SeqArgs make_seq(Chain &c, uint32_t s) {
+    SeqArgs A;
+    A.P = c.P;
+    A.y = y;
+    A.Y2 = Y2;
+    A.L2pt = c.L2pt;
+    A.cnew = c.cnew;
+    A.choice = c.choice;
+    A.status = c.status;
+    A.Koff = c.Koff;
+    A.R = c.R;
+    A.scr = seq_scr;
+    A.scr_stride = seq_stride;
+    A.G = kSeqWaves;
+    A.Wmin = kSeqWmin;
+    A.Wmax = kSeqWmax;
+    A.seed = cfg.seed;
+    A.chain = c.gid;
+    A.sweep = s;
+    return A;
   }
 
   Sweep make_sweep(Chain &c, uint32_t s) {
@@ -3047,25 +2411,14 @@ class ParallelSampler : public Sampler {
     A.L2pt = c.L2pt;
     A.cnew = c.cnew;
     A.Koff = c.Koff;
-    A.scratch = lp_scratch;
     A.choice = c.choice;
-    A.blist = c.blist;
-    A.p2meta = c.p2meta;
-    A.p2_c = c.p2_c;
-    A.p2_tup = c.p2_tup;
-    A.n2 = c.n2;
-    A.l2 = c.l2;
-    A.S1_2T = c.S1_2T;
-    A.lp2 = c.lp2;
-    A.btab = c.btab;
-    A.nbirth = c.nbirth;
     A.status = c.status;
     A.yt = yt;
     A.S1t = c.S1t;
     A.SP = SP;
     A.vmax = vmax;
     A.T = c.T;
-    A.sumK = (int32_t)lp_cap;
+    A.sumK = sumK(c);
     A.seed = cfg.seed;
     A.chain = c.gid;
     A.sweep = s;
@@ -3146,8 +2499,10 @@ class ParallelSampler : public Sampler {
   }
 
   void sweep_chain(Chain &c, uint32_t s) {
-    ensure_lp((size_t)sumK(c));   // Koff is current: uploaded by the previous stats update
     Sweep A = make_sweep(c, s);
+    const SeqArgs Q0 = make_seq(c, s);
+    hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
+    MVC_HIP(hipGetLastError());
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
     // phase 1 in customer batches: lp producer (MFMA or generic), then draw
     int Kmax = 0, Kmin = 1 << 30;
@@ -3164,8 +2519,9 @@ class ParallelSampler : public Sampler {
     const size_t need = (nbatch_sz / 64) * per64;
     const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && sk <= MVC_Z_VMAX * 64 &&
                           zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
-    if (!use_zreg && zdraw_shared_bytes(V, c.T, sk) > 160 * 1024)
-      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: V x tables too large for the draw kernel's LDS tables");
+    // phase A on the two-kernel path needs the draw's LDS tables; beyond them
+    // the repair's eval kernel evaluates the sweep from customer 0 instead
+    const bool phaseA = use_zreg || zdraw_shared_bytes(V, c.T, sk) <= 160 * 1024;
     // fused phase 1 (lp never leaves registers): T <= 64, K_v <= 64, every
     // view's S1 B-fragments in LDS at once, fully unrolled k-step pairs
     size_t s1t_d = 0;
@@ -3184,14 +2540,14 @@ class ParallelSampler : public Sampler {
     }
     const bool use_fused = !no_fused && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                            (spp == 4 || spp == 8 || spp == 16) && fz_lds <= 160 * 1024;
-    if (!use_fused && need > lpb_cap) {   // the lp buffer only exists for the two-kernel path
+    if (phaseA && !use_fused && need > lpb_cap) {   // the lp buffer only exists for the two-kernel path
       if (lpb) hipFree(lpb);
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
     }
     bool zpath_lpall = false;
     timers.begin("zresample", &e0);
-    if (use_fused) {
+    if (phaseA && use_fused) {
       const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / fz_lds));
       const int ntile = (n + 15) / 16;
       const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + fz_waves - 1) / fz_waves));
@@ -3203,7 +2559,7 @@ class ParallelSampler : public Sampler {
       }
       MVC_HIP(hipGetLastError());
     }
-    for (size_t b0 = 0; !use_fused && b0 < (size_t)n; b0 += nbatch_sz) {
+    for (size_t b0 = 0; phaseA && !use_fused && b0 < (size_t)n; b0 += nbatch_sz) {
       const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
       hipEvent_t el = nullptr, ed = nullptr;
       timers.begin("lp", &el);
@@ -3254,43 +2610,120 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
-    zpath = (use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0);
-    timers.begin("commit", &e1);
-    MVC_HIP(hipMemsetAsync(c.cnt, 0, sizeof(int32_t) * TC, stream));
-    hipLaunchKernelGGL(mvc_par_count_kernel, dim3(kCountBlocks), dim3(256), 0, stream, n, c.T,
-                       (const int32_t *)c.choice, c.cnt, c.flags);
+    zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0)) : 32;
+    repair(c, s, phaseA);
+  }
+
+  // Phase A's choices are exact up to the first customer that does not stay;
+  // from there the repair rounds commit movers in customer order
+  // (mvc_repair.h), then compaction and the MH.  One host
+  // synchronisation per batch of rounds; at steady state a single batch of
+  // one round.  A birth beyond the capacity grows every chain and resumes.
+  void repair(Chain &c, uint32_t s, bool phaseA) {
+    hipEvent_t e1 = nullptr;
+    timers.begin("repair", &e1);
+    SeqArgs Q = make_seq(c, s);
+    const dim3 eg(kSeqWaves / 4), eb(256);
+    if (phaseA)
+      hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
+                         stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
+    else
+      hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
     MVC_HIP(hipGetLastError());
-    hipLaunchKernelGGL(mvc_par_blist_kernel, dim3(kCountBlocks), dim3(256), 0, stream, n, (const int32_t *)c.choice,
-                       (const int32_t *)c.flags, c.blist, c.brank, c.nbirth);
-    MVC_HIP(hipGetLastError());
-    timers.end("commit", e1);
-    hipEvent_t eb = nullptr;
-    timers.begin("births", &eb);
-    hipLaunchKernelGGL(mvc_par_births_kernel, dim3(1), dim3(64), 0, stream, A);
-    MVC_HIP(hipGetLastError());
-    timers.end("births", eb);
-    timers.begin("commit", &e1);
-    hipLaunchKernelGGL(mvc_par_commit_kernel, dim3(1), dim3(256), 0, stream, c.P, c.T, (const int32_t *)c.cnt,
-                       (const int32_t *)c.p2meta, (const int32_t *)c.p2_c, (const int32_t *)c.p2_tup, c.pos_new,
-                       c.tmp_dish, c.tmp_nt, c.lcnt, c.jmap, c.status, c.dish_old);
-    MVC_HIP(hipGetLastError());
-    hipLaunchKernelGGL(mvc_par_relabel_kernel, dim3(std::min(4096, (n + 255) / 256)), dim3(256), 0, stream, n, V,
-                       TC, KC, (const int32_t *)c.choice, (const int32_t *)c.pos_new, (const int32_t *)c.brank,
-                       (const int32_t *)c.btab, c.status, c.P.z, (const int32_t *)c.dish_old,
-                       (const int32_t *)c.jmap, (const int32_t *)c.P.dish, c.dold, c.dnew, c.mflag);
-    MVC_HIP(hipGetLastError());
-    timers.end("commit", e1);
-    // the one host synchronisation of a sweep: new T and dish counts
-    MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
-    MVC_HIP(hipStreamSynchronize(stream));
-    if (st_host[V + 1] != 0)
-      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: table (4096) or dish (4095 per view) capacity exceeded");
-    const std::vector<int32_t> Kold = c.K;
-    c.T = st_host[0];
-    for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
-    update_stats(c, Kold, st_host + V + 4);
+    int rounds = 1;
+    for (;;) {
+      for (int r = 0; r < rounds; ++r) {
+        hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
+        hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
+      }
+      MVC_HIP(hipGetLastError());
+      MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
+      MVC_HIP(hipStreamSynchronize(stream));
+      if (rs_host->overflow) {
+        grow_capacity(rs_host->overflow);
+        Q = make_seq(c, s);
+        continue;
+      }
+      if (rs_host->done) break;
+      rounds = std::min(rounds * 4, 1024);
+    }
+    const bool moved = rs_host->moves > 0;
+    if (moved) {
+      hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, Q, c.pos_new, c.jmap);
+      hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
+                         stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
+      MVC_HIP(hipGetLastError());
+    }
+    timers.end("repair", e1);
+    c.last[0] = rs_host->moves;
+    c.last[1] = rs_host->births;
+    c.last[2] = rs_host->rounds;
+    c.last[3] = rs_host->newdish;
     launch_hyper(c, 1, s);
-    (void)e2;
+    if (moved) {   // new T and dish counts for the next sweep's launch shapes
+      MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
+      MVC_HIP(hipStreamSynchronize(stream));
+      c.T = st_host[0];
+      for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
+      tile_s1(c);   // S1 changed: the next phase A's MFMA B-fragments
+    }
+  }
+
+  // Double the table (flags & 1) and/or dish (flags & 2) capacity of every
+  // chain, keeping the contents (oracle: unbounded, multiview_utils.cpp:
+  // 209-216, 251-258).  The repair step that overflowed changed nothing and
+  // is redone.
+  void grow_capacity(int flags) {
+    const int TC2 = (flags & 1) ? std::min(kParTC, 2 * TC) : TC;
+    const int KC2 = (flags & 2) ? std::min(kParKC, 2 * KC + 1) : KC;
+    if (TC2 == TC && KC2 == KC)
+      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: more than 4096 tables or 4095 dishes per view");
+    flush_saves();
+    for (SaveSlot &q : saves) {   // the ring slots are capacity-sized
+      for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp})
+        if (p) hipFree(p);
+      for (void *p : {(void *)q.hz, (void *)q.hdish, (void *)q.hdid, (void *)q.hhyp})
+        if (p) hipHostFree(p);
+      if (q.snap) hipEventDestroy(q.snap);
+      if (q.done) hipEventDestroy(q.done);
+      q = SaveSlot();
+    }
+    const int TC1 = TC, KC1 = KC;
+    TC = TC2;
+    KC = KC2;
+    for (Chain &c : chains) {
+      const ParState old = c.P;
+      std::vector<void *> old_owned;
+      std::swap(old_owned, c.owned);
+      const int32_t *old_pos = c.pos_new, *old_jmap = c.jmap;
+      (void)old_pos; (void)old_jmap;
+      alloc_cap(c);
+      ParState &P = c.P;
+      auto cp2 = [&](void *dst, size_t dpitch, const void *src, size_t spitch, size_t width, size_t rows) {
+        MVC_HIP(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, rows, hipMemcpyDeviceToDevice, stream));
+      };
+      cp2(P.n_t, 4 * TC2, old.n_t, 4 * TC1, 4 * TC1, 1);
+      cp2(P.dish, 4 * TC2, old.dish, 4 * TC1, 4 * TC1, V);
+      cp2(P.lmass, 8 * TC2, old.lmass, 8 * TC1, 8 * TC1, 1);
+      cp2(P.d_id, 4 * KC2, old.d_id, 4 * KC1, 4 * KC1, V);
+      cp2(P.d_n, 4 * KC2, old.d_n, 4 * KC1, 4 * KC1, V);
+      cp2(P.d_l, 4 * KC2, old.d_l, 4 * KC1, 4 * KC1, V);
+      cp2(P.S1T, 8 * KC2, old.S1T, 8 * KC1, 8 * KC1, (size_t)V * D);
+      cp2(P.S2, 8 * KC2, old.S2, 8 * KC1, 8 * KC1, V);
+      cp2(P.Q, 8 * KC2, old.Q, 8 * KC1, 8 * KC1, V);
+      cp2(P.c0, 8 * KC2, old.c0, 8 * KC1, 8 * KC1, V);
+      cp2(P.cb, 8 * KC2, old.cb, 8 * KC1, 8 * KC1, V);
+      MVC_HIP(hipMemsetAsync(&c.R->overflow, 0, sizeof(int32_t), stream));
+      MVC_HIP(hipStreamSynchronize(stream));
+      // everything not capacity-sized moves over; the old capacity arrays go
+      const std::vector<void *> cap_old = {old.n_t, old.dish, old.lmass, old.d_id, old.d_n, old.d_l, old.S1T,
+                                           old.S2, old.Q, old.c0, old.cb, (void *)old_pos, (void *)old_jmap};
+      for (void *p : old_owned) {
+        if (std::find(cap_old.begin(), cap_old.end(), p) != cap_old.end()) hipFree(p);
+        else c.owned.push_back(p);
+      }
+    }
+    alloc_seq_scratch();
   }
 
   void sweep(int n_sweeps) override {
@@ -3304,6 +2737,12 @@ class ParallelSampler : public Sampler {
   }
 
   void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
+
+  bool repair_stats(int chain, int32_t *out) override {
+    if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    for (int k = 0; k < 4; ++k) out[k] = chains[chain].last[k];
+    return true;
+  }
 
   const int32_t *device_labels(int chain) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
@@ -3356,7 +2795,12 @@ class ParallelSampler : public Sampler {
   void set_state(int chain, const int32_t *table_of, int32_t T, const int32_t *dish_of, const double *hyper) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
     const UserState U = check_user_state(n, V, table_of, T, dish_of);
-    if (T > TC) throw Error(MVC_ERR_UNSUPPORTED, "set_state: more tables than the parallel-mode capacity (4096)");
+    int Kmax = 0;
+    for (int v = 0; v < V; ++v) Kmax = std::max(Kmax, (int)U.ids[v].size());
+    while (T > TC || Kmax > KC) {
+      MVC_HIP(hipStreamSynchronize(stream));
+      grow_capacity((T > TC ? 1 : 0) | (Kmax > KC ? 2 : 0));
+    }
     Chain &c = chains[chain];
     std::vector<int32_t> dish((size_t)V * TC, 0), did((size_t)V * KC, 0), dn((size_t)V * KC, 0), dl((size_t)V * KC, 0);
     c.K.assign(V, 0);
@@ -3384,8 +2828,9 @@ class ParallelSampler : public Sampler {
     up(P.Kact, c.K.data(), sizeof(int32_t) * V);
     up(P.next_id, U.next_id.data(), sizeof(int32_t) * V);
     up(P.hyper, hyper, sizeof(double) * (3 * V + 2));
-    std::vector<int32_t> st(V + 4, 0);
+    std::vector<int32_t> st(2 * V + 4, 0);
     st[0] = T;
+    for (int v = 0; v < V; ++v) st[1 + v] = c.K[v];
     up(c.status, st.data(), sizeof(int32_t) * st.size());
     MVC_HIP(hipStreamSynchronize(stream));
     c.T = T;

@@ -241,6 +241,16 @@ class Sampler:
         -1 exact schedule / no sweep yet."""
         return int(self._lib.mvc_sampler_zpath(self._h))
 
+    def repair_stats(self, chain=0):
+        """Counters of the chain's last parallel sweep: dict
+        moves (customers that changed table), births, rounds (in-order repair
+        steps), newdish (dishes opened)."""
+        out = np.zeros(4, dtype=np.int32)
+        st = self._lib.mvc_sampler_repair_stats(self._h, chain, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if st != L.MVC_OK:
+            raise L.MvcError(st, "repair_stats failed")
+        return dict(zip(("moves", "births", "rounds", "newdish"), (int(x) for x in out)))
+
     def set_timing(self, timing):
         """Switch HIP-event timing: False, True (every phase) or "coarse"."""
         st = self._lib.mvc_sampler_set_timing(self._h, _timing_flags(timing))

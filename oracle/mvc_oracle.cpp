@@ -14,16 +14,23 @@
 // Philox4x32-10 known-answer vectors, (b) accuracy checks of its math against
 // glibc / scipy, and (c) invariant checks in tests/.
 //
-// Two samplers:
+// Three samplers:
 //   * ExactSampler   — the reference schedule (multiview_gibbs.cpp:134-212),
 //     D = 1, sequential RNG stream.  Template parameter selects the math:
 //     LibmMath (std::exp/std::log exactly like the reference) or PortableMath
 //     (include/mvc_pmath.h, bit-identical to the GPU).
-//   * ParallelSampler — the parallel-z ("mode P") schedule specified in
-//     every customer is resampled against the state frozen at
-//     sweep start (sequential per-customer reductions), births resolved in
-//     index order (tree64 reductions), deterministic stats rebuild, EPPF via
-//     lgamma.
+//   * SeqSampler (mode 1, "parallel" in the C ABI) — the SAME sequential
+//     schedule (customer i+1 sees customer i's move) with the GPU-shaped
+//     per-customer conditional of DESIGN.md §4.2-4.3, any D, counter-
+//     addressed Philox draws.  libmvc_hip.so executes this chain with a
+//     data-parallel speculative pass plus an in-order repair (DESIGN.md
+//     §4.8); the GPU is checked against it bit for bit.
+//   * ParallelSampler::run (mode 3, JACOBI) — round 1's schedule: every
+//     customer resampled against the state frozen at sweep start.  It does
+//     not leave the posterior invariant (tests/test_posterior.py shows the
+//     bias) and is kept only as that documented negative result; its
+//     per-customer conditional (resample_customer, eval_view_seq) is the one
+//     SeqSampler evaluates.
 //
 // Build: oracle/Makefile  (g++ -O2 -ffp-contract=off, no fast-math).
 #include <stdint.h>
@@ -88,6 +95,7 @@ struct Result {
   std::vector<double> alpha_g, sigma_g;    // S
   std::vector<int> trace_T;                // per sweep: T after the sweep
   std::vector<uint64_t> trace_draws;       // per sweep: sequential draws used so far
+  std::vector<int64_t> trace_moves, trace_births, trace_newdish;  // SeqSampler, per sweep
   // final sufficient statistics (parallel sampler): per view, live dishes in
   // ascending raw id; S1 [K][D], S2 [K], n_vk [K]
   std::vector<std::vector<double>> fS1, fS2;
@@ -1053,7 +1061,11 @@ struct ParallelSampler {
       }
     }
     double S = pw16(col);
-    const int Kact = K - ((l0p == 0) ? 1 : 0);
+    // K_act: dishes with l' > 0 (mid-sweep the sequential schedule keeps
+    // dishes that died this sweep in the list with l = 0)
+    int Kact = 0;
+    for (int j = 0; j < K; ++j)
+      if (((j == j0) ? l0p : lk[v][j]) > 0) ++Kact;
     double wn = alpha[v] + (double)Kact * sigma[v];
     if (wn < 0.0) wn = 0.0;
     S = S + wn * mvc_exp(lfn - m);
@@ -1477,6 +1489,170 @@ struct ParallelSampler {
   }
 };
 
+// ===========================================================================
+// SeqSampler: the sequential schedule of the reference (multiview_gibbs.cpp:
+// 157-200: customer i+1 sees customer i's move) with the GPU-shaped
+// per-customer conditional of DESIGN.md §4.2-4.3.  This is the specification
+// of the parallel-execution ("speculative") schedule that libmvc_hip.so runs:
+// the GPU evaluates every customer against the sweep-start state in one
+// data-parallel pass and then repairs, in customer order, exactly the
+// decisions that earlier moves could have changed.  The
+// Markov kernel is the reference's systematic-scan collapsed Gibbs sweep.
+//
+// Differences from the reference that do not change the kernel:
+//  * a customer's own removal is virtual (self-dish coefficients, §4.2):
+//    staying is a bitwise no-op on the sums; stats change only on a move;
+//  * table positions are stable within a sweep (a table that empties keeps
+//    its slot with weight 0; multiview_utils.cpp:175-190 swaps the last table
+//    in instead), a birth appends a position, dead tables are compacted
+//    (order kept) after the sweep — the inverse CDF scans a fixed order;
+//  * dead dish slots (l = 0) are dropped at the end of the sweep (the
+//    reference keeps them forever, multiview_utils.cpp:251-258; they carry
+//    no weight), raw ids keep growing;
+//  * uniforms are counter-addressed: table draw Philox(i, sweep, chain,
+//    TAG_Z), dish draw of a birth Philox(i, sweep, chain, TAG_DISH+1+v).
+// ===========================================================================
+struct SeqSampler : ParallelSampler {
+  int64_t moves = 0, births = 0, newdish = 0;
+
+  void refresh_dish(int v, int j) {
+    const double *s = &S1[v][(size_t)j * D];
+    Qd[v][j] = fma_dot(s, s, D);
+    cf[v][j] = coef(nk[v][j], Qd[v][j], tau[v], L2pt[v]);
+  }
+
+  // new dish slot in view v (raw id next_id[v]); returns its list index
+  int open_dish(int v) {
+    ids[v].push_back(next_id[v]++);
+    nk[v].push_back(0);
+    lk[v].push_back(0);
+    S1[v].resize(S1[v].size() + D, 0.0);
+    S2[v].push_back(0.0);
+    Qd[v].push_back(0.0);
+    cf[v].push_back(coef(0, 0.0, tau[v], L2pt[v]));
+    ++newdish;
+    return (int)ids[v].size() - 1;
+  }
+
+  // dish of a birth in view v: tree64 over the leaves w_j exp(lp_j - m) of
+  // the included dishes (ascending list index) and the new dish (last);
+  // r = u S; returns a list index, ids[v].size() = a new dish.
+  int draw_dish(int i, int v, bool alive, int j0, int s) const {
+    ViewEval E;
+    eval_view(i, v, alive, j0, E);
+    const int K = (int)ids[v].size();
+    if (!(E.S > 0.0)) return K;
+    Tree64 td;
+    td.build(E.leaves);
+    const double rv = mvc_uniform(seed, (uint32_t)i, (uint32_t)s, chain, MVC_TAG_DISH + 1u + (uint32_t)v) * E.S;
+    return (int)td.select(rv);
+  }
+
+  void move(int i, int p0, int p1) {
+    n_t[p0]--;
+    if (n_t[p0] == 0) {
+      T_ne--;
+      for (int v = 0; v < V; ++v) { lk[v][dish[v][p0]]--; Ltot[v]--; }
+    }
+    if (n_t[p1] == 0) {
+      T_ne++;
+      for (int v = 0; v < V; ++v) { lk[v][dish[v][p1]]++; Ltot[v]++; }
+    }
+    n_t[p1]++;
+    for (int v = 0; v < V; ++v) {
+      const int j0 = dish[v][p0], j1 = dish[v][p1];
+      if (j0 == j1) continue;
+      const double *yi = y + ((size_t)v * n + i) * D;
+      double *a = &S1[v][(size_t)j0 * D];
+      double *b = &S1[v][(size_t)j1 * D];
+      for (int d = 0; d < D; ++d) a[d] = a[d] - yi[d];
+      for (int d = 0; d < D; ++d) b[d] = b[d] + yi[d];
+      S2[v][j0] = S2[v][j0] - Y2[(size_t)v * n + i];
+      S2[v][j1] = S2[v][j1] + Y2[(size_t)v * n + i];
+      nk[v][j0]--;
+      nk[v][j1]++;
+      refresh_dish(v, j0);
+      refresh_dish(v, j1);
+    }
+    z[i] = p1;
+  }
+
+  // drop empty tables (order kept) and dead dishes (l = 0; order kept)
+  void compact() {
+    std::vector<int> pos_new(T, -1);
+    int Tn = 0;
+    for (int p = 0; p < T; ++p)
+      if (n_t[p] > 0) pos_new[p] = Tn++;
+    std::vector<int> nt2(Tn);
+    std::vector<std::vector<int>> dish2(V, std::vector<int>(Tn));
+    for (int p = 0; p < T; ++p)
+      if (pos_new[p] >= 0) {
+        nt2[pos_new[p]] = n_t[p];
+        for (int v = 0; v < V; ++v) dish2[v][pos_new[p]] = dish[v][p];
+      }
+    for (int i = 0; i < n; ++i) z[i] = pos_new[z[i]];
+    for (int v = 0; v < V; ++v) {
+      const int K = (int)ids[v].size();
+      std::vector<int> jmap(K, -1), ids2, nk2, lk2;
+      std::vector<double> s1, s2;
+      for (int j = 0; j < K; ++j) {
+        if (lk[v][j] <= 0) continue;
+        jmap[j] = (int)ids2.size();
+        ids2.push_back(ids[v][j]);
+        nk2.push_back(nk[v][j]);
+        lk2.push_back(lk[v][j]);
+        s1.insert(s1.end(), S1[v].begin() + (size_t)j * D, S1[v].begin() + (size_t)(j + 1) * D);
+        s2.push_back(S2[v][j]);
+      }
+      for (int p = 0; p < Tn; ++p) dish2[v][p] = jmap[dish2[v][p]];
+      ids[v] = ids2; nk[v] = nk2; lk[v] = lk2; S1[v] = s1; S2[v] = s2;
+    }
+    T = Tn;
+    n_t = nt2;
+    dish = dish2;
+  }
+
+  void sweep_once(int s) {
+    sweep_constants();
+    for (int i = 0; i < n; ++i) {
+      const int p0 = z[i];
+      const int c = resample_customer(i, s);
+      if (c == p0) continue;
+      ++moves;
+      if (c >= 0) {
+        move(i, p0, c);
+        continue;
+      }
+      ++births;
+      const bool alive = (n_t[p0] - 1) > 0;
+      std::vector<int> tup(V);
+      for (int v = 0; v < V; ++v) tup[v] = draw_dish(i, v, alive, dish[v][p0], s);
+      for (int v = 0; v < V; ++v)
+        if (tup[v] == (int)ids[v].size()) tup[v] = open_dish(v);
+      const int p1 = T++;
+      n_t.push_back(0);
+      for (int v = 0; v < V; ++v) dish[v].push_back(tup[v]);
+      move(i, p0, p1);
+    }
+    compact();
+  }
+
+  void run(int M, int burn_in, int thin, Result &R) {
+    R.dish_off.push_back(0);
+    for (int s = 0; s < M; ++s) {
+      moves = births = newdish = 0;
+      sweep_once(s);
+      update_hyper(s);
+      R.trace_T.push_back(T);
+      R.trace_draws.push_back(init_rng.draws);
+      R.trace_moves.push_back(moves);
+      R.trace_births.push_back(births);
+      R.trace_newdish.push_back(newdish);
+      if (s >= burn_in && ((s - burn_in) % thin == 0)) save(R);
+    }
+  }
+};
+
 }  // namespace
 
 // ===========================================================================
@@ -1509,6 +1685,14 @@ void *mvo_run(const double *y, int n, int V, int D, int M, int burn_in, int thin
       };
       if (math == 0) { ExactSampler<LibmMath> S; go(S); }
       else { ExactSampler<PortableMath> S; go(S); }
+    } else if (mode == 1) {
+      SeqSampler P;
+      P.n = n; P.V = V; P.D = D; P.y = y;
+      P.seed = seed; P.chain = (uint32_t)chain;
+      P.init_rng = SeqRng{seed, (uint32_t)chain, 0};
+      P.initialize();
+      P.run(M, burn_in, thin, *R);
+      R->fS1 = P.S1; R->fS2 = P.S2; R->fnk = P.nk; R->D = D;
     } else {
       ParallelSampler P;
       P.n = n; P.V = V; P.D = D; P.y = y;
@@ -1546,6 +1730,14 @@ void *mvo_run_from(const double *y, int n, int V, int D, int M, int burn_in, int
       };
       if (math == 0) { ExactSampler<LibmMath> S; go(S); }
       else { ExactSampler<PortableMath> S; go(S); }
+    } else if (mode == 1) {
+      SeqSampler P;
+      P.n = n; P.V = V; P.D = D; P.y = y;
+      P.seed = seed; P.chain = (uint32_t)chain;
+      P.init_rng = SeqRng{seed, (uint32_t)chain, 0};
+      P.load_state(table_of, T, dish_of, hyper);
+      P.run(M, burn_in, thin, *R);
+      R->fS1 = P.S1; R->fS2 = P.S2; R->fnk = P.nk; R->D = D;
     } else {
       ParallelSampler P;
       P.n = n; P.V = V; P.D = D; P.y = y;
@@ -1602,6 +1794,15 @@ void mvo_copy_trace(void *h, int *T, uint64_t *draws) {
   Result *R = (Result *)h;
   memcpy(T, R->trace_T.data(), sizeof(int) * R->trace_T.size());
   memcpy(draws, R->trace_draws.data(), sizeof(uint64_t) * R->trace_draws.size());
+}
+void mvo_copy_trace_moves(void *h, int64_t *moves, int64_t *births, int64_t *newdish) {
+  Result *R = (Result *)h;
+  const size_t m = R->trace_moves.size();
+  for (size_t s = 0; s < R->trace_T.size(); ++s) {
+    moves[s] = s < m ? R->trace_moves[s] : -1;
+    births[s] = s < m ? R->trace_births[s] : -1;
+    newdish[s] = s < m ? R->trace_newdish[s] : -1;
+  }
 }
 void mvo_free(void *h) { delete (Result *)h; }
 

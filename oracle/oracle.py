@@ -16,7 +16,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libmvc_oracle.so")
 _lib = None
 
-EXACT, PARALLEL = 0, 1
+# EXACT: the reference schedule, literal (D = 1).  PARALLEL: the same
+# sequential schedule with the GPU-shaped conditional and counter-addressed
+# Philox draws -- the spec libmvc_hip.so's parallel mode executes (DESIGN.md
+# §4.8).  JACOBI: every customer against the sweep-start state (round 1's
+# schedule; kept only to document that it does NOT sample the reference's
+# posterior, tests/test_posterior.py).
+EXACT, PARALLEL, JACOBI = 0, 1, 3
 LIBM, PORTABLE = 0, 1
 
 
@@ -48,6 +54,8 @@ def lib():
         L.mvo_copy_dish_of.argtypes = [vp, i32, ip]
         L.mvo_copy_hyper.argtypes = [vp, dp, dp, dp, dp, dp]
         L.mvo_copy_trace.argtypes = [vp, ip, ctypes.POINTER(ctypes.c_uint64)]
+        L.mvo_copy_trace_moves.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                                           ctypes.POINTER(ctypes.c_int64)]
         L.mvo_free.argtypes = [vp]
         L.mvo_stats_K.restype = i32
         L.mvo_stats_K.argtypes = [vp, i32]
@@ -122,6 +130,9 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=Non
         td = np.empty(nsw, dtype=np.uint64)
         L.mvo_copy_trace(h, tT.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
                          td.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+        tm, tb, tn = (np.empty(nsw, dtype=np.int64) for _ in range(3))
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.mvo_copy_trace_moves(h, tm.ctypes.data_as(i64p), tb.ctypes.data_as(i64p), tn.ctypes.data_as(i64p))
         return {
             "table_of": table_of,
             "dish_of": dish_of,
@@ -132,6 +143,9 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=Non
             "sigma_global": sg,
             "trace_T": tT,
             "trace_draws": td,
+            "trace_moves": tm,         # PARALLEL mode: customers that changed table, per sweep (else -1)
+            "trace_births": tb,
+            "trace_newdish": tn,
             "stats": stats,            # parallel mode: final S1 [K][D], S2, n per view
         }
     finally:

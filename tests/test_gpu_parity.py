@@ -204,6 +204,95 @@ def test_dropin_output_shape():
     assert cl.shape == (200, 5)
 
 
+def test_parallel_capacity_growth():
+    """Tiny initial capacities (16 tables, 15 dishes per view): the cold start
+    of New_Simulation.R's shape opens ~70 tables in its first sweeps, so the
+    repair's births overflow and every chain is grown and resumed (oracle:
+    unbounded, multiview_utils.cpp:209-216, 251-258); the chain is unchanged."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(1999)
+    s = m.Sampler(y, seed=5, mode="parallel", table_cap=16, dish_cap=15)
+    ref = O.run(y, 12, 0, 1, seed=5, mode=O.PARALLEL)
+    grew = False
+    for it in range(12):
+        s.sweep(1)
+        t, d, h = s.state()
+        grew |= d.shape[1] > 16
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+        assert h["alpha_global"] == ref["alpha_global"][it]
+    assert grew
+    s.close()
+
+
+def _check_sweeps(s, ref, sweeps, stats=True):
+    for it in range(sweeps):
+        s.sweep(1)
+        t, d, h = s.state()
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+        assert np.array_equal(h["tau_v"], ref["tau_v"][:, it]), it
+        assert h["sigma_global"] == ref["sigma_global"][it], it
+    if stats:
+        for v in range(len(ref["stats"])):
+            g, r = s.stats(v), ref["stats"][v]
+            assert np.array_equal(g["n"], r["n"]) and np.array_equal(g["S1"], r["S1"]), v
+            assert np.array_equal(g["S2"], r["S2"]), v
+
+
+def test_config2_full_size_cold_and_warm():
+    """BASELINE configs[1] at its full size (N = 100k, V = 2, D = 64, K = 16):
+    3 sweeps from the reference initialisation (thousands of movers per sweep:
+    the in-order repair carries the sweep) and 3 warm sweeps, bitwise."""
+    m = _mvc()
+    from mvc_amd import data
+    N, V, D, K = 100_000, 2, 64, 16
+    y, z = data.synthetic(N, V, D, K, seed=1999)
+    s = m.Sampler(y, seed=11, mode="parallel")
+    ref = O.run(y, 3, 0, 1, seed=11, mode=O.PARALLEL)
+    _check_sweeps(s, ref, 3)
+    assert s.repair_stats()["moves"] == ref["trace_moves"][-1]
+    s.close()
+    st = _warm_state(z, V, K)
+    s = m.Sampler(y, seed=11, mode="parallel")   # fresh handle: sweep counter 0, like the oracle
+    s.set_state(*st)
+    ref = O.run(y, 3, 0, 1, seed=11, mode=O.PARALLEL, state=st)
+    _check_sweeps(s, ref, 3)
+    s.close()
+
+
+def test_config4_full_size_warm_sweep():
+    """BASELINE configs[3] shard at its full size (N = 1M, V = 4, D = 128,
+    K = 64): one warm sweep of the benchmarked path, bitwise vs the oracle."""
+    m = _mvc()
+    from mvc_amd import data
+    N, V, D, K = 1_000_000, 4, 128, 64
+    y, z = data.synthetic(N, V, D, K, seed=1999)
+    st = _warm_state(z, V, K)
+    s = m.Sampler(y, seed=1999, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 1, 0, 1, seed=1999, mode=O.PARALLEL, state=st)
+    _check_sweeps(s, ref, 1)
+    assert s.zpath() & 2   # the MFMA producer
+    s.close()
+
+
+def test_config5_shape_reduced_n():
+    """BASELINE configs[4]'s shape (V = 8, D = 256, K = 256 generating
+    clusters: K_v = 256 ... 2) at N = 20k, warm start, bitwise."""
+    m = _mvc()
+    from mvc_amd import data
+    N, V, D, K = 20_000, 8, 256, 256
+    y, z = data.synthetic(N, V, D, K, seed=5)
+    st = _warm_state(z, V, K)
+    s = m.Sampler(y, seed=3, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 2, 0, 1, seed=3, mode=O.PARALLEL, state=st)
+    _check_sweeps(s, ref, 2)
+    s.close()
+
+
 # ---------------------------------------------------------------- MFMA path, warm start
 def _warm_state(z, V, K):
     from mvc_amd import data  # noqa: F401

@@ -1,0 +1,99 @@
+"""Posterior equivalence of the schedules (SURVEY.md §8c tolerance row).
+
+The GPU's parallel mode executes oracle mode PARALLEL (SeqSampler: the
+reference's sequential sweep, multiview_gibbs.cpp:157-200, with the GPU-shaped
+conditional and counter-addressed Philox draws).  Its draws are not
+comparable one by one with the reference schedule's (a different random
+stream), so this checks the Markov kernels: posterior means over >= 16
+independent chains of the reference schedule (mode EXACT, glibc libm, the
+literal restatement of the reference) and of mode PARALLEL must agree within
+4 * sqrt(MCSE_1^2 + MCSE_2^2), with MCSE = sd(chain means) / sqrt(chains).
+
+Quantities: alpha_g, sigma_g, the number of tables, alpha_v, sigma_v, tau_v
+(multiview_hyper.cpp:233-292) and the co-clustering matrix.  The matrix has
+~10^4 correlated entries, so at 4 sigma a few may exceed by chance: every
+entry must be within 6 sigma and at most 0.1 % of them beyond 4 sigma.
+
+test_jacobi_schedule_is_biased keeps round 1's schedule (every customer
+against the sweep-start state) as a documented negative result: on the
+configs[0] shape it drifts to sigma_g ~ 0.9 and ~300 tables (the reference:
+sigma_g ~ 0.08, ~8 tables), which is why the GPU no longer runs it.
+"""
+import os
+import sys
+from multiprocessing import get_context
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
+
+from oracle import oracle as O  # noqa: E402
+from mvc_amd import data  # noqa: E402
+
+CHAINS = 16
+
+
+def _shape(name):
+    if name == "newsim":      # New_Simulation.R:47-60 (n = 200, V = 5)
+        return data.new_simulation(1999)[0]
+    return data.config1(1)[0]  # BASELINE configs[0] (n = 500, V = 2)
+
+
+def _chain(args):
+    name, mode, chain, M, burn = args
+    y = _shape(name)
+    r = O.run(y, M, burn, 1, seed=2024, chain=chain, mode=mode, math=O.LIBM)
+    tab = np.stack(r["table_of"])
+    n = tab.shape[1]
+    cc = np.zeros((n, n))
+    for t in tab:
+        cc += t[:, None] == t[None, :]
+    cc /= len(tab)
+    Ts = np.array([d.shape[1] for d in r["dish_of"]], dtype=np.float64)
+    feats = np.concatenate([[r["alpha_global"].mean(), r["sigma_global"].mean(), Ts.mean()],
+                            r["alpha_v"].mean(1), r["sigma_v"].mean(1), r["tau_v"].mean(1)])
+    return feats, cc
+
+
+def _chains(name, mode, M, burn, chains=CHAINS):
+    with get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
+        out = pool.map(_chain, [(name, mode, c, M, burn) for c in range(chains)])
+    return np.stack([o[0] for o in out]), np.stack([o[1] for o in out])
+
+
+def _zscores(a, b):
+    C1, C2 = a.shape[0], b.shape[0]
+    se = np.sqrt(a.var(0, ddof=1) / C1 + b.var(0, ddof=1) / C2)
+    d = np.abs(a.mean(0) - b.mean(0))
+    z = np.where(se > 0, d / np.where(se > 0, se, 1.0), np.where(d > 0, np.inf, 0.0))
+    return z
+
+
+def _names(V):
+    return (["alpha_g", "sigma_g", "T"] + [f"alpha_{v}" for v in range(V)] + [f"sigma_{v}" for v in range(V)]
+            + [f"tau_{v}" for v in range(V)])
+
+
+@pytest.mark.parametrize("name,M,burn", [("newsim", 4000, 1000), ("config1", 3000, 1000)])
+def test_parallel_schedule_matches_reference_posterior(name, M, burn):
+    fe, ce = _chains(name, O.EXACT, M, burn)
+    fp, cp = _chains(name, O.PARALLEL, M, burn)
+    z = _zscores(fe, fp)
+    names = _names(_shape(name).shape[0])
+    bad = [(n_, round(float(z_), 2)) for n_, z_ in zip(names, z) if z_ > 4.0]
+    assert not bad, f"posterior means differ beyond 4 MCSE: {bad}"
+    iu = np.triu_indices(ce.shape[1], 1)
+    zc = _zscores(ce[:, iu[0], iu[1]], cp[:, iu[0], iu[1]])
+    assert zc.max() < 6.0, f"co-clustering entry at {zc.max():.2f} MCSE"
+    assert (zc > 4.0).mean() <= 1e-3, f"{(zc > 4.0).mean():.4%} of co-clustering entries beyond 4 MCSE"
+
+
+def test_jacobi_schedule_is_biased():
+    fe, _ = _chains("config1", O.EXACT, 2000, 500, chains=8)
+    fj, _ = _chains("config1", O.JACOBI, 2000, 500, chains=8)
+    z = _zscores(fe, fj)
+    # sigma_g and the table count are far outside any Monte-Carlo tolerance
+    assert z[1] > 10 and z[2] > 10
+    assert fj[:, 1].mean() > 0.5 > fe[:, 1].mean()
