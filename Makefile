@@ -11,7 +11,7 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 OBJS := $(PKG)/build/mvc_exact.o $(PKG)/build/mvc_parallel.o $(PKG)/build/mvc_spec.o $(PKG)/build/mvc_ari.o \
         $(PKG)/build/mvc_api.o
 HDRS := $(ROOT)/include/mvc.h $(ROOT)/include/mvc_pmath.h $(ROOT)/include/mvc_philox.h \
-        $(SRC)/mvc_internal.h $(SRC)/mvc_host.h
+        $(SRC)/mvc_internal.h $(SRC)/mvc_host.h $(SRC)/mvc_repair.h
 
 all: $(LIB) oracle
 

@@ -17,8 +17,11 @@ bracketed by barrier + device sync and the max over ranks is reported.
 
 Output: one JSON line on rank 0 (driver contract), including the roofline of
 the dominant kernel (zresample) measured with HIP events on the sampler's
-stream, and a CPU baseline (the oracle's port of the same sweep, timed on a
-bounded subsample on one host core).
+stream, and a CPU baseline (the oracle's restatement of the same chain, one
+full sweep on one host core).  With N = 1 it also reports (key `extra`) the
+GPU on the north_star literal (D = 1) and configs[1], the exact schedule on
+configs[0], a cold start on configs[1], and the reference's algorithm
+(oracle ExactSampler, libm) on the host at the north_star literal.
 """
 import argparse
 import json
@@ -49,7 +52,8 @@ def parse():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1999)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=0, help="customers in the CPU baseline sample (0 = auto)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra lines (other configs, exact schedule, cold start, reference CPU)")
     return ap.parse_args()
 
 
@@ -76,26 +80,136 @@ def measured_traffic(config):
         return None
 
 
-def cpu_baseline(y, z, V, K, D, seed, n_sample=0, target_s=12.0):
-    """Oracle port of the same parallel sweep on a bounded subsample, 1 core.
-    The sample size is calibrated on a 2000-customer probe to ~target_s."""
+def host_cpu():
+    """The host CPU model and core count (lscpu 'Model name', os.cpu_count)."""
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count()}
+
+
+def cpu_baseline(y, z, V, K, D, seed, budget_s=30.0):
+    """The oracle's restatement of the same chain (SeqSampler: the reference's
+    sequential schedule with this build's D-dim conditional and counters;
+    oracle/mvc_oracle.cpp), one full sweep over all N customers from the same
+    warm state, on one host core (one chain -> min(chains, nproc) = 1 core).
+    A 2000-customer probe predicts the sweep; only if it would exceed
+    budget_s does it time a prefix and extrapolate (said in `sample`)."""
     from oracle import oracle as O
-    if not n_sample:
-        m = min(2000, y.shape[1])
-        t0 = time.perf_counter()
-        O.run(np.ascontiguousarray(y[:, :m]), 1, 0, 1, seed, chain=0, mode=O.PARALLEL, state=warm_state(z[:m], V, K))
-        per = (time.perf_counter() - t0) / m
-        n_sample = int(min(y.shape[1], max(m, target_s / max(per, 1e-9))))
+    N = y.shape[1]
+    m = min(2000, N)
+    t0 = time.perf_counter()
+    O.run(np.ascontiguousarray(y[:, :m]), 1, 0, 1, seed, chain=0, mode=O.PARALLEL, state=warm_state(z[:m], V, K))
+    per = (time.perf_counter() - t0) / m
+    n_sample = N if per * N <= budget_s else int(max(m, budget_s / max(per, 1e-9)))
     ys = np.ascontiguousarray(y[:, :n_sample])
     st = warm_state(z[:n_sample], V, K)
     t0 = time.perf_counter()
     O.run(ys, 1, 0, 1, seed, chain=0, mode=O.PARALLEL, state=st)
     dt = time.perf_counter() - t0
-    sweeps_per_s = 1.0 / (dt * (y.shape[1] / n_sample))   # cost is linear in N at fixed K, T
+    sweeps_per_s = 1.0 / (dt * (N / n_sample))
+    what = (f"1 full sweep over all {N} customers, {dt:.2f} s" if n_sample == N else
+            f"1 sweep over the first {n_sample} of {N} customers, {dt:.2f} s, extrapolated linearly to N")
     return {"value": sweeps_per_s, "unit": "sweeps/s", "cores": 1, "kind": "port",
-            "sample": f"1 parallel sweep of the oracle (oracle/mvc_oracle.cpp ParallelSampler, g++ -O2, "
-                      f"portable math) over the first {n_sample} of {y.shape[1]} customers from the same warm "
-                      f"state, {dt:.2f} s, extrapolated linearly to N"}
+            "host": host_cpu(),
+            "sample": f"oracle SeqSampler (the sequential schedule the GPU runs; oracle/mvc_oracle.cpp, g++ -O2, "
+                      f"portable math), same warm state and data: {what}"}
+
+
+def reference_schedule_cpu(seed, budget_s=20.0):
+    """The reference's own algorithm (oracle ExactSampler<LibmMath>: a
+    line-by-line restatement of multiview_gibbs.cpp / multiview_utils.cpp /
+    multiview_hyper.cpp with glibc libm, D = 1) at the north_star literal
+    (N = 1M, V = 4, K = 64, D = 1), warm start at the generating partition,
+    one full sweep on one core (one chain)."""
+    from oracle import oracle as O
+    from mvc_amd import data
+    N, V, D, K, desc = CONFIGS["ns"]
+    y, z = data.synthetic(N, V, D, K, seed=seed)
+    y2 = np.ascontiguousarray(y[:, :, 0])
+    m = 20000
+    t0 = time.perf_counter()
+    O.run(np.ascontiguousarray(y2[:, :m]), 1, 0, 1, seed, chain=0, mode=O.EXACT, math=O.LIBM,
+          state=warm_state(z[:m], V, K))
+    per = (time.perf_counter() - t0) / m
+    n_sample = N if per * N <= budget_s else int(max(m, budget_s / max(per, 1e-9)))
+    t0 = time.perf_counter()
+    O.run(np.ascontiguousarray(y2[:, :n_sample]), 1, 0, 1, seed, chain=0, mode=O.EXACT, math=O.LIBM,
+          state=warm_state(z[:n_sample], V, K))
+    dt = time.perf_counter() - t0
+    return {"workload": desc, "value": 1.0 / (dt * (N / n_sample)), "unit": "sweeps/s", "cores": 1,
+            "kind": "reference-algorithm restatement (oracle ExactSampler<LibmMath>)", "host": host_cpu(),
+            "sample": (f"1 full sweep over all {N} customers, {dt:.2f} s" if n_sample == N else
+                       f"1 sweep over the first {n_sample} of {N} customers, {dt:.2f} s, extrapolated to N")}
+
+
+def gpu_line(config, seed, device, steps=10, warmup=3):
+    """sweeps/s of the GPU (parallel-mode handle, the sequential schedule) on
+    another BASELINE config, warm start at the generating partition."""
+    from mvc_amd import data
+    from mvc_amd.sampler import Sampler
+    N, V, D, K, desc = CONFIGS[config]
+    y, z = data.synthetic(N, V, D, K, seed=seed)
+    s = Sampler(y, seed=seed, mode="parallel", device=device)
+    s.set_state(*warm_state(z, V, K))
+    s.sweep(warmup)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.sweep(steps)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    rep = s.repair_stats()
+    s.close()
+    return {"workload": desc, "value": round(steps / dt, 3), "unit": "sweeps/s", "steps": steps,
+            "moves_last_sweep": rep["moves"]}
+
+
+def gpu_exact_line(seed, device, chains=256, sweeps=200):
+    """BASELINE configs[0] (the New_Simulation.R problem, N = 500, V = 2, K = 3,
+    200 sweeps) on the exact schedule (mode E: the reference's arithmetic,
+    one wavefront per chain): `chains` independent chains in one handle."""
+    from mvc_amd import data
+    from mvc_amd.sampler import Sampler
+    y, _ = data.config1(seed=1)
+    s = Sampler(y, seed=seed, mode="exact", n_chains=chains, device=device)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.sweep(sweeps)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    s.close()
+    return {"workload": "BASELINE configs[0]: New_Simulation shape N=500 V=2 K=3 (D=1), cold start, exact schedule",
+            "chains": chains, "sweeps": sweeps, "value": round(chains * sweeps / dt, 1),
+            "unit": "chain-sweeps/s", "per_chain_sweeps_per_s": round(sweeps / dt, 2)}
+
+
+def cold_start(seed, device, sweeps=4):
+    """BASELINE configs[1] (N = 100k, V = 2, D = 64, K = 16) from the
+    reference's initialisation (4 tables, 2 dishes per view,
+    multiview_gibbs.cpp:12-103): seconds, tables and movers per sweep."""
+    from mvc_amd import data
+    from mvc_amd.sampler import Sampler
+    N, V, D, K, desc = CONFIGS["c2"]
+    y, _ = data.synthetic(N, V, D, K, seed=seed)
+    s = Sampler(y, seed=seed, mode="parallel", device=device)
+    s.synchronize()
+    rows = []
+    for _ in range(sweeps):
+        t0 = time.perf_counter()
+        s.sweep(1)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        rep = s.repair_stats()
+        rows.append({"s": round(dt, 4), "T": int(s.state()[1].shape[1]), "moves": rep["moves"],
+                     "births": rep["births"]})
+    s.close()
+    return {"workload": desc + ", cold start", "sweeps": rows}
 
 
 def main():
@@ -221,8 +335,18 @@ def main():
         "kernel_ms_note": "per-phase HIP-event times from 3 sweeps after the timed region",
         "data_gen_s": round(t_gen, 2),
     }
+    if world == 1 and not args.no_extras:
+        # other BASELINE configs and schedules, after the timed region (rank 0, N = 1)
+        out["extra"] = {
+            "north_star_literal_gpu": gpu_line("ns", args.seed, local),
+            "configs1_gpu": gpu_line("c2", args.seed, local),
+            "exact_schedule_gpu": gpu_exact_line(args.seed, local),
+            "cold_start_gpu": cold_start(args.seed, local),
+        }
+        if not args.no_cpu_baseline:
+            out["extra"]["reference_schedule_cpu"] = reference_schedule_cpu(args.seed)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(y, z, V, K, D, args.seed, args.cpu_sample)
+        out["cpu_baseline"] = cpu_baseline(y, z, V, K, D, args.seed)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -143,7 +143,7 @@ int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms
 void mvc_sampler_reset_timers(mvc_sampler *s);
 /* Adjusted Rand index of the chain's current table labels against truth[n]
  * (host array, any int32 labels), computed on the device from exact pair
- * counts in mclust::adjustedRandIndex's operation order (the ARI of
+ * counts in mcclust::arandi's operation order (the ARI of
  * New_Simulation.R:189).  MVC_ERR_UNSUPPORTED when range(labels) x
  * range(truth) > 2^26 contingency cells. */
 int mvc_sampler_ari(mvc_sampler *s, int chain, const int32_t *truth, double *ari, char *err, size_t errlen);

@@ -1,5 +1,5 @@
 // mvc_ari.hip — adjusted Rand index of two labelings on the device (SURVEY
-// §8f f4: the caller's ARI, New_Simulation.R:6,189, mclust::adjustedRandIndex).
+// §8f f4: the caller's ARI, New_Simulation.R:5,189, mcclust::arandi).
 //
 // Three passes over HBM-resident labels, all integer work (order-free, so the
 // result does not depend on the launch shape):
@@ -8,9 +8,13 @@
 //      the table fits in LDS, else global atomics);
 //   3. the three pair sums  a = sum C(n_ij,2), sa = sum C(row,2),
 //      sb = sum C(col,2)  in uint64.
-// The host combines the exact integers in mclust's operation order
-// (adjustedRandIndex: a, b = sa - a, c = sb - a, d = C(n,2) - a - b - c), so
-// for n < 2^26 the fp64 result equals mclust's bit for bit.
+// The host combines the exact integers in mcclust::arandi's operation order
+// (adjust = TRUE):  correc = sa * sb / C(n,2);
+//                   (a - correc) / (0.5 sa + 0.5 sb - correc).
+// R's choose(k, 2) of a count is the exact integer as a double for k < 2^26
+// (nmath choose.c: n * ((n - 1) / 2), then rounded to an integer), and sums
+// of exact integers below 2^53 are exact in any order, so the fp64 result
+// equals arandi's bit for bit; a 1 x 1 table gives 0 / 0 = NaN, as in R.
 #include <algorithm>
 #include <climits>
 #include <vector>
@@ -127,14 +131,17 @@ struct DMem {
 
 namespace mvc {
 
-// mclust::adjustedRandIndex on exact pair counts, in its operation order.
-double ari_from_pairs(uint64_t a_, uint64_t sa, uint64_t sb, int64_t n, bool one_by_one) {
-  if (one_by_one) return 1.0;   // mclust: a 1 x 1 table is full agreement
-  const double a = (double)a_, b = (double)(sa - a_), c = (double)(sb - a_);
-  const double tot = (double)((uint64_t)n * (uint64_t)(n - 1) / 2);
-  const double d = ((tot - a) - b) - c;
-  const double e = (a + b) * (a + c) / (((a + b) + c) + d);
-  return (a - e) / ((((a + b) + a) + c) / 2.0 - e);
+// mcclust::arandi (adjust = TRUE) on exact pair counts, in R's left-to-right
+// operation order:
+//   correc <- sum(choose(tab.1,2)) * sum(choose(tab.2,2)) / choose(n,2)
+//   (sum(choose(tab.12,2)) - correc) /
+//       (0.5*sum(choose(tab.1,2)) + 0.5*sum(choose(tab.2,2)) - correc)
+// A 1 x 1 table (or n < 2) gives NaN there (0/0); IEEE does the same here.
+double ari_from_pairs(uint64_t a_, uint64_t sa_, uint64_t sb_, int64_t n) {
+  const double a = (double)a_, sa = (double)sa_, sb = (double)sb_;
+  const double nn = (double)((uint64_t)n * (uint64_t)(n - 1) / 2);
+  const double correc = (sa * sb) / nn;
+  return (a - correc) / ((0.5 * sa + 0.5 * sb) - correc);
 }
 
 // ARI of two device label arrays on `stream` (synchronises it).
@@ -169,7 +176,7 @@ double ari_device(const int32_t *da, const int32_t *db, int64_t n, hipStream_t s
   unsigned long long s[3];
   MVC_HIP(hipMemcpyAsync(s, sums.p, sizeof(s), hipMemcpyDeviceToHost, stream));
   MVC_HIP(hipStreamSynchronize(stream));
-  return ari_from_pairs(s[0], s[1], s[2], n, ra == 1 && rb == 1);
+  return ari_from_pairs(s[0], s[1], s[2], n);
 }
 
 }  // namespace mvc

@@ -93,9 +93,9 @@ class Sampler {
 };
 
 // Adjusted Rand index (mvc_ari.hip): exact pair counts on the device, combined
-// in mclust::adjustedRandIndex's operation order.
+// in mcclust::arandi's operation order (New_Simulation.R:189).
 double ari_device(const int32_t *da, const int32_t *db, int64_t n, hipStream_t stream);
-double ari_from_pairs(uint64_t a, uint64_t sa, uint64_t sb, int64_t n, bool one_by_one);
+double ari_from_pairs(uint64_t a, uint64_t sa, uint64_t sb, int64_t n);
 
 // Validated host view of a user-supplied state (warm start / resume).
 struct UserState {

@@ -1704,7 +1704,7 @@ constexpr int kHypWaves = 5, kHypThreads = 64 * kHypWaves, kHypGlobalWaveT = 512
 extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(MHArgs A) {
   ParState &P = A.P;
   const int tid = threadIdx.x;
-  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
+  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
   __shared__ int s_i[8];
 #ifdef MVC_HYP_PROF
   const uint64_t t0 = wall_clock64();
@@ -1947,6 +1947,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
 // Host side of the parallel schedule.
 // ===========================================================================
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -1962,6 +1963,8 @@ constexpr size_t kLpbBudget = (size_t)1 << 28;   // phase-1 lp buffer: 2 GiB of 
 constexpr int kSeqWaves = 1024;    // waves of the repair eval grid (SeqArgs.G)
 constexpr int kSeqWmin = 1024;     // repair window after a mover
 constexpr int kSeqWmax = 1 << 16;  // cap of the window doubling over mover-free stretches
+constexpr int kSeqRunLimit = 64;   // stays in a row after which the run kernel hands over to grid windows
+constexpr size_t kSeqLdsBudget = 150 * 1024;   // run kernel: per-wave LDS scratch of all its waves
 
 template <class Tp>
 Tp *dmalloc(size_t count) {
@@ -2017,6 +2020,9 @@ class ParallelSampler : public Sampler {
   int fz_waves = MVC_FZ_THREADS / 64;   // waves per block of the fused kernel (MVC_FZ_WAVES: fewer)
   int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
   int n_cu = 256;
+  bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
+  int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
+  int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
 
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
@@ -2108,6 +2114,11 @@ class ParallelSampler : public Sampler {
     fused_attr<4, 4>();
     fused_attr<8, 8>();
     fused_attr<16, MVC_FZ_RP16>();
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_run_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
+    if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
+    if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
+    if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh.data());
     MVC_HIP(hipStreamSynchronize(stream));
@@ -2503,7 +2514,7 @@ class ParallelSampler : public Sampler {
     const SeqArgs Q0 = make_seq(c, s);
     hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
     MVC_HIP(hipGetLastError());
-    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+    hipEvent_t e0 = nullptr;
     // phase 1 in customer batches: lp producer (MFMA or generic), then draw
     int Kmax = 0, Kmin = 1 << 30;
     for (int k : c.K) { Kmax = std::max(Kmax, k); Kmin = std::min(Kmin, k); }
@@ -2614,11 +2625,48 @@ class ParallelSampler : public Sampler {
     repair(c, s, phaseA);
   }
 
+  // LDS layout of the run kernel's per-wave scratch for T tables and dish
+  // lists Klist, with room for growth (a birth past it makes the kernel exit
+  // with R->restride; the host then relaunches with a new layout).  Falls back
+  // to the per-wave global scratch when even a few waves do not fit.
+  SeqLds run_layout(int T, const int32_t *Klist) const {
+    int kmax = 1;
+    for (int v = 0; v < V; ++v) kmax = std::max(kmax, (int)Klist[v]);
+    SeqLds L{};
+    L.limit = run_limit;
+    // in order of preference: S1 cached with room to grow, then without S1,
+    // then tight margins without S1
+    for (int attempt = 0; attempt < 3; ++attempt) {
+      const bool s1 = attempt == 0;
+      const int kgrow = attempt < 2 ? std::max(8, kmax / 2) : 4;
+      const int tgrow = attempt < 2 ? std::max(64, T / 2) : 16;
+      L.ks = (kmax + kgrow + 7) / 8 * 8;
+      L.ts = (T + tgrow + 15) / 16 * 16;
+      L.s1 = s1 ? 1 : 0;
+      L.cache_dbl = seq_lds_cache(V, D, L.ks, L.ts, s1);
+      L.stride = seq_lds_stride(V, D, L.ks, L.ts);
+      const int64_t room = (int64_t)kSeqLdsBudget / 8 - L.cache_dbl;
+      L.nws = room > 0 ? (int)std::min<int64_t>(run_waves, room / L.stride) : 0;
+      if (L.nws >= std::min(run_waves, s1 ? 4 : 2)) {
+        L.lds = 1;
+        return L;
+      }
+    }
+    L.lds = 0;   // per-wave global scratch (SeqScratch(A, w)): capacity-sized, never restrides
+    L.s1 = 0;
+    L.nws = run_waves;
+    L.stride = 0;
+    L.cache_dbl = 0;
+    return L;
+  }
+
   // Phase A's choices are exact up to the first customer that does not stay;
-  // from there the repair rounds commit movers in customer order
-  // (mvc_repair.h), then compaction and the MH.  One host
-  // synchronisation per batch of rounds; at steady state a single batch of
-  // one round.  A birth beyond the capacity grows every chain and resumes.
+  // from there the repair commits movers in customer order (mvc_repair.h,
+  // DESIGN.md §4.8), then compaction and the MH.  Each round is the run
+  // kernel (dense movers: commit + 8-customer speculation in a device loop)
+  // and a grid window (sparse movers).  One host synchronisation per batch of
+  // rounds; at steady state a single batch of one round.  A birth beyond the
+  // capacity grows every chain and resumes.
   void repair(Chain &c, uint32_t s, bool phaseA) {
     hipEvent_t e1 = nullptr;
     timers.begin("repair", &e1);
@@ -2630,10 +2678,16 @@ class ParallelSampler : public Sampler {
     else
       hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
     MVC_HIP(hipGetLastError());
+    SeqLds L = run_layout(c.T, c.K.data());
     int rounds = 1;
     for (;;) {
       for (int r = 0; r < rounds; ++r) {
-        hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
+        if (repair_grid_only)
+          hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
+        else
+          hipLaunchKernelGGL(mvc_seq_run_kernel, dim3(1), dim3(kSeqRunThreads),
+                             L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws)) : 0,
+                             stream, Q, L);
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
       }
       MVC_HIP(hipGetLastError());
@@ -2642,6 +2696,11 @@ class ParallelSampler : public Sampler {
       if (rs_host->overflow) {
         grow_capacity(rs_host->overflow);
         Q = make_seq(c, s);
+        continue;
+      }
+      if (rs_host->restride) {
+        L = run_layout(rs_host->T, rs_host->Klist);
+        MVC_HIP(hipMemsetAsync(&c.R->restride, 0, sizeof(int32_t), stream));
         continue;
       }
       if (rs_host->done) break;
@@ -2655,6 +2714,13 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipGetLastError());
     }
     timers.end("repair", e1);
+#ifdef MVC_RUN_PROF
+    fprintf(stderr, "runprof moves %d iters %llu | view %.1f tables %.1f exp+blocks %.1f select %.1f | commit %.1f spec %.1f decide %.1f (us per iter)\n",
+            rs_host->moves, rs_host->prof[7], rs_host->prof[0] * 0.01 / std::max(1ull, rs_host->prof[7]),
+            rs_host->prof[1] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[2] * 0.01 / std::max(1ull, rs_host->prof[7]),
+            rs_host->prof[3] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[4] * 0.01 / std::max(1ull, rs_host->prof[7]),
+            rs_host->prof[5] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[6] * 0.01 / std::max(1ull, rs_host->prof[7]));
+#endif
     c.last[0] = rs_host->moves;
     c.last[1] = rs_host->births;
     c.last[2] = rs_host->rounds;

@@ -34,9 +34,53 @@ struct Repair {
   int32_t overflow;   // 1: a birth needs a table slot beyond TC; 2: a dish slot beyond KC
   int32_t T;          // table positions (births append; dead tables keep their slot)
   int32_t T_ne;       // tables with n_t > 0
+  int32_t mode;       // kSeqScan: windows on the grid (mvc_seq_eval_kernel); kSeqRun: the one-block run kernel
+  int32_t pchoice;    // choice of customer cur when pend (its exact conditional draw)
+  int32_t streak;     // consecutive stays seen by the run kernel since its last mover
+  int32_t restride;   // 1: the run kernel's LDS layout is too small for T / the dish lists (host relaunches)
   int32_t moves, births, newdish, rounds;
-  int32_t Klist[MVC_MAXV];   // dish list length per view (dishes that died this sweep stay, l = 0)
+  int32_t Klist[MVC_MAXV];
+  unsigned long long prof[8];   // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz)   // dish list length per view (dishes that died this sweep stay, l = 0)
 };
+
+constexpr int32_t kSeqScan = 0, kSeqRun = 1;
+
+// MVC_RUN_PROF builds (scripts/build_variant.sh NAME -DMVC_RUN_PROF): wave 0
+// of the run kernel accumulates wall-clock ticks (100 MHz) per phase; thread 0
+// prints them when the kernel exits.  Tuning aid only.
+#ifdef MVC_RUN_PROF
+#define RUN_T0() uint64_t _rt = wall_clock64()
+#define RUN_MARK(k) do { const uint64_t _n = wall_clock64(); \
+    if (threadIdx.x == 0 && blockDim.x == kSeqRunThreads) A.R->prof[k] += _n - _rt; _rt = _n; } while (0)
+#else
+#define RUN_T0() do {} while (0)
+#define RUN_MARK(k) do {} while (0)
+#endif
+// run kernel block: 8 waves (256 VGPRs each: the per-customer evaluation
+// spills at the 128 VGPRs of a 16-wave block)
+constexpr int kSeqRunThreads = 512, kSeqRunWaves = kSeqRunThreads / 64;
+
+// LDS layout of the run kernel's per-wave scratch (host-chosen at launch):
+// lp [V][ks] | e [ts + 16] | B, C [ts/16 + 2]; nws waves speculate.
+// lds = 0: the per-wave global scratch (SeqArgs.scr) instead.
+// LDS of the run kernel: the state cache (SCache: n_t [ts], dish [V][ts],
+// d_l, d_n [V][ks], Klist, Ltot [V], T, T_ne; c0, cb, Q [V][ks]; S1T
+// [V][D][ks] when s1) and per-wave scratch lp [V][ks] | e [ts + 16] | B, C
+// [ts/16 + 2] | y rows [V][D] | Y2 [V].
+struct SeqLds {
+  int32_t lds, nws, ks, ts;
+  int32_t limit;        // stays in a row after which the run kernel hands over to the grid windows
+  int32_t s1;           // S1 cached in LDS
+  int64_t cache_dbl;    // doubles of the state cache (the per-wave scratch follows)
+  int64_t stride;       // doubles per wave
+};
+__host__ __device__ inline int64_t seq_lds_stride(int V, int D, int ks, int ts) {
+  return (int64_t)V * ks + ts + 16 + 2 * (ts / 16 + 2) + (int64_t)V * D + V;
+}
+__host__ __device__ inline int64_t seq_lds_cache(int V, int D, int ks, int ts, bool s1) {
+  const int64_t ints = (int64_t)ts + (int64_t)V * ts + 2 * (int64_t)V * ks + 2 * V + 2;
+  return (ints + 1) / 2 + 3 * (int64_t)V * ks + (s1 ? (int64_t)V * D * ks : 0);
+}
 
 struct SeqArgs {
   ParState P;
@@ -62,13 +106,27 @@ namespace {
 // [TC/16+1] | running totals [TC/16+1] | dish-draw tree levels
 struct SeqScratch {
   double *lp, *e, *B, *C, *tree;
+  double *ys;   // run kernel: the customer's y rows [V][D] and Y2 [V]
+  int lps;   // lp stride per view
   __device__ SeqScratch(const SeqArgs &A, int wave) {
     double *base = A.scr + (int64_t)wave * A.scr_stride;
+    lps = A.P.KC;
     lp = base;
     e = lp + (size_t)A.P.V * A.P.KC;
     B = e + A.P.TC + 16;
     C = B + A.P.TC / 16 + 2;
     tree = C + A.P.TC / 16 + 2;
+    ys = nullptr;
+  }
+  // run kernel, LDS: lp [V][ks] | e [ts + 16] | B | C | y rows (no dish-draw tree)
+  __device__ SeqScratch(double *base, int V, int ks, int ts) {
+    lps = ks;
+    lp = base;
+    e = lp + (size_t)V * ks;
+    B = e + ts + 16;
+    C = B + ts / 16 + 2;
+    ys = C + ts / 16 + 2;
+    tree = nullptr;
   }
 };
 __host__ inline int64_t seq_scratch_stride(int V, int TC, int KC) {
@@ -89,45 +147,162 @@ __device__ __forceinline__ double pw16_seq(const double *x) {
     for (int c = 0; c < 16; c += 2 * h) a[c] = a[c] + a[c + h];
   return a[0];
 }
-// oracle pw16_select
+// oracle pw16_select: the pw16 levels in registers (static indices only, so
+// nothing goes to scratch), descent left iff R == 0 || r < L.
 __device__ __forceinline__ int pw16_select_seq(const double *x, double r) {
-  double lv[5][16];
+  double l0[16], l1[8], l2[4], l3[2];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) lv[0][c] = x[c];
+  for (int c = 0; c < 16; ++c) l0[c] = x[c];
 #pragma unroll
-  for (int k = 0, h = 1; k < 4; ++k, h <<= 1)
+  for (int c = 0; c < 8; ++c) l1[c] = l0[2 * c] + l0[2 * c + 1];
 #pragma unroll
-    for (int c = 0; c < 16; c += 2 * h) lv[k + 1][c] = lv[k][c] + lv[k][c + h];
-  int lo = 0;
-  for (int k = 3, h = 8; k >= 0; --k, h >>= 1) {
-    const double L = lv[k][lo], R = lv[k][lo + h];
+  for (int c = 0; c < 4; ++c) l2[c] = l1[2 * c] + l1[2 * c + 1];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) l3[c] = l2[2 * c] + l2[2 * c + 1];
+  int idx = 0;   // node index at the current level
+  auto step = [&](double L, double R) {
+    idx *= 2;
     if (!(R == 0.0 || r < L)) {
       r = r - L;
-      lo += h;
+      idx += 1;
     }
+  };
+  step(l3[0], l3[1]);
+  {
+    double L = l2[0], R = l2[1];
+#pragma unroll
+    for (int q = 1; q < 2; ++q) if (q == idx) { L = l2[2 * q]; R = l2[2 * q + 1]; }
+    step(L, R);
   }
+  {
+    double L = l1[0], R = l1[1];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) if (q == idx) { L = l1[2 * q]; R = l1[2 * q + 1]; }
+    step(L, R);
+  }
+  {
+    double L = l0[0], R = l0[1];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) if (q == idx) { L = l0[2 * q]; R = l0[2 * q + 1]; }
+    step(L, R);
+  }
+  return idx;
+}
+
+// pw16_select across a wave: lane l < 16 holds element l; r wave-uniform.
+// Levels by DPP row shifts (node c at offset h = x[c] + x[c + h], the pw16
+// association), descent left iff R == 0 || r < L.
+__device__ __forceinline__ int pw16_select_wave(double x, double r) {
+  const double l1 = x + down_d<1>(x);
+  const double l2 = l1 + down_d<2>(l1);
+  const double l3 = l2 + down_d<4>(l2);
+  int lo = 0;
+#define MVC_PW16_DESCEND(VAL, H)                              \
+  {                                                           \
+    const double a = readlane_d((VAL), lo);                   \
+    const double b = readlane_d((VAL), lo + (H));             \
+    if (!(b == 0.0 || r < a)) { r = r - a; lo = lo + (H); }   \
+  }
+  MVC_PW16_DESCEND(l3, 8)
+  MVC_PW16_DESCEND(l2, 4)
+  MVC_PW16_DESCEND(l1, 2)
+  MVC_PW16_DESCEND(x, 1)
+#undef MVC_PW16_DESCEND
   return lo;
 }
 
 __device__ __forceinline__ int wave_count(bool p) { return __popcll(__ballot(p)); }
 
+// acc + sum_d a[d] b[d * bs], one fma chain in ascending d (the oracle's
+// fma_dot order).  The loads of each 8-wide batch are issued before its
+// fmas, so a chain of D fmas waits on D/8 memory latencies, not D.
+__device__ __forceinline__ double fma_dot_strided(const double *a, const double *b, size_t bs, int D, double acc) {
+  int d = 0;
+  for (; d + 8 <= D; d += 8) {
+    double xa[8], xb[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      xa[u] = a[d + u];
+      xb[u] = b[(size_t)(d + u) * bs];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_fma(xa[u], xb[u], acc);
+  }
+  for (; d < D; ++d) acc = __builtin_fma(a[d], b[(size_t)d * bs], acc);
+  return acc;
+}
+__device__ __forceinline__ double fma_sq_strided(const double *b, size_t bs, int D) {
+  double acc = 0.0;
+  int d = 0;
+  for (; d + 16 <= D; d += 16) {
+    double xb[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) xb[u] = b[(size_t)(d + u) * bs];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) acc = __builtin_fma(xb[u], xb[u], acc);
+  }
+  for (; d < D; ++d) acc = __builtin_fma(b[(size_t)d * bs], b[(size_t)d * bs], acc);
+  return acc;
+}
+
+// Where the per-customer evaluation reads the mutable chain state: the global
+// arrays (grid kernels), or the run kernel's LDS cache of them (same values;
+// the commit writes both).  Dish arrays are [v * ks + j], tables [v * ts + p],
+// S1 [(v * D + d) * s1s + j].
+struct SView {
+  const int32_t *n_t, *dish;
+  const int32_t *d_l, *d_n;
+  const double *c0, *cb, *Q;
+  const double *S1T;
+  const int32_t *Klist, *Ltot, *T, *T_ne;
+  int ts, ks, s1s;
+};
+__device__ __forceinline__ SView global_view(const SeqArgs &A) {
+  const ParState &P = A.P;
+  SView G;
+  G.n_t = P.n_t; G.dish = P.dish;
+  G.d_l = P.d_l; G.d_n = P.d_n;
+  G.c0 = P.c0; G.cb = P.cb; G.Q = P.Q;
+  G.S1T = P.S1T;
+  G.Klist = A.R->Klist; G.Ltot = P.Ltot; G.T = &A.R->T; G.T_ne = &A.R->T_ne;
+  G.ts = P.TC; G.ks = P.KC; G.s1s = P.KC;
+  return G;
+}
+
+// The customer's data: y rows [V][D] and Y2 [V], either in global memory or
+// staged in the wave's LDS scratch (run kernel).
+struct Cust {
+  const double *y;    // y[v * ystride + d]
+  size_t ystride;
+  const double *Y2;   // Y2[v * y2stride]
+  size_t y2stride;
+};
+__device__ __forceinline__ Cust global_cust(const SeqArgs &A, int i) {
+  Cust c;
+  c.y = A.y + (size_t)i * A.P.D;
+  c.ystride = (size_t)A.P.n * A.P.D;
+  c.Y2 = A.Y2 + i;
+  c.y2stride = (size_t)A.P.n;
+  return c;
+}
+
 // lp of every listed dish of view v for customer i (the customer's own dish
 // j0 with itself removed) into lp[0..K); oracle
 // eval_view_seq / eval_view.  Returns the number of included dishes (l' > 0)
 // and their max in *mx.
-__device__ int seq_view_lp(const SeqArgs &A, int i, int v, bool alive, int j0, double *lp, double *mx_out) {
+__device__ int seq_view_lp(const SeqArgs &A, const SView &W, const Cust &C, int v, bool alive, int j0, double *lp,
+                           double *mx_out) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
-  const int V = P.V, D = P.D, KC = P.KC, n = P.n;
-  const int K = A.R->Klist[v];
-  const double tau = P.hyper[v], sigma = P.hyper[2 * V + v];
-  (void)sigma;
-  const double Y2i = A.Y2[(size_t)v * n + i];
+  const int D = P.D, ks = W.ks;
+  const int K = W.Klist[v];
+  const double tau = P.hyper[v];
+  const double Y2i = C.Y2[(size_t)v * C.y2stride];
   const double hy = 0.5 * Y2i;
   const double h = (-0.5 * Y2i) / tau;
-  const double *yrow = A.y + ((size_t)v * n + i) * D;
-  const double *S1v = P.S1T + (size_t)v * D * KC;
-  const int l0 = P.d_l[v * KC + j0];
+  const double *yrow = C.y + (size_t)v * C.ystride;
+  const double *S1v = W.S1T + (size_t)v * D * W.s1s;
+  const int l0 = W.d_l[v * ks + j0];
   const int l0p = alive ? l0 : l0 - 1;
   double mx = -MVC_PM_INF;
   int nl = 0;
@@ -135,19 +310,18 @@ __device__ int seq_view_lp(const SeqArgs &A, int i, int v, bool alive, int j0, d
     const int j = base + lane;
     bool inc = false;
     if (j < K) {
-      double G = 0.0;
-      for (int d = 0; d < D; ++d) G = __builtin_fma(yrow[d], S1v[(size_t)d * KC + j], G);
+      const double G = fma_dot_strided(yrow, S1v + j, (size_t)W.s1s, D, 0.0);
       double val;
       int l;
       if (j == j0) {
         l = l0p;
         const double Gp = G - Y2i;
-        const double Qp = (P.Q[v * KC + j] - 2.0 * G) + Y2i;
-        const Coef c = coef(P.d_n[v * KC + j] - 1, Qp, tau, A.L2pt[v], D);
+        const double Qp = (W.Q[v * ks + j] - 2.0 * G) + Y2i;
+        const Coef c = coef(W.d_n[v * ks + j] - 1, Qp, tau, A.L2pt[v], D);
         val = __builtin_fma(Gp + hy, c.cb, c.c0) + h;
       } else {
-        l = P.d_l[v * KC + j];
-        val = __builtin_fma(G + hy, P.cb[v * KC + j], P.c0[v * KC + j]) + h;
+        l = W.d_l[v * ks + j];
+        val = __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
       }
       lp[j] = val;
       inc = l > 0;
@@ -161,24 +335,25 @@ __device__ int seq_view_lp(const SeqArgs &A, int i, int v, bool alive, int j0, d
 
 // lm_v of oracle eval_view_seq (column partials j mod 16 in ascending j,
 // pw16 over the columns, then the new dish); lp[] from seq_view_lp.
-__device__ double seq_view_marg(const SeqArgs &A, int i, int v, bool alive, int j0, double *lp) {
+__device__ double seq_view_marg(const SeqArgs &A, const SView &W, const Cust &C, int v, bool alive, int j0,
+                                double *lp) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
-  const int V = P.V, KC = P.KC, n = P.n;
-  const int K = A.R->Klist[v];
+  const int V = P.V, ks = W.ks;
+  const int K = W.Klist[v];
   const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
   double m;
-  const int Kact = seq_view_lp(A, i, v, alive, j0, lp, &m);
+  const int Kact = seq_view_lp(A, W, C, v, alive, j0, lp, &m);
   __threadfence_block();
-  const double Y2i = A.Y2[(size_t)v * n + i];
+  const double Y2i = C.Y2[(size_t)v * C.y2stride];
   const double h = (-0.5 * Y2i) / tau;
   const double lfn = A.cnew[v] + h;
   if (lfn > m) m = lfn;
-  const int l0p = alive ? P.d_l[v * KC + j0] : P.d_l[v * KC + j0] - 1;
+  const int l0p = alive ? W.d_l[v * ks + j0] : W.d_l[v * ks + j0] - 1;
   double col = 0.0;
   if (lane < 16) {
     for (int j = lane; j < K; j += 16) {
-      const int l = (j == j0) ? l0p : P.d_l[v * KC + j];
+      const int l = (j == j0) ? l0p : W.d_l[v * ks + j];
       if (l > 0) {
         double w = (double)l - sigma;
         if (w < 0.0) w = 0.0;
@@ -193,36 +368,38 @@ __device__ double seq_view_marg(const SeqArgs &A, int i, int v, bool alive, int 
   double wn = alpha + (double)Kact * sigma;
   if (wn < 0.0) wn = 0.0;
   S = S + wn * mvc_exp(lfn - m);
-  const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
+  const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
   if (denom <= 0.0) return lfn;
   return (m + mvc_log(S)) - mvc_log(denom);
 }
 
 // Exact conditional draw of customer i against the current state (oracle
 // ParallelSampler::resample_customer): a table position, or -1 = birth.
-__device__ int seq_resample(const SeqArgs &A, int i, const SeqScratch &S) {
+// p0 = z[i] (the customer's table before this sweep's decision).
+__device__ int seq_resample(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
-  const int V = P.V, KC = P.KC, TC = P.TC;
-  const int p0 = P.z[i];
-  const bool alive = (P.n_t[p0] - 1) > 0;
+  const int V = P.V, ts = W.ts;
+  const bool alive = (W.n_t[p0] - 1) > 0;
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
-  const int Tne_i = A.R->T_ne - (alive ? 0 : 1);
+  const int Tne_i = *W.T_ne - (alive ? 0 : 1);
+  RUN_T0();
   double s_new = mvc_log(ag + sg * (double)Tne_i);
   for (int v = 0; v < V; ++v)
-    s_new = s_new + seq_view_marg(A, i, v, alive, P.dish[v * TC + p0], S.lp + (size_t)v * KC);
+    s_new = s_new + seq_view_marg(A, W, C, v, alive, W.dish[v * ts + p0], S.lp + (size_t)v * S.lps);
   __threadfence_block();
-  const int T = A.R->T;
+  RUN_MARK(0);
+  const int T = *W.T;
   const int TB = (T + 15) / 16;
   double M = -MVC_PM_INF;
   for (int p = lane; p < TB * 16; p += 64) {
     double sp = -MVC_PM_INF;
     if (p < T) {
-      const int np = P.n_t[p] - (p == p0 ? 1 : 0);
+      const int np = W.n_t[p] - (p == p0 ? 1 : 0);
       const double mass = (double)np - sg;
       if (np >= 1 && mass > 0.0) {
         sp = mvc_log(mass);
-        for (int v = 0; v < V; ++v) sp = sp + S.lp[(size_t)v * KC + P.dish[v * TC + p]];
+        for (int v = 0; v < V; ++v) sp = sp + S.lp[(size_t)v * S.lps + W.dish[v * ts + p]];
       }
     }
     S.e[p] = sp;
@@ -231,6 +408,7 @@ __device__ int seq_resample(const SeqArgs &A, int i, const SeqScratch &S) {
   M = wave_max(M);
   if (s_new > M) M = s_new;
   __threadfence_block();
+  RUN_MARK(1);
   for (int p = lane; p < TB * 16; p += 64) {
     const double x = S.e[p];
     S.e[p] = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
@@ -238,35 +416,37 @@ __device__ int seq_resample(const SeqArgs &A, int i, const SeqScratch &S) {
   __threadfence_block();
   for (int b = lane; b < TB; b += 64) S.B[b] = pw16_seq(S.e + (size_t)b * 16);
   __threadfence_block();
-  int pick = 0;
-  if (lane == 0) {
-    double tot = 0.0;
-    for (int b = 0; b < TB; ++b) {
-      tot = tot + S.B[b];
-      S.C[b] = tot;
+  RUN_MARK(2);
+  // running block totals C_b (wave-uniform loops over the LDS block sums;
+  // the second pass recomputes the same sums to find the block)
+  double tot = 0.0;
+  for (int b = 0; b < TB; ++b) tot = tot + S.B[b];
+  const double Wt = mvc_exp(s_new - M) + tot;
+  double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
+  int pick = -1;
+  if (r < tot) {
+    int b = 0;
+    double cprev = 0.0;
+    for (;; ++b) {
+      const double cb = cprev + S.B[b];
+      if (r < cb) break;
+      cprev = cb;
     }
-    const double W = mvc_exp(s_new - M) + tot;
-    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-    if (!(r < tot)) {
-      pick = -1;
-    } else {
-      int b = 0;
-      while (!(r < S.C[b])) ++b;
-      r = r - (b > 0 ? S.C[b - 1] : 0.0);
-      pick = b * 16 + pw16_select_seq(S.e + (size_t)b * 16, r);
-    }
+    r = r - cprev;
+    const double x = lane < 16 ? S.e[(size_t)b * 16 + lane] : 0.0;
+    pick = b * 16 + pw16_select_wave(x, r);
   }
-  return readlane_i(pick, 0);
+  RUN_MARK(3);
+  return pick;
 }
 
 // tree64 over x[0..m) (oracle Tree64::build): level arrays stored one after
-// the other from `lv`; returns the root.  nlev receives the number of levels
-// (leaves included), off[] their offsets.
-__device__ double seq_tree_build(double *lv, int m, int *off, int &nlev) {
+// the other from `lv` (level k starts at the sum of the lower levels' counts);
+// returns the root.  nlev receives the number of levels (leaves included).
+__device__ double seq_tree_build(double *lv, int m, int &nlev) {
   const int lane = threadIdx.x & 63;
   int o = 0, cnt = m;
-  nlev = 0;
-  off[nlev++] = 0;
+  nlev = 1;
   double root = 0.0;
   do {
     const int nc = (cnt + 63) / 64;
@@ -281,20 +461,23 @@ __device__ double seq_tree_build(double *lv, int m, int *off, int &nlev) {
     __threadfence_block();
     o = o2;
     cnt = nc;
-    off[nlev++] = o;
+    ++nlev;
   } while (cnt > 1);
   return root;
 }
 // oracle Tree64::select
-__device__ int seq_tree_select(const double *lv, int m, const int *off, int nlev, double r) {
+__device__ int seq_tree_select(const double *lv, int m, int nlev, double r) {
   const int lane = threadIdx.x & 63;
   int idx = 0;
   for (int k = nlev - 2; k >= 0; --k) {
-    int cnt = m;
-    for (int q = 0; q < k; ++q) cnt = (cnt + 63) / 64;
+    int cnt = m, off = 0;
+    for (int q = 0; q < k; ++q) {
+      off += cnt;
+      cnt = (cnt + 63) / 64;
+    }
     const int base = idx * 64;
     const int c = min(64, cnt - base);
-    const double x = lane < c ? lv[off[k] + base + lane] : 0.0;
+    const double x = lane < c ? lv[off + base + lane] : 0.0;
     Tree64Levels L;
     wave_tree_sum_levels(x, L);
     const int l = wave_tree_select(L, x, r);
@@ -305,27 +488,28 @@ __device__ int seq_tree_select(const double *lv, int m, const int *off, int nlev
 
 // Dish of a birth in view v (oracle SeqSampler::draw_dish): leaves w_j
 // exp(lp_j - m) of the included dishes, the new dish last; tree64; r = u S.
-// Returns a list index; Klist[v] = a new dish.
-__device__ int seq_dish_draw(const SeqArgs &A, int i, int v, bool alive, int j0, const SeqScratch &S) {
+// lp: [K] scratch, tree: the tree64 levels' scratch.  Returns a list index;
+// Klist[v] = a new dish.
+__device__ int seq_dish_draw(const SeqArgs &A, const SView &W, const Cust &C, int i, int v, bool alive, int j0,
+                             double *lp, double *tree) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
-  const int V = P.V, KC = P.KC, n = P.n;
-  const int K = A.R->Klist[v];
+  const int V = P.V, ks = W.ks;
+  const int K = W.Klist[v];
   const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-  double *lp = S.lp + (size_t)v * KC;
   double m;
-  const int Kact = seq_view_lp(A, i, v, alive, j0, lp, &m);
+  const int Kact = seq_view_lp(A, W, C, v, alive, j0, lp, &m);
   __threadfence_block();
-  const double Y2i = A.Y2[(size_t)v * n + i];
+  const double Y2i = C.Y2[(size_t)v * C.y2stride];
   const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
   if (lfn > m) m = lfn;
   double wn = alpha + (double)Kact * sigma;
   if (wn < 0.0) wn = 0.0;
-  const int l0p = alive ? P.d_l[v * KC + j0] : P.d_l[v * KC + j0] - 1;
+  const int l0p = alive ? W.d_l[v * ks + j0] : W.d_l[v * ks + j0] - 1;
   for (int e = lane; e <= K; e += 64) {
     double leaf = 0.0;
     if (e < K) {
-      const int l = (e == j0) ? l0p : P.d_l[v * KC + e];
+      const int l = (e == j0) ? l0p : W.d_l[v * ks + e];
       if (l > 0) {
         double w = (double)l - sigma;
         if (w < 0.0) w = 0.0;
@@ -334,14 +518,14 @@ __device__ int seq_dish_draw(const SeqArgs &A, int i, int v, bool alive, int j0,
     } else {
       leaf = wn * mvc_exp(lfn - m);
     }
-    S.tree[e] = leaf;
+    tree[e] = leaf;
   }
   __threadfence_block();
-  int off[8], nlev;
-  const double tot = seq_tree_build(S.tree, K + 1, off, nlev);
+  int nlev;
+  const double tot = seq_tree_build(tree, K + 1, nlev);
   if (!(tot > 0.0)) return K;
   const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_DISH + 1u + (uint32_t)v) * tot;
-  return seq_tree_select(S.tree, K + 1, off, nlev, r);
+  return seq_tree_select(tree, K + 1, nlev, r);
 }
 
 }  // namespace
@@ -359,9 +543,14 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->W = A.Wmin;
   R->done = 0;
   R->overflow = 0;
+  R->mode = kSeqScan;
+  R->pchoice = 0;
+  R->streak = 0;
+  R->restride = 0;
   R->T = A.status[0];
   R->T_ne = A.status[V + 3];
   R->moves = R->births = R->newdish = R->rounds = 0;
+  for (int k = 0; k < 8; ++k) R->prof[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
 }
 
@@ -380,148 +569,249 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_first_kernel(int n, co
   }
 }
 
-// One repair step (one block of 256 = 4 waves).
-extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A) {
+namespace {
+
+// The run kernel's LDS copies of the mutable state (layout: SeqLds); every
+// write of the commit goes to the global arrays and, when present, here.
+struct SCache {
+  int32_t *n_t, *dish, *d_l, *d_n, *Klist, *Ltot, *T, *T_ne;
+  double *c0, *cb, *Q, *S1T;   // S1T == nullptr: S1 is read from global memory
+  int ts, ks;
+};
+__device__ __forceinline__ SView cache_view(const SCache &c, const SeqArgs &A) {
+  SView W;
+  W.n_t = c.n_t; W.dish = c.dish; W.d_l = c.d_l; W.d_n = c.d_n;
+  W.c0 = c.c0; W.cb = c.cb; W.Q = c.Q;
+  W.S1T = c.S1T ? c.S1T : A.P.S1T;
+  W.s1s = c.S1T ? c.ks : A.P.KC;
+  W.Klist = c.Klist; W.Ltot = c.Ltot; W.T = c.T; W.T_ne = c.T_ne;
+  W.ts = c.ts; W.ks = c.ks;
+  return W;
+}
+
+// Commit customer i's exact choice c (a table position, or -1 = birth) to the
+// state (oracle SeqSampler::sweep_once body + move); p0 = z[i].  The state is
+// read through W (global or the LDS cache cc) and written to the global
+// arrays and cc.  Block-cooperative: every thread of the block calls it.  A
+// birth draws its dishes against the current state first (wave w < nwd:
+// views w, w + nwd, ...; lp scratch lpw, tree64 scratch treew); if the new table or a
+// new dish does not fit the capacity the state is left unchanged,
+// R->overflow is set and false is returned (the host grows the capacity and
+// the commit is redone, bit for bit: its draws are counter-addressed).
+// cnt: the moves / births / new-dish counters (R->moves... or the run
+// kernel's LDS copies).
+__device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, int i, int p0, int c, double *lpw,
+                           double *treew, int32_t *cnt, int nwd) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
-  __shared__ int s_go, s_ovf, s_i, s_p0, s_c, s_dies, s_born;
+  const int ks = W.ks, ts = W.ts;
+  __shared__ int s_ovf, s_c, s_dies, s_born;
   __shared__ int s_tup[MVC_MAXV], s_j0[MVC_MAXV], s_j1[MVC_MAXV];
+  if (c < 0) {
+    // a birth: dishes drawn against the current state, then the table
+    const bool alive = (W.n_t[p0] - 1) > 0;
+    const Cust C = global_cust(A, i);
+    for (int v = w; v < V && w < nwd; v += nwd) {   // waves w < nwd own a scratch (lpw, treew)
+      const int t = seq_dish_draw(A, W, C, i, v, alive, W.dish[v * ts + p0], lpw, treew);
+      if (lane == 0) s_tup[v] = t;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const int T = *W.T;
+      int ovf = (T + 1 > TC) ? 1 : 0;
+      for (int v = 0; v < V; ++v)
+        if (s_tup[v] == W.Klist[v] && W.Klist[v] + 1 > KC) ovf |= 2;
+      if (ovf) R->overflow = ovf;
+      s_ovf = ovf;
+    }
+    __syncthreads();
+    if (s_ovf) return false;   // nothing changed
+    for (int v = 0; v < V; ++v) {
+      const int j = W.Klist[v];
+      if (s_tup[v] != j) continue;   // uniform (shared + state reads after the barrier)
+      for (int d = tid; d < D; d += blockDim.x) {
+        P.S1T[((size_t)v * D + d) * KC + j] = 0.0;
+        if (cc && cc->S1T) cc->S1T[((size_t)v * D + d) * ks + j] = 0.0;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int v = 0; v < V; ++v) {
+        const int j = W.Klist[v];
+        if (s_tup[v] == j) {
+          P.d_id[v * KC + j] = P.next_id[v]++;
+          P.d_n[v * KC + j] = 0;
+          P.d_l[v * KC + j] = 0;
+          P.S2[v * KC + j] = 0.0;
+          P.Q[v * KC + j] = 0.0;
+          R->Klist[v] = j + 1;
+          if (cc) {
+            cc->d_n[v * ks + j] = 0;
+            cc->d_l[v * ks + j] = 0;
+            cc->Q[v * ks + j] = 0.0;
+            cc->Klist[v] = j + 1;
+          }
+          cnt[2] += 1;
+        }
+      }
+      const int p1 = *W.T;
+      R->T = p1 + 1;
+      P.n_t[p1] = 0;
+      for (int v = 0; v < V; ++v) P.dish[v * TC + p1] = s_tup[v];
+      if (cc) {
+        *cc->T = p1 + 1;
+        cc->n_t[p1] = 0;
+        for (int v = 0; v < V; ++v) cc->dish[v * ts + p1] = s_tup[v];
+      }
+      cnt[1] += 1;
+      s_c = p1;
+    }
+    __syncthreads();
+    c = s_c;
+  }
+  // move i: p0 -> c (oracle SeqSampler::move)
+  if (tid == 0) {
+    const int nt0 = W.n_t[p0] - 1, ntc = W.n_t[c];
+    s_dies = nt0 == 0;
+    s_born = ntc == 0;
+    P.n_t[p0] = nt0;
+    P.n_t[c] = ntc + 1;
+    if (cc) {
+      cc->n_t[p0] = nt0;
+      cc->n_t[c] = ntc + 1;
+    }
+    for (int v = 0; v < V; ++v) {
+      s_j0[v] = W.dish[v * ts + p0];
+      s_j1[v] = W.dish[v * ts + c];
+    }
+    int Tne = *W.T_ne;
+    if (s_dies) --Tne;
+    if (s_born) ++Tne;
+    R->T_ne = Tne;
+    if (cc) *cc->T_ne = Tne;
+    P.z[i] = c;
+  }
+  __syncthreads();
+  if (tid < V && (s_dies || s_born)) {   // table counts of the two tables' dishes
+    const int v = tid;
+    int L = W.Ltot[v];
+    if (s_dies) {
+      const int j = s_j0[v];
+      const int l = W.d_l[v * ks + j] - 1;
+      P.d_l[v * KC + j] = l;
+      if (cc) cc->d_l[v * ks + j] = l;
+      --L;
+    }
+    if (s_born) {
+      const int j = s_j1[v];
+      const int l = W.d_l[v * ks + j] + 1;   // after the decrement above when j == s_j0[v]
+      P.d_l[v * KC + j] = l;
+      if (cc) cc->d_l[v * ks + j] = l;
+      ++L;
+    }
+    P.Ltot[v] = L;
+    if (cc) cc->Ltot[v] = L;
+  }
+  for (int e = tid; e < V * D; e += blockDim.x) {
+    const int v = e / D, d = e - v * D;
+    const int j0 = s_j0[v], j1 = s_j1[v];
+    if (j0 == j1) continue;
+    const double yd = A.y[((size_t)v * n + i) * D + d];
+    const double *src = W.S1T + ((size_t)v * D + d) * W.s1s;
+    const double a0 = src[j0] - yd, a1 = src[j1] + yd;
+    double *col = P.S1T + ((size_t)v * D + d) * KC;
+    col[j0] = a0;
+    col[j1] = a1;
+    if (cc && cc->S1T) {
+      double *cl = cc->S1T + ((size_t)v * D + d) * ks;
+      cl[j0] = a0;
+      cl[j1] = a1;
+    }
+  }
+  if (tid < V) {
+    const int v = tid, j0 = s_j0[v], j1 = s_j1[v];
+    if (j0 != j1) {
+      const double y2 = A.Y2[(size_t)v * n + i];
+      P.S2[v * KC + j0] = P.S2[v * KC + j0] - y2;
+      P.S2[v * KC + j1] = P.S2[v * KC + j1] + y2;
+      const int n0 = W.d_n[v * ks + j0] - 1, n1 = W.d_n[v * ks + j1] + 1;
+      P.d_n[v * KC + j0] = n0;
+      P.d_n[v * KC + j1] = n1;
+      if (cc) {
+        cc->d_n[v * ks + j0] = n0;
+        cc->d_n[v * ks + j1] = n1;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * V) {   // Q and the coefficients of the two dishes (oracle refresh_dish)
+    const int v = tid >> 1, j = (tid & 1) ? s_j1[v] : s_j0[v];
+    if (s_j0[v] != s_j1[v]) {
+      const double q = fma_sq_strided(W.S1T + (size_t)v * D * W.s1s + j, (size_t)W.s1s, D);
+      const Coef cf = coef(W.d_n[v * ks + j], q, P.hyper[v], A.L2pt[v], D);
+      P.Q[v * KC + j] = q;
+      P.c0[v * KC + j] = cf.c0;
+      P.cb[v * KC + j] = cf.cb;
+      if (cc) {
+        cc->Q[v * ks + j] = q;
+        cc->c0[v * ks + j] = cf.c0;
+        cc->cb[v * ks + j] = cf.cb;
+      }
+    }
+  }
+  if (tid == 0) cnt[0] += 1;
+  __syncthreads();
+  return true;
+}
+
+// Resolve the grid window evaluated by the last mvc_seq_eval_kernel (thread 0).
+__device__ void seq_resolve_window(const SeqArgs &A, Repair *R) {
+  const int n = A.P.n;
+  if (R->done || R->overflow || !(R->win1 > R->win0)) return;
+  const int f = R->fmin;
+  if (f < R->win1) {   // the first mover of the window: its choice is exact
+    R->cur = f;
+    R->pend = 1;
+    R->pchoice = A.choice[f];
+    R->W = A.Wmin;
+  } else {             // a mover-free window: every customer in it is final
+    R->cur = R->win1;
+    R->W = min(2 * R->W, A.Wmax);
+  }
+  R->win0 = R->win1 = 0;
+  R->fmin = n;
+}
+
+}  // namespace
+
+// Grid-window repair step (one block of 256 = 4 waves): resolve the last
+// window, commit its first mover, open the next window.
+extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A) {
+  Repair *R = A.R;
+  const int tid = threadIdx.x;
+  const int n = A.P.n;
+  __shared__ int s_go, s_i, s_c;
   if (tid == 0) {
     const int go = !(R->done || R->overflow);
-    if (go && R->win1 > R->win0) {
-      const int f = R->fmin;
-      if (f < R->win1) {
-        R->cur = f;
-        R->pend = 1;
-        R->W = A.Wmin;
-      } else {
-        R->cur = R->win1;
-        R->W = min(2 * R->W, A.Wmax);
-      }
-      R->win0 = R->win1 = 0;
-      R->fmin = n;
-    }
+    seq_resolve_window(A, R);
     if (go) R->rounds += 1;
     s_go = go && R->pend;
-    s_ovf = 0;
     if (s_go) {
       s_i = R->cur;
-      s_p0 = P.z[s_i];
-      s_c = A.choice[s_i];
+      s_c = R->pchoice;
     }
   }
   __syncthreads();
   if (s_go) {
-    const int i = s_i, p0 = s_p0;
-    int c = s_c;
-    if (c < 0) {
-      // a birth: dishes drawn against the current state, then the table
-      const bool alive = (P.n_t[p0] - 1) > 0;
-      const SeqScratch S(A, w);
-      for (int v = w; v < V; v += 4) {
-        const int t = seq_dish_draw(A, i, v, alive, P.dish[v * TC + p0], S);
-        if (lane == 0) s_tup[v] = t;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        int ovf = (R->T + 1 > TC) ? 1 : 0;
-        for (int v = 0; v < V; ++v)
-          if (s_tup[v] == R->Klist[v] && R->Klist[v] + 1 > KC) ovf |= 2;
-        if (ovf) R->overflow = ovf;
-        s_ovf = ovf;
-      }
-      __syncthreads();
-      if (s_ovf) return;   // nothing changed: the host grows and relaunches this step
-      for (int v = 0; v < V; ++v) {
-        if (s_tup[v] != R->Klist[v]) continue;   // uniform (shared + global reads after the barrier)
-        const int j = R->Klist[v];
-        for (int d = tid; d < D; d += blockDim.x) P.S1T[((size_t)v * D + d) * KC + j] = 0.0;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        for (int v = 0; v < V; ++v) {
-          if (s_tup[v] == R->Klist[v]) {
-            const int j = R->Klist[v];
-            P.d_id[v * KC + j] = P.next_id[v]++;
-            P.d_n[v * KC + j] = 0;
-            P.d_l[v * KC + j] = 0;
-            P.S2[v * KC + j] = 0.0;
-            P.Q[v * KC + j] = 0.0;
-            R->Klist[v] = j + 1;
-            R->newdish += 1;
-          }
-        }
-        const int p1 = R->T;
-        R->T = p1 + 1;
-        P.n_t[p1] = 0;
-        for (int v = 0; v < V; ++v) P.dish[v * TC + p1] = s_tup[v];
-        R->births += 1;
-        s_c = p1;
-      }
-      __syncthreads();
-      c = s_c;
-    }
-    // move i: p0 -> c (oracle SeqSampler::move)
+    const SeqScratch S(A, tid >> 6);
+    if (!seq_commit(A, global_view(A), nullptr, s_i, A.P.z[s_i], s_c, S.lp, S.tree, &R->moves, blockDim.x >> 6))
+      return;   // overflow: the host grows and relaunches this step
     if (tid == 0) {
-      P.n_t[p0] -= 1;
-      s_dies = P.n_t[p0] == 0;
-      s_born = P.n_t[c] == 0;
-      if (s_dies) {
-        R->T_ne -= 1;
-        for (int v = 0; v < V; ++v) { P.d_l[v * KC + P.dish[v * TC + p0]] -= 1; P.Ltot[v] -= 1; }
-      }
-      if (s_born) {
-        R->T_ne += 1;
-        for (int v = 0; v < V; ++v) { P.d_l[v * KC + P.dish[v * TC + c]] += 1; P.Ltot[v] += 1; }
-      }
-      P.n_t[c] += 1;
-      for (int v = 0; v < V; ++v) {
-        s_j0[v] = P.dish[v * TC + p0];
-        s_j1[v] = P.dish[v * TC + c];
-      }
-      P.z[i] = c;
-    }
-    __syncthreads();
-    for (int e = tid; e < V * D; e += blockDim.x) {
-      const int v = e / D, d = e - v * D;
-      const int j0 = s_j0[v], j1 = s_j1[v];
-      if (j0 == j1) continue;
-      const double yd = A.y[((size_t)v * n + i) * D + d];
-      double *col = P.S1T + ((size_t)v * D + d) * KC;
-      col[j0] = col[j0] - yd;
-      col[j1] = col[j1] + yd;
-    }
-    if (tid < V) {
-      const int v = tid, j0 = s_j0[v], j1 = s_j1[v];
-      if (j0 != j1) {
-        const double y2 = A.Y2[(size_t)v * n + i];
-        P.S2[v * KC + j0] = P.S2[v * KC + j0] - y2;
-        P.S2[v * KC + j1] = P.S2[v * KC + j1] + y2;
-        P.d_n[v * KC + j0] -= 1;
-        P.d_n[v * KC + j1] += 1;
-      }
-    }
-    __syncthreads();
-    if (tid < 2 * V) {   // Q and the coefficients of the two dishes (oracle refresh_dish)
-      const int v = tid >> 1, j = (tid & 1) ? s_j1[v] : s_j0[v];
-      if (s_j0[v] != s_j1[v]) {
-        const double *col = P.S1T + (size_t)v * D * KC + j;
-        double q = 0.0;
-        for (int d = 0; d < D; ++d) q = __builtin_fma(col[(size_t)d * KC], col[(size_t)d * KC], q);
-        P.Q[v * KC + j] = q;
-        const Coef cf = coef(P.d_n[v * KC + j], q, P.hyper[v], A.L2pt[v], D);
-        P.c0[v * KC + j] = cf.c0;
-        P.cb[v * KC + j] = cf.cb;
-      }
-    }
-    if (tid == 0) {
-      R->cur = i + 1;
+      R->cur = s_i + 1;
       R->pend = 0;
-      R->moves += 1;
     }
-    __syncthreads();
   }
   if (tid == 0 && !(R->done || R->overflow)) {
     if (R->cur >= n) {
@@ -534,23 +824,260 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A
   }
 }
 
+// The run kernel's repair cursor (LDS, owned by thread 0 while the kernel
+// runs; read from R at entry and written back at exit).
+struct RunCursor {
+  int go, stop, cur, pend, pc, pp0, mode, streak, done, i;
+  int32_t cnt[3];                 // moves, births, new dishes
+  int ch[kSeqRunWaves], p0[kSeqRunWaves];
+};
+
+namespace {
+
+// The run kernel's loop, for state read through the LDS cache (kLds) or the
+// global arrays.  Returns through ovf / restride why it stopped early.
+template <bool kLds>
+__device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
+                             double *tree, RunCursor &U, int &ovf, int &restride) {
+  const ParState &P = A.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int V = P.V, D = P.D, n = P.n;
+  for (;;) {
+    // invariant here: U.mode == kSeqRun || U.pend, not done
+    RUN_T0();
+    if (U.pend) {
+      if (!seq_commit(A, Wv, ccp, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt, kLds ? L.nws : (int)(blockDim.x >> 6))) {
+        // overflow: the host grows and relaunches
+        ovf = 1;
+        return;
+      }
+      if (tid == 0) {
+        U.cur = U.cur + 1;
+        U.pend = 0;
+        U.streak = 0;
+      }
+    }
+    if (tid == 0) {
+      U.stop = 0;
+      if (U.cur >= n) {
+        U.done = 1;
+        U.stop = 1;
+      } else if (kLds) {   // the LDS layout must hold the current lists plus one birth
+        int bad = *Wv.T >= L.ts ? 1 : 0;
+        for (int v = 0; v < V; ++v) bad |= Wv.Klist[v] >= L.ks ? 1 : 0;
+        if (bad) U.stop = 2;
+      }
+      U.i = U.cur;
+    }
+    __syncthreads();
+    RUN_MARK(4);
+    if (U.stop) {
+      restride = U.stop == 2;
+      return;
+    }
+    const int i = U.i + w;
+    if (w < L.nws && i < n) {
+      const int p0 = P.z[i];   // customers after cur keep their sweep-start table until committed
+      Cust C;
+      if (kLds) {   // stage the customer's rows in LDS: one memory latency for the whole evaluation
+        for (int e = lane; e < V * D; e += 64) {
+          const int v = e / D, d = e - v * D;
+          S.ys[e] = A.y[((size_t)v * n + i) * D + d];
+        }
+        if (lane < V) S.ys[V * D + lane] = A.Y2[(size_t)lane * n + i];
+        __threadfence_block();
+        C.y = S.ys;
+        C.ystride = (size_t)D;
+        C.Y2 = S.ys + (size_t)V * D;
+        C.y2stride = 1;
+      } else {
+        C = global_cust(A, i);
+      }
+      const int c = seq_resample(A, Wv, C, i, p0, S);
+      if (lane == 0) {
+        U.ch[w] = c;
+        U.p0[w] = p0;
+      }
+    }
+    __syncthreads();
+    RUN_MARK(5);
+    if (tid == 0) {
+      int f = -1;
+      const int m = min(L.nws, n - U.i);
+      for (int k = 0; k < m; ++k)
+        if (U.ch[k] != U.p0[k]) { f = k; break; }
+      if (f >= 0) {
+        U.cur = U.i + f;
+        U.pend = 1;
+        U.pc = U.ch[f];
+        U.pp0 = U.p0[f];
+      } else {
+        U.cur = U.i + m;
+        U.streak += m;
+        if (U.streak >= L.limit) U.mode = kSeqScan;
+        if (U.cur >= n) U.done = 1;
+      }
+      U.go = !U.done && (U.mode == kSeqRun || U.pend);
+    }
+    __syncthreads();
+    RUN_MARK(6);
+#ifdef MVC_RUN_PROF
+    if (tid == 0) A.R->prof[7] += 1;
+#endif
+    if (!U.go) return;
+  }
+}
+
+}  // namespace
+
+// The run kernel (one block of kSeqRunThreads = 8 waves): the
+// repair where movers are dense.  It commits the pending mover, then its nws
+// waves evaluate the next nws customers against the current state in
+// parallel; the first of them that does not stay is the next mover, the
+// ones before it are final.  A loop on the device: no launch and no
+// grid-wide synchronisation per mover.  The state the evaluations read is an
+// LDS copy (SCache, filled at launch, written through by the commits), so a
+// customer costs one memory latency (its y rows) plus LDS work.  After
+// L.limit stays in a row the movers are sparse: the kernel opens a grid
+// window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
+extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
+  extern __shared__ double seq_sm[];
+  Repair *R = A.R;
+  ParState &P = A.P;
+  const int tid = threadIdx.x, w = tid >> 6, nt = blockDim.x;
+  const int V = P.V, D = P.D, n = P.n, KC = P.KC, TC = P.TC;
+  __shared__ RunCursor U;
+  if (tid == 0) {
+    const int go = !(R->done || R->overflow || R->restride);
+    if (go && R->win1 > R->win0) {
+      seq_resolve_window(A, R);
+      if (R->pend) {
+        R->mode = kSeqRun;
+        R->streak = 0;
+      }
+    }
+    if (go) R->rounds += 1;
+    U.go = go;
+    U.cur = R->cur;
+    U.pend = R->pend;
+    U.pc = R->pchoice;
+    U.pp0 = U.pend ? P.z[U.cur] : 0;
+    U.mode = R->mode;
+    U.streak = R->streak;
+    U.done = R->done;
+    U.cnt[0] = R->moves;
+    U.cnt[1] = R->births;
+    U.cnt[2] = R->newdish;
+  }
+  __syncthreads();
+  if (!U.go || !(U.mode == kSeqRun || U.pend)) {
+    if (tid == 0 && U.go && !(R->win1 > R->win0)) {   // scan mode: open the next grid window
+      if (R->cur >= n && !R->pend) {
+        R->done = 1;
+      } else {
+        R->win0 = R->cur;
+        R->win1 = min(n, R->cur + R->W);
+        R->fmin = n;
+      }
+    }
+    return;
+  }
+  int ovf = 0, restride = 0;
+  double *tree = SeqScratch(A, w).tree;   // global per-wave scratch: the dish draws' tree64 levels
+  if (L.lds) {   // the state cache, from the global state at launch
+    SCache cc{};
+    const int ts = L.ts, ks = L.ks;
+    int32_t *ip = (int32_t *)seq_sm;
+    cc.ts = ts;
+    cc.ks = ks;
+    cc.n_t = ip; ip += ts;
+    cc.dish = ip; ip += V * ts;
+    cc.d_l = ip; ip += V * ks;
+    cc.d_n = ip; ip += V * ks;
+    cc.Klist = ip; ip += V;
+    cc.Ltot = ip; ip += V;
+    cc.T = ip++;
+    cc.T_ne = ip++;
+    double *dp = seq_sm + (ip - (int32_t *)seq_sm + 1) / 2;
+    cc.c0 = dp; dp += V * ks;
+    cc.cb = dp; dp += V * ks;
+    cc.Q = dp; dp += V * ks;
+    cc.S1T = L.s1 ? dp : nullptr;
+    const int T = R->T;
+    for (int k = tid; k < T; k += nt) cc.n_t[k] = P.n_t[k];
+    for (int k = tid; k < V * T; k += nt) {
+      const int v = k / T, p = k - v * T;
+      cc.dish[v * ts + p] = P.dish[v * TC + p];
+    }
+    for (int k = tid; k < V * ks; k += nt) {
+      const int v = k / ks, j = k - v * ks;
+      if (j < R->Klist[v]) {
+        cc.d_l[k] = P.d_l[v * KC + j];
+        cc.d_n[k] = P.d_n[v * KC + j];
+        cc.c0[k] = P.c0[v * KC + j];
+        cc.cb[k] = P.cb[v * KC + j];
+        cc.Q[k] = P.Q[v * KC + j];
+      }
+    }
+    if (L.s1) {
+      for (int k = tid; k < V * D * ks; k += nt) {
+        const int row = k / ks, j = k - row * ks;
+        if (j < R->Klist[row / D]) cc.S1T[k] = P.S1T[(size_t)row * KC + j];
+      }
+    }
+    if (tid < V) {
+      cc.Klist[tid] = R->Klist[tid];
+      cc.Ltot[tid] = P.Ltot[tid];
+    }
+    if (tid == 0) {
+      *cc.T = R->T;
+      *cc.T_ne = R->T_ne;
+    }
+    __syncthreads();
+    seq_run_loop<true>(A, L, cache_view(cc, A), &cc, SeqScratch(seq_sm + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
+                       tree, U, ovf, restride);
+  } else {
+    seq_run_loop<false>(A, L, global_view(A), nullptr, SeqScratch(A, w), tree, U, ovf, restride);
+  }
+  if (tid == 0) {   // write the cursor back; open a grid window when handing over
+    R->cur = U.cur;
+    R->pend = U.pend;
+    R->pchoice = U.pc;
+    R->mode = U.mode;
+    R->streak = U.streak;
+    R->moves = U.cnt[0];
+    R->births = U.cnt[1];
+    R->newdish = U.cnt[2];
+    if (restride) R->restride = 1;
+    if (U.done && !U.pend) {
+      R->done = 1;
+    } else if (!ovf && !restride && U.mode == kSeqScan && !U.pend) {
+      R->win0 = U.cur;
+      R->win1 = min(n, U.cur + R->W);
+      R->fmin = n;
+    }
+  }
+}
+
 // The exact conditional of every customer of the pending window against the
 // current state, one wavefront per customer; the first mover by atomicMin.
 extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel(SeqArgs A) {
   Repair *R = A.R;
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (R->done || R->overflow) return;
+  if (R->done || R->overflow || R->restride) return;
   const int w0 = R->win0, w1 = R->win1;
   if (w1 <= w0) return;
   const SeqScratch S(A, gw);
+  const SView W = global_view(A);
   for (int i = w0 + gw; i < w1; i += A.G) {
     const int f = readlane_i(__hip_atomic_load(&R->fmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0);
     if (i > f) break;   // a mover before i: i is re-evaluated after it
-    const int c = seq_resample(A, i, S);
+    const int p0 = A.P.z[i];
+    const int c = seq_resample(A, W, global_cust(A, i), i, p0, S);
     if (lane == 0) {
       A.choice[i] = c;
-      if (c != A.P.z[i]) atomicMin(&R->fmin, i);
+      if (c != p0) atomicMin(&R->fmin, i);
     }
   }
 }

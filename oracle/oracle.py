@@ -199,28 +199,32 @@ def tree64_select(x, r):
 
 
 def ari(a, b):
-    """Adjusted Rand index, restating mclust::adjustedRandIndex (the ARI of
-    New_Simulation.R:6,189; mclust is an R package absent here): exact pair
-    counts a, b, c, d from the contingency table, then its fp64 expression in
-    R's left-to-right operation order.  Pinned against scikit-learn's
-    adjusted_rand_score (the same Hubert-Arabie index) in tests/test_ari.py."""
-    from collections import Counter
-    a = np.asarray(a).ravel()
-    b = np.asarray(b).ravel()
+    """Adjusted Rand index, restating mcclust::arandi(cl1, cl2, adjust = TRUE)
+    (the ARI of New_Simulation.R:5,189; mcclust is an R package absent here,
+    restated from its published source):
+        tab.1 <- table(cl1); tab.2 <- table(cl2); tab.12 <- table(cl1, cl2)
+        correc <- sum(choose(tab.1,2)) * sum(choose(tab.2,2)) / choose(n,2)
+        (sum(choose(tab.12,2)) - correc) /
+            (0.5*sum(choose(tab.1,2)) + 0.5*sum(choose(tab.2,2)) - correc)
+    R's choose(k, 2) of a count is the exact integer (nmath choose.c), so the
+    three pair sums are exact integers; the fp64 expression then runs in R's
+    left-to-right order.  A 1 x 1 table is 0/0 = NaN, as in R.  Pinned
+    against scikit-learn's adjusted_rand_score (the same Hubert-Arabie index)
+    in tests/test_ari.py."""
+    a = np.asarray(a).ravel().astype(np.int64)
+    b = np.asarray(b).ravel().astype(np.int64)
     assert a.shape == b.shape
     n = int(a.size)
-    tab = Counter(zip(a.tolist(), b.tolist()))
-    rows = Counter(a.tolist())
-    cols = Counter(b.tolist())
-    if len(rows) == 1 and len(cols) == 1:
-        return 1.0
-    ch2 = lambda k: k * (k - 1) // 2  # noqa: E731
-    A = sum(ch2(v) for v in tab.values())
-    B = sum(ch2(v) for v in rows.values()) - A
-    C = sum(ch2(v) for v in cols.values()) - A
-    Dd = ch2(n) - A - B - C
-    a_, b_, c_ = float(A), float(B), float(C)
-    d_ = ((float(ch2(n)) - a_) - b_) - c_
-    assert d_ == float(Dd)
-    e = (a_ + b_) * (a_ + c_) / (((a_ + b_) + c_) + d_)
-    return (a_ - e) / ((((a_ + b_) + a_) + c_) / 2.0 - e)
+
+    def pair_sum(labels):   # sum(choose(table(labels), 2)), exact integer
+        _, cnt = np.unique(labels, return_counts=True, axis=0)
+        cnt = cnt.astype(np.int64)
+        return int(np.sum(cnt * (cnt - 1) // 2))
+
+    A = pair_sum(np.stack([a, b], axis=1))
+    SA, SB = pair_sum(a), pair_sum(b)
+    a_, sa, sb = np.float64(A), np.float64(SA), np.float64(SB)
+    nn = np.float64(n * (n - 1) // 2)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        correc = (sa * sb) / nn
+        return float((a_ - correc) / ((np.float64(0.5) * sa + np.float64(0.5) * sb) - correc))

@@ -1,8 +1,8 @@
-"""ARI (the caller's mclust::adjustedRandIndex, New_Simulation.R:189).
+"""ARI (the caller's mcclust::arandi, New_Simulation.R:5,189).
 
 CPU: the oracle restatement pinned against scikit-learn's adjusted_rand_score
-(the same Hubert-Arabie index; mclust itself is an R package absent here) and
-known answers.  GPU: the device ARI (C ABI) equals the oracle bit for bit,
+(the same Hubert-Arabie index; mcclust itself is an R package absent here) and
+known answers, including arandi's NaN for a 1 x 1 table.  GPU: the device ARI (C ABI) equals the oracle bit for bit,
 including on a sampler's own state."""
 import numpy as np
 import pytest
@@ -31,8 +31,10 @@ def test_oracle_ari_known_answers():
     a = np.array([0, 0, 1, 1, 2, 2])
     assert O.ari(a, a) == 1.0
     assert O.ari(a, 5 - a) == 1.0                     # label permutation
-    assert O.ari(np.zeros(7, int), np.ones(7, int)) == 1.0   # mclust: 1 x 1 table
-    # mclust documentation-style example: two 3-cluster labelings of 6 items
+    assert np.isnan(O.ari(np.zeros(7, int), np.ones(7, int)))   # arandi: 1 x 1 table is 0/0
+    # two 3-cluster labelings of 6 items: a = 2, sa = 6, sb = 3, C(6,2) = 15,
+    # correc = 18/15 = 1.2, (2 - 1.2) / (4.5 - 1.2) in R's fp64 order
+    assert O.ari([0, 0, 0, 1, 1, 1], [0, 0, 1, 1, 2, 2]) == (2.0 - 18.0 / 15.0) / ((0.5 * 6 + 0.5 * 3) - 18.0 / 15.0)
     assert np.isclose(O.ari([0, 0, 0, 1, 1, 1], [0, 0, 1, 1, 2, 2]), 0.24242424242424243)
 
 
@@ -41,6 +43,7 @@ def test_device_ari_bitwise_vs_oracle():
     import mvc_amd
     for a, b in _cases():
         assert mvc_amd.ari(a, b) == O.ari(a, b)
+    assert np.isnan(mvc_amd.ari(np.zeros(9, int), np.full(9, 4)))   # arandi: 1 x 1 table
     rng = np.random.default_rng(3)
     a = rng.integers(0, 64, 1_000_000)
     b = np.where(rng.random(a.size) < 0.1, rng.integers(0, 64, a.size), a % 16)

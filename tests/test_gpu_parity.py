@@ -534,3 +534,22 @@ def test_timing_levels_do_not_change_the_chain():
         assert np.array_equal(np.asarray(a), np.asarray(b))
     s.close()
     ref.close()
+
+
+@pytest.mark.parametrize("waves,repair", [("1", "run"), ("3", "run"), ("8", "grid")])
+def test_repair_shapes_same_chain(waves, repair, monkeypatch):
+    """The repair's execution shape does not change the chain: the run kernel
+    evaluating 1 or 3 customers per step (fewer waves than the V = 5 views,
+    so birth dish draws wrap over the waves), and the grid-window path alone
+    (MVC_REPAIR=grid), all bitwise vs oracle SeqSampler through the births of
+    a cold start."""
+    monkeypatch.setenv("MVC_RUN_WAVES", waves)
+    monkeypatch.setenv("MVC_REPAIR", repair)
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(1999)
+    s = m.Sampler(y, seed=13, mode="parallel")
+    ref = O.run(y, 10, 0, 1, seed=13, mode=O.PARALLEL)
+    _check_sweeps(s, ref, 10, stats=False)
+    assert sum(ref["trace_births"]) > 0
+    s.close()

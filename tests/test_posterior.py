@@ -97,3 +97,41 @@ def test_jacobi_schedule_is_biased():
     # sigma_g and the table count are far outside any Monte-Carlo tolerance
     assert z[1] > 10 and z[2] > 10
     assert fj[:, 1].mean() > 0.5 > fe[:, 1].mean()
+
+
+@pytest.mark.gpu
+def test_gpu_parallel_chains_match_reference_posterior():
+    """The same check with the GPU's own chains: 16 parallel-mode chains in one
+    handle on the MI355X (libmvc_hip.so, the sequential schedule executed as
+    a data-parallel pass + in-order repair) against 16 reference-schedule
+    chains of the oracle (mode EXACT, glibc libm) on the configs[0] shape."""
+    sys.path.insert(0, os.path.join(ROOT, "multiview-clustering_amd"))
+    import mvc_amd
+    M, burn = 2500, 500
+    fe, ce = _chains("config1", O.EXACT, M, burn)
+    y = _shape("config1")
+    V, n = y.shape[0], y.shape[1]
+    s = mvc_amd.Sampler(y, seed=2024, mode="parallel", n_chains=CHAINS)
+    feats = np.zeros((CHAINS, 3 + 3 * V))
+    cc = np.zeros((CHAINS, n, n))
+    acc = [[] for _ in range(CHAINS)]
+    for it in range(M):
+        s.sweep(1)
+        if it < burn:
+            continue
+        for c in range(CHAINS):
+            t, d, h = s.state(chain=c)
+            cc[c] += t[:, None] == t[None, :]
+            acc[c].append(np.concatenate([[h["alpha_global"], h["sigma_global"], d.shape[1]],
+                                          h["alpha_v"], h["sigma_v"], h["tau_v"]]))
+    s.close()
+    for c in range(CHAINS):
+        feats[c] = np.mean(acc[c], axis=0)
+    cc /= (M - burn)
+    z = _zscores(fe, feats)
+    bad = [(n_, round(float(z_), 2)) for n_, z_ in zip(_names(V), z) if z_ > 4.0]
+    assert not bad, f"GPU posterior means differ from the reference schedule beyond 4 MCSE: {bad}"
+    iu = np.triu_indices(n, 1)
+    zc = _zscores(ce[:, iu[0], iu[1]], cc[:, iu[0], iu[1]])
+    assert zc.max() < 6.0, f"co-clustering entry at {zc.max():.2f} MCSE"
+    assert (zc > 4.0).mean() <= 1e-3
