@@ -158,7 +158,7 @@ class Sampler:
 
     def ari(self, truth, chain=0):
         """Adjusted Rand index of the chain's current table labels against
-        truth[n] (mclust::adjustedRandIndex, New_Simulation.R:189), on the device."""
+        truth[n] (mcclust::arandi, New_Simulation.R:189), on the device."""
         t = np.ascontiguousarray(truth, dtype=np.int32)
         if t.shape != (self.n,):
             raise ValueError(f"truth must have shape ({self.n},)")
@@ -274,7 +274,7 @@ class Sampler:
 
 # ---- spec primitives on the device (parity tests) ----
 def ari(a, b, device=0):
-    """Adjusted Rand index of two int32 labelings (mclust::adjustedRandIndex,
+    """Adjusted Rand index of two int32 labelings (mcclust::arandi,
     the ARI of New_Simulation.R:189), computed on the device."""
     a = np.ascontiguousarray(a, dtype=np.int32)
     b = np.ascontiguousarray(b, dtype=np.int32)
