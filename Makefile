@@ -6,7 +6,7 @@ SRC := $(PKG)/csrc
 LIB := $(PKG)/lib/libmvc_hip.so
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
-HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+HIPFLAGS := $(EXTRA) -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
             -I$(ROOT)/include -I$(SRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-const-variable
 OBJS := $(PKG)/build/mvc_exact.o $(PKG)/build/mvc_parallel.o $(PKG)/build/mvc_spec.o $(PKG)/build/mvc_ari.o \
         $(PKG)/build/mvc_api.o

@@ -25,10 +25,15 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--sweeps", type=int, default=5)
     ap.add_argument("--budget-s", type=float, default=120.0)
+    ap.add_argument("--warm", action="store_true", help="start at the generating partition (bench.py warm_state)")
+    ap.add_argument("--seed", type=int, default=7)
     a = ap.parse_args()
     N, V, D, K = CONFIGS[a.config]
-    y, _ = data.synthetic(N, V, D, K, seed=1999)
-    s = mvc_amd.Sampler(y, seed=7, mode="parallel")
+    y, z = data.synthetic(N, V, D, K, seed=1999)
+    s = mvc_amd.Sampler(y, seed=a.seed, mode="parallel")
+    if a.warm:
+        import bench
+        s.set_state(*bench.warm_state(z, V, K))
     s.synchronize()
     t_all = time.perf_counter()
     for it in range(a.sweeps):
