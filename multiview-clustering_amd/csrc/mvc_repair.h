@@ -64,9 +64,8 @@ constexpr int kSeqRunThreads = 512, kSeqRunWaves = kSeqRunThreads / 64;
 // lp [V][ks] | e [ts + 16] | B, C [ts/16 + 2]; nws waves speculate.
 // lds = 0: the per-wave global scratch (SeqArgs.scr) instead.
 // LDS of the run kernel: the state cache (SCache: n_t [ts], dish [V][ts],
-// d_l, d_n [V][ks], Klist, Ltot [V], T, T_ne; c0, cb, Q [V][ks]; S1T
-// [V][D][ks] when s1) and per-wave scratch lp [V][ks] | e [ts + 16] | B, C
-// [ts/16 + 2] | y rows [V][D] | Y2 [V].
+// d_l, d_n [V][ks], Klist, Ltot [V], T, T_ne; c0, cb, Q, xm, ym, cbm [V][ks];
+// lmass [ts]; S1T [V][D][ks] when s1) and the per-wave scratch (SeqScratch).
 struct SeqLds {
   int32_t lds, nws, ks, ts;
   int32_t limit;        // stays in a row after which the run kernel hands over to the grid windows
@@ -75,11 +74,11 @@ struct SeqLds {
   int64_t stride;       // doubles per wave
 };
 __host__ __device__ inline int64_t seq_lds_stride(int V, int D, int ks, int ts) {
-  return (int64_t)V * ks + ts + 16 + 2 * (ts / 16 + 2) + (int64_t)V * D + V;
+  return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + 2;
 }
 __host__ __device__ inline int64_t seq_lds_cache(int V, int D, int ks, int ts, bool s1) {
   const int64_t ints = (int64_t)ts + (int64_t)V * ts + 2 * (int64_t)V * ks + 2 * V + 2;
-  return (ints + 1) / 2 + 3 * (int64_t)V * ks + (s1 ? (int64_t)V * D * ks : 0);
+  return (ints + 1) / 2 + 6 * (int64_t)V * ks + ts + (s1 ? (int64_t)V * D * ks : 0);
 }
 
 struct SeqArgs {
@@ -102,38 +101,44 @@ struct SeqArgs {
 
 namespace {
 
-// per-wave scratch: lp [V][KC] | table scores / weights [TC] | block sums
-// [TC/16+1] | running totals [TC/16+1] | dish-draw tree levels
+// per-wave scratch: lp [V][ks] | aux [V][ks] (dish terms) | table scores /
+// weights [ts + 16] | block sums [ts/16 + 2] | per-view max [V] | view
+// offsets [V + 1] | (run kernel) y rows [V][D] + Y2 [V] | (global) the
+// dish-draw tree levels
 struct SeqScratch {
-  double *lp, *e, *B, *C, *tree;
+  double *lp, *aux, *e, *B, *mv, *tree;
+  int32_t *koff;
   double *ys;   // run kernel: the customer's y rows [V][D] and Y2 [V]
-  int lps;   // lp stride per view
-  __device__ SeqScratch(const SeqArgs &A, int wave) {
-    double *base = A.scr + (int64_t)wave * A.scr_stride;
-    lps = A.P.KC;
-    lp = base;
-    e = lp + (size_t)A.P.V * A.P.KC;
-    B = e + A.P.TC + 16;
-    C = B + A.P.TC / 16 + 2;
-    tree = C + A.P.TC / 16 + 2;
-    ys = nullptr;
-  }
-  // run kernel, LDS: lp [V][ks] | e [ts + 16] | B | C | y rows (no dish-draw tree)
-  __device__ SeqScratch(double *base, int V, int ks, int ts) {
+  int lps;      // lp / aux stride per view
+  __device__ void carve(double *base, int V, int ks, int ts) {
     lps = ks;
     lp = base;
-    e = lp + (size_t)V * ks;
+    aux = lp + (size_t)V * ks;
+    e = aux + (size_t)V * ks;
     B = e + ts + 16;
-    C = B + ts / 16 + 2;
-    ys = C + ts / 16 + 2;
+    mv = B + ts / 16 + 2;
+    koff = (int32_t *)(mv + V);   // [V + 1] view offsets, then [V] K_act
+    ys = mv + V + V + 2;
+  }
+  __device__ SeqScratch(const SeqArgs &A, int wave) {
+    carve(A.scr + (int64_t)wave * A.scr_stride, A.P.V, A.P.KC, A.P.TC);
+    tree = ys;   // the global scratch has no staged rows
+    ys = nullptr;
+  }
+  // run kernel, LDS (no dish-draw tree)
+  __device__ SeqScratch(double *base, int V, int ks, int ts) {
+    carve(base, V, ks, ts);
     tree = nullptr;
   }
 };
+__host__ __device__ inline int64_t seq_scratch_head(int V, int ks, int ts) {
+  return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2;
+}
 __host__ inline int64_t seq_scratch_stride(int V, int TC, int KC) {
   // tree levels: K+1 leaves, then ceil(./64) ... (< (K+1)/63 + 3 more)
   const int64_t leaves = (int64_t)KC + 1;
   const int64_t tree = leaves + leaves / 63 + 8;
-  return (int64_t)V * KC + TC + 16 + 2 * (TC / 16 + 2) + tree + 64;
+  return seq_scratch_head(V, KC, TC) + tree + 64;
 }
 
 // oracle pw16: pairs (c, c + h) for h = 1, 2, 4, 8
@@ -253,6 +258,8 @@ struct SView {
   const int32_t *n_t, *dish;
   const int32_t *d_l, *d_n;
   const double *c0, *cb, *Q;
+  const double *xm, *ym, *cbm;   // self-removal coefficient parts (nullptr: computed per use)
+  const double *lmass;           // [ts] log(n_t - sigma_g)
   const double *S1T;
   const int32_t *Klist, *Ltot, *T, *T_ne;
   int ts, ks, s1s;
@@ -263,6 +270,8 @@ __device__ __forceinline__ SView global_view(const SeqArgs &A) {
   G.n_t = P.n_t; G.dish = P.dish;
   G.d_l = P.d_l; G.d_n = P.d_n;
   G.c0 = P.c0; G.cb = P.cb; G.Q = P.Q;
+  G.xm = G.ym = G.cbm = nullptr;
+  G.lmass = P.lmass;
   G.S1T = P.S1T;
   G.Klist = A.R->Klist; G.Ltot = P.Ltot; G.T = &A.R->T; G.T_ne = &A.R->T_ne;
   G.ts = P.TC; G.ks = P.KC; G.s1s = P.KC;
@@ -333,108 +342,228 @@ __device__ int seq_view_lp(const SeqArgs &A, const SView &W, const Cust &C, int 
   return nl;
 }
 
-// lm_v of oracle eval_view_seq (column partials j mod 16 in ascending j,
-// pw16 over the columns, then the new dish); lp[] from seq_view_lp.
-__device__ double seq_view_marg(const SeqArgs &A, const SView &W, const Cust &C, int v, bool alive, int j0,
-                                double *lp) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int V = P.V, ks = W.ks;
-  const int K = W.Klist[v];
-  const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-  double m;
-  const int Kact = seq_view_lp(A, W, C, v, alive, j0, lp, &m);
-  __threadfence_block();
-  const double Y2i = C.Y2[(size_t)v * C.y2stride];
-  const double h = (-0.5 * Y2i) / tau;
-  const double lfn = A.cnew[v] + h;
-  if (lfn > m) m = lfn;
-  const int l0p = alive ? W.d_l[v * ks + j0] : W.d_l[v * ks + j0] - 1;
-  double col = 0.0;
-  if (lane < 16) {
-    for (int j = lane; j < K; j += 16) {
-      const int l = (j == j0) ? l0p : W.d_l[v * ks + j];
-      if (l > 0) {
-        double w = (double)l - sigma;
-        if (w < 0.0) w = 0.0;
-        col = col + w * mvc_exp(lp[j] - m);
-      }
-    }
-  }
-  double cols[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) cols[c] = readlane_d(col, c);
-  double S = pw16_seq(cols);
-  double wn = alpha + (double)Kact * sigma;
-  if (wn < 0.0) wn = 0.0;
-  S = S + wn * mvc_exp(lfn - m);
-  const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
-  if (denom <= 0.0) return lfn;
-  return (m + mvc_log(S)) - mvc_log(denom);
+// pw16 of the 16 lanes of each row (pairs (c, c + h), h = 1, 2, 4, 8: the
+// oracle's pw16 association), broadcast to the row.
+__device__ __forceinline__ double row_pw16(double x) {
+  x = x + down_d<1>(x);
+  x = x + down_d<2>(x);
+  x = x + down_d<4>(x);
+  x = x + down_d<8>(x);
+  return row_bcast0_d(x);
+}
+__device__ __forceinline__ int row16_isum(int x) {
+  x += __shfl_xor(x, 1, 64);
+  x += __shfl_xor(x, 2, 64);
+  x += __shfl_xor(x, 4, 64);
+  x += __shfl_xor(x, 8, 64);
+  return x;
 }
 
 // Exact conditional draw of customer i against the current state (oracle
-// ParallelSampler::resample_customer): a table position, or -1 = birth.
-// p0 = z[i] (the customer's table before this sweep's decision).
+// ParallelSampler::resample_customer + eval_view_seq): a table position, or
+// -1 = birth.  p0 = z[i] (the customer's table before this sweep's
+// decision).  One wavefront, shaped for latency (the repair's serial chain):
+// every view's dishes in one lane-parallel pass (lp, then the weighted
+// terms), the per-view column sums / pw16 / marginal of four views at once
+// on the four 16-lane rows, table weights with their block sums by row DPP,
+// running block totals through readlanes.  Same operations in the same
+// order per quantity as the oracle, so the same bits.
 __device__ int seq_resample(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S) {
   const ParState &P = A.P;
-  const int lane = threadIdx.x & 63;
-  const int V = P.V, ts = W.ts;
-  const bool alive = (W.n_t[p0] - 1) > 0;
+  const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
+  const int V = P.V, D = P.D, ts = W.ts, ks = W.ks, lps = S.lps;
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const int np0 = W.n_t[p0] - 1;
+  const bool alive = np0 > 0;
   const int Tne_i = *W.T_ne - (alive ? 0 : 1);
+  const double mass0 = (double)np0 - sg;
+  const double lmass0 = (np0 >= 1 && mass0 > 0.0) ? mvc_log(mass0) : 0.0;   // the own table, customer removed
   RUN_T0();
-  double s_new = mvc_log(ag + sg * (double)Tne_i);
-  for (int v = 0; v < V; ++v)
-    s_new = s_new + seq_view_marg(A, W, C, v, alive, W.dish[v * ts + p0], S.lp + (size_t)v * S.lps);
+  if (lane == 0) {   // offsets of the views in the concatenated dish list
+    int acc = 0;
+    for (int v = 0; v < V; ++v) {
+      S.koff[v] = acc;
+      acc += W.Klist[v];
+    }
+    S.koff[V] = acc;
+  }
   __threadfence_block();
+  const int NK = S.koff[V];
+  // pass 1: lp of every listed dish (the own dish j0 with the customer removed)
+  for (int g0 = 0; g0 < NK; g0 += 64) {
+    const int g = g0 + lane;
+    if (g < NK) {
+      int v = 0;
+      while (g >= S.koff[v + 1]) ++v;
+      const int j = g - S.koff[v];
+      const double tau = P.hyper[v];
+      const double Y2i = C.Y2[(size_t)v * C.y2stride];
+      const double hy = 0.5 * Y2i;
+      const double h = (-0.5 * Y2i) / tau;
+      const double G = fma_dot_strided(C.y + (size_t)v * C.ystride, W.S1T + (size_t)v * D * W.s1s + j, (size_t)W.s1s, D, 0.0);
+      double val;
+      if (j == W.dish[v * ts + p0]) {
+        const double Gp = G - Y2i;
+        const double Qp = (W.Q[v * ks + j] - 2.0 * G) + Y2i;
+        double c0, cb;
+        if (W.xm) {
+          c0 = W.xm[v * ks + j] - (0.5 * Qp) / W.ym[v * ks + j];
+          cb = W.cbm[v * ks + j];
+        } else {
+          const Coef c = coef(W.d_n[v * ks + j] - 1, Qp, tau, A.L2pt[v], D);
+          c0 = c.c0;
+          cb = c.cb;
+        }
+        val = __builtin_fma(Gp + hy, cb, c0) + h;
+      } else {
+        val = __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
+      }
+      S.lp[v * lps + j] = val;
+    }
+  }
+  __threadfence_block();
+  // per view (four views at once, view vg + row): max over the included
+  // dishes (l' > 0) and the new dish, and K_act
+  double lfn_r = 0.0, m_r = 0.0;   // of this row's view, per group (recomputed below)
+  for (int vg = 0; vg < V; vg += 4) {
+    const int v = vg + row;
+    double mx = -MVC_PM_INF;
+    int cnt = 0;
+    if (v < V) {
+      const int K = W.Klist[v];
+      const int j0 = W.dish[v * ts + p0];
+      for (int j = col; j < K; j += 16) {
+        const int l = W.d_l[v * ks + j] - ((j == j0 && !alive) ? 1 : 0);
+        if (l > 0) {
+          ++cnt;
+          const double x = S.lp[v * lps + j];
+          if (x > mx) mx = x;
+        }
+      }
+    }
+    mx = row16_max(mx);
+    cnt = row16_isum(cnt);
+    if (v < V && col == 0) {
+      const double Y2i = C.Y2[(size_t)v * C.y2stride];
+      const double lfn = A.cnew[v] + (-0.5 * Y2i) / P.hyper[v];
+      S.mv[v] = lfn > mx ? lfn : mx;
+      S.koff[V + 1 + v] = cnt;   // K_act (koff has room: [V + 1] offsets then [V] counts)
+    }
+  }
+  __threadfence_block();
+  // pass 2: the weighted terms w_j exp(lp_j - m_v) of every included dish, 0 otherwise
+  for (int g0 = 0; g0 < NK; g0 += 64) {
+    const int g = g0 + lane;
+    if (g < NK) {
+      int v = 0;
+      while (g >= S.koff[v + 1]) ++v;
+      const int j = g - S.koff[v];
+      const int l = W.d_l[v * ks + j] - ((j == W.dish[v * ts + p0] && !alive) ? 1 : 0);
+      double t = 0.0;
+      if (l > 0) {
+        double w = (double)l - P.hyper[2 * V + v];
+        if (w < 0.0) w = 0.0;
+        t = w * mvc_exp(S.lp[v * lps + j] - S.mv[v]);
+      }
+      S.aux[v * lps + j] = t;
+    }
+  }
+  __threadfence_block();
+  // per view (four at once): column partials j mod 16 in ascending j, pw16,
+  // the new dish, lm_v; s_new in view order
+  double s_new = mvc_log(ag + sg * (double)Tne_i);
+  for (int vg = 0; vg < V; vg += 4) {
+    const int v = vg + row;
+    double lm = 0.0;
+    double cs = 0.0;
+    if (v < V) {
+      const int K = W.Klist[v];
+      for (int j = col; j < K; j += 16) cs = cs + S.aux[v * lps + j];
+    }
+    double Sv = row_pw16(cs);
+    if (v < V) {
+      const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+      const double Y2i = C.Y2[(size_t)v * C.y2stride];
+      const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
+      const double m = S.mv[v];
+      double wn = alpha + (double)S.koff[V + 1 + v] * sigma;
+      if (wn < 0.0) wn = 0.0;
+      Sv = Sv + wn * mvc_exp(lfn - m);
+      const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
+      lm = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - mvc_log(denom);
+    }
+    for (int r = 0; r < 4 && vg + r < V; ++r) s_new = s_new + readlane_d(lm, 16 * r);
+  }
+  (void)lfn_r; (void)m_r;
   RUN_MARK(0);
+  // table scores: log(n_p' - sigma_g) + sum_v lp_{v, dish_v(p)} (view order)
   const int T = *W.T;
   const int TB = (T + 15) / 16;
   double M = -MVC_PM_INF;
-  for (int p = lane; p < TB * 16; p += 64) {
+  for (int q0 = 0; q0 < TB * 16; q0 += 64) {
+    const int p = q0 + lane;
     double sp = -MVC_PM_INF;
     if (p < T) {
       const int np = W.n_t[p] - (p == p0 ? 1 : 0);
       const double mass = (double)np - sg;
       if (np >= 1 && mass > 0.0) {
-        sp = mvc_log(mass);
-        for (int v = 0; v < V; ++v) sp = sp + S.lp[(size_t)v * S.lps + W.dish[v * ts + p]];
+        sp = (p == p0) ? lmass0 : W.lmass[p];
+        for (int v = 0; v < V; ++v) sp = sp + S.lp[v * lps + W.dish[v * ts + p]];
       }
     }
-    S.e[p] = sp;
+    if (p < TB * 16) S.e[p] = sp;
     if (sp > M) M = sp;
   }
   M = wave_max(M);
   if (s_new > M) M = s_new;
   __threadfence_block();
   RUN_MARK(1);
-  for (int p = lane; p < TB * 16; p += 64) {
-    const double x = S.e[p];
-    S.e[p] = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
+  // weights exp(sp - M) (0 for excluded / padding), block sums by row pw16
+  for (int q0 = 0; q0 < TB * 16; q0 += 64) {
+    const int p = q0 + lane;
+    double wgt = 0.0;
+    if (p < TB * 16) {
+      const double x = S.e[p];
+      wgt = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
+      S.e[p] = wgt;
+    }
+    const double Bv = row_pw16(wgt);
+    const int b = (q0 >> 4) + row;
+    if (col == 0 && b < TB) S.B[b] = Bv;
   }
   __threadfence_block();
-  for (int b = lane; b < TB; b += 64) S.B[b] = pw16_seq(S.e + (size_t)b * 16);
-  __threadfence_block();
   RUN_MARK(2);
-  // running block totals C_b (wave-uniform loops over the LDS block sums;
-  // the second pass recomputes the same sums to find the block)
+  // running block totals C_b (in block order) through readlanes of the block sums
   double tot = 0.0;
-  for (int b = 0; b < TB; ++b) tot = tot + S.B[b];
+  for (int b0 = 0; b0 < TB; b0 += 64) {
+    const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
+    const int nb = min(64, TB - b0);
+    for (int k = 0; k < nb; ++k) tot = tot + readlane_d(Bl, k);
+  }
   const double Wt = mvc_exp(s_new - M) + tot;
   double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
   int pick = -1;
   if (r < tot) {
-    int b = 0;
-    double cprev = 0.0;
-    for (;; ++b) {
-      const double cb = cprev + S.B[b];
-      if (r < cb) break;
-      cprev = cb;
+    double c = 0.0, cprev = 0.0;
+    int bsel = TB - 1;
+    bool found = false;
+    for (int b0 = 0; b0 < TB && !found; b0 += 64) {
+      const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
+      const int nb = min(64, TB - b0);
+      for (int k = 0; k < nb; ++k) {
+        const double c2 = c + readlane_d(Bl, k);
+        if (r < c2) {
+          bsel = b0 + k;
+          cprev = c;
+          found = true;
+          break;
+        }
+        c = c2;
+      }
     }
     r = r - cprev;
-    const double x = lane < 16 ? S.e[(size_t)b * 16 + lane] : 0.0;
-    pick = b * 16 + pw16_select_wave(x, r);
+    const double x = lane < 16 ? S.e[bsel * 16 + lane] : 0.0;
+    pick = bsel * 16 + pw16_select_wave(x, r);
   }
   RUN_MARK(3);
   return pick;
@@ -575,18 +704,31 @@ namespace {
 // write of the commit goes to the global arrays and, when present, here.
 struct SCache {
   int32_t *n_t, *dish, *d_l, *d_n, *Klist, *Ltot, *T, *T_ne;
-  double *c0, *cb, *Q, *S1T;   // S1T == nullptr: S1 is read from global memory
+  double *c0, *cb, *Q, *xm, *ym, *cbm, *lmass;
+  double *S1T;   // nullptr: S1 is read from global memory
   int ts, ks;
 };
 __device__ __forceinline__ SView cache_view(const SCache &c, const SeqArgs &A) {
   SView W;
   W.n_t = c.n_t; W.dish = c.dish; W.d_l = c.d_l; W.d_n = c.d_n;
   W.c0 = c.c0; W.cb = c.cb; W.Q = c.Q;
+  W.xm = c.xm; W.ym = c.ym; W.cbm = c.cbm; W.lmass = c.lmass;
   W.S1T = c.S1T ? c.S1T : A.P.S1T;
   W.s1s = c.S1T ? c.ks : A.P.KC;
   W.Klist = c.Klist; W.Ltot = c.Ltot; W.T = c.T; W.T_ne = c.T_ne;
   W.ts = c.ts; W.ks = c.ks;
   return W;
+}
+
+// The parts of coef(n - 1, Qp) that do not depend on the customer (the own
+// dish's self-removed coefficient, §4.2): c0 = xm - (0.5 Qp) / ym, cb = cbm.
+__device__ __forceinline__ void self_coef_parts(int n_, double tau, double L2pt, int D, double &xm, double &ym,
+                                                double &cbm) {
+  const double a = tau + (double)(n_ - 1);
+  const double b = tau + (double)n_;
+  xm = (double)D * ((-0.5 * L2pt) - 0.5 * mvc_log(b / a));
+  ym = (tau * a) * b;
+  cbm = 1.0 / (tau * b);
 }
 
 // Commit customer i's exact choice c (a table position, or -1 = birth) to the
@@ -678,9 +820,15 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, int i, 
     s_born = ntc == 0;
     P.n_t[p0] = nt0;
     P.n_t[c] = ntc + 1;
+    const double sg = P.hyper[3 * V + 1];
+    const double lm0 = mvc_log((double)nt0 - sg), lmc = mvc_log((double)(ntc + 1) - sg);
+    P.lmass[p0] = lm0;
+    P.lmass[c] = lmc;
     if (cc) {
       cc->n_t[p0] = nt0;
       cc->n_t[c] = ntc + 1;
+      cc->lmass[p0] = lm0;
+      cc->lmass[c] = lmc;
     }
     for (int v = 0; v < V; ++v) {
       s_j0[v] = W.dish[v * ts + p0];
@@ -758,6 +906,8 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, int i, 
         cc->Q[v * ks + j] = q;
         cc->c0[v * ks + j] = cf.c0;
         cc->cb[v * ks + j] = cf.cb;
+        self_coef_parts(W.d_n[v * ks + j], P.hyper[v], A.L2pt[v], D, cc->xm[v * ks + j], cc->ym[v * ks + j],
+                        cc->cbm[v * ks + j]);
       }
     }
   }
@@ -1002,9 +1152,16 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(
     cc.c0 = dp; dp += V * ks;
     cc.cb = dp; dp += V * ks;
     cc.Q = dp; dp += V * ks;
+    cc.xm = dp; dp += V * ks;
+    cc.ym = dp; dp += V * ks;
+    cc.cbm = dp; dp += V * ks;
+    cc.lmass = dp; dp += ts;
     cc.S1T = L.s1 ? dp : nullptr;
     const int T = R->T;
-    for (int k = tid; k < T; k += nt) cc.n_t[k] = P.n_t[k];
+    for (int k = tid; k < T; k += nt) {
+      cc.n_t[k] = P.n_t[k];
+      cc.lmass[k] = P.lmass[k];
+    }
     for (int k = tid; k < V * T; k += nt) {
       const int v = k / T, p = k - v * T;
       cc.dish[v * ts + p] = P.dish[v * TC + p];
@@ -1017,6 +1174,7 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(
         cc.c0[k] = P.c0[v * KC + j];
         cc.cb[k] = P.cb[v * KC + j];
         cc.Q[k] = P.Q[v * KC + j];
+        self_coef_parts(cc.d_n[k], P.hyper[v], A.L2pt[v], D, cc.xm[k], cc.ym[k], cc.cbm[k]);
       }
     }
     if (L.s1) {
