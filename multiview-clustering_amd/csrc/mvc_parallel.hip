@@ -2023,6 +2023,7 @@ class ParallelSampler : public Sampler {
   bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
   int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
+  bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
 
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
@@ -2119,6 +2120,7 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
+    if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh.data());
     MVC_HIP(hipStreamSynchronize(stream));
@@ -2649,6 +2651,15 @@ class ParallelSampler : public Sampler {
       L.nws = room > 0 ? (int)std::min<int64_t>(run_waves, room / L.stride) : 0;
       if (L.nws >= std::min(run_waves, s1 ? 4 : 2)) {
         L.lds = 1;
+        // the staged-row ring in what is left: a power of two >= 2 nws customers
+        const int64_t slot = seq_ring_slot(V, D);
+        const int64_t left = room - (int64_t)L.nws * L.stride;
+        int rn = 0;
+        if (use_ring)
+          for (int r = 256; r >= 2 * L.nws; r >>= 1)
+            if ((int64_t)r * slot <= left) { rn = r; break; }
+        L.ring = rn;
+        L.pfn = rn ? std::max(1, rn / 2) : 0;
         return L;
       }
     }
@@ -2686,7 +2697,7 @@ class ParallelSampler : public Sampler {
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
         else
           hipLaunchKernelGGL(mvc_seq_run_kernel, dim3(1), dim3(kSeqRunThreads),
-                             L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws)) : 0,
+                             L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
                              stream, Q, L);
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
       }

@@ -72,7 +72,12 @@ struct SeqLds {
   int32_t s1;           // S1 cached in LDS
   int64_t cache_dbl;    // doubles of the state cache (the per-wave scratch follows)
   int64_t stride;       // doubles per wave
+  int32_t ring;         // customers in the staged-row ring (power of 2, after the per-wave scratch; 0: none)
+  int32_t pfn;          // customers prefetched into the ring per step
 };
+// ring slot: y rows [V][D], Y2 [V], z (as a double)
+__host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
+
 __host__ __device__ inline int64_t seq_lds_stride(int V, int D, int ks, int ts) {
   return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + 2;
 }
@@ -742,21 +747,20 @@ __device__ __forceinline__ void self_coef_parts(int n_, double tau, double L2pt,
 // the commit is redone, bit for bit: its draws are counter-addressed).
 // cnt: the moves / births / new-dish counters (R->moves... or the run
 // kernel's LDS copies).
-__device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, int i, int p0, int c, double *lpw,
-                           double *treew, int32_t *cnt, int nwd) {
+__device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const Cust &Ci, int i, int p0, int c,
+                           double *lpw, double *treew, int32_t *cnt, int nwd) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, n = P.n;
+  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC;
   const int ks = W.ks, ts = W.ts;
   __shared__ int s_ovf, s_c, s_dies, s_born;
   __shared__ int s_tup[MVC_MAXV], s_j0[MVC_MAXV], s_j1[MVC_MAXV];
   if (c < 0) {
     // a birth: dishes drawn against the current state, then the table
     const bool alive = (W.n_t[p0] - 1) > 0;
-    const Cust C = global_cust(A, i);
     for (int v = w; v < V && w < nwd; v += nwd) {   // waves w < nwd own a scratch (lpw, treew)
-      const int t = seq_dish_draw(A, W, C, i, v, alive, W.dish[v * ts + p0], lpw, treew);
+      const int t = seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew);
       if (lane == 0) s_tup[v] = t;
     }
     __syncthreads();
@@ -866,7 +870,7 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, int i, 
     const int v = e / D, d = e - v * D;
     const int j0 = s_j0[v], j1 = s_j1[v];
     if (j0 == j1) continue;
-    const double yd = A.y[((size_t)v * n + i) * D + d];
+    const double yd = Ci.y[(size_t)v * Ci.ystride + d];
     const double *src = W.S1T + ((size_t)v * D + d) * W.s1s;
     const double a0 = src[j0] - yd, a1 = src[j1] + yd;
     double *col = P.S1T + ((size_t)v * D + d) * KC;
@@ -881,7 +885,7 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, int i, 
   if (tid < V) {
     const int v = tid, j0 = s_j0[v], j1 = s_j1[v];
     if (j0 != j1) {
-      const double y2 = A.Y2[(size_t)v * n + i];
+      const double y2 = Ci.Y2[(size_t)v * Ci.y2stride];
       P.S2[v * KC + j0] = P.S2[v * KC + j0] - y2;
       P.S2[v * KC + j1] = P.S2[v * KC + j1] + y2;
       const int n0 = W.d_n[v * ks + j0] - 1, n1 = W.d_n[v * ks + j1] + 1;
@@ -956,7 +960,8 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A
   __syncthreads();
   if (s_go) {
     const SeqScratch S(A, tid >> 6);
-    if (!seq_commit(A, global_view(A), nullptr, s_i, A.P.z[s_i], s_c, S.lp, S.tree, &R->moves, blockDim.x >> 6))
+    if (!seq_commit(A, global_view(A), nullptr, global_cust(A, s_i), s_i, A.P.z[s_i], s_c, S.lp, S.tree, &R->moves,
+                    blockDim.x >> 6))
       return;   // overflow: the host grows and relaunches this step
     if (tid == 0) {
       R->cur = s_i + 1;
@@ -978,6 +983,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A
 // runs; read from R at entry and written back at exit).
 struct RunCursor {
   int go, stop, cur, pend, pc, pp0, mode, streak, done, i;
+  int fill;                       // ring: customers [.., fill) are staged (slot = customer % ring)
   int32_t cnt[3];                 // moves, births, new dishes
   int ch[kSeqRunWaves], p0[kSeqRunWaves];
 };
@@ -986,17 +992,77 @@ namespace {
 
 // The run kernel's loop, for state read through the LDS cache (kLds) or the
 // global arrays.  Returns through ovf / restride why it stopped early.
+// The staged-row ring of the run kernel: slot k holds customer c with
+// c % ring == k (y rows [V][D], Y2 [V], z).
+struct Ring {
+  double *base;
+  int n, slot;
+  __device__ double *at(int c) const { return base + (int64_t)(c & (n - 1)) * slot; }
+  __device__ Cust cust(int c, int V, int D) const {
+    Cust C;
+    C.y = at(c);
+    C.ystride = (size_t)D;
+    C.Y2 = at(c) + (size_t)V * D;
+    C.y2stride = 1;
+    return C;
+  }
+};
+// Asynchronous fill of the ring with customers [c0, c1) (c1 - c0 <= ring,
+// within one pass of the ring): direct global -> LDS dword loads
+// (global_load_lds_dword: no registers, completion on vmcnt), the dword
+// range of the slots split over the waves, 64 dwords per instruction.  The
+// caller waits (s_waitcnt + barrier) before anyone reads the slots.  Slot
+// dwords: y rows [V][D] (2 per double), Y2 [V], then z (int) twice.
+__device__ __forceinline__ void ring_fill_async(const SeqArgs &A, const Ring &G, int c0, int c1) {
+  const int V = A.P.V, D = A.P.D, n = A.P.n;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int sdw = 2 * G.slot;
+  int c = c0;
+  while (c < c1) {   // contiguous runs of slots (split at the ring's end)
+    const int k0 = c & (G.n - 1);
+    const int run = min(c1 - c, G.n - k0);
+    const int cnt = run * sdw;
+    char *dst0 = (char *)(G.base + (int64_t)k0 * G.slot);
+    for (int q = w; q * 64 < cnt; q += nw) {
+      const int k = q * 64 + lane;
+      if (k < cnt) {
+        const int cc = c + k / sdw, dw = k - (k / sdw) * sdw, e = dw >> 1, half = dw & 1;
+        const int32_t *src;
+        if (e < V * D) {
+          const int v = e / D, d = e - v * D;
+          src = (const int32_t *)(A.y + ((size_t)v * n + cc) * D + d) + half;
+        } else if (e < V * D + V) {
+          src = (const int32_t *)(A.Y2 + (size_t)(e - V * D) * n + cc) + half;
+        } else {
+          src = A.P.z + cc;
+        }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(dst0 + (int64_t)q * 256), 4, 0, 0);
+      }
+    }
+    c += run;
+  }
+}
+__device__ __forceinline__ int ring_z(const Ring &G, int c, int V, int D) {
+  return ((const int32_t *)(G.at(c) + (size_t)V * D + V))[0];
+}
+
+// The run kernel's loop, for state read through the LDS cache (kLds) or the
+// global arrays.  Returns through ovf / restride why it stopped early.
 template <bool kLds>
 __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
-                             double *tree, RunCursor &U, int &ovf, int &restride) {
+                             const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride) {
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
+  const bool ring = kLds && G.n > 0;
   for (;;) {
     // invariant here: U.mode == kSeqRun || U.pend, not done
     RUN_T0();
     if (U.pend) {
-      if (!seq_commit(A, Wv, ccp, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt, kLds ? L.nws : (int)(blockDim.x >> 6))) {
+      const bool staged = ring && U.cur < U.fill && U.cur >= U.fill - G.n;
+      const Cust Ci = staged ? G.cust(U.cur, V, D) : global_cust(A, U.cur);
+      if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt, kLds ? L.nws : (int)(blockDim.x >> 6))) {
         // overflow: the host grows and relaunches
         ovf = 1;
         return;
@@ -1025,11 +1091,33 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       restride = U.stop == 2;
       return;
     }
-    const int i = U.i + w;
+    const int i0 = U.i;
+    const int need = min(n, i0 + L.nws);
+    int fill_next = 0;
+    if (ring) {
+      // this step's customers must be staged: a synchronous fill when the
+      // ring fell behind (kernel start, after a window jump)
+      const int f0 = max(U.fill, i0);
+      if (f0 < need) {
+        ring_fill_async(A, G, f0, need);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+      }
+      // prefetch the customers after them, up to a ring ahead; they land
+      // while this step evaluates (waited for before the decision barrier)
+      const int p0c = max(f0, need), p1c = min(n, min(i0 + G.n, p0c + L.pfn));
+      if (p1c > p0c) ring_fill_async(A, G, p0c, p1c);
+      fill_next = max(p1c, need);   // U.fill is written after the decision barrier (every wave read it above)
+    }
+    const int i = i0 + w;
     if (w < L.nws && i < n) {
-      const int p0 = P.z[i];   // customers after cur keep their sweep-start table until committed
+      int p0;
       Cust C;
-      if (kLds) {   // stage the customer's rows in LDS: one memory latency for the whole evaluation
+      if (ring) {
+        C = G.cust(i, V, D);
+        p0 = ring_z(G, i, V, D);
+      } else if (kLds) {   // stage the customer's rows in LDS: one memory latency for the whole evaluation
+        p0 = P.z[i];   // customers after cur keep their sweep-start table until committed
         for (int e = lane; e < V * D; e += 64) {
           const int v = e / D, d = e - v * D;
           S.ys[e] = A.y[((size_t)v * n + i) * D + d];
@@ -1041,6 +1129,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         C.Y2 = S.ys + (size_t)V * D;
         C.y2stride = 1;
       } else {
+        p0 = P.z[i];
         C = global_cust(A, i);
       }
       const int c = seq_resample(A, Wv, C, i, p0, S);
@@ -1049,9 +1138,11 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         U.p0[w] = p0;
       }
     }
+    if (ring) __builtin_amdgcn_s_waitcnt(0);   // this wave's prefetch has landed
     __syncthreads();
     RUN_MARK(5);
     if (tid == 0) {
+      if (ring) U.fill = fill_next;
       int f = -1;
       const int m = min(L.nws, n - U.i);
       for (int k = 0; k < m; ++k)
@@ -1115,6 +1206,7 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(
     U.mode = R->mode;
     U.streak = R->streak;
     U.done = R->done;
+    U.fill = U.cur;   // nothing staged yet
     U.cnt[0] = R->moves;
     U.cnt[1] = R->births;
     U.cnt[2] = R->newdish;
@@ -1192,10 +1284,15 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(
       *cc.T_ne = R->T_ne;
     }
     __syncthreads();
+    Ring G;
+    G.n = L.ring;
+    G.slot = (int)seq_ring_slot(V, D);
+    G.base = seq_sm + L.cache_dbl + (int64_t)L.nws * L.stride;
     seq_run_loop<true>(A, L, cache_view(cc, A), &cc, SeqScratch(seq_sm + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
-                       tree, U, ovf, restride);
+                       G, tree, U, ovf, restride);
   } else {
-    seq_run_loop<false>(A, L, global_view(A), nullptr, SeqScratch(A, w), tree, U, ovf, restride);
+    Ring G{nullptr, 0, 0};
+    seq_run_loop<false>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
     R->cur = U.cur;
