@@ -358,30 +358,29 @@ int mvc_sampler_get_stats(mvc_sampler *s, int chain, int view, int32_t *n_dishes
 int mvc_sampler_kernel_time(mvc_sampler *s, const char *kernel, double *total_ms, int64_t *launches) {
   if (!s || !s->impl || !kernel) return MVC_ERR_ARG;
   try {
-    s->impl->synchronize();
+    s->impl->kernel_time(kernel, total_ms, launches);
   } catch (...) {
     return MVC_ERR_HIP;
   }
-  auto &acc = s->impl->timers.acc;
-  auto it = acc.find(kernel);
-  if (total_ms) *total_ms = it == acc.end() ? 0.0 : it->second.first;
-  if (launches) *launches = it == acc.end() ? 0 : it->second.second;
   return MVC_OK;
 }
 
 void mvc_sampler_reset_timers(mvc_sampler *s) {
-  if (s && s->impl) s->impl->timers.reset();
+  if (s && s->impl) {
+    try {
+      s->impl->reset_timers();
+    } catch (...) {
+    }
+  }
 }
 
 int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags) {
   if (!s || !s->impl) return MVC_ERR_ARG;
   try {
-    s->impl->synchronize();
+    s->impl->set_timing((flags & MVC_FLAG_TIMING) != 0, (flags & MVC_FLAG_TIMING_COARSE) != 0);
   } catch (...) {
     return MVC_ERR_HIP;
   }
-  s->impl->timers.on = (flags & MVC_FLAG_TIMING) != 0;
-  s->impl->timers.coarse = (flags & MVC_FLAG_TIMING_COARSE) != 0;
   return MVC_OK;
 }
 

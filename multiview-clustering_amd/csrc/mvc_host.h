@@ -85,6 +85,20 @@ class Sampler {
   // out[0] customers that moved, out[1] births, out[2] repair rounds,
   // out[3] dishes opened.  False for the exact schedule.
   virtual bool repair_stats(int chain, int32_t *out) { (void)chain; (void)out; return false; }
+  // HIP-event timing (mvc_sampler_set_timing / reset_timers / kernel_time)
+  virtual void set_timing(bool on, bool coarse) {
+    synchronize();
+    timers.on = on;
+    timers.coarse = coarse;
+  }
+  virtual void reset_timers() { timers.reset(); }
+  virtual bool kernel_time(const char *name, double *ms, int64_t *launches) {
+    synchronize();
+    auto it = timers.acc.find(name);
+    if (ms) *ms = it == timers.acc.end() ? 0.0 : it->second.first;
+    if (launches) *launches = it == timers.acc.end() ? 0 : it->second.second;
+    return true;
+  }
   mvc_config cfg;
   int sweeps_done = 0;
   int zpath = -1;                        // mvc_sampler_zpath

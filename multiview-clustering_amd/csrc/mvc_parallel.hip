@@ -1948,6 +1948,9 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
 // ===========================================================================
 #include <algorithm>
 #include <cstdio>
+#include <exception>
+#include <memory>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -2033,6 +2036,18 @@ class ParallelSampler : public Sampler {
   }
 
   ParallelSampler(const mvc_config &cf, const double *const *views) {
+    std::vector<double> yh((size_t)cf.n_views * cf.n * cf.dim);
+    for (int v = 0; v < cf.n_views; ++v)
+      std::memcpy(&yh[(size_t)v * cf.n * cf.dim], views[v], sizeof(double) * (size_t)cf.n * cf.dim);
+    init(cf, yh.data(), nullptr);
+  }
+  // yh: the views, contiguous [V][n][D] on the host.  share: another
+  // sampler on the same device and data whose device copies of y, Y2 and the
+  // MFMA tiling this one reads instead of making its own (ChainSet).
+  ParallelSampler(const mvc_config &cf, const double *yh, const ParallelSampler *share) { init(cf, yh, share); }
+
+  bool owns_y = true;
+  void init(const mvc_config &cf, const double *yh_in, const ParallelSampler *share) {
     cfg = cf;
     n = cf.n; V = cf.n_views; D = cf.dim;
     // initial capacities (mvc_config.table_cap / dish_cap); a birth beyond
@@ -2053,20 +2068,26 @@ class ParallelSampler : public Sampler {
     timers.stream = stream;
     timers.on = (cf.flags & MVC_FLAG_TIMING) != 0;
     timers.coarse = (cf.flags & MVC_FLAG_TIMING_COARSE) != 0;
-    std::vector<double> yh((size_t)V * n * D);
-    for (int v = 0; v < V; ++v) std::memcpy(&yh[(size_t)v * n * D], views[v], sizeof(double) * (size_t)n * D);
-    y = dmalloc<double>(yh.size());
-    Y2 = dmalloc<double>((size_t)V * n);
     vmax = dmalloc<double>((size_t)V * n);
-    MVC_HIP(hipMemcpyAsync(y, yh.data(), sizeof(double) * yh.size(), hipMemcpyHostToDevice, stream));
-    hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
-    MVC_HIP(hipGetLastError());
+    if (share) {   // the data arrays of another sampler (constant after its construction)
+      owns_y = false;
+      y = share->y;
+      Y2 = share->Y2;
+      yt = share->yt;
+      SP = share->SP;
+    } else {
+      y = dmalloc<double>((size_t)V * n * D);
+      Y2 = dmalloc<double>((size_t)V * n);
+      MVC_HIP(hipMemcpyAsync(y, yh_in, sizeof(double) * (size_t)V * n * D, hipMemcpyHostToDevice, stream));
+      hipLaunchKernelGGL(mvc_par_y2_kernel, dim3(1024), dim3(256), 0, stream, n, V, D, (const double *)y, Y2);
+      MVC_HIP(hipGetLastError());
+    }
     // the MFMA tiling yt is a second copy of y: build it only when it fits
     // beside y with room for the lp buffer and the chains' state (at N = 10M,
     // D = 256 the two copies would not fit in 288 GB; the generic producer
     // then runs on y alone)
     size_t yt_bytes = 0;
-    if (D % 4 == 0 && D >= 16 && V <= MVC_Z_VMAX) {
+    if (!share && D % 4 == 0 && D >= 16 && V <= MVC_Z_VMAX) {
       const int sp = ((D / 4 + MVC_ZR - 1) / MVC_ZR) * MVC_ZR;
       yt_bytes = sizeof(double) * (size_t)V * (((size_t)n + 15) / 16) * sp * 64;
       size_t mfree = 0, mtotal = 0;
@@ -2122,7 +2143,7 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     chains.resize(cf.n_chains);
-    for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh.data());
+    for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh_in);
     MVC_HIP(hipStreamSynchronize(stream));
   }
 
@@ -2214,8 +2235,10 @@ class ParallelSampler : public Sampler {
       for (void *p : c.owned) hipFree(p);
       if (c.hpin) hipHostFree(c.hpin);
     }
-    for (void *p : {(void *)y, (void *)Y2, (void *)yt, (void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2,
-                    (void *)fz_discard, (void *)vmax})
+    if (owns_y)
+      for (void *p : {(void *)y, (void *)Y2, (void *)yt})
+        if (p) hipFree(p);
+    for (void *p : {(void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2, (void *)fz_discard, (void *)vmax})
       if (p) hipFree(p);
     if (st_host) hipHostFree(st_host);
     if (rs_host) hipHostFree(rs_host);
@@ -2917,7 +2940,102 @@ class ParallelSampler : public Sampler {
   }
 };
 
+// Several chains on one device, concurrently (BASELINE config 3:
+// 8 chains on one MI355X).  Each chain is a one-chain ParallelSampler with
+// its own stream, phase-A buffers and repair state, sharing the device copy
+// of the data; sweep() drives them from one host thread per chain, so one
+// chain's latency-bound repair (one CU) overlaps the others' work.  Chain c
+// keeps its global id first_chain + c, so every draw is the one the serial
+// loop would make: the chains are bitwise the same.
+class ChainSet : public Sampler {
+ public:
+  std::vector<std::unique_ptr<ParallelSampler>> subs;
+  ChainSet(const mvc_config &cf, const double *const *views) {
+    cfg = cf;
+    const int V = cf.n_views, n = cf.n, D = cf.dim;
+    std::vector<double> yh((size_t)V * n * D);
+    for (int v = 0; v < V; ++v) std::memcpy(&yh[(size_t)v * n * D], views[v], sizeof(double) * (size_t)n * D);
+    for (int c = 0; c < cf.n_chains; ++c) {
+      mvc_config one = cf;
+      one.n_chains = 1;
+      one.first_chain = cf.first_chain + c;
+      subs.emplace_back(new ParallelSampler(one, yh.data(), c == 0 ? nullptr : subs[0].get()));
+    }
+    stream = subs[0]->stream;
+  }
+  ~ChainSet() override {
+    while (!subs.empty()) subs.pop_back();   // the data owner (chain 0) last
+  }
+  template <class F>
+  void each(F f) {
+    std::vector<std::thread> ts;
+    std::vector<std::exception_ptr> errs(subs.size());
+    for (size_t c = 0; c < subs.size(); ++c)
+      ts.emplace_back([&, c] {
+        try {
+          MVC_HIP(hipSetDevice(cfg.device));
+          f(*subs[c]);
+        } catch (...) {
+          errs[c] = std::current_exception();
+        }
+      });
+    for (auto &t : ts) t.join();
+    for (auto &e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  ParallelSampler &at(int chain) {
+    if (chain < 0 || chain >= (int)subs.size()) throw Error(MVC_ERR_ARG, "chain out of range");
+    return *subs[chain];
+  }
+  void sweep(int n_sweeps) override {
+    for (auto &s : subs) {   // timing flags set on the handle apply to every chain
+      s->timers.on = timers.on;
+      s->timers.coarse = timers.coarse;
+    }
+    each([&](ParallelSampler &s) { s.sweep(n_sweeps); });
+    sweeps_done += n_sweeps;
+    zpath = subs[0]->zpath;
+  }
+  void synchronize() override {
+    for (auto &s : subs) s->synchronize();
+  }
+  void get_state(int chain, int32_t *t, int32_t *T, int32_t *d, int32_t cap, double *h) override {
+    at(chain).get_state(0, t, T, d, cap, h);
+  }
+  void get_dish_counts(int chain, int32_t *k) override { at(chain).get_dish_counts(0, k); }
+  void get_stats(int chain, int view, int32_t *K, double *S1, double *S2, int32_t *n_vk, int32_t cap) override {
+    at(chain).get_stats(0, view, K, S1, S2, n_vk, cap);
+  }
+  void set_state(int chain, const int32_t *t, int32_t T, const int32_t *d, const double *h) override {
+    at(chain).set_state(0, t, T, d, h);
+  }
+  bool save_async(int chain, const SampleFn &fn) override {
+    return at(chain).save_async(0, [fn, chain](int, int T, const int32_t *t, const int32_t *d, const double *h) {
+      fn(chain, T, t, d, h);
+    });
+  }
+  void flush_saves() override {
+    for (auto &s : subs) s->flush_saves();
+  }
+  const int32_t *device_labels(int chain) override { return at(chain).device_labels(0); }
+  bool repair_stats(int chain, int32_t *out) override { return at(chain).repair_stats(0, out); }
+  // timing: chain 0's timers (every chain runs the same kernels)
+  void set_timing(bool on, bool coarse) override {
+    timers.on = on;
+    timers.coarse = coarse;
+    for (auto &s : subs) s->set_timing(on, coarse);
+  }
+  void reset_timers() override {
+    for (auto &s : subs) s->reset_timers();
+  }
+  bool kernel_time(const char *name, double *ms, int64_t *launches) override {
+    return subs[0]->kernel_time(name, ms, launches);
+  }
+};
+
 Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views) {
+  const char *e = getenv("MVC_CHAIN_THREADS");   // =0: one handle runs its chains one after another
+  if (cfg.n_chains > 1 && !(e && e[0] == '0')) return new ChainSet(cfg, views);
   return new ParallelSampler(cfg, views);
 }
 

@@ -553,3 +553,30 @@ def test_repair_shapes_same_chain(waves, repair, monkeypatch):
     _check_sweeps(s, ref, 10, stats=False)
     assert sum(ref["trace_births"]) > 0
     s.close()
+
+
+def test_chains_concurrent_equal_serial(monkeypatch):
+    """Several chains in one handle run concurrently (ChainSet: a stream and a
+    host thread per chain, shared device data); every chain equals the same
+    chain run alone (first_chain = c) and the serial loop (MVC_CHAIN_THREADS=0),
+    bit for bit, through a cold start with births."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(1999)
+    C, M = 4, 8
+    conc = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
+    conc.sweep(M)
+    monkeypatch.setenv("MVC_CHAIN_THREADS", "0")
+    ser = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
+    ser.sweep(M)
+    for c in range(C):
+        one = m.Sampler(y, seed=21, mode="parallel", first_chain=c)
+        one.sweep(M)
+        t1, d1, h1 = one.state()
+        for s in (conc, ser):
+            t, d, h = s.state(chain=c)
+            assert np.array_equal(t, t1) and np.array_equal(d, d1), c
+            assert h["sigma_global"] == h1["sigma_global"] and np.array_equal(h["tau_v"], h1["tau_v"])
+        one.close()
+    conc.close()
+    ser.close()
