@@ -27,7 +27,6 @@ namespace {
 
 constexpr double kEps = 1e-6;
 constexpr int kStatsChunk = 4096;   // must equal oracle kStatsChunk
-constexpr int kMaxChunks = 64;      // two-level tree64: <= 4096 elements
 
 struct Coef { double c0, cb; };
 __device__ __forceinline__ Coef coef(int n_, double Q, double tau, double L2pt, int D) {
@@ -1656,13 +1655,15 @@ struct BlockCtx {
   size_t half;      // scratch half size
 };
 
-// tree64 over n <= 4096 leaves produced by leaf(e), executed by the whole
-// block of 256; the 64-leaf chunk sums go through LDS (second level = one
-// butterfly over <= 64 partials).  Same association as oracle Tree64::build.
+// tree64 over n <= 64^3 leaves produced by leaf(e), executed by the whole
+// block: 64-leaf chunk sums into LDS (level 1), chunk sums of those (level
+// 2), then the root.  Same association as oracle Tree64::build (each level's
+// node c = butterfly64 of the 64 nodes below it, zero-padded).
 template <class F>
 __device__ double block_tree64(int64_t n, F leaf) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  __shared__ double s_part[64];
+  __shared__ double s_p1[4096];
+  __shared__ double s_p2[64];
   __shared__ double s_root;
   if (n <= 0) return 0.0;
   const int m = (int)((n + 63) / 64);
@@ -1670,13 +1671,24 @@ __device__ double block_tree64(int64_t n, F leaf) {
     const int64_t e = (int64_t)c * 64 + lane;
     const double x = e < n ? leaf(e) : 0.0;
     const double s = wave_tree_sum(x);
-    if (lane == 0) s_part[c] = s;
+    if (lane == 0) s_p1[c] = s;
   }
   __syncthreads();
+  const int m2 = (m + 63) / 64;
+  if (m > 1) {
+    for (int c = w; c < m2; c += nw) {
+      const int e = c * 64 + lane;
+      const double s = wave_tree_sum(e < m ? s_p1[e] : 0.0);
+      if (lane == 0) s_p2[c] = s;
+    }
+    __syncthreads();
+  }
   if (w == 0) {
-    const double x = lane < m ? s_part[lane] : 0.0;
-    const double r = (m == 1) ? x : wave_tree_sum(x);
-    if (lane == 0) s_root = (m == 1) ? s_part[0] : r;
+    double r;
+    if (m == 1) r = s_p1[0];
+    else if (m2 == 1) r = s_p2[0];
+    else r = wave_tree_sum(lane < m2 ? s_p2[lane] : 0.0);
+    if (lane == 0) s_root = r;
   }
   __syncthreads();
   const double r = s_root;
@@ -1833,21 +1845,37 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     };
     {
       __shared__ double s_wpart[kHypWaves][64];
+      __shared__ double s_wpart2[kHypWaves][64];
       const int lane = tid & 63, wv = tid >> 6;
-      auto wtree = [&](int64_t nn, auto leaf) -> double {   // tree64 by one wavefront (nn <= 4096)
+      // tree64 by one wavefront, nn <= 64^3 leaves: 64-leaf chunk sums,
+      // reduced 64 at a time into level-2 nodes, then the root (oracle
+      // Tree64::build's association)
+      auto wtree = [&](int64_t nn, auto leaf) -> double {
         if (nn <= 0) return 0.0;
         const int mch = (int)((nn + 63) / 64);
+        const int m2 = (mch + 63) / 64;
         double root = 0.0;
-        for (int c = 0; c < mch; ++c) {
-          const int64_t e = (int64_t)c * 64 + lane;
-          const double x = e < nn ? leaf(e) : 0.0;
-          const double cs = wave_tree_sum(x);
-          if (mch == 1) root = cs;
-          else if (lane == 0) s_wpart[wv][c] = cs;
+        for (int c2 = 0; c2 < m2; ++c2) {
+          const int cn = min(64, mch - c2 * 64);
+          double l2 = 0.0;
+          for (int cc = 0; cc < cn; ++cc) {
+            const int64_t e = ((int64_t)c2 * 64 + cc) * 64 + lane;
+            const double x = e < nn ? leaf(e) : 0.0;
+            const double cs = wave_tree_sum(x);
+            if (mch == 1) l2 = cs;
+            else if (lane == 0) s_wpart[wv][cc] = cs;
+          }
+          if (mch > 1) {
+            wave_lds_sync();
+            l2 = wave_tree_sum(lane < cn ? s_wpart[wv][lane] : 0.0);
+            wave_lds_sync();
+          }
+          if (m2 == 1) root = l2;
+          else if (lane == 0) s_wpart2[wv][c2] = l2;
         }
-        if (mch > 1) {
+        if (m2 > 1) {
           wave_lds_sync();
-          root = wave_tree_sum(lane < mch ? s_wpart[wv][lane] : 0.0);
+          root = wave_tree_sum(lane < m2 ? s_wpart2[wv][lane] : 0.0);
           wave_lds_sync();
         }
         return root;
@@ -1960,8 +1988,8 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
 namespace mvc {
 
 namespace {
-constexpr int kParTC = 4096;   // table capacity (two-level tree64)
-constexpr int kParKC = 4095;   // live dishes per view (+1 new element <= 4096)
+constexpr int kParTC = 1 << 18;   // table capacity (three-level tree64 of the MH's global EPPF)
+constexpr int kParKC = (1 << 18) - 1;   // live dishes per view (+1 new element: three-level tree64)
 constexpr size_t kLpbBudget = (size_t)1 << 28;   // phase-1 lp buffer: 2 GiB of doubles per batch
 constexpr int kSeqWaves = 1024;    // waves of the repair eval grid (SeqArgs.G)
 constexpr int kSeqWmin = 1024;     // repair window after a mover
@@ -2411,10 +2439,15 @@ class ParallelSampler : public Sampler {
     timers.end("hyper", ev);
   }
 
+  // per-wave global scratch of the repair's grid windows: kSeqWaves waves,
+  // fewer when tables / dishes number in the tens of thousands (<= 2 GiB)
+  int seq_waves = kSeqWaves;
   void alloc_seq_scratch() {
     if (seq_scr) hipFree(seq_scr);
     seq_stride = seq_scratch_stride(V, TC, KC);
-    seq_scr = dmalloc<double>((size_t)kSeqWaves * seq_stride);
+    const int64_t fit = ((int64_t)1 << 28) / seq_stride;
+    seq_waves = (int)std::max<int64_t>(kSeqRunWaves, std::min<int64_t>(kSeqWaves, fit / 4 * 4));
+    seq_scr = dmalloc<double>((size_t)seq_waves * seq_stride);
   }
 
   SeqArgs make_seq(Chain &c, uint32_t s) {
@@ -2430,7 +2463,7 @@ class ParallelSampler : public Sampler {
     A.R = c.R;
     A.scr = seq_scr;
     A.scr_stride = seq_stride;
-    A.G = kSeqWaves;
+    A.G = seq_waves;
     A.Wmin = kSeqWmin;
     A.Wmax = kSeqWmax;
     A.seed = cfg.seed;
@@ -2705,7 +2738,7 @@ class ParallelSampler : public Sampler {
     hipEvent_t e1 = nullptr;
     timers.begin("repair", &e1);
     SeqArgs Q = make_seq(c, s);
-    const dim3 eg(kSeqWaves / 4), eb(256);
+    const dim3 eg(seq_waves / 4), eb(256);
     if (phaseA)
       hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
                          stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
@@ -2777,7 +2810,7 @@ class ParallelSampler : public Sampler {
     const int TC2 = (flags & 1) ? std::min(kParTC, 2 * TC) : TC;
     const int KC2 = (flags & 2) ? std::min(kParKC, 2 * KC + 1) : KC;
     if (TC2 == TC && KC2 == KC)
-      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: more than 4096 tables or 4095 dishes per view");
+      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: more than 262144 tables or 262143 dishes per view");
     flush_saves();
     for (SaveSlot &q : saves) {   // the ring slots are capacity-sized
       for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp})

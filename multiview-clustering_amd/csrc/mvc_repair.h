@@ -505,19 +505,46 @@ __device__ int seq_resample(const SeqArgs &A, const SView &W, const Cust &C, int
   const int T = *W.T;
   const int TB = (T + 15) / 16;
   double M = -MVC_PM_INF;
-  for (int q0 = 0; q0 < TB * 16; q0 += 64) {
-    const int p = q0 + lane;
-    double sp = -MVC_PM_INF;
-    if (p < T) {
-      const int np = W.n_t[p] - (p == p0 ? 1 : 0);
-      const double mass = (double)np - sg;
-      if (np >= 1 && mass > 0.0) {
-        sp = (p == p0) ? lmass0 : W.lmass[p];
-        for (int v = 0; v < V; ++v) sp = sp + S.lp[v * lps + W.dish[v * ts + p]];
-      }
+  // four 64-table chunks per step: their count / log-mass / dish loads are
+  // issued together, then the lp gathers (hundreds of tables in the early
+  // sweeps of a cold start: the loads, not the adds, are the latency)
+  constexpr int kU = 4;
+  for (int q0 = 0; q0 < TB * 16; q0 += 64 * kU) {
+    int np[kU];
+    double lm[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = q0 + 64 * u + lane;
+      np[u] = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+      lm[u] = p < T ? ((p == p0) ? lmass0 : W.lmass[p]) : 0.0;
     }
-    if (p < TB * 16) S.e[p] = sp;
-    if (sp > M) M = sp;
+    double sp[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = q0 + 64 * u + lane;
+      const double mass = (double)np[u] - sg;
+      sp[u] = (p < T && np[u] >= 1 && mass > 0.0) ? lm[u] : -MVC_PM_INF;
+    }
+    for (int v = 0; v < V; ++v) {
+      int dj[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = q0 + 64 * u + lane;
+        dj[u] = (sp[u] != -MVC_PM_INF) ? W.dish[v * ts + p] : 0;
+      }
+      double lv[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) lv[u] = S.lp[v * lps + dj[u]];
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (sp[u] != -MVC_PM_INF) sp[u] = sp[u] + lv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int p = q0 + 64 * u + lane;
+      if (p < TB * 16) S.e[p] = sp[u];
+      if (sp[u] > M) M = sp[u];
+    }
   }
   M = wave_max(M);
   if (s_new > M) M = s_new;

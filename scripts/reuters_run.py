@@ -1,0 +1,62 @@
+"""BASELINE config 3: Reuters-21578 views (mvc_amd.reuters), K = 6 topics,
+8 chains on one MI355X (concurrent, ChainSet), from the reference's cold
+initialisation.  Prints one JSON line per sweep (seconds, tables per chain)
+and, every --ari-every sweeps, the ARI (mcclust::arandi on the device) of
+each chain's tables against the top-6 TOPICS of the scored documents.
+
+    python scripts/reuters_run.py --sweeps 20 --chains 8
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
+
+import numpy as np  # noqa: E402
+
+import mvc_amd  # noqa: E402
+from mvc_amd import reuters  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sweeps", type=int, default=20)
+    ap.add_argument("--chains", type=int, default=8)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--ari-every", type=int, default=5)
+    ap.add_argument("--budget-s", type=float, default=150.0)
+    a = ap.parse_args()
+    y = reuters.views()
+    lab, names, _ = reuters.topic_truth()
+    sel = lab >= 0
+    s = mvc_amd.Sampler(y, seed=a.seed, mode="parallel", n_chains=a.chains)
+    s.synchronize()
+    t_all = time.perf_counter()
+    for it in range(a.sweeps):
+        t0 = time.perf_counter()
+        s.sweep(1)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        rec = {"sweep": it, "s": round(dt, 4)}
+        Ts, aris, moves = [], [], []
+        for c in range(a.chains):
+            t, d, h = s.state(chain=c)
+            Ts.append(int(d.shape[1]))
+            moves.append(s.repair_stats(chain=c)["moves"])
+            if (it + 1) % a.ari_every == 0 or it == a.sweeps - 1:
+                aris.append(round(float(mvc_amd.ari(t[sel], lab[sel])), 4))
+        rec["T"] = Ts
+        rec["moves"] = moves
+        if aris:
+            rec["ari_top6"] = aris
+        print(json.dumps(rec), flush=True)
+        if time.perf_counter() - t_all > a.budget_s:
+            break
+    s.close()
+
+
+if __name__ == "__main__":
+    main()
