@@ -262,6 +262,18 @@ def main():
 
     kms, kcnt = s.kernel_time("zresample")
     sweep_ms, _ = s.kernel_time("sweep")
+    # posterior-mean accumulators over 10 more saved sweeps (after the timed
+    # region), reduced across ranks with R-hat
+    from mvc_amd import dist as mdist
+    s.set_timing(False)
+    cstats = None
+    for _ in range(10):
+        s.sweep(1)
+        _, _, h = s.state()
+        hv = np.concatenate([h["alpha_v"], h["sigma_v"], h["tau_v"], [h["alpha_global"], h["sigma_global"]]])
+        if cstats is None:
+            cstats = mdist.ChainStats(hv.size)
+        cstats.add(0, hv)
     n_detail = 3
     s.set_timing(True)
     s.reset_timers()
@@ -276,14 +288,11 @@ def main():
     zpath = s.zpath()
     s.close()
 
-    # optional cross-chain reduce of the hyperparameters (one all-reduce over
-    # RCCL, outside the timed region; reported, never fed back: DESIGN.md §7)
-    from mvc_amd import dist as mdist
-    hv = np.concatenate([hyper_now["alpha_v"], hyper_now["sigma_v"], hyper_now["tau_v"],
-                         [hyper_now["alpha_global"], hyper_now["sigma_global"]]])
-    acc = mdist.HyperAccumulator(hv.size)
-    acc.add(hv[None, :])
-    pooled_mean, _, pooled_n = acc.reduce(device=f"cuda:{local}" if dist is not None else None)
+    # the cross-chain reduce of the hyperparameter accumulators (one
+    # all-reduce over RCCL, outside the timed region; reported, never fed
+    # back: DESIGN.md §7)
+    red = cstats.reduce(device=f"cuda:{local}" if dist is not None else None)
+    pooled_mean = red["mean"]
 
     if rank != 0:
         if dist is not None:
@@ -328,8 +337,10 @@ def main():
                 "lp_producer": ("fused" if zpath & 8 else "mfma-all-views" if zpath & 16
                                 else "mfma" if (zpath & 3) == 2 else "generic"),
                 "draw": "fused" if zpath & 8 else "registers" if zpath & 4 else "lds-checkpoints"},
-        "hyper_pooled_mean": {"chains": pooled_n, "alpha_global": round(float(pooled_mean[-2]), 6),
-                              "sigma_global": round(float(pooled_mean[-1]), 6)},
+        "hyper_pooled": {"chains": red["chains"], "draws": red["count"],
+                         "alpha_global": round(float(pooled_mean[-2]), 6),
+                         "sigma_global": round(float(pooled_mean[-1]), 6),
+                         "rhat_max": None if red["rhat"] is None else round(float(np.nanmax(red["rhat"])), 4)},
         "nvk_sweeps_per_s": round(value * N * V * K, 1),
         "kernel_ms_per_sweep": {k: round(v, 4) for k, v in parts.items()},
         "repair_last_sweep": repair,

@@ -12,7 +12,11 @@
 //
 //   MVC_HIP_LIB   path of libmvc_hip.so (default: "libmvc_hip.so" via the
 //                 dynamic loader's search path)
-//   MVC_MODE      "exact" (default: the reference schedule) or "parallel"
+//   MVC_MODE      "exact" (the reference's arithmetic, one wavefront per chain;
+//                 scalar views only, as the reference) or "parallel" (the same
+//                 sequential schedule as a data-parallel pass + in-order
+//                 repair; any D).  Default: exact for scalar views, parallel
+//                 when the views are n x D matrices.
 //   MVC_DEVICE    HIP device ordinal (default 0)
 //
 // The Philox key is drawn from R's RNG (two unif_rand() calls), so set.seed()
@@ -119,7 +123,11 @@ Rcpp::List run_gibbs_cpp(const Rcpp::List &data_views, int M, int burn_in, int t
   const uint64_t lo = (uint64_t)(R::unif_rand() * 4294967296.0);
   cfg.seed = (hi << 32) | lo;
   const char *mode = std::getenv("MVC_MODE");
-  cfg.mode = (mode && std::string(mode) == "parallel") ? 1 : 0;
+  const std::string m = mode ? mode : (D > 1 ? "parallel" : "exact");
+  if (m != "exact" && m != "parallel") Rcpp::stop("MVC_MODE must be \"exact\" or \"parallel\"");
+  if (m == "exact" && D > 1)
+    Rcpp::stop("MVC_MODE=exact needs scalar views (the reference's D = 1); unset it or use parallel for n x D matrices");
+  cfg.mode = m == "parallel" ? 1 : 0;
   const char *dev = std::getenv("MVC_DEVICE");
   cfg.device = dev ? std::atoi(dev) : 0;
 

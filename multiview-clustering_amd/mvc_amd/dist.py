@@ -9,6 +9,11 @@ reduce of the hyperparameter posterior-mean accumulators (multiview_hyper.cpp
 one all-reduce of 2 (3V + 2) + 1 doubles, over RCCL (backend "nccl", a GPU
 tensor) on MI355X or gloo on CPU.  The reduced values are reported, never fed
 back into the chains (that would couple them and break the MCMC).
+
+ChainStats keeps running sums per chain over the saved sweeps; its reduce
+is one all-reduce of the pooled sums plus the per-chain means / variances
+that the Gelman-Rubin potential scale reduction (R-hat) needs, so every rank
+gets the pooled posterior means and R-hat over all chains of the node.
 """
 import numpy as np
 
@@ -79,3 +84,77 @@ class HyperAccumulator:
         mean = buf[:w] / cnt
         var = np.maximum(buf[w:2 * w] / cnt - mean * mean, 0.0)
         return mean, var, int(round(cnt))
+
+
+class ChainStats:
+    """Running sums of each local chain's saved hyperparameter draws
+    (rows of hyper_matrix: alpha_v, sigma_v, tau_v, alpha_global,
+    sigma_global) for pooled posterior means and R-hat across ranks."""
+
+    def __init__(self, width, n_chains=1):
+        self.width = int(width)
+        self.s1 = np.zeros((n_chains, self.width))
+        self.s2 = np.zeros((n_chains, self.width))
+        self.n = np.zeros(n_chains, dtype=np.int64)
+
+    def add(self, chain, H):
+        H = np.atleast_2d(np.asarray(H, dtype=np.float64))
+        if H.shape[1] != self.width:
+            raise ValueError(f"expected {self.width} hyperparameters per draw, got {H.shape[1]}")
+        self.s1[chain] += H.sum(axis=0)
+        self.s2[chain] += (H * H).sum(axis=0)
+        self.n[chain] += H.shape[0]
+
+    def packed(self):
+        """[pooled s1 | pooled s2 | pooled count | sum_j mean_j | sum_j mean_j^2 |
+        sum_j var_j (ddof 1) | chains | sum_j n_j]; chains with < 2 draws are
+        left out of the R-hat terms."""
+        w = self.width
+        ok = self.n >= 2
+        n = self.n[ok].astype(np.float64)[:, None]
+        mean = self.s1[ok] / n if ok.any() else np.zeros((0, w))
+        var = (self.s2[ok] - n * mean * mean) / (n - 1) if ok.any() else np.zeros((0, w))
+        return np.concatenate([self.s1.sum(0), self.s2.sum(0), [float(self.n.sum())],
+                               mean.sum(0), (mean * mean).sum(0), np.maximum(var, 0.0).sum(0),
+                               [float(ok.sum()), float(self.n[ok].sum())]])
+
+    def reduce(self, device=None):
+        """All-reduce (sum) over the default process group (local values
+        without one).  Returns dict(mean, var, count, chains, rhat): pooled
+        mean / variance over every draw of every chain, and the Gelman-Rubin
+        R-hat per hyperparameter (chains of equal length assumed; None with
+        fewer than 2 chains)."""
+        buf = self.packed()
+        try:
+            import torch
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                t = torch.from_numpy(buf.copy())
+                if device is not None:
+                    t = t.to(device)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                buf = t.cpu().numpy()
+        except ImportError:
+            pass
+        w = self.width
+        s1, s2, cnt = buf[:w], buf[w:2 * w], buf[2 * w]
+        sm, smm, sv = buf[2 * w + 1:3 * w + 1], buf[3 * w + 1:4 * w + 1], buf[4 * w + 1:5 * w + 1]
+        m, ntot = buf[5 * w + 1], buf[5 * w + 2]
+        out = {"count": int(round(cnt)), "chains": int(round(m))}
+        if cnt <= 0:
+            out.update(mean=np.full(w, np.nan), var=np.full(w, np.nan), rhat=None)
+            return out
+        mean = s1 / cnt
+        out["mean"] = mean
+        out["var"] = np.maximum(s2 / cnt - mean * mean, 0.0)
+        if m < 2:
+            out["rhat"] = None
+            return out
+        n = ntot / m                                   # draws per chain
+        grand = sm / m
+        B = n / (m - 1) * np.maximum(smm - m * grand * grand, 0.0)   # between-chain variance
+        W = sv / m                                     # mean within-chain variance
+        vplus = (n - 1) / n * W + B / n
+        with np.errstate(divide="ignore", invalid="ignore"):
+            out["rhat"] = np.where(W > 0, np.sqrt(vplus / W), np.nan)
+        return out

@@ -104,3 +104,20 @@ def test_c_abi_example_compiles():
         subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-o",
                         os.path.join(d, "ex"), os.path.join(ROOT, "examples", "mvc_abi_example.c"), "-ldl"],
                        check=True)
+
+
+def test_rcpp_dropin_compiles():
+    """The Rcpp drop-in (multiview-clustering_amd/R/multiview_gibbs.cpp) is
+    compile-checked against a declarations-only stub of the Rcpp API subset
+    it uses (tests/rcpp_stub/Rcpp.h; R and Rcpp are absent here)."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([gxx, "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                        "-I", os.path.join(root, "tests", "rcpp_stub"),
+                        os.path.join(root, "multiview-clustering_amd", "R", "multiview_gibbs.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

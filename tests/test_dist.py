@@ -25,6 +25,18 @@ def _chain(chain):
     return dist.hyper_matrix(r)
 
 
+def _rhat(chains):
+    """Gelman-Rubin R-hat of equal-length chains (textbook formula)."""
+    X = np.stack(chains)                  # [m][n][w]
+    m, n = X.shape[0], X.shape[1]
+    means = X.mean(axis=1)
+    B = n * means.var(axis=0, ddof=1)
+    W = X.var(axis=1, ddof=1).mean(axis=0)
+    vplus = (n - 1) / n * W + B / n
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return np.where(W > 0, np.sqrt(vplus / W), np.nan)
+
+
 def _worker(rank, world, port, out):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -39,7 +51,11 @@ def _worker(rank, world, port, out):
     acc = dist.HyperAccumulator(H.shape[1])
     acc.add(H)
     mean, var, cnt = acc.reduce()
-    out[rank] = (mean, var, cnt)
+    cs = dist.ChainStats(H.shape[1])
+    for row in H:                 # running sums, one saved sweep at a time
+        cs.add(0, row)
+    r = cs.reduce()
+    out[rank] = (mean, var, cnt, r["mean"], r["rhat"], r["chains"])
     tdist.barrier()
     tdist.destroy_process_group()
 
@@ -52,10 +68,17 @@ def test_two_rank_hyper_reduce_over_gloo():
     out = mgr.dict()
     mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
     H = np.concatenate([_chain(0), _chain(1)])
+    H0, H1 = _chain(0), _chain(1)
+    rhat_ref = _rhat([H0, H1])
     for rank in range(world):
-        mean, var, cnt = out[rank]
+        mean, var, cnt, pmean, rhat, chains = out[rank]
         assert cnt == H.shape[0]
         assert np.allclose(mean, H.mean(axis=0), rtol=1e-12, atol=0)
         assert np.allclose(var, H.var(axis=0), rtol=1e-9, atol=1e-15)
+        assert chains == 2
+        assert np.allclose(pmean, H.mean(axis=0), rtol=1e-12, atol=0)
+        ok = np.isfinite(rhat_ref)
+        assert np.array_equal(ok, np.isfinite(rhat))
+        assert np.allclose(rhat[ok], rhat_ref[ok], rtol=1e-9)
     # the two chains are genuinely different streams
     assert not np.array_equal(_chain(0), _chain(1))
