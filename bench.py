@@ -39,6 +39,8 @@ CONFIGS = {
     "c4": (1_000_000, 4, 128, 64, "BASELINE configs[3] shard: synthetic N=1M V=4 D=128 K=64, 1 chain/GPU"),
     "c2": (100_000, 2, 64, 16, "BASELINE configs[1]: synthetic N=100k V=2 D=64 K=16, 1 chain"),
     "ns": (1_000_000, 4, 1, 64, "north_star literal: synthetic N=1M V=4 D=1 K=64, 1 chain/GPU"),
+    "c5s": (1_000_000, 8, 256, 256, "BASELINE configs[4] shape (V=8 D=256 K=256) at N=1M (N=10M: 164 GB of y, "
+                                    "beyond the box's host-memory cap for the synthetic generator), 1 chain"),
 }
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_F64_TFLOPS = 78.6       # fp64 MFMA / vector dense peak (spec)
@@ -335,7 +337,8 @@ def main():
                 "arith_intensity": round(flops_alg / bytes_alg, 3), "ridge": round(ridge, 3),
                 "bytes_per_launch": bytes_alg, "flops_per_launch": flops_alg, "pass_ms": round(k_avg_s * 1e3, 4),
                 "lp_producer": ("fused" if zpath & 8 else "mfma-all-views" if zpath & 16
-                                else "mfma" if (zpath & 3) == 2 else "generic"),
+                                else "mfma" if (zpath & 3) == 2 else "mfma-dish-blocks" if zpath & 64
+                                else "generic"),
                 "draw": "fused" if zpath & 8 else "registers" if zpath & 4 else "lds-checkpoints"},
         "hyper_pooled": {"chains": red["chains"], "draws": red["count"],
                          "alpha_global": round(float(pooled_mean[-2]), 6),

@@ -375,6 +375,161 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
   }
 }
 
+// MFMA lp producer for one block of up to 16*NTB dishes of view v (dishes
+// jb0 .. jb0 + kb), for views with K_v > 64 or when the tiled copy yt was not
+// built (BASELINE config 5: N = 10M, D = 256, K = 256 -- y alone is 164 GB).
+// Same tile and epilogue as mvc_par_lpview_kernel, with the A-fragments read
+// from y itself (row-major: lane = (row, k), k-step s covers d = 4s + k, so
+// the fma chain over d stays in ascending order: the same bits) or from yt,
+// and the dish block's B-fragments in LDS.  A view with K_v > 16*NTB is one
+// launch per dish block (y re-read per block: at D = 256, K = 256 the
+// arithmetic intensity stays ~16 flop/B, above the fp64 ridge).  The first
+// block writes the view maximum m_v of each customer, later blocks max it in.
+template <int NTB>
+__global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int jb0, int kb, int first, int b0, int nb,
+                                                            double *lpb, double *discard) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
+  const int col = lane & 15, grp = lane >> 4;
+  const int V = P.V, D = P.D, KC = P.KC, n = P.n, T = A.T;
+  const int SP = A.SP;                              // k-steps (padded to MVC_ZR)
+  const int koff = A.Koff[v], K = A.Koff[v + 1] - koff, sumK = A.Koff[V];
+  const double tau = P.hyper[v], L2pt = A.L2pt[v];
+  double *Bs = (double *)smem;                      // [SP][NTB][64]
+  double *wsp = Bs + (size_t)SP * NTB * 64;         // per wave: y2s[16], selfG[16], mrest[16]
+  double *y2s = wsp + w * 48;
+  double *selfG = y2s + 16;
+  double *mrest = selfG + 16;
+  int *ip = (int *)(wsp + 4 * 48);
+  int *t_dish = ip;                                 // [T]
+  int *t_n = t_dish + T;                            // [T]
+  int *zs = t_n + T + w * 16;                       // per wave [16]
+  {   // B-fragments of the dish block: Bs[(s * NTB + t) * 64 + lane] = S1[d = 4s + grp][j = jb0 + 16t + col]
+    const double *S1v = P.S1T + (size_t)v * D * KC;
+    for (int e = tid; e < SP * NTB * 64; e += blockDim.x) {
+      const int ln = e & 63, st = e >> 6, t = st % NTB, ss = st / NTB;
+      const int d = 4 * ss + (ln >> 4), j = jb0 + 16 * t + (ln & 15);
+      Bs[e] = (d < D && j < jb0 + kb) ? S1v[(size_t)d * KC + j] : 0.0;
+    }
+  }
+  for (int p = tid; p < T; p += blockDim.x) {
+    t_dish[p] = P.dish[v * P.TC + p];
+    t_n[p] = P.n_t[p];
+  }
+  __syncthreads();
+  const double cnew = A.cnew[v];
+  const int ntile = (nb + 15) >> 4;
+  const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
+  double *const dslot = discard + lane;
+  const double *yv = A.y + (size_t)v * n * D;
+  for (int tile = gw; tile < ntile; tile += NWT) {
+    const int li0 = tile * 16;
+    const int li_row = min(li0 + col, nb - 1);
+    const int pz = P.z[b0 + li_row];
+    const double y2 = A.Y2[(size_t)v * n + b0 + li_row];
+    const double *yrow = yv + (size_t)(b0 + li_row) * D;   // this lane's row (col), k = grp
+    const bool rok = li0 + col < nb;
+    mvc_d4 acc[NTB];
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+    // A-fragments: 4 k-steps of loads in flight ahead of the MFMAs
+    constexpr int RA = 8;
+    double ar[RA];
+#pragma unroll
+    for (int u = 0; u < RA; ++u) {
+      const int d = 4 * u + grp;
+      ar[u] = (rok && d < D && u < SP) ? yrow[d] : 0.0;
+    }
+    for (int s0 = 0; s0 < SP; s0 += RA) {
+#pragma unroll
+      for (int u = 0; u < RA; ++u) {
+        const int sstep = s0 + u;
+        const double a = ar[u];
+        const int dn = 4 * (sstep + RA) + grp;
+        ar[u] = (rok && dn < D && sstep + RA < SP) ? yrow[dn] : 0.0;
+        const double *bk = Bs + (size_t)sstep * NTB * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bk[t * 64], acc[t], 0, 0, 0);
+      }
+    }
+    // ---- epilogue (as mvc_par_lpview_kernel, dishes jb0 + 16 t + col)
+    if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
+    wave_lds_sync();
+    double hy[4], hr[4];
+    int j0[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double y2r = y2s[grp + 4 * r];
+      hy[r] = 0.5 * y2r;
+      hr[r] = (-0.5 * y2r) / tau;
+      j0[r] = t_dish[zs[grp + 4 * r]];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // G of the own dish (when in this block) -> LDS
+      const int jl = j0[r] - jb0;
+      double g = acc[0][r];
+#pragma unroll
+      for (int t = 1; t < NTB; ++t)
+        if ((jl >> 4) == t) g = acc[t][r];
+      if (jl >= 0 && jl < kb && col == (jl & 15)) selfG[grp + 4 * r] = g;
+    }
+    double mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[r] = -MVC_PM_INF;
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) {
+      const int j = jb0 + 16 * t + col;
+      const int jc = min(j, K - 1);
+      const double c0j = P.c0[v * KC + jc], cbj = P.cb[v * KC + jc];
+      const bool inj = j < jb0 + kb;
+      const bool inc = inj && P.d_l[v * KC + jc] > 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+        const int li = li0 + grp + 4 * r;
+        double *dst = (inj && li < nb) ? lpb + lpb_index(li, koff + j, sumK) : dslot;
+        *dst = val;
+        if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double mr = row16_max(mx[r]);
+      if (col == 0) mrest[grp + 4 * r] = mr;
+    }
+    wave_lds_sync();
+    {   // own dish (when in this block) and the view maximum, one row per lane
+      const int jj = t_dish[pz];
+      const bool own = jj >= jb0 && jj < jb0 + kb;
+      double m = mrest[col];
+      const double hself = (-0.5 * y2) / tau;
+      const bool ok = lane < 16 && li0 + col < nb;
+      if (own) {
+        const double G = selfG[col];
+        const double Gp = G - y2;
+        const double Qp = (P.Q[v * KC + jj] - 2.0 * G) + y2;
+        const Coef cf = coef(P.d_n[v * KC + jj] - 1, Qp, tau, L2pt, D);
+        const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
+        double *dst = ok ? lpb + lpb_index(li0 + col, koff + jj, sumK) : dslot;
+        *dst = sv;
+        const int l0p = P.d_l[v * KC + jj] - ((t_n[pz] - 1) > 0 ? 0 : 1);
+        if (l0p > 0 && sv > m) m = sv;
+      }
+      const double lfn = cnew + hself;
+      if (lfn > m) m = lfn;
+      double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
+      if (!first && ok) m = dmax(m, *dm);   // max is exact: the block order does not matter
+      *dm = m;
+    }
+    wave_lds_sync();
+  }
+}
+__host__ inline size_t lpbig_shared_bytes(int SP, int NTB, int T) {
+  return 8 * ((size_t)SP * NTB * 64 + 4 * 48) + 4 * (2 * (size_t)T + 4 * 16) + 64;
+}
+
 // Generic lp producer: one lane per customer (any D).
 extern "C" __global__ __launch_bounds__(256) void mvc_par_lpgen_kernel(Sweep A, int b0, int nb, double *lpb) {
   const ParState &P = A.P;
@@ -2052,6 +2207,8 @@ class ParallelSampler : public Sampler {
   int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
   int n_cu = 256;
   bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
+  bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
+  bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
   int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
@@ -2167,6 +2324,13 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_run_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
+    if (const char *e = getenv("MVC_BIG")) {
+      no_big = e[0] == '0';
+      force_big = e[0] == '1';
+    }
+    for (const void *f : {(const void *)mvc_par_lpbig_kernel<4>, (const void *)mvc_par_lpbig_kernel<2>,
+                          (const void *)mvc_par_lpbig_kernel<1>})
+      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
@@ -2577,8 +2741,15 @@ class ParallelSampler : public Sampler {
     int Kmax = 0, Kmin = 1 << 30;
     for (int k : c.K) { Kmax = std::max(Kmax, k); Kmin = std::min(Kmin, k); }
     const int sk = sumK(c);
-    const bool use_mfma = !force_generic && c.s1t_ok && Kmin >= 1 && Kmax <= MVC_Z_KMAX &&
+    const bool use_mfma = !force_generic && !force_big && c.s1t_ok && Kmin >= 1 && Kmax <= MVC_Z_KMAX &&
                           lpview_shared_bytes(SP, (Kmax + 15) / 16, Kmax, c.T) <= 160 * 1024;
+    // the dish-block MFMA producer (y read directly) where the tiled path does not apply
+    const int SPb = ((D / 4 + MVC_ZR - 1) / MVC_ZR) * MVC_ZR;
+    int big_ntb = 0;
+    for (int nt : {4, 2, 1})
+      if (!big_ntb && lpbig_shared_bytes(SPb, nt, c.T) <= 80 * 1024) big_ntb = nt;
+    if (!big_ntb && lpbig_shared_bytes(SPb, 1, c.T) <= 160 * 1024) big_ntb = 1;
+    const bool use_big = !use_mfma && !force_generic && !no_big && D % 4 == 0 && D >= 16 && Kmin >= 1 && big_ntb > 0;
     // batch: multiple of 64 customers, lp buffer <= kLpbBudget doubles
     const size_t per64 = (size_t)std::max(1, sk) * 64;
     size_t nb_max = std::max<size_t>(64, (kLpbBudget / per64) * 64);
@@ -2655,6 +2826,25 @@ class ParallelSampler : public Sampler {
           launch_lpview(NT, dim3(grid), dim3(64 * bw), lds, A, v, (int)b0, nb);
           MVC_HIP(hipGetLastError());
         }
+      } else if (use_big) {
+        // K_v > 64 or no tiled copy: dish blocks of 16 * NTB, A-fragments from y
+        const int ntile = (nb + 15) / 16;
+        for (int v = 0; v < V; ++v) {
+          for (int jb0 = 0, first = 1; jb0 < c.K[v]; jb0 += 16 * big_ntb, first = 0) {
+            const int kb = std::min(16 * big_ntb, c.K[v] - jb0);
+            const size_t lds = lpbig_shared_bytes(SPb, big_ntb, c.T);
+            const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
+            const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + 3) / 4));
+            Sweep Ab = A;
+            Ab.SP = SPb;
+            switch (big_ntb) {
+              case 4: hipLaunchKernelGGL((mvc_par_lpbig_kernel<4>), dim3(grid), dim3(256), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              case 2: hipLaunchKernelGGL((mvc_par_lpbig_kernel<2>), dim3(grid), dim3(256), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              default: hipLaunchKernelGGL((mvc_par_lpbig_kernel<1>), dim3(grid), dim3(256), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+            }
+            MVC_HIP(hipGetLastError());
+          }
+        }
       } else {
         hipLaunchKernelGGL(mvc_par_lpgen_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256), 0, stream, A,
                            (int)b0, nb, lpb);
@@ -2679,7 +2869,8 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
-    zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0)) : 32;
+    zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0) |
+                      (use_big ? 64 : 0)) : 32;
     repair(c, s, phaseA);
   }
 

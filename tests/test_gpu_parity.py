@@ -580,3 +580,25 @@ def test_chains_concurrent_equal_serial(monkeypatch):
         one.close()
     conc.close()
     ser.close()
+
+
+@pytest.mark.parametrize("force", ["", "1"])
+def test_dish_block_producer(force, monkeypatch):
+    """The dish-block MFMA producer (mvc_par_lpbig_kernel: A-fragments from y
+    itself, dishes in blocks of 64, the view maximum combined over blocks):
+    K_v = 128 / 64 / 32 at D = 32 (two dish blocks in view 0), warm, and
+    forced onto a K <= 64 shape that the tiled producer would take; bitwise
+    vs the oracle."""
+    if force:
+        monkeypatch.setenv("MVC_BIG", "1")
+    m = _mvc()
+    from mvc_amd import data
+    N, V, D, K = (6000, 3, 32, 128) if not force else (4100, 4, 64, 64)
+    y, z = data.synthetic(N, V, D, K, seed=17)
+    st = _warm_state(z, V, K)
+    s = m.Sampler(y, seed=5, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 3, 0, 1, seed=5, mode=O.PARALLEL, state=st)
+    _check_sweeps(s, ref, 3)
+    assert s.zpath() & 64   # the dish-block producer ran
+    s.close()
