@@ -386,7 +386,7 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
 // arithmetic intensity stays ~16 flop/B, above the fp64 ridge).  The first
 // block writes the view maximum m_v of each customer, later blocks max it in.
 template <int NTB>
-__global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int jb0, int kb, int first, int b0, int nb,
+__global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int jb0, int kb, int first, int b0, int nb,
                                                             double *lpb, double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
@@ -402,10 +402,19 @@ __global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int 
   double *y2s = wsp + w * 48;
   double *selfG = y2s + 16;
   double *mrest = selfG + 16;
-  int *ip = (int *)(wsp + 4 * 48);
-  int *t_dish = ip;                                 // [T]
+  double *b_c0 = wsp + BW * 48;                     // [16 NTB] the block's dish coefficients
+  double *b_cb = b_c0 + 16 * NTB;
+  int *ip = (int *)(b_cb + 16 * NTB);
+  int *b_l = ip;                                    // [16 NTB] table counts l of the block's dishes
+  int *t_dish = b_l + 16 * NTB;                     // [T]
   int *t_n = t_dish + T;                            // [T]
   int *zs = t_n + T + w * 16;                       // per wave [16]
+  for (int e = tid; e < 16 * NTB; e += blockDim.x) {
+    const int jc = min(jb0 + e, K - 1);
+    b_c0[e] = P.c0[v * KC + jc];
+    b_cb[e] = P.cb[v * KC + jc];
+    b_l[e] = P.d_l[v * KC + jc];
+  }
   {   // B-fragments of the dish block: Bs[(s * NTB + t) * 64 + lane] = S1[d = 4s + grp][j = jb0 + 16t + col]
     const double *S1v = P.S1T + (size_t)v * D * KC;
     for (int e = tid; e < SP * NTB * 64; e += blockDim.x) {
@@ -435,13 +444,17 @@ __global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int 
 #pragma unroll
     for (int t = 0; t < NTB; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
     // A-fragments: 4 k-steps of loads in flight ahead of the MFMAs
-    constexpr int RA = 8;
+    constexpr int RA = 16;
     double ar[RA];
 #pragma unroll
     for (int u = 0; u < RA; ++u) {
       const int d = 4 * u + grp;
       ar[u] = (rok && d < D && u < SP) ? yrow[d] : 0.0;
     }
+    // B-fragments one k-step ahead (LDS latency off the MFMA issue path)
+    double bc[NTB];
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) bc[t] = Bs[t * 64 + lane];
     for (int s0 = 0; s0 < SP; s0 += RA) {
 #pragma unroll
       for (int u = 0; u < RA; ++u) {
@@ -449,9 +462,14 @@ __global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int 
         const double a = ar[u];
         const int dn = 4 * (sstep + RA) + grp;
         ar[u] = (rok && dn < D && sstep + RA < SP) ? yrow[dn] : 0.0;
-        const double *bk = Bs + (size_t)sstep * NTB * 64 + lane;
+        double bn[NTB];
+        const double *bk = Bs + (size_t)min(sstep + 1, SP - 1) * NTB * 64 + lane;
 #pragma unroll
-        for (int t = 0; t < NTB; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bk[t * 64], acc[t], 0, 0, 0);
+        for (int t = 0; t < NTB; ++t) bn[t] = bk[t * 64];
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bc[t], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) bc[t] = bn[t];
       }
     }
     // ---- epilogue (as mvc_par_lpview_kernel, dishes jb0 + 16 t + col)
@@ -481,10 +499,9 @@ __global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int 
 #pragma unroll
     for (int t = 0; t < NTB; ++t) {
       const int j = jb0 + 16 * t + col;
-      const int jc = min(j, K - 1);
-      const double c0j = P.c0[v * KC + jc], cbj = P.cb[v * KC + jc];
+      const double c0j = b_c0[16 * t + col], cbj = b_cb[16 * t + col];
       const bool inj = j < jb0 + kb;
-      const bool inc = inj && P.d_l[v * KC + jc] > 0;
+      const bool inc = inj && b_l[16 * t + col] > 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
@@ -526,8 +543,8 @@ __global__ __launch_bounds__(256) void mvc_par_lpbig_kernel(Sweep A, int v, int 
     wave_lds_sync();
   }
 }
-__host__ inline size_t lpbig_shared_bytes(int SP, int NTB, int T) {
-  return 8 * ((size_t)SP * NTB * 64 + 4 * 48) + 4 * (2 * (size_t)T + 4 * 16) + 64;
+__host__ inline size_t lpbig_shared_bytes(int SP, int NTB, int T, int waves) {
+  return 8 * ((size_t)SP * NTB * 64 + (size_t)waves * 48 + 32 * NTB) + 4 * (16 * NTB + 2 * (size_t)T + (size_t)waves * 16) + 64;
 }
 
 // Generic lp producer: one lane per customer (any D).
@@ -2743,12 +2760,17 @@ class ParallelSampler : public Sampler {
     const int sk = sumK(c);
     const bool use_mfma = !force_generic && !force_big && c.s1t_ok && Kmin >= 1 && Kmax <= MVC_Z_KMAX &&
                           lpview_shared_bytes(SP, (Kmax + 15) / 16, Kmax, c.T) <= 160 * 1024;
-    // the dish-block MFMA producer (y read directly) where the tiled path does not apply
+    // the dish-block MFMA producer (y read directly) where the tiled path does
+    // not apply: the widest dish block whose B-fragments fit, 8 waves per block
+    // (one block per CU) when they take more than half the LDS, else 4 waves
+    // and two blocks per CU -- two waves per SIMD either way
     const int SPb = ((D / 4 + MVC_ZR - 1) / MVC_ZR) * MVC_ZR;
-    int big_ntb = 0;
-    for (int nt : {4, 2, 1})
-      if (!big_ntb && lpbig_shared_bytes(SPb, nt, c.T) <= 80 * 1024) big_ntb = nt;
-    if (!big_ntb && lpbig_shared_bytes(SPb, 1, c.T) <= 160 * 1024) big_ntb = 1;
+    int big_ntb = 0, big_waves = 4;
+    for (int nt : {4, 2, 1}) {
+      if (big_ntb) break;
+      if (lpbig_shared_bytes(SPb, nt, c.T, 4) <= 80 * 1024) { big_ntb = nt; big_waves = 4; }
+      else if (lpbig_shared_bytes(SPb, nt, c.T, 8) <= 150 * 1024) { big_ntb = nt; big_waves = 8; }
+    }
     const bool use_big = !use_mfma && !force_generic && !no_big && D % 4 == 0 && D >= 16 && Kmin >= 1 && big_ntb > 0;
     // batch: multiple of 64 customers, lp buffer <= kLpbBudget doubles
     const size_t per64 = (size_t)std::max(1, sk) * 64;
@@ -2832,15 +2854,15 @@ class ParallelSampler : public Sampler {
         for (int v = 0; v < V; ++v) {
           for (int jb0 = 0, first = 1; jb0 < c.K[v]; jb0 += 16 * big_ntb, first = 0) {
             const int kb = std::min(16 * big_ntb, c.K[v] - jb0);
-            const size_t lds = lpbig_shared_bytes(SPb, big_ntb, c.T);
-            const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / lds));
-            const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + 3) / 4));
+            const size_t lds = lpbig_shared_bytes(SPb, big_ntb, c.T, big_waves);
+            const int per_cu = big_waves == 8 ? 1 : 2;
+            const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + big_waves - 1) / big_waves));
             Sweep Ab = A;
             Ab.SP = SPb;
             switch (big_ntb) {
-              case 4: hipLaunchKernelGGL((mvc_par_lpbig_kernel<4>), dim3(grid), dim3(256), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
-              case 2: hipLaunchKernelGGL((mvc_par_lpbig_kernel<2>), dim3(grid), dim3(256), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
-              default: hipLaunchKernelGGL((mvc_par_lpbig_kernel<1>), dim3(grid), dim3(256), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              case 4: hipLaunchKernelGGL((mvc_par_lpbig_kernel<4>), dim3(grid), dim3(64 * big_waves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              case 2: hipLaunchKernelGGL((mvc_par_lpbig_kernel<2>), dim3(grid), dim3(64 * big_waves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              default: hipLaunchKernelGGL((mvc_par_lpbig_kernel<1>), dim3(grid), dim3(64 * big_waves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
             }
             MVC_HIP(hipGetLastError());
           }
