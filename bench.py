@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--seed", type=int, default=1999)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard", action="store_true",
+                    help="N > 1: ONE chain split over the N GPUs (within-chain N-sharding of phase A, an RCCL "
+                         "all-gather of the choices per sweep; strong scaling) instead of one chain per GPU")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra lines (other configs, exact schedule, cold start, reference CPU)")
     return ap.parse_args()
@@ -226,7 +229,8 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # RCCL over xGMI; MVC_BENCH_BACKEND=gloo only to rehearse several ranks on one GPU
+        dist.init_process_group(os.environ.get("MVC_BENCH_BACKEND", "nccl"))
 
     def barrier_sync():
         torch.cuda.synchronize()
@@ -243,8 +247,12 @@ def main():
     # coarse timing in the timed region: HIP events around the z-resample pass
     # (the roofline) and the sweep only; the per-phase breakdown is taken on
     # extra sweeps after the timed region (each event pair idles the GPU ~5 us)
-    s = Sampler(y, seed=args.seed, mode="parallel", first_chain=rank, device=local, timing="coarse")
+    shard = args.shard and world > 1
+    s = Sampler(y, seed=args.seed, mode="parallel", first_chain=0 if shard else rank, device=local, timing="coarse")
     s.set_state(*warm_state(z, V, K))
+    if shard:   # every rank holds the whole chain; phase A split, choices all-gathered
+        from mvc_amd.dist import ShardExchange
+        s.set_shard(rank, world, ShardExchange(N, rank, world, device=local))
     s.sweep(args.warmup)
     s.synchronize()
     s.reset_timers()
@@ -268,14 +276,13 @@ def main():
     # region), reduced across ranks with R-hat
     from mvc_amd import dist as mdist
     s.set_timing(False)
-    cstats = None
+    cstats = mdist.ChainStats(3 * V + 2)
     for _ in range(10):
         s.sweep(1)
         _, _, h = s.state()
         hv = np.concatenate([h["alpha_v"], h["sigma_v"], h["tau_v"], [h["alpha_global"], h["sigma_global"]]])
-        if cstats is None:
-            cstats = mdist.ChainStats(hv.size)
-        cstats.add(0, hv)
+        if not (shard and rank != 0):   # a sharded chain is counted once
+            cstats.add(0, hv)
     n_detail = 3
     s.set_timing(True)
     s.reset_timers()
@@ -302,8 +309,11 @@ def main():
         return
 
     k_avg_s = (kms / max(1, kcnt)) / 1e3
-    bytes_alg = N * (8 * V * D + 8)                 # y read once + z read + choice write
-    flops_alg = 2.0 * N * float(kdish.sum()) * D    # G = Y S1^T per view (MFMA fp64)
+    # customers of rank 0's pass: the whole chain, or its shard (--shard)
+    from mvc_amd.dist import shard_len
+    n_pass = min(N, shard_len(N, world)) if shard else N
+    bytes_alg = n_pass * (8 * V * D + 8)                 # y read once + z read + choice write
+    flops_alg = 2.0 * n_pass * float(kdish.sum()) * D    # G = Y S1^T per view (MFMA fp64)
     hbm_gbs = bytes_alg / k_avg_s / 1e9
     tflops = flops_alg / k_avg_s / 1e12
     ridge = PEAK_F64_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)
@@ -313,7 +323,7 @@ def main():
             if flops_alg / bytes_alg > ridge else
             {"bound": "hbm", "achieved": round(hbm_gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
              "frac": round(hbm_gbs / PEAK_HBM_GBS, 4), "traffic": traffic})
-    value = world * args.steps / elapsed
+    value = (1 if shard else world) * args.steps / elapsed
     out = {
         "metric": "Gibbs sweeps/sec (N×V×K) at 1/2/4/8 MI355X; % HBM roofline",
         "value": round(value, 4),
@@ -323,12 +333,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if shard else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": desc, "N": N, "V": V, "D": D, "K": K, "chains": world,
-                   "schedule": "sequential (reference) schedule, data-parallel pass + in-order repair (DESIGN.md §4.8)", "parallelism": f"chains{world}",
+        "config": {"workload": desc, "N": N, "V": V, "D": D, "K": K, "chains": 1 if shard else world,
+                   "schedule": "sequential (reference) schedule, data-parallel pass + in-order repair (DESIGN.md §4.8)",
+                   "parallelism": f"shard{world}" if shard else f"chains{world}",
                    "tables_at_end": int(T), "dishes_at_end": kdish.tolist()},
         "roofline": roof,
         "hbm": {"pass": "z-resample (lp producer + draw, DESIGN.md §5)", "achieved_gbs": round(hbm_gbs, 1),

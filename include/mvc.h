@@ -162,6 +162,22 @@ int mvc_sampler_zpath(mvc_sampler *s);
  * out[3] dishes opened.  MVC_ERR_UNSUPPORTED for the exact schedule.  (No
  * reference counterpart: diagnostics of this implementation.) */
 int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out);
+/* Within-chain N-sharding (one chain split over `world` processes, one GPU
+ * each, every rank holding the whole data and state).  Phase A of each sweep
+ * (the data-parallel evaluation against the sweep-start state) covers only
+ * this rank's customers, shard `rank` = [rank S, min(n, (rank+1) S)) with
+ * S = mvc_shard_len(n, world).  The handle copies its shard's choices into
+ * `exchange` (device memory, world * S int32), synchronises its stream and
+ * calls all_gather(user), which must return once every rank's shard is in
+ * `exchange` (e.g. an RCCL all-gather in place); then every rank runs the
+ * same in-order repair, compaction and MH on the same state, so the ranks
+ * stay identical to each other and to the unsharded chain, bit for bit.
+ * world = 1 turns sharding off.  One chain per handle; MVC_ERR_UNSUPPORTED
+ * for the exact schedule or several chains.  (No reference counterpart: the
+ * reference runs one chain in one process.) */
+int mvc_sampler_set_shard(mvc_sampler *s, int32_t rank, int32_t world, int32_t *exchange,
+                          void (*all_gather)(void *), void *user);
+int64_t mvc_shard_len(int64_t n, int32_t world);
 /* Opaque HIP stream the handle launches on (hipStream_t as void*). */
 void *mvc_sampler_stream(mvc_sampler *s);
 void mvc_sampler_destroy(mvc_sampler *s);

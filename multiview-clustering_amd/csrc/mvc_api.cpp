@@ -395,6 +395,18 @@ int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out) {
   }
 }
 
+int mvc_sampler_set_shard(mvc_sampler *s, int32_t rank, int32_t world, int32_t *exchange,
+                          void (*all_gather)(void *), void *user) {
+  if (!s || !s->impl) return MVC_ERR_ARG;
+  try {
+    return s->impl->set_shard(rank, world, exchange, all_gather, user) ? MVC_OK : MVC_ERR_UNSUPPORTED;
+  } catch (const mvc::Error &e) {
+    return e.code;
+  }
+}
+
+int64_t mvc_shard_len(int64_t n, int32_t world) { return mvc::shard_len(n, world); }
+
 void *mvc_sampler_stream(mvc_sampler *s) { return (s && s->impl) ? (void *)s->impl->stream : nullptr; }
 
 void mvc_sampler_destroy(mvc_sampler *s) { delete s; }

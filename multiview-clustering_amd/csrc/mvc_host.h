@@ -85,6 +85,12 @@ class Sampler {
   // out[0] customers that moved, out[1] births, out[2] repair rounds,
   // out[3] dishes opened.  False for the exact schedule.
   virtual bool repair_stats(int chain, int32_t *out) { (void)chain; (void)out; return false; }
+  // Within-chain N-sharding (mvc_sampler_set_shard): false where unsupported
+  // (the exact schedule, several chains per handle).
+  virtual bool set_shard(int rank, int world, int32_t *exch, void (*cb)(void *), void *user) {
+    (void)rank; (void)world; (void)exch; (void)cb; (void)user;
+    return false;
+  }
   // HIP-event timing (mvc_sampler_set_timing / reset_timers / kernel_time)
   virtual void set_timing(bool on, bool coarse) {
     synchronize();
@@ -110,6 +116,13 @@ class Sampler {
 // in mcclust::arandi's operation order (New_Simulation.R:189).
 double ari_device(const int32_t *da, const int32_t *db, int64_t n, hipStream_t stream);
 double ari_from_pairs(uint64_t a, uint64_t sa, uint64_t sb, int64_t n);
+
+// Customers per shard of within-chain N-sharding: ceil(n / world) rounded up
+// to 64 (the phase-A batches' alignment); shard r is [r S, min(n, (r+1) S)).
+inline int64_t shard_len(int64_t n, int world) {
+  const int64_t w = world < 1 ? 1 : world;
+  return ((n + w - 1) / w + 63) / 64 * 64;
+}
 
 // Validated host view of a user-supplied state (warm start / resume).
 struct UserState {

@@ -1536,7 +1536,7 @@ __host__ __device__ inline size_t lpall_shared_bytes(size_t s1t_doubles, int V, 
 }
 
 template <int NT, int SPPT, int RP>
-__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int li0, int nb, int pz, double y2,
+__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int b0, int li0, int nb, int pz, double y2,
                                          const mvc_d2 *cur, const mvc_d2 *nxt, mvc_d2 (&ring)[RP], double *lpb,
                                          double *dslot, double *y2s, double *selfG, double *mrest, int *zs) {
   const ParState &P = A.P;
@@ -1608,29 +1608,29 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
     if (l0p > 0 && sv > m) m = sv;
     const double lfn = cnew + hself;
     if (lfn > m) m = lfn;
-    double *dm = ok ? A.vmax + (size_t)v * n + li0 + col : dslot;
+    double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
     *dm = m;
   }
   wave_lds_sync();
 }
 
 template <int SPPT, int RP, uint32_t PAT, int VI>
-__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int li0, int nb, int pz,
+__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int b0, int li0, int nb, int pz,
                                           const double (&y2v)[MVC_Z_VMAX], const mvc_d2 *ybase, size_t vstride,
                                           size_t tcur, size_t tnext, mvc_d2 (&ring)[RP], double *lpb, double *dslot,
                                           double *y2s, double *selfG, double *mrest, int *zs) {
   if constexpr (VI < fz_pat_v(PAT)) {
     const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
     const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
-    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, li0, nb, pz, y2v[VI], cur, nxt, ring, lpb, dslot, y2s, selfG,
+    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, b0, li0, nb, pz, y2v[VI], cur, nxt, ring, lpb, dslot, y2s, selfG,
                                            mrest, zs);
-    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, li0, nb, pz, y2v, ybase, vstride, tcur, tnext, ring, lpb, dslot, y2s,
+    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, b0, li0, nb, pz, y2v, ybase, vstride, tcur, tnext, ring, lpb, dslot, y2s,
                                      selfG, mrest, zs);
   }
 }
 
 template <int SPPT, int RP, uint32_t PAT>
-__global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, double *lpb, double *discard) {
+__global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int nb, double *lpb, double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int tid = threadIdx.x;
@@ -1680,13 +1680,15 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, double *lpb
   const LpaLds L{Bs, f_c0, f_cb, f_Q, f_dn, f_dl, f_tix, f_nt, s_koff, s_boff};
   double *y2s = wsp, *selfG = wsp + 16, *mrest = wsp + 32;
 
-  const int ntile = (n + 15) >> 4;
+  // customers [b0, b0 + nb) (b0 a multiple of 16): local tiles; yt, z, Y2 and
+  // vmax are indexed by customer, the lp buffer by batch position
+  const int ntile = (nb + 15) >> 4, tb0 = b0 >> 4;
   const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
   if (gw >= ntile) return;                         // whole wave: no barriers below
   const int nmy = (ntile - gw + NWT - 1) / NWT;
-  const size_t vstride = (size_t)ntile * SPPT * 64;
+  const size_t vstride = (size_t)((n + 15) >> 4) * SPPT * 64;
   const mvc_d2 *ybase = (const mvc_d2 *)A.yt + lane;
-  auto toff = [&](int m) -> size_t { return (size_t)(gw + min(m, nmy - 1) * NWT) * SPPT * 64; };
+  auto toff = [&](int m) -> size_t { return (size_t)(tb0 + gw + min(m, nmy - 1) * NWT) * SPPT * 64; };
   mvc_d2 ring[RP];
   {
     const mvc_d2 *c0p = ybase + toff(0);
@@ -1696,12 +1698,12 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, double *lpb
   double *const dslot = discard + lane;
   for (int m = 0; m < nmy; ++m) {
     const int li0 = (gw + m * NWT) * 16;
-    const int li_row = min(li0 + col, n - 1);
+    const int li_row = min(b0 + li0 + col, n - 1);
     const int pz = P.z[li_row];
     double y2v[MVC_Z_VMAX];
 #pragma unroll
     for (int v = 0; v < MVC_Z_VMAX; ++v) y2v[v] = v < V ? A.Y2[(size_t)v * n + li_row] : 0.0;
-    lpa_views<SPPT, RP, PAT, 0>(A, L, li0, n, pz, y2v, ybase, vstride, toff(m), toff(m + 1), ring, lpb, dslot, y2s,
+    lpa_views<SPPT, RP, PAT, 0>(A, L, b0, li0, nb, pz, y2v, ybase, vstride, toff(m), toff(m + 1), ring, lpb, dslot, y2s,
                                 selfG, mrest, zs);
   }
 }
@@ -2219,6 +2221,12 @@ class ParallelSampler : public Sampler {
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   size_t lpb_batch = 0;           // MVC_LPB_BATCH: customers per phase-1 batch (0: kLpbBudget)
   bool no_fused = true;           // MVC_FUSED=1: the fused phase-1 kernel where it applies (experimental: slower today)
+  // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
+  // rank's customers only; exch_cb all-gathers the choices into shard_exch
+  int shard_rank = 0, shard_world = 1;
+  int32_t *shard_exch = nullptr;
+  void (*shard_cb)(void *) = nullptr;
+  void *shard_user = nullptr;
   bool no_lpall = false;          // MVC_LPALL=0: per-view producer launches even where the all-views producer applies
   int fz_waves = MVC_FZ_THREADS / 64;   // waves per block of the fused kernel (MVC_FZ_WAVES: fewer)
   int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
@@ -2228,6 +2236,7 @@ class ParallelSampler : public Sampler {
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
   int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
+  int team_w = 1;                 // waves per customer in the run kernel (MVC_TEAM; default by V)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
 
   template <class Tp>
@@ -2338,8 +2347,8 @@ class ParallelSampler : public Sampler {
     fused_attr<4, 4>();
     fused_attr<8, 8>();
     fused_attr<16, MVC_FZ_RP16>();
-    MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_run_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
+    for (const void *f : {(const void *)mvc_seq_run_kernel<false>, (const void *)mvc_seq_run_kernel<true>})
+      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {
       no_big = e[0] == '0';
@@ -2350,6 +2359,15 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
+    // MVC_TEAM=2/4: a customer's views split over a team of waves (fewer
+    // customers per step, each evaluated with more lanes).  Measured slower
+    // than one wave per customer at configs[1] and configs[3] cold starts and
+    // 4 % faster on the D = 1 literal, so off by default.
+    team_w = 1;
+    if (const char *e = getenv("MVC_TEAM")) {
+      const int t = atoi(e);
+      team_w = (t >= 4 && V >= 4) ? 4 : (t >= 2 && V >= 2) ? 2 : 1;
+    }
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh_in);
@@ -2719,12 +2737,12 @@ class ParallelSampler : public Sampler {
     }
   }
   template <int SPPT, int RP>
-  void launch_lpall(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A) {
+  void launch_lpall(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A, int b0, int nb) {
     double *disc = lpb + lpb_cap;
     switch (pat) {
 #define X(p)                                                                                       \
   case p:                                                                                          \
-    hipLaunchKernelGGL((mvc_par_lpall_kernel<SPPT, RP, p>), grid, block, lds, stream, A, lpb, disc); \
+    hipLaunchKernelGGL((mvc_par_lpall_kernel<SPPT, RP, p>), grid, block, lds, stream, A, b0, nb, lpb, disc); \
     break;
       MVC_FZ_PATS(X)
 #undef X
@@ -2800,7 +2818,7 @@ class ParallelSampler : public Sampler {
       break;
       default: pat_ok = false;
     }
-    const bool use_fused = !no_fused && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
+    const bool use_fused = !no_fused && shard_world == 1 && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                            (spp == 4 || spp == 8 || spp == 16) && fz_lds <= 160 * 1024;
     if (phaseA && !use_fused && need > lpb_cap) {   // the lp buffer only exists for the two-kernel path
       if (lpb) hipFree(lpb);
@@ -2821,20 +2839,23 @@ class ParallelSampler : public Sampler {
       }
       MVC_HIP(hipGetLastError());
     }
-    for (size_t b0 = 0; phaseA && !use_fused && b0 < (size_t)n; b0 += nbatch_sz) {
-      const int nb = (int)std::min(nbatch_sz, (size_t)n - b0);
+    // this rank's customers [lo, hi) (the whole chain unless sharded)
+    const size_t S = (size_t)shard_len(n, shard_world);
+    const size_t lo = std::min((size_t)n, (size_t)shard_rank * S), hi = std::min((size_t)n, lo + S);
+    for (size_t b0 = lo; phaseA && !use_fused && b0 < hi; b0 += nbatch_sz) {
+      const int nb = (int)std::min(nbatch_sz, hi - b0);
       hipEvent_t el = nullptr, ed = nullptr;
       timers.begin("lp", &el);
       const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, 8);
-      const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB && b0 == 0 && nb == n &&
+      const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                              (spp == 4 || spp == 8 || spp == 16) && lpa_lds <= 160 * 1024;
       if (use_lpall) {
-        const int ntile = (n + 15) / 16;
+        const int ntile = (nb + 15) / 16;
         const int grid = std::max(1, std::min(n_cu, (ntile + 7) / 8));
         switch (spp) {
-          case 4: launch_lpall<4, 4>(fz_pat, dim3(grid), dim3(512), lpa_lds, A); break;
-          case 8: launch_lpall<8, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A); break;
-          default: launch_lpall<16, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A); break;
+          case 4: launch_lpall<4, 4>(fz_pat, dim3(grid), dim3(512), lpa_lds, A, (int)b0, nb); break;
+          case 8: launch_lpall<8, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A, (int)b0, nb); break;
+          default: launch_lpall<16, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A, (int)b0, nb); break;
         }
         zpath_lpall = true;
       } else if (use_mfma) {
@@ -2891,6 +2912,17 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
+    if (phaseA && shard_world > 1) {
+      // the other ranks' phase-A choices: this shard into the exchange buffer,
+      // the caller's all-gather (synchronous), every shard back.  Each rank
+      // then runs the same repair on the same state: no other exchange.
+      if (hi > lo)
+        MVC_HIP(hipMemcpyAsync(shard_exch + lo, c.choice + lo, (hi - lo) * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                               stream));
+      MVC_HIP(hipStreamSynchronize(stream));
+      shard_cb(shard_user);
+      MVC_HIP(hipMemcpyAsync(c.choice, shard_exch, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, stream));
+    }
     zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0) |
                       (use_big ? 64 : 0)) : 32;
     repair(c, s, phaseA);
@@ -2917,9 +2949,11 @@ class ParallelSampler : public Sampler {
       L.cache_dbl = seq_lds_cache(V, D, L.ks, L.ts, s1);
       L.stride = seq_lds_stride(V, D, L.ks, L.ts);
       const int64_t room = (int64_t)kSeqLdsBudget / 8 - L.cache_dbl;
-      L.nws = room > 0 ? (int)std::min<int64_t>(run_waves, room / L.stride) : 0;
-      if (L.nws >= std::min(run_waves, s1 ? 4 : 2)) {
+      const int cap = std::min(run_waves, kSeqRunWaves / team_w);   // customers per step
+      L.nws = room > 0 ? (int)std::min<int64_t>(cap, room / L.stride) : 0;
+      if (L.nws >= std::min(cap, s1 ? 4 : 2)) {
         L.lds = 1;
+        L.tw = team_w;
         // the staged-row ring in what is left: a power of two >= 2 nws customers
         const int64_t slot = seq_ring_slot(V, D);
         const int64_t left = room - (int64_t)L.nws * L.stride;
@@ -2933,6 +2967,7 @@ class ParallelSampler : public Sampler {
       }
     }
     L.lds = 0;   // per-wave global scratch (SeqScratch(A, w)): capacity-sized, never restrides
+    L.tw = 1;
     L.s1 = 0;
     L.nws = run_waves;
     L.stride = 0;
@@ -2965,7 +3000,7 @@ class ParallelSampler : public Sampler {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
         else
-          hipLaunchKernelGGL(mvc_seq_run_kernel, dim3(1), dim3(kSeqRunThreads),
+          hipLaunchKernelGGL(L.tw > 1 ? mvc_seq_run_kernel<true> : mvc_seq_run_kernel<false>, dim3(1), dim3(kSeqRunThreads),
                              L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
                              stream, Q, L);
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
@@ -3084,6 +3119,17 @@ class ParallelSampler : public Sampler {
 
   void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
 
+  bool set_shard(int rank, int world, int32_t *exch, void (*cb)(void *), void *user) override {
+    if (world < 1 || rank < 0 || rank >= world || (world > 1 && (!exch || !cb)))
+      throw Error(MVC_ERR_ARG, "set_shard: rank / world / exchange");
+    synchronize();
+    shard_rank = rank;
+    shard_world = world;
+    shard_exch = exch;
+    shard_cb = cb;
+    shard_user = user;
+    return true;
+  }
   bool repair_stats(int chain, int32_t *out) override {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
     for (int k = 0; k < 4; ++k) out[k] = chains[chain].last[k];

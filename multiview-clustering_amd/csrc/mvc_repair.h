@@ -74,12 +74,14 @@ struct SeqLds {
   int64_t stride;       // doubles per wave
   int32_t ring;         // customers in the staged-row ring (power of 2, after the per-wave scratch; 0: none)
   int32_t pfn;          // customers prefetched into the ring per step
+  int32_t tw;           // waves per customer (1: seq_resample; 2, 4: seq_resample_team); nws customers per step
 };
 // ring slot: y rows [V][D], Y2 [V], z (as a double)
 __host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
 
 __host__ __device__ inline int64_t seq_lds_stride(int V, int D, int ks, int ts) {
-  return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + 2;
+  // ... + ys [V][D] + Y2 [V] + (teams) lm_v [V] + member maxima [4]
+  return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + V + 4;
 }
 __host__ __device__ inline int64_t seq_lds_cache(int V, int D, int ks, int ts, bool s1) {
   const int64_t ints = (int64_t)ts + (int64_t)V * ts + 2 * (int64_t)V * ks + 2 * V + 2;
@@ -601,6 +603,244 @@ __device__ int seq_resample(const SeqArgs &A, const SView &W, const Cust &C, int
   return pick;
 }
 
+// seq_resample by a team of tw waves (run kernel, tw = 2 or 4): member r owns
+// views r, r + tw, ... (their lp, terms, marginals) and the 64-table chunks
+// q = r mod tw (scores, weights, block sums); member 0 draws.  The team
+// shares S (lp / aux / e / B per view / table; mv, K_act, lm_v, member
+// maxima).  Every quantity is the same operations in the same order as in
+// seq_resample, so the same bits.  Block-wide: every wave of the block calls
+// it (act = false: no customer, barriers only); three __syncthreads.
+// Returns the pick on member 0.
+__device__ int seq_resample_team(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
+                                 int r, int tw, bool act) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
+  const int V = P.V, D = P.D, ts = W.ts, ks = W.ks, lps = S.lps;
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  double *lmv = S.ys + (size_t)V * D + V, *mxr = lmv + V;
+  int32_t *kact = S.koff + V + 1;
+  int np0 = 0, Tne_i = 0;
+  bool alive = false;
+  double lmass0 = 0.0;
+  RUN_T0();
+  if (act) {
+    np0 = W.n_t[p0] - 1;
+    alive = np0 > 0;
+    Tne_i = *W.T_ne - (alive ? 0 : 1);
+    const double mass0 = (double)np0 - sg;
+    lmass0 = (np0 >= 1 && mass0 > 0.0) ? mvc_log(mass0) : 0.0;
+    const int nvr = r < V ? (V - r + tw - 1) / tw : 0;   // views of this member
+    int NK = 0;
+    for (int q = 0; q < nvr; ++q) NK += W.Klist[r + q * tw];
+    // pass 1: lp of the member's listed dishes (concatenated in view order)
+    for (int g0 = 0; g0 < NK; g0 += 64) {
+      const int g = g0 + lane;
+      if (g < NK) {
+        int v = r, off = 0;
+        while (g >= off + W.Klist[v]) { off += W.Klist[v]; v += tw; }
+        const int j = g - off;
+        const double tau = P.hyper[v];
+        const double Y2i = C.Y2[(size_t)v * C.y2stride];
+        const double hy = 0.5 * Y2i;
+        const double h = (-0.5 * Y2i) / tau;
+        const double G = fma_dot_strided(C.y + (size_t)v * C.ystride, W.S1T + (size_t)v * D * W.s1s + j, (size_t)W.s1s, D, 0.0);
+        double val;
+        if (j == W.dish[v * ts + p0]) {
+          const double Gp = G - Y2i;
+          const double Qp = (W.Q[v * ks + j] - 2.0 * G) + Y2i;
+          double c0, cb;
+          if (W.xm) {
+            c0 = W.xm[v * ks + j] - (0.5 * Qp) / W.ym[v * ks + j];
+            cb = W.cbm[v * ks + j];
+          } else {
+            const Coef c = coef(W.d_n[v * ks + j] - 1, Qp, tau, A.L2pt[v], D);
+            c0 = c.c0;
+            cb = c.cb;
+          }
+          val = __builtin_fma(Gp + hy, cb, c0) + h;
+        } else {
+          val = __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
+        }
+        S.lp[v * lps + j] = val;
+      }
+    }
+    __threadfence_block();
+    // max / K_act of four member views at once (one per row)
+    for (int q0 = 0; q0 < nvr; q0 += 4) {
+      const int v = r + (q0 + row) * tw;
+      double mx = -MVC_PM_INF;
+      int cnt = 0;
+      if (q0 + row < nvr) {
+        const int K = W.Klist[v];
+        const int j0 = W.dish[v * ts + p0];
+        for (int j = col; j < K; j += 16) {
+          const int l = W.d_l[v * ks + j] - ((j == j0 && !alive) ? 1 : 0);
+          if (l > 0) {
+            ++cnt;
+            const double x = S.lp[v * lps + j];
+            if (x > mx) mx = x;
+          }
+        }
+      }
+      mx = row16_max(mx);
+      cnt = row16_isum(cnt);
+      if (q0 + row < nvr && col == 0) {
+        const double Y2i = C.Y2[(size_t)v * C.y2stride];
+        const double lfn = A.cnew[v] + (-0.5 * Y2i) / P.hyper[v];
+        S.mv[v] = lfn > mx ? lfn : mx;
+        kact[v] = cnt;
+      }
+    }
+    __threadfence_block();
+    // pass 2: weighted terms of the member's included dishes
+    for (int g0 = 0; g0 < NK; g0 += 64) {
+      const int g = g0 + lane;
+      if (g < NK) {
+        int v = r, off = 0;
+        while (g >= off + W.Klist[v]) { off += W.Klist[v]; v += tw; }
+        const int j = g - off;
+        const int l = W.d_l[v * ks + j] - ((j == W.dish[v * ts + p0] && !alive) ? 1 : 0);
+        double t = 0.0;
+        if (l > 0) {
+          double w = (double)l - P.hyper[2 * V + v];
+          if (w < 0.0) w = 0.0;
+          t = w * mvc_exp(S.lp[v * lps + j] - S.mv[v]);
+        }
+        S.aux[v * lps + j] = t;
+      }
+    }
+    __threadfence_block();
+    // column partials / pw16 / new dish / lm_v of four member views at once
+    for (int q0 = 0; q0 < nvr; q0 += 4) {
+      const int v = r + (q0 + row) * tw;
+      double cs = 0.0;
+      if (q0 + row < nvr) {
+        const int K = W.Klist[v];
+        for (int j = col; j < K; j += 16) cs = cs + S.aux[v * lps + j];
+      }
+      double Sv = row_pw16(cs);
+      if (q0 + row < nvr && col == 0) {
+        const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+        const double Y2i = C.Y2[(size_t)v * C.y2stride];
+        const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
+        const double m = S.mv[v];
+        double wn = alpha + (double)kact[v] * sigma;
+        if (wn < 0.0) wn = 0.0;
+        Sv = Sv + wn * mvc_exp(lfn - m);
+        const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
+        lmv[v] = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - mvc_log(denom);
+      }
+    }
+  }
+  __syncthreads();
+  RUN_MARK(0);
+  // s_new in view order (every member); table scores of the member's chunks
+  double s_new = 0.0, M = -MVC_PM_INF;
+  const int T = *W.T;
+  const int TB = (T + 15) / 16;
+  if (act) {
+    s_new = mvc_log(ag + sg * (double)Tne_i);
+    for (int v = 0; v < V; ++v) s_new = s_new + lmv[v];
+    constexpr int kU = 4;
+    const int nch = TB * 16;   // padded table slots; chunk c covers [64 c, 64 c + 64)
+    for (int c0 = r; c0 * 64 < nch; c0 += tw * kU) {
+      int np[kU];
+      double lm[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        np[u] = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+        lm[u] = p < T ? ((p == p0) ? lmass0 : W.lmass[p]) : 0.0;
+      }
+      double sp[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        const double mass = (double)np[u] - sg;
+        sp[u] = (p < T && np[u] >= 1 && mass > 0.0) ? lm[u] : -MVC_PM_INF;
+      }
+      for (int v = 0; v < V; ++v) {
+        int dj[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int p = (c0 + u * tw) * 64 + lane;
+          dj[u] = (sp[u] != -MVC_PM_INF) ? W.dish[v * ts + p] : 0;
+        }
+        double lv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) lv[u] = S.lp[v * lps + dj[u]];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (sp[u] != -MVC_PM_INF) sp[u] = sp[u] + lv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        if (p < nch) S.e[p] = sp[u];
+        if (sp[u] > M) M = sp[u];
+      }
+    }
+    M = wave_max(M);
+    if (lane == 0) mxr[r] = M;
+  }
+  __syncthreads();
+  RUN_MARK(1);
+  if (act) {
+    for (int k = 0; k < tw; ++k) M = mxr[k] > M ? mxr[k] : M;
+    if (s_new > M) M = s_new;
+    // weights and block sums of the member's chunks
+    for (int c0 = r; c0 * 64 < TB * 16; c0 += tw) {
+      const int p = c0 * 64 + lane;
+      double wgt = 0.0;
+      if (p < TB * 16) {
+        const double x = S.e[p];
+        wgt = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
+        S.e[p] = wgt;
+      }
+      const double Bv = row_pw16(wgt);
+      const int b = c0 * 4 + row;
+      if (col == 0 && b < TB) S.B[b] = Bv;
+    }
+  }
+  __syncthreads();
+  RUN_MARK(2);
+  int pick = -1;
+  if (act && r == 0) {
+    double tot = 0.0;
+    for (int b0 = 0; b0 < TB; b0 += 64) {
+      const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
+      const int nb = min(64, TB - b0);
+      for (int k = 0; k < nb; ++k) tot = tot + readlane_d(Bl, k);
+    }
+    const double Wt = mvc_exp(s_new - M) + tot;
+    double u = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
+    if (u < tot) {
+      double c = 0.0, cprev = 0.0;
+      int bsel = TB - 1;
+      bool found = false;
+      for (int b0 = 0; b0 < TB && !found; b0 += 64) {
+        const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
+        const int nb = min(64, TB - b0);
+        for (int k = 0; k < nb; ++k) {
+          const double c2 = c + readlane_d(Bl, k);
+          if (u < c2) {
+            bsel = b0 + k;
+            cprev = c;
+            found = true;
+            break;
+          }
+          c = c2;
+        }
+      }
+      u = u - cprev;
+      const double x = lane < 16 ? S.e[bsel * 16 + lane] : 0.0;
+      pick = bsel * 16 + pw16_select_wave(x, u);
+    }
+  }
+  RUN_MARK(3);
+  return pick;
+}
+
 // tree64 over x[0..m) (oracle Tree64::build): level arrays stored one after
 // the other from `lv` (level k starts at the sum of the lower levels' counts);
 // returns the root.  nlev receives the number of levels (leaves included).
@@ -1076,7 +1316,7 @@ __device__ __forceinline__ int ring_z(const Ring &G, int c, int V, int D) {
 
 // The run kernel's loop, for state read through the LDS cache (kLds) or the
 // global arrays.  Returns through ovf / restride why it stopped early.
-template <bool kLds>
+template <bool kLds, bool kTeam>
 __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
                              const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride) {
   const ParState &P = A.P;
@@ -1089,7 +1329,10 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
     if (U.pend) {
       const bool staged = ring && U.cur < U.fill && U.cur >= U.fill - G.n;
       const Cust Ci = staged ? G.cust(U.cur, V, D) : global_cust(A, U.cur);
-      if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt, kLds ? L.nws : (int)(blockDim.x >> 6))) {
+      // dish draws of a birth: wave w < nwd, lp scratch = its slice of its team's lp
+      const int tw = kTeam ? L.tw : 1;
+      if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp + (size_t)(w % tw) * L.ks, tree, U.cnt,
+                      kLds ? L.nws * tw : (int)(blockDim.x >> 6))) {
         // overflow: the host grows and relaunches
         ovf = 1;
         return;
@@ -1136,8 +1379,29 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       if (p1c > p0c) ring_fill_async(A, G, p0c, p1c);
       fill_next = max(p1c, need);   // U.fill is written after the decision barrier (every wave read it above)
     }
+    if (kTeam) {   // teams of tw waves, one customer each
+      const int team = w / L.tw, r = w % L.tw;
+      const int i = i0 + team;
+      const bool act = team < L.nws && i < n;
+      int p0 = 0;
+      Cust C{};
+      if (act) {
+        if (ring) {
+          C = G.cust(i, V, D);
+          p0 = ring_z(G, i, V, D);
+        } else {
+          p0 = P.z[i];
+          C = global_cust(A, i);
+        }
+      }
+      const int c = seq_resample_team(A, Wv, C, i, p0, S, r, L.tw, act);
+      if (act && r == 0 && lane == 0) {
+        U.ch[team] = c;
+        U.p0[team] = p0;
+      }
+    }
     const int i = i0 + w;
-    if (w < L.nws && i < n) {
+    if (!kTeam && w < L.nws && i < n) {
       int p0;
       Cust C;
       if (ring) {
@@ -1208,7 +1472,10 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 // customer costs one memory latency (its y rows) plus LDS work.  After
 // L.limit stays in a row the movers are sparse: the kernel opens a grid
 // window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
-extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
+// kTeam: the instance for L.tw > 1 (teams of waves per customer; LDS layouts
+// only), compiled separately so each keeps its own register allocation.
+template <bool kTeam>
+__global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
   extern __shared__ double seq_sm[];
   Repair *R = A.R;
   ParState &P = A.P;
@@ -1315,11 +1582,12 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(
     G.n = L.ring;
     G.slot = (int)seq_ring_slot(V, D);
     G.base = seq_sm + L.cache_dbl + (int64_t)L.nws * L.stride;
-    seq_run_loop<true>(A, L, cache_view(cc, A), &cc, SeqScratch(seq_sm + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
-                       G, tree, U, ovf, restride);
-  } else {
+    seq_run_loop<true, kTeam>(A, L, cache_view(cc, A), &cc,
+                              SeqScratch(seq_sm + L.cache_dbl + (int64_t)(w / L.tw) * L.stride, V, L.ks, L.ts), G,
+                              tree, U, ovf, restride);
+  } else if constexpr (!kTeam) {
     Ring G{nullptr, 0, 0};
-    seq_run_loop<false>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
+    seq_run_loop<false, false>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
     R->cur = U.cur;

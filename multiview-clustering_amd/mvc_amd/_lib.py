@@ -20,6 +20,10 @@ FLAG_TIMING_COARSE = 4
 TRACE_ALPHA_V, TRACE_SIGMA_V, TRACE_TAU_V, TRACE_ALPHA_GLOBAL, TRACE_SIGMA_GLOBAL = range(5)
 
 
+# all_gather callback of mvc_sampler_set_shard: void (*)(void *user)
+SHARD_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
 class MvcError(RuntimeError):
     """Error returned through the C ABI (status code + message)."""
 
@@ -95,6 +99,8 @@ def lib():
         "mvc_sampler_ari": (i32, [vp, i32, ip, dp, cp, sz]),
         "mvc_ari": (i32, [i32, ip, ip, i64, dp, cp, sz]),
         "mvc_sampler_stream": (vp, [vp]),
+        "mvc_sampler_set_shard": (i32, [vp, i32, i32, vp, vp, vp]),
+        "mvc_shard_len": (i64, [i64, i32]),
         "mvc_sampler_destroy": (None, [vp]),
         "mvc_device_math": (i32, [i32, i32, dp, dp, i64, cp, sz]),
         "mvc_device_seq_uniforms": (i32, [i32, u64, u32, u64, dp, i64, cp, sz]),

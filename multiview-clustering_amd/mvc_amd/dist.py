@@ -158,3 +158,48 @@ class ChainStats:
         with np.errstate(divide="ignore", invalid="ignore"):
             out["rhat"] = np.where(W > 0, np.sqrt(vplus / W), np.nan)
         return out
+
+
+def shard_len(n, world):
+    """Customers per shard (mvc_shard_len): ceil(n / world) rounded up to 64."""
+    w = max(1, int(world))
+    return ((n + w - 1) // w + 63) // 64 * 64
+
+
+class ShardExchange:
+    """The phase-A choice exchange of within-chain N-sharding
+    (Sampler.set_shard, include/mvc.h mvc_sampler_set_shard).
+
+    Owns a device buffer of world * shard_len(n) int32 (a torch tensor on
+    this rank's GPU).  The handle copies its shard into it and calls
+    all_gather() from its sweep; with backend "nccl" (RCCL over xGMI) that is
+    one in-place all-gather of 4 n bytes, with "gloo" the shards go through
+    host memory (tests: several ranks sharing one GPU).  Returns after the
+    exchange has completed on the device."""
+
+    def __init__(self, n, rank, world, device=0, group=None):
+        import torch
+        import torch.distributed as dist
+        self.n, self.rank, self.world = n, rank, world
+        self.S = shard_len(n, world)
+        self.group = group
+        self.dev = torch.device("cuda", device)
+        self.buf = torch.zeros(world * self.S, dtype=torch.int32, device=self.dev)
+        self.ptr = self.buf.data_ptr()
+        self._dist = dist
+        self._torch = torch
+        self._nccl = dist.get_backend(group) == "nccl"
+        self.calls = 0
+
+    def all_gather(self):
+        dist, torch = self._dist, self._torch
+        self.calls += 1
+        mine = self.buf[self.rank * self.S:(self.rank + 1) * self.S]
+        if self._nccl:
+            dist.all_gather_into_tensor(self.buf, mine, group=self.group)
+            torch.cuda.synchronize(self.dev)
+        else:
+            host = [torch.empty(self.S, dtype=torch.int32) for _ in range(self.world)]
+            dist.all_gather(host, mine.cpu(), group=self.group)
+            self.buf.copy_(torch.cat(host).to(self.dev))
+            torch.cuda.synchronize(self.dev)

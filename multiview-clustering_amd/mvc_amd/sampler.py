@@ -147,6 +147,9 @@ class Sampler:
     def sweep(self, n_sweeps=1):
         buf = L.errbuf()
         L.check(self._lib.mvc_sampler_sweep(self._h, n_sweeps, buf, len(buf)), buf)
+        err, self._shard_err = getattr(self, "_shard_err", None), None
+        if err is not None:
+            raise RuntimeError("shard exchange failed") from err
 
     def synchronize(self):
         buf = L.errbuf()
@@ -250,6 +253,31 @@ class Sampler:
         if st != L.MVC_OK:
             raise L.MvcError(st, "repair_stats failed")
         return dict(zip(("moves", "births", "rounds", "newdish"), (int(x) for x in out)))
+
+    def set_shard(self, rank, world, exchange=None):
+        """Within-chain N-sharding (mvc_sampler_set_shard): phase A of each
+        sweep covers this rank's customers only; ``exchange`` (e.g.
+        ``dist.ShardExchange``) owns the device buffer (``exchange.ptr``,
+        world * shard_len int32) and its ``all_gather()`` fills every shard.
+        world = 1 turns sharding off."""
+        if world > 1 and exchange is None:
+            raise ValueError("set_shard: world > 1 needs an exchange")
+        self._shard_cb = None
+        ptr = None
+        if world > 1:
+            def _cb(_user):
+                try:
+                    exchange.all_gather()
+                except BaseException as e:   # an exception cannot cross the C frame: re-raised by sweep()
+                    self._shard_err = e
+            self._shard_cb = L.SHARD_CB(_cb)   # kept alive with the handle
+            ptr = ctypes.c_void_p(exchange.ptr)
+        self._shard_ex = exchange
+        st = self._lib.mvc_sampler_set_shard(self._h, rank, world, ptr,
+                                             ctypes.cast(self._shard_cb, ctypes.c_void_p) if self._shard_cb else None,
+                                             None)
+        if st != 0:
+            raise L.MvcError(st, "set_shard failed")
 
     def set_timing(self, timing):
         """Switch HIP-event timing: False, True (every phase) or "coarse"."""

@@ -555,6 +555,25 @@ def test_repair_shapes_same_chain(waves, repair, monkeypatch):
     s.close()
 
 
+@pytest.mark.parametrize("team,waves,V", [("1", "8", 5), ("2", "8", 5), ("4", "8", 5), ("4", "1", 5),
+                                          ("2", "3", 3), ("4", "8", 4)])
+def test_repair_team_shapes(team, waves, V, monkeypatch):
+    """The run kernel evaluating each customer with a team of 1, 2 or 4 waves
+    (views split unevenly over the members when V = 3 or 5; one customer per
+    step with MVC_RUN_WAVES=1) gives the oracle SeqSampler chain bit for bit,
+    through the births of a cold start (D = 16: S1 in the LDS cache)."""
+    monkeypatch.setenv("MVC_TEAM", team)
+    monkeypatch.setenv("MVC_RUN_WAVES", waves)
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.synthetic(3000, V, 16, 6, seed=60 + V)
+    s = m.Sampler(y, seed=17, mode="parallel")
+    ref = O.run(y, 6, 0, 1, seed=17, mode=O.PARALLEL)
+    _check_sweeps(s, ref, 6)
+    assert sum(ref["trace_births"]) > 0 and s.repair_stats()["moves"] == ref["trace_moves"][-1]
+    s.close()
+
+
 def test_chains_concurrent_equal_serial(monkeypatch):
     """Several chains in one handle run concurrently (ChainSet: a stream and a
     host thread per chain, shared device data); every chain equals the same
@@ -601,4 +620,60 @@ def test_dish_block_producer(force, monkeypatch):
     ref = O.run(y, 3, 0, 1, seed=5, mode=O.PARALLEL, state=st)
     _check_sweeps(s, ref, 3)
     assert s.zpath() & 64   # the dish-block producer ran
+    s.close()
+
+
+def test_lpall_batches(monkeypatch):
+    """The all-views producer over customer batches (MVC_LPB_BATCH: the lp
+    buffer holds one batch, the draw follows each batch; the last batch
+    ragged): bitwise vs the oracle, warm, V = 4 at D = 32."""
+    monkeypatch.setenv("MVC_LPB_BATCH", "1024")
+    m = _mvc()
+    from mvc_amd import data
+    N, V, D, K = 5000, 4, 32, 16
+    y, z = data.synthetic(N, V, D, K, seed=23)
+    st = _warm_state(z, V, K)
+    s = m.Sampler(y, seed=9, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 3, 0, 1, seed=9, mode=O.PARALLEL, state=st)
+    _check_sweeps(s, ref, 3)
+    assert s.zpath() & 16   # the all-views producer ran
+    s.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shard_ranks_equal_unsharded(world, tmp_path):
+    """Within-chain N-sharding (mvc_sampler_set_shard): `world` processes on
+    one GPU each evaluate phase A for their shard, all-gather the choices
+    (gloo through host memory) and run the same repair; every rank's chain
+    equals the unsharded chain bit for bit, through a cold start (movers
+    in every sweep, the last shard ragged)."""
+    import socket
+    import subprocess
+    import sys
+    N, V, D, K, sweeps = 20000 + 37, 3, 16, 8, 4
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    here = os.path.dirname(os.path.abspath(__file__))
+    procs = [subprocess.Popen([sys.executable, os.path.join(here, "shard_worker.py"), str(r), str(world), str(port),
+                               str(tmp_path / f"r{r}.npz"), str(N), str(V), str(D), str(K), str(sweeps)])
+             for r in range(world)]
+    rcs = [p.wait(timeout=150) for p in procs]
+    assert rcs == [0] * world, rcs
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.synthetic(N, V, D, K, seed=31)
+    s = m.Sampler(y, seed=5, mode="parallel")
+    for it in range(sweeps):
+        s.sweep(1)
+        t, d, h = s.state()
+        for r in range(world):
+            z = np.load(tmp_path / f"r{r}.npz")
+            assert np.array_equal(z["t"][it], t), (r, it)
+            assert np.array_equal(z["tau"][it], h["tau_v"]), (r, it)
+            if it == sweeps - 1:
+                assert np.array_equal(z["d"], d) and int(z["moves"]) == s.repair_stats()["moves"], r
+                assert int(z["calls"]) == sweeps, r   # one exchange per sweep
+    assert s.repair_stats()["moves"] > 0
     s.close()
