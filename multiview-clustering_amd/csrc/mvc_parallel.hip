@@ -637,7 +637,13 @@ __device__ __forceinline__ int pw16_select(const double (&a)[16], double r) {
 __host__ __device__ inline size_t zdraw_shared_bytes(int V, int T, int sumK) {
   return 8 * ((size_t)MVC_ZD_NCP * 256 + (size_t)T) + 4 * ((size_t)V * T + (size_t)sumK + (size_t)V + 1) + 64;
 }
-extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, int b0, int nb, const double *lpb) {
+// kSc: the table scores are computed once (one gather pass) into the
+// coalesced scratch sc[p * nb + li] and re-read by the weight and select
+// passes; without it they are re-gathered from the lp buffer in each pass.
+// The view maximum m_v comes from the producer (vmax), as in the register
+// draw, so each lp row is read once by the view pass.
+template <bool kSc>
+__global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, int b0, int nb, const double *lpb, double *sc) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
@@ -680,31 +686,13 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
       const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
       const int *dl = s_dl + koff;
       const double *lpv = lpi + (size_t)koff * 16;
-      // loads in batches of 8 (several round trips overlap); the reductions
-      // themselves stay sequential in dish order
-      double m = -MVC_PM_INF;
-      int j = 0;
-      for (; j + 8 <= K; j += 8) {
-        double x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = lpv[(size_t)(j + u) * 16];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int l = (j + u == j0) ? l0p : dl[j + u];
-          if (l > 0 && x[u] > m) m = x[u];
-        }
-      }
-      for (; j < K; ++j) {
-        const int l = (j == j0) ? l0p : dl[j];
-        const double x = lpv[(size_t)j * 16];
-        if (l > 0 && x > m) m = x;
-      }
-      if (lfn > m) m = lfn;
+      // m_v: the max over the included dishes and the new dish, from the producer
+      const double m = A.vmax[(size_t)v * n + i];
       // 16 column partials (dish j -> column j & 15, ascending j), then pw16
       double col[16];
 #pragma unroll
       for (int c = 0; c < 16; ++c) col[c] = 0.0;
-      for (j = 0; j < K; j += 16) {
+      for (int j = 0; j < K; j += 16) {
         double x[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) x[u] = lpv[(size_t)min(j + u, K - 1) * 16];
@@ -748,12 +736,16 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
       }
     };
     double M = -MVC_PM_INF;
+    double *scl = sc + li;   // kSc: table p's score at scl[p * nb]
     for (int p = 0; p < T; p += 4) {
       double sp[4];
       score4(p, sp);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (p + u < T && sp[u] > M) M = sp[u];
+        if (p + u < T) {
+          if (sp[u] > M) M = sp[u];
+          if constexpr (kSc) scl[(size_t)(p + u) * nb] = sp[u];
+        }
     }
     if (s_new > M) M = s_new;
     // weights in blocks of 16 positions: block sums pw16, running totals
@@ -762,7 +754,12 @@ extern "C" __global__ __launch_bounds__(256) void mvc_par_zdraw_kernel(Sweep A, 
 #pragma unroll
       for (int q = 0; q < 16; q += 4) {
         double sp[4];
-        score4(16 * b + q, sp);
+        if constexpr (kSc) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sp[u] = scl[(size_t)min(16 * b + q + u, T - 1) * nb];
+        } else {
+          score4(16 * b + q, sp);
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const bool in = 16 * b + q + u < T && sp[u] != -MVC_PM_INF;
@@ -2211,6 +2208,8 @@ class ParallelSampler : public Sampler {
   Repair *rs_host = nullptr;      // pinned copy of a chain's Repair after each batch
   double *lpb = nullptr;          // phase-1 lp buffer (lpb_index layout)
   double *vmax = nullptr;         // [V][n] view maxima of the draw (producer -> draw)
+  double *zsc = nullptr;          // generic draw: table scores [T][batch] (mvc_par_zdraw_kernel<true>)
+  size_t zsc_cap = 0;             // doubles
   size_t lpb_cap = 0;             // doubles
   size_t lp_cap = 0;               // doubles per wave
   double *part1 = nullptr, *part2 = nullptr;
@@ -2333,8 +2332,8 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
       n_cu = std::max(1, prop.multiProcessorCount);
     }
-    MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zdraw_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
+    for (const void *f : {(const void *)mvc_par_zdraw_kernel<true>, (const void *)mvc_par_zdraw_kernel<false>})
+      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lpview_attr<4, 4>();
     lpview_attr<8, 8>();
     lpview_attr<16, 8>();
@@ -2465,7 +2464,8 @@ class ParallelSampler : public Sampler {
     if (owns_y)
       for (void *p : {(void *)y, (void *)Y2, (void *)yt})
         if (p) hipFree(p);
-    for (void *p : {(void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2, (void *)fz_discard, (void *)vmax})
+    for (void *p : {(void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2, (void *)fz_discard, (void *)vmax,
+                    (void *)zsc})
       if (p) hipFree(p);
     if (st_host) hipHostFree(st_host);
     if (rs_host) hipHostFree(rs_host);
@@ -2905,9 +2905,22 @@ class ParallelSampler : public Sampler {
       else if (use_zreg)
         hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<64>, zg, dim3(256), zdraw_reg_shared_bytes(V, 64, sk), stream, A,
                            (int)b0, nb, (const double *)lpb);
-      else
-        hipLaunchKernelGGL(mvc_par_zdraw_kernel, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
-                           zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb);
+      else {
+        // the table-score scratch (T x nb doubles) when it stays under 1 GiB
+        const size_t scn = (size_t)c.T * (size_t)nb;
+        const bool use_sc = scn * sizeof(double) <= ((size_t)1 << 30);
+        if (use_sc && scn > zsc_cap) {
+          if (zsc) MVC_HIP(hipFree(zsc));
+          zsc_cap = scn + scn / 2;
+          zsc = dmalloc<double>(zsc_cap);
+        }
+        if (use_sc)
+          hipLaunchKernelGGL(mvc_par_zdraw_kernel<true>, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
+                             zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb, zsc);
+        else
+          hipLaunchKernelGGL(mvc_par_zdraw_kernel<false>, dim3(std::min(4096, (nb + 255) / 256)), dim3(256),
+                             zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb, zsc);
+      }
       MVC_HIP(hipGetLastError());
       timers.end("draw", ed);
     }
