@@ -2445,9 +2445,34 @@ class ParallelSampler : public Sampler {
     }
   }
 
+  // Buffers replaced while sweeping (capacity growth, scratch resizes) are
+  // retired, not freed: hipFree / hipHostFree synchronise the whole device,
+  // which would stall every other chain sharing the GPU (ChainSet) behind
+  // this chain's growth.  They are freed with the handle, or once they add
+  // up to more than 4 GiB.
+  std::vector<void *> retired_dev, retired_host;
+  size_t retired_bytes = 0;
+  void retire(void *p, size_t bytes = 0) {
+    if (!p) return;
+    retired_dev.push_back(p);
+    retired_bytes += bytes;
+    if (retired_bytes > ((size_t)4 << 30)) free_retired();
+  }
+  void retire_host(void *p) {
+    if (p) retired_host.push_back(p);
+  }
+  void free_retired() {
+    for (void *p : retired_dev) hipFree(p);
+    for (void *p : retired_host) hipHostFree(p);
+    retired_dev.clear();
+    retired_host.clear();
+    retired_bytes = 0;
+  }
+
   ~ParallelSampler() override {
     if (stream) hipStreamSynchronize(stream);
     if (cstream) hipStreamSynchronize(cstream);
+    free_retired();
     for (SaveSlot &q : saves) {
       for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp})
         if (p) hipFree(p);
@@ -2577,8 +2602,8 @@ class ParallelSampler : public Sampler {
   void rebuild_views(Chain &c, uint64_t vmask) {
     const int sk = sumK(c);
     if ((size_t)sk > part_cap) {
-      if (part1) hipFree(part1);
-      if (part2) hipFree(part2);
+      retire(part1);
+      retire(part2);
       part_cap = (size_t)sk + 64;
       part1 = dmalloc<double>((size_t)nchunk * part_cap * D);
       part2 = dmalloc<double>((size_t)nchunk * part_cap);
@@ -2642,7 +2667,7 @@ class ParallelSampler : public Sampler {
   // fewer when tables / dishes number in the tens of thousands (<= 2 GiB)
   int seq_waves = kSeqWaves;
   void alloc_seq_scratch() {
-    if (seq_scr) hipFree(seq_scr);
+    retire(seq_scr, sizeof(double) * (size_t)seq_waves * seq_stride);
     seq_stride = seq_scratch_stride(V, TC, KC);
     const int64_t fit = ((int64_t)1 << 28) / seq_stride;
     seq_waves = (int)std::max<int64_t>(kSeqRunWaves, std::min<int64_t>(kSeqWaves, fit / 4 * 4));
@@ -2821,7 +2846,7 @@ class ParallelSampler : public Sampler {
     const bool use_fused = !no_fused && shard_world == 1 && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                            (spp == 4 || spp == 8 || spp == 16) && fz_lds <= 160 * 1024;
     if (phaseA && !use_fused && need > lpb_cap) {   // the lp buffer only exists for the two-kernel path
-      if (lpb) hipFree(lpb);
+      retire(lpb, sizeof(double) * (lpb_cap + 64));
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
     }
@@ -2910,7 +2935,7 @@ class ParallelSampler : public Sampler {
         const size_t scn = (size_t)c.T * (size_t)nb;
         const bool use_sc = scn * sizeof(double) <= ((size_t)1 << 30);
         if (use_sc && scn > zsc_cap) {
-          if (zsc) MVC_HIP(hipFree(zsc));
+          retire(zsc, sizeof(double) * zsc_cap);
           zsc_cap = scn + scn / 2;
           zsc = dmalloc<double>(zsc_cap);
         }
@@ -3074,10 +3099,8 @@ class ParallelSampler : public Sampler {
       throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: more than 262144 tables or 262143 dishes per view");
     flush_saves();
     for (SaveSlot &q : saves) {   // the ring slots are capacity-sized
-      for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp})
-        if (p) hipFree(p);
-      for (void *p : {(void *)q.hz, (void *)q.hdish, (void *)q.hdid, (void *)q.hhyp})
-        if (p) hipHostFree(p);
+      for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp}) retire(p);
+      for (void *p : {(void *)q.hz, (void *)q.hdish, (void *)q.hdid, (void *)q.hhyp}) retire_host(p);
       if (q.snap) hipEventDestroy(q.snap);
       if (q.done) hipEventDestroy(q.done);
       q = SaveSlot();
@@ -3113,7 +3136,7 @@ class ParallelSampler : public Sampler {
       const std::vector<void *> cap_old = {old.n_t, old.dish, old.lmass, old.d_id, old.d_n, old.d_l, old.S1T,
                                            old.S2, old.Q, old.c0, old.cb, (void *)old_pos, (void *)old_jmap};
       for (void *p : old_owned) {
-        if (std::find(cap_old.begin(), cap_old.end(), p) != cap_old.end()) hipFree(p);
+        if (std::find(cap_old.begin(), cap_old.end(), p) != cap_old.end()) retire(p);
         else c.owned.push_back(p);
       }
     }
