@@ -2236,6 +2236,8 @@ class ParallelSampler : public Sampler {
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
   int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
   int team_w = 1;                 // waves per customer in the run kernel (MVC_TEAM; default by V)
+  bool use_wide = true;           // MVC_WIDE=0: global-scratch run kernel speculates one customer per wave
+  bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
 
   template <class Tp>
@@ -2368,6 +2370,8 @@ class ParallelSampler : public Sampler {
       team_w = (t >= 4 && V >= 4) ? 4 : (t >= 2 && V >= 2) ? 2 : 1;
     }
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
+    if (const char *e = getenv("MVC_WIDE")) use_wide = e[0] != '0';
+    if (const char *e = getenv("MVC_RUN_LDS")) force_global = e[0] == '0';
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh_in);
     MVC_HIP(hipStreamSynchronize(stream));
@@ -2977,7 +2981,7 @@ class ParallelSampler : public Sampler {
     L.limit = run_limit;
     // in order of preference: S1 cached with room to grow, then without S1,
     // then tight margins without S1
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    for (int attempt = force_global ? 3 : 0; attempt < 3; ++attempt) {
       const bool s1 = attempt == 0;
       const int kgrow = attempt < 2 ? std::max(8, kmax / 2) : 4;
       const int tgrow = attempt < 2 ? std::max(64, T / 2) : 16;
@@ -3005,9 +3009,12 @@ class ParallelSampler : public Sampler {
       }
     }
     L.lds = 0;   // per-wave global scratch (SeqScratch(A, w)): capacity-sized, never restrides
-    L.tw = 1;
+    // the whole block on one customer (seq_resample_wide): the dish / table
+    // lists are long here, and where the state outgrows the LDS nearly every
+    // customer moves (cold-start transients), so speculation buys little
+    L.tw = use_wide ? kSeqRunWaves : 1;
     L.s1 = 0;
-    L.nws = run_waves;
+    L.nws = use_wide ? 1 : run_waves;
     L.stride = 0;
     L.cache_dbl = 0;
     return L;

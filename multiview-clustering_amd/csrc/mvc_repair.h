@@ -127,15 +127,18 @@ struct SeqScratch {
     koff = (int32_t *)(mv + V);   // [V + 1] view offsets, then [V] K_act
     ys = mv + V + V + 2;
   }
+  double *wide;   // global scratch: the wide evaluation's shared values (seq_wide_len)
   __device__ SeqScratch(const SeqArgs &A, int wave) {
     carve(A.scr + (int64_t)wave * A.scr_stride, A.P.V, A.P.KC, A.P.TC);
     tree = ys;   // the global scratch has no staged rows
     ys = nullptr;
+    wide = A.scr + (int64_t)(wave + 1) * A.scr_stride - (17 * A.P.V + 16);
   }
   // run kernel, LDS (no dish-draw tree)
   __device__ SeqScratch(double *base, int V, int ks, int ts) {
     carve(base, V, ks, ts);
     tree = nullptr;
+    wide = nullptr;
   }
 };
 __host__ __device__ inline int64_t seq_scratch_head(int V, int ks, int ts) {
@@ -145,7 +148,8 @@ __host__ inline int64_t seq_scratch_stride(int V, int TC, int KC) {
   // tree levels: K+1 leaves, then ceil(./64) ... (< (K+1)/63 + 3 more)
   const int64_t leaves = (int64_t)KC + 1;
   const int64_t tree = leaves + leaves / 63 + 8;
-  return seq_scratch_head(V, KC, TC) + tree + 64;
+  // + the wide evaluation's lm_v [V], member maxima [8], per-member view maxima / counts [8][V] x 2
+  return seq_scratch_head(V, KC, TC) + tree + 64 + 17 * (int64_t)V + 16;
 }
 
 // oracle pw16: pairs (c, c + h) for h = 1, 2, 4, 8
@@ -841,6 +845,289 @@ __device__ int seq_resample_team(const SeqArgs &A, const SView &W, const Cust &C
   return pick;
 }
 
+// seq_resample by the whole block for ONE customer (run kernel, global-scratch
+// layout: T or the dish lists too large for the LDS cache, e.g. the Reuters
+// transient with T ~ 18k tables and thousands of dishes per view).  Member r
+// of the tw waves takes every tw-th 64-dish chunk of the concatenated dish
+// list (two dishes per lane in flight) for the lp and the terms, a stride of
+// the per-view max / count scans, and every tw-th 64-table chunk; member 0
+// does the order-sensitive sums (column partials, running block totals) and
+// the draw.  Same operations in the same order per quantity as seq_resample,
+// so the same bits.  Block-wide (seven __syncthreads); S is the team's
+// scratch (wave 0's), S.wide its shared values.  Returns the pick on member 0.
+__device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
+                                 int r, int tw, bool act) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
+  const int V = P.V, D = P.D, ts = W.ts, ks = W.ks, lps = S.lps;
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  double *lmv = S.wide, *mxr = lmv + V, *pmx = mxr + 8, *pcnt = pmx + 8 * V;
+  int32_t *kact = S.koff + V + 1;
+  int np0 = 0, Tne_i = 0, NK = 0;
+  bool alive = false;
+  double lmass0 = 0.0;
+  if (act) {
+    np0 = W.n_t[p0] - 1;
+    alive = np0 > 0;
+    Tne_i = *W.T_ne - (alive ? 0 : 1);
+    const double mass0 = (double)np0 - sg;
+    lmass0 = (np0 >= 1 && mass0 > 0.0) ? mvc_log(mass0) : 0.0;
+    for (int v = 0; v < V; ++v) NK += W.Klist[v];
+  }
+  auto locate = [&](int g, int &v, int &j) {
+    v = 0;
+    int off = 0;
+    while (v + 1 < V && g >= off + W.Klist[v]) { off += W.Klist[v]; ++v; }
+    j = g - off;
+  };
+  auto lp_val = [&](int v, int j, double G) -> double {
+    const double tau = P.hyper[v];
+    const double Y2i = C.Y2[(size_t)v * C.y2stride];
+    const double hy = 0.5 * Y2i;
+    const double h = (-0.5 * Y2i) / tau;
+    if (j == W.dish[v * ts + p0]) {
+      const double Gp = G - Y2i;
+      const double Qp = (W.Q[v * ks + j] - 2.0 * G) + Y2i;
+      const Coef c = coef(W.d_n[v * ks + j] - 1, Qp, tau, A.L2pt[v], D);
+      return __builtin_fma(Gp + hy, c.cb, c.c0) + h;
+    }
+    return __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
+  };
+  // pass 1: lp, two dishes per lane (chunks c and c + tw), two fma chains in ascending d
+  if (act) {
+    for (int c = r; 64 * c < NK; c += 2 * tw) {
+      const int ga = 64 * c + lane, gb = 64 * (c + tw) + lane;
+      const bool va = ga < NK, vb = gb < NK;
+      int v_a = 0, j_a = 0, v_b = 0, j_b = 0;
+      if (va) locate(ga, v_a, j_a);
+      if (vb) locate(gb, v_b, j_b);
+      const double *ya = C.y + (size_t)v_a * C.ystride, *yb = C.y + (size_t)v_b * C.ystride;
+      const double *sa = W.S1T + (size_t)v_a * D * W.s1s + j_a, *sb = W.S1T + (size_t)v_b * D * W.s1s + j_b;
+      const size_t bs = (size_t)W.s1s;
+      double acc_a = 0.0, acc_b = 0.0;
+      int d = 0;
+      for (; d + 8 <= D; d += 8) {
+        double xa[8], za[8], xb[8], zb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          xa[u] = ya[d + u];
+          za[u] = sa[(size_t)(d + u) * bs];
+          xb[u] = yb[d + u];
+          zb[u] = sb[(size_t)(d + u) * bs];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc_a = __builtin_fma(xa[u], za[u], acc_a);
+          acc_b = __builtin_fma(xb[u], zb[u], acc_b);
+        }
+      }
+      for (; d < D; ++d) {
+        acc_a = __builtin_fma(ya[d], sa[(size_t)d * bs], acc_a);
+        acc_b = __builtin_fma(yb[d], sb[(size_t)d * bs], acc_b);
+      }
+      if (va) S.lp[v_a * lps + j_a] = lp_val(v_a, j_a, acc_a);
+      if (vb) S.lp[v_b * lps + j_b] = lp_val(v_b, j_b, acc_b);
+    }
+  }
+  __syncthreads();
+  // per-member max / count of the included dishes, four views at once (rows)
+  if (act) {
+    for (int vg = 0; vg < V; vg += 4) {
+      const int v = vg + row;
+      double mx = -MVC_PM_INF;
+      int cnt = 0;
+      if (v < V) {
+        const int K = W.Klist[v];
+        const int j0 = W.dish[v * ts + p0];
+        for (int j = col + 16 * r; j < K; j += 16 * tw) {
+          const int l = W.d_l[v * ks + j] - ((j == j0 && !alive) ? 1 : 0);
+          if (l > 0) {
+            ++cnt;
+            const double x = S.lp[v * lps + j];
+            if (x > mx) mx = x;
+          }
+        }
+      }
+      mx = row16_max(mx);
+      cnt = row16_isum(cnt);
+      if (v < V && col == 0) {
+        pmx[r * V + v] = mx;
+        pcnt[r * V + v] = (double)cnt;
+      }
+    }
+  }
+  __syncthreads();
+  if (act && r == 0) {   // combine the members (max and count: order-free), the new dish
+    for (int v = lane; v < V; v += 64) {
+      double mx = -MVC_PM_INF;
+      int cnt = 0;
+      for (int q = 0; q < tw; ++q) {
+        const double x = pmx[q * V + v];
+        if (x > mx) mx = x;
+        cnt += (int)pcnt[q * V + v];
+      }
+      const double Y2i = C.Y2[(size_t)v * C.y2stride];
+      const double lfn = A.cnew[v] + (-0.5 * Y2i) / P.hyper[v];
+      S.mv[v] = lfn > mx ? lfn : mx;
+      kact[v] = cnt;
+    }
+  }
+  __syncthreads();
+  // pass 2: the weighted terms of the member's chunks
+  if (act) {
+    for (int c = r; 64 * c < NK; c += tw) {
+      const int g = 64 * c + lane;
+      if (g < NK) {
+        int v, j;
+        locate(g, v, j);
+        const int l = W.d_l[v * ks + j] - ((j == W.dish[v * ts + p0] && !alive) ? 1 : 0);
+        double t = 0.0;
+        if (l > 0) {
+          double wgt = (double)l - P.hyper[2 * V + v];
+          if (wgt < 0.0) wgt = 0.0;
+          t = wgt * mvc_exp(S.lp[v * lps + j] - S.mv[v]);
+        }
+        S.aux[v * lps + j] = t;
+      }
+    }
+  }
+  __syncthreads();
+  // member 0: column partials in ascending j, pw16, the new dish, lm_v
+  if (act && r == 0) {
+    for (int vg = 0; vg < V; vg += 4) {
+      const int v = vg + row;
+      double cs = 0.0;
+      if (v < V) {
+        const int K = W.Klist[v];
+        const double *ax = S.aux + (size_t)v * lps;
+        int j = col;
+        for (; j + 16 * 7 < K; j += 16 * 8) {
+          double x[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) x[u] = ax[j + 16 * u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) cs = cs + x[u];
+        }
+        for (; j < K; j += 16) cs = cs + ax[j];
+      }
+      double Sv = row_pw16(cs);
+      if (v < V && col == 0) {
+        const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+        const double Y2i = C.Y2[(size_t)v * C.y2stride];
+        const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
+        const double m = S.mv[v];
+        double wn = alpha + (double)kact[v] * sigma;
+        if (wn < 0.0) wn = 0.0;
+        Sv = Sv + wn * mvc_exp(lfn - m);
+        const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
+        lmv[v] = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - mvc_log(denom);
+      }
+    }
+  }
+  __syncthreads();
+  // s_new in view order (every member); scores of the member's 64-table chunks
+  double s_new = 0.0, M = -MVC_PM_INF;
+  const int T = act ? *W.T : 0;
+  const int TB = (T + 15) / 16;
+  if (act) {
+    s_new = mvc_log(ag + sg * (double)Tne_i);
+    for (int v = 0; v < V; ++v) s_new = s_new + lmv[v];
+    constexpr int kU = 4;
+    const int nch = TB * 16;
+    for (int c0 = r; c0 * 64 < nch; c0 += tw * kU) {
+      int np[kU];
+      double lm[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        np[u] = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+        lm[u] = p < T ? ((p == p0) ? lmass0 : W.lmass[p]) : 0.0;
+      }
+      double sp[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        const double mass = (double)np[u] - sg;
+        sp[u] = (p < T && np[u] >= 1 && mass > 0.0) ? lm[u] : -MVC_PM_INF;
+      }
+      for (int v = 0; v < V; ++v) {
+        int dj[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int p = (c0 + u * tw) * 64 + lane;
+          dj[u] = (sp[u] != -MVC_PM_INF) ? W.dish[v * ts + p] : 0;
+        }
+        double lv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) lv[u] = S.lp[v * lps + dj[u]];
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (sp[u] != -MVC_PM_INF) sp[u] = sp[u] + lv[u];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        if (p < nch) S.e[p] = sp[u];
+        if (sp[u] > M) M = sp[u];
+      }
+    }
+    M = wave_max(M);
+    if (lane == 0) mxr[r] = M;
+  }
+  __syncthreads();
+  if (act) {
+    for (int k = 0; k < tw; ++k) M = mxr[k] > M ? mxr[k] : M;
+    if (s_new > M) M = s_new;
+    for (int c0 = r; c0 * 64 < TB * 16; c0 += tw) {
+      const int p = c0 * 64 + lane;
+      double wgt = 0.0;
+      if (p < TB * 16) {
+        const double x = S.e[p];
+        wgt = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
+        S.e[p] = wgt;
+      }
+      const double Bv = row_pw16(wgt);
+      const int b = c0 * 4 + row;
+      if (col == 0 && b < TB) S.B[b] = Bv;
+    }
+  }
+  __syncthreads();
+  int pick = -1;
+  if (act && r == 0) {
+    double tot = 0.0;
+    for (int b0 = 0; b0 < TB; b0 += 64) {
+      const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
+      const int nb = min(64, TB - b0);
+      for (int k = 0; k < nb; ++k) tot = tot + readlane_d(Bl, k);
+    }
+    const double Wt = mvc_exp(s_new - M) + tot;
+    double u = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
+    if (u < tot) {
+      double c = 0.0, cprev = 0.0;
+      int bsel = TB - 1;
+      bool found = false;
+      for (int b0 = 0; b0 < TB && !found; b0 += 64) {
+        const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
+        const int nb = min(64, TB - b0);
+        for (int k = 0; k < nb; ++k) {
+          const double c2 = c + readlane_d(Bl, k);
+          if (u < c2) {
+            bsel = b0 + k;
+            cprev = c;
+            found = true;
+            break;
+          }
+          c = c2;
+        }
+      }
+      u = u - cprev;
+      const double x = lane < 16 ? S.e[bsel * 16 + lane] : 0.0;
+      pick = bsel * 16 + pw16_select_wave(x, u);
+    }
+  }
+  return pick;
+}
+
 // tree64 over x[0..m) (oracle Tree64::build): level arrays stored one after
 // the other from `lv` (level k starts at the sum of the lower levels' counts);
 // returns the root.  nlev receives the number of levels (leaves included).
@@ -1330,7 +1617,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       const bool staged = ring && U.cur < U.fill && U.cur >= U.fill - G.n;
       const Cust Ci = staged ? G.cust(U.cur, V, D) : global_cust(A, U.cur);
       // dish draws of a birth: wave w < nwd, lp scratch = its slice of its team's lp
-      const int tw = kTeam ? L.tw : 1;
+      const int tw = (kTeam && kLds) ? L.tw : 1;   // LDS teams share a scratch; global scratch is per wave
       if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp + (size_t)(w % tw) * L.ks, tree, U.cnt,
                       kLds ? L.nws * tw : (int)(blockDim.x >> 6))) {
         // overflow: the host grows and relaunches
@@ -1379,7 +1666,17 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       if (p1c > p0c) ring_fill_async(A, G, p0c, p1c);
       fill_next = max(p1c, need);   // U.fill is written after the decision barrier (every wave read it above)
     }
-    if (kTeam) {   // teams of tw waves, one customer each
+    if constexpr (kTeam && !kLds) {   // global scratch: the whole block on one customer
+      const int i = i0;
+      const bool act = i < n;
+      const int p0 = act ? P.z[i] : 0;
+      const int c = seq_resample_wide(A, Wv, global_cust(A, act ? i : 0), i, p0, SeqScratch(A, 0), w, L.tw, act);
+      if (act && w == 0 && lane == 0) {
+        U.ch[0] = c;
+        U.p0[0] = p0;
+      }
+    }
+    if constexpr (kTeam && kLds) {   // teams of tw waves, one customer each
       const int team = w / L.tw, r = w % L.tw;
       const int i = i0 + team;
       const bool act = team < L.nws && i < n;
@@ -1585,9 +1882,9 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     seq_run_loop<true, kTeam>(A, L, cache_view(cc, A), &cc,
                               SeqScratch(seq_sm + L.cache_dbl + (int64_t)(w / L.tw) * L.stride, V, L.ks, L.ts), G,
                               tree, U, ovf, restride);
-  } else if constexpr (!kTeam) {
+  } else {
     Ring G{nullptr, 0, 0};
-    seq_run_loop<false, false>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
+    seq_run_loop<false, kTeam>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
     R->cur = U.cur;

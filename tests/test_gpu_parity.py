@@ -677,3 +677,22 @@ def test_shard_ranks_equal_unsharded(world, tmp_path):
                 assert int(z["calls"]) == sweeps, r   # one exchange per sweep
     assert s.repair_stats()["moves"] > 0
     s.close()
+
+
+@pytest.mark.parametrize("wide,V", [("1", 3), ("0", 3), ("1", 5)])
+def test_repair_global_wide(wide, V, monkeypatch):
+    """The run kernel on its global-scratch layout (MVC_RUN_LDS=0, as when
+    the state outgrows the LDS): the whole block evaluating one customer
+    (seq_resample_wide: dishes, tables and scans split over the 8 waves) or
+    one customer per wave (MVC_WIDE=0); bitwise vs oracle SeqSampler through
+    the births of a cold start."""
+    monkeypatch.setenv("MVC_RUN_LDS", "0")
+    monkeypatch.setenv("MVC_WIDE", wide)
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.synthetic(3000, V, 16, 6, seed=80 + V)
+    s = m.Sampler(y, seed=19, mode="parallel")
+    ref = O.run(y, 5, 0, 1, seed=19, mode=O.PARALLEL)
+    _check_sweeps(s, ref, 5)
+    assert sum(ref["trace_births"]) > 0 and s.repair_stats()["moves"] == ref["trace_moves"][-1]
+    s.close()
