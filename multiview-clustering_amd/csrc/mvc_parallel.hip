@@ -2348,7 +2348,8 @@ class ParallelSampler : public Sampler {
     fused_attr<4, 4>();
     fused_attr<8, 8>();
     fused_attr<16, MVC_FZ_RP16>();
-    for (const void *f : {(const void *)mvc_seq_run_kernel<false>, (const void *)mvc_seq_run_kernel<true>})
+    for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<1>,
+                        (const void *)mvc_seq_run_kernel<2>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {
@@ -3045,7 +3046,8 @@ class ParallelSampler : public Sampler {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
         else
-          hipLaunchKernelGGL(L.tw > 1 ? mvc_seq_run_kernel<true> : mvc_seq_run_kernel<false>, dim3(1), dim3(kSeqRunThreads),
+          hipLaunchKernelGGL(L.tw == 1 ? mvc_seq_run_kernel<0> : L.lds ? mvc_seq_run_kernel<1> : mvc_seq_run_kernel<2>,
+                             dim3(1), dim3(kSeqRunThreads),
                              L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
                              stream, Q, L);
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);

@@ -866,6 +866,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
   int np0 = 0, Tne_i = 0, NK = 0;
   bool alive = false;
   double lmass0 = 0.0;
+  RUN_T0();
   if (act) {
     np0 = W.n_t[p0] - 1;
     alive = np0 > 0;
@@ -999,16 +1000,22 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
       double cs = 0.0;
       if (v < V) {
         const int K = W.Klist[v];
-        const double *ax = S.aux + (size_t)v * lps;
-        int j = col;
-        for (; j + 16 * 7 < K; j += 16 * 8) {
-          double x[8];
+        // this lane's column j = col, col + 16, ... in ascending j: batches of
+        // 16 values, the next batch's loads in flight while one is summed
+        const double *ax = S.aux + (size_t)v * lps + col;
+        const int cnt = K > col ? (K - col + 15) >> 4 : 0;
+        double xa[16], xb[16];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) x[u] = ax[j + 16 * u];
+        for (int u = 0; u < 16; ++u) xa[u] = u < cnt ? ax[16 * u] : 0.0;
+        for (int e0 = 0; e0 < cnt; e0 += 16) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) cs = cs + x[u];
+          for (int u = 0; u < 16; ++u) xb[u] = e0 + 16 + u < cnt ? ax[16 * (e0 + 16 + u)] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (e0 + u < cnt) cs = cs + xa[u];
+#pragma unroll
+          for (int u = 0; u < 16; ++u) xa[u] = xb[u];
         }
-        for (; j < K; j += 16) cs = cs + ax[j];
       }
       double Sv = row_pw16(cs);
       if (v < V && col == 0) {
@@ -1025,6 +1032,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
     }
   }
   __syncthreads();
+  RUN_MARK(0);
   // s_new in view order (every member); scores of the member's 64-table chunks
   double s_new = 0.0, M = -MVC_PM_INF;
   const int T = act ? *W.T : 0;
@@ -1032,7 +1040,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
   if (act) {
     s_new = mvc_log(ag + sg * (double)Tne_i);
     for (int v = 0; v < V; ++v) s_new = s_new + lmv[v];
-    constexpr int kU = 4;
+    constexpr int kU = 8;   // 8 chunks per step: the loads are the latency
     const int nch = TB * 16;
     for (int c0 = r; c0 * 64 < nch; c0 += tw * kU) {
       int np[kU];
@@ -1075,6 +1083,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
     if (lane == 0) mxr[r] = M;
   }
   __syncthreads();
+  RUN_MARK(1);
   if (act) {
     for (int k = 0; k < tw; ++k) M = mxr[k] > M ? mxr[k] : M;
     if (s_new > M) M = s_new;
@@ -1092,12 +1101,23 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
     }
   }
   __syncthreads();
+  RUN_MARK(2);
   int pick = -1;
   if (act && r == 0) {
-    double tot = 0.0;
-    for (int b0 = 0; b0 < TB; b0 += 64) {
-      const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
-      const int nb = min(64, TB - b0);
+    // running block totals in block order; lane q keeps the total before
+    // 64-block chunk q (TB <= 4096), so the draw walks one chunk only
+    double tot = 0.0, cst = 0.0;
+    const int nch = (TB + 63) >> 6;
+    auto ldB = [&](int q) -> double { return (q < nch && 64 * q + lane < TB) ? S.B[64 * q + lane] : 0.0; };
+    double B1 = ldB(0), B2 = ldB(1), B3 = ldB(2), B4 = ldB(3);   // four chunks in flight
+    for (int q = 0; q < nch; ++q) {
+      const double Bl = B1;
+      B1 = B2;
+      B2 = B3;
+      B3 = B4;
+      B4 = ldB(q + 4);
+      if (lane == q) cst = tot;
+      const int nb = min(64, TB - 64 * q);
       for (int k = 0; k < nb; ++k) tot = tot + readlane_d(Bl, k);
     }
     const double Wt = mvc_exp(s_new - M) + tot;
@@ -1106,7 +1126,16 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
       double c = 0.0, cprev = 0.0;
       int bsel = TB - 1;
       bool found = false;
-      for (int b0 = 0; b0 < TB && !found; b0 += 64) {
+      int bstart = 0;
+      if (nch <= 64) {   // the first chunk whose end total exceeds u (totals are nondecreasing)
+        const double nxt = __shfl_down(cst, 1, 64);
+        const double cend = (lane + 1 < nch) ? nxt : tot;
+        const uint64_t hit = __ballot(lane < nch && u < cend);
+        const int q = hit ? (int)__ffsll((long long)hit) - 1 : 0;
+        bstart = 64 * q;
+        c = readlane_d(cst, q);
+      }
+      for (int b0 = bstart; b0 < TB && !found; b0 += 64) {
         const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
         const int nb = min(64, TB - b0);
         for (int k = 0; k < nb; ++k) {
@@ -1125,6 +1154,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
       pick = bsel * 16 + pw16_select_wave(x, u);
     }
   }
+  RUN_MARK(3);
   return pick;
 }
 
@@ -1178,18 +1208,31 @@ __device__ int seq_tree_select(const double *lv, int m, int nlev, double r) {
 // exp(lp_j - m) of the included dishes, the new dish last; tree64; r = u S.
 // lp: [K] scratch, tree: the tree64 levels' scratch.  Returns a list index;
 // Klist[v] = a new dish.
+// lpre (optional): the customer's lp row of view v against the current
+// state with its max (incl. the new dish) mpre and count kpre, as the wide
+// evaluation left them (seq_resample_wide: the same values seq_view_lp gives).
 __device__ int seq_dish_draw(const SeqArgs &A, const SView &W, const Cust &C, int i, int v, bool alive, int j0,
-                             double *lp, double *tree) {
+                             double *lpw, double *tree, const double *lpre = nullptr, double mpre = 0.0,
+                             int kpre = 0) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63;
   const int V = P.V, ks = W.ks;
   const int K = W.Klist[v];
   const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-  double m;
-  const int Kact = seq_view_lp(A, W, C, v, alive, j0, lp, &m);
-  __threadfence_block();
   const double Y2i = C.Y2[(size_t)v * C.y2stride];
   const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
+  double m;
+  int Kact;
+  const double *lp;
+  if (lpre) {
+    lp = lpre;
+    m = mpre;
+    Kact = kpre;
+  } else {
+    Kact = seq_view_lp(A, W, C, v, alive, j0, lpw, &m);
+    __threadfence_block();
+    lp = lpw;
+  }
   if (lfn > m) m = lfn;
   double wn = alpha + (double)Kact * sigma;
   if (wn < 0.0) wn = 0.0;
@@ -1302,7 +1345,7 @@ __device__ __forceinline__ void self_coef_parts(int n_, double tau, double L2pt,
 // cnt: the moves / births / new-dish counters (R->moves... or the run
 // kernel's LDS copies).
 __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const Cust &Ci, int i, int p0, int c,
-                           double *lpw, double *treew, int32_t *cnt, int nwd) {
+                           double *lpw, double *treew, int32_t *cnt, int nwd, const SeqScratch *pre = nullptr) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1314,7 +1357,9 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
     // a birth: dishes drawn against the current state, then the table
     const bool alive = (W.n_t[p0] - 1) > 0;
     for (int v = w; v < V && w < nwd; v += nwd) {   // waves w < nwd own a scratch (lpw, treew)
-      const int t = seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew);
+      const int t = pre ? seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew,
+                                        pre->lp + (size_t)v * pre->lps, pre->mv[v], pre->koff[V + 1 + v])
+                        : seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew);
       if (lane == 0) s_tup[v] = t;
     }
     __syncthreads();
@@ -1538,6 +1583,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A
 struct RunCursor {
   int go, stop, cur, pend, pc, pp0, mode, streak, done, i;
   int fill;                       // ring: customers [.., fill) are staged (slot = customer % ring)
+  int lpc;                        // wide evaluation: the customer whose lp rows wave 0's scratch holds (-1: none)
   int32_t cnt[3];                 // moves, births, new dishes
   int ch[kSeqRunWaves], p0[kSeqRunWaves];
 };
@@ -1618,8 +1664,11 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       const Cust Ci = staged ? G.cust(U.cur, V, D) : global_cust(A, U.cur);
       // dish draws of a birth: wave w < nwd, lp scratch = its slice of its team's lp
       const int tw = (kTeam && kLds) ? L.tw : 1;   // LDS teams share a scratch; global scratch is per wave
+      // wide evaluation of this very customer against this state: its lp rows are reused by the dish draws
+      const SeqScratch S0(A, 0);
+      const bool reuse = kTeam && !kLds && U.lpc == U.cur;
       if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp + (size_t)(w % tw) * L.ks, tree, U.cnt,
-                      kLds ? L.nws * tw : (int)(blockDim.x >> 6))) {
+                      kLds ? L.nws * tw : (int)(blockDim.x >> 6), reuse ? &S0 : nullptr)) {
         // overflow: the host grows and relaunches
         ovf = 1;
         return;
@@ -1740,6 +1789,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         U.pend = 1;
         U.pc = U.ch[f];
         U.pp0 = U.p0[f];
+        U.lpc = (kTeam && !kLds) ? U.cur : -1;
       } else {
         U.cur = U.i + m;
         U.streak += m;
@@ -1769,9 +1819,9 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 // customer costs one memory latency (its y rows) plus LDS work.  After
 // L.limit stays in a row the movers are sparse: the kernel opens a grid
 // window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
-// kTeam: the instance for L.tw > 1 (teams of waves per customer; LDS layouts
-// only), compiled separately so each keeps its own register allocation.
-template <bool kTeam>
+// One instance per evaluation shape, compiled separately so each keeps its
+// own register allocation.
+template <int kMode>   // 0: one wave per customer; 1: LDS teams (L.tw > 1, LDS layout); 2: wide (L.tw > 1, global layout)
 __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
   extern __shared__ double seq_sm[];
   Repair *R = A.R;
@@ -1798,6 +1848,7 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     U.streak = R->streak;
     U.done = R->done;
     U.fill = U.cur;   // nothing staged yet
+    U.lpc = -1;
     U.cnt[0] = R->moves;
     U.cnt[1] = R->births;
     U.cnt[2] = R->newdish;
@@ -1879,12 +1930,12 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     G.n = L.ring;
     G.slot = (int)seq_ring_slot(V, D);
     G.base = seq_sm + L.cache_dbl + (int64_t)L.nws * L.stride;
-    seq_run_loop<true, kTeam>(A, L, cache_view(cc, A), &cc,
+    seq_run_loop<true, kMode == 1>(A, L, cache_view(cc, A), &cc,
                               SeqScratch(seq_sm + L.cache_dbl + (int64_t)(w / L.tw) * L.stride, V, L.ks, L.ts), G,
                               tree, U, ovf, restride);
   } else {
     Ring G{nullptr, 0, 0};
-    seq_run_loop<false, kTeam>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
+    seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
     R->cur = U.cur;
