@@ -2348,8 +2348,8 @@ class ParallelSampler : public Sampler {
     fused_attr<4, 4>();
     fused_attr<8, 8>();
     fused_attr<16, MVC_FZ_RP16>();
-    for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<1>,
-                        (const void *)mvc_seq_run_kernel<2>})
+    // (instance 2 runs the global-scratch layout only: no dynamic LDS)
+  for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<1>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {

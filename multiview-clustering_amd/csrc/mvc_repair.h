@@ -894,8 +894,54 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
     }
     return __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
   };
+  // the customer's y rows in LDS (V D <= 2048): pass 1's y operands become
+  // LDS reads, so its global loads are S1 only (16 per dish in flight)
+  constexpr int kWideY = 2048;
+  __shared__ double s_yw[kWideY];
+  const bool ylds = V * D <= kWideY;
+  if (ylds) {
+    if (act)
+      for (int e = threadIdx.x; e < V * D; e += blockDim.x) {
+        const int v = e / D, d = e - v * D;
+        s_yw[e] = C.y[(size_t)v * C.ystride + d];
+      }
+    __syncthreads();
+  }
   // pass 1: lp, two dishes per lane (chunks c and c + tw), two fma chains in ascending d
-  if (act) {
+  if (act && ylds) {
+    for (int c = r; 64 * c < NK; c += 2 * tw) {
+      const int ga = 64 * c + lane, gb = 64 * (c + tw) + lane;
+      const bool va = ga < NK, vb = gb < NK;
+      int v_a = 0, j_a = 0, v_b = 0, j_b = 0;
+      if (va) locate(ga, v_a, j_a);
+      if (vb) locate(gb, v_b, j_b);
+      const int oa = v_a * D, ob = v_b * D;
+      const double *sa = W.S1T + (size_t)v_a * D * W.s1s + j_a, *sb = W.S1T + (size_t)v_b * D * W.s1s + j_b;
+      const size_t bs = (size_t)W.s1s;
+      double acc_a = 0.0, acc_b = 0.0;
+      int d = 0;
+      for (; d + 16 <= D; d += 16) {
+        double za[16], zb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          za[u] = sa[(size_t)(d + u) * bs];
+          zb[u] = sb[(size_t)(d + u) * bs];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          acc_a = __builtin_fma(s_yw[oa + d + u], za[u], acc_a);
+          acc_b = __builtin_fma(s_yw[ob + d + u], zb[u], acc_b);
+        }
+      }
+      for (; d < D; ++d) {
+        acc_a = __builtin_fma(s_yw[oa + d], sa[(size_t)d * bs], acc_a);
+        acc_b = __builtin_fma(s_yw[ob + d], sb[(size_t)d * bs], acc_b);
+      }
+      if (va) S.lp[v_a * lps + j_a] = lp_val(v_a, j_a, acc_a);
+      if (vb) S.lp[v_b * lps + j_b] = lp_val(v_b, j_b, acc_b);
+    }
+  }
+  if (act && !ylds) {
     for (int c = r; 64 * c < NK; c += 2 * tw) {
       const int ga = 64 * c + lane, gb = 64 * (c + tw) + lane;
       const bool va = ga < NK, vb = gb < NK;
