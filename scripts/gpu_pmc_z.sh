@@ -8,7 +8,7 @@ run() {
   local name=$1; shift
   timeout -k 10 600 rocprofv3 --kernel-trace --kernel-include-regex "lpview|lpall|lpgen|zdraw|zfused" --pmc "$@" \
       -d gpurun_out/pmcz_${TAG}_$name -o run --output-format csv -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/pmcz_${TAG}_$name.log 2>&1 || { echo "pmc $name failed"; exit 1; }
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-extras > gpurun_out/pmcz_${TAG}_$name.log 2>&1 || { echo "pmc $name failed"; exit 1; }
 }
 run fetch FETCH_SIZE
 run write WRITE_SIZE
