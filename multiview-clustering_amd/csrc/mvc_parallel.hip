@@ -52,6 +52,7 @@ struct Sweep {
   const double *S1t;      // MFMA B-fragment layout of S1 (mvc_par_s1tile_kernel)
   int32_t SP;             // k-steps per view in yt/S1t (D/4 rounded up to MVC_ZR)
   double *vmax;           // [V][n] the view maximum m_v of each customer (producer -> draw)
+  int32_t lmv;            // 1: the all-views producer puts the view term lm_v in vmax instead (register draw)
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
@@ -928,7 +929,7 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     int tot = 0;
     for (int v = 0; v < V; ++v) {
       const int K = s_koff[v + 1] - s_koff[v];
-      const bool st = s_lmin[v] != 0 && K <= 16 && tot + K <= MVC_ZSTAGE;
+      const bool st = !A.lmv && s_lmin[v] != 0 && K <= 16 && tot + K <= MVC_ZSTAGE;
       s_soff[v] = st ? tot : -1;
       tot += st ? K : 0;
     }
@@ -943,7 +944,9 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     const bool alive = (P.n_t[p0] - 1) > 0;
     const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
     double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
-    for (int v = 0; v < V; ++v) {
+    // A.lmv: the producer formed each view's term lm_v (in vmax)
+    for (int v = 0; A.lmv && v < V; ++v) s_new = s_new + A.vmax[(size_t)v * n + i];
+    for (int v = 0; !A.lmv && v < V; ++v) {
       const int koff = __builtin_amdgcn_readfirstlane(s_koff[v]);
       const int K = __builtin_amdgcn_readfirstlane(s_koff[v + 1]) - koff;
       const int j0 = s_tix[p0 * V + v] - koff;
@@ -1528,7 +1531,7 @@ struct LpaLds {
   const int *dn, *dl, *tix, *nt, *koff, *boff;
 };
 __host__ __device__ inline size_t lpall_shared_bytes(size_t s1t_doubles, int V, int sumK, int waves) {
-  return 16 * 4 + 8 * (s1t_doubles + 3 * (size_t)sumK + (size_t)waves * 48) +
+  return 16 * 4 + 8 * (s1t_doubles + 3 * (size_t)sumK + (size_t)waves * 80) +
          4 * (2 * (size_t)sumK + (size_t)MVC_FZ_TB * 16 * V + MVC_FZ_TB * 16 + (size_t)waves * 16) + 64;
 }
 
@@ -1589,25 +1592,83 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
     if (col == 0) mrest[grp + 4 * r] = mr;
   }
   wave_lds_sync();
-  {   // own dish, one row per lane
-    const double G = selfG[col];
-    const int kk = L.tix[pz * V + v];
-    const double Gp = G - y2;
-    const double Qp = (L.Q[kk] - 2.0 * G) + y2;
-    const Coef cf = coef(L.dn[kk] - 1, Qp, tau, L2pt, D);
-    const double hself = (-0.5 * y2) / tau;
-    const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
-    const bool ok = lane < 16 && li0 + col < nb;
-    double *dst = ok ? lpb + lpb_index(li0 + col, kk, sumK) : dslot;
-    *dst = sv;
-    const int l0p = L.dl[kk] - ((L.nt[pz] - 1) > 0 ? 0 : 1);
-    double m = mrest[col];
-    if (l0p > 0 && sv > m) m = sv;
-    const double lfn = cnew + hself;
-    if (lfn > m) m = lfn;
-    double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
-    *dm = m;
+  // own dish, one row per lane
+  const double G = selfG[col];
+  const int kk = L.tix[pz * V + v];
+  const double Gp = G - y2;
+  const double Qp = (L.Q[kk] - 2.0 * G) + y2;
+  const Coef cf = coef(L.dn[kk] - 1, Qp, tau, L2pt, D);
+  const double hself = (-0.5 * y2) / tau;
+  const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
+  const bool ok = lane < 16 && li0 + col < nb;
+  double *dst = ok ? lpb + lpb_index(li0 + col, kk, sumK) : dslot;
+  *dst = sv;
+  const bool alive = (L.nt[pz] - 1) > 0;
+  const int l0p = L.dl[kk] - (alive ? 0 : 1);
+  double m = mrest[col];
+  if (l0p > 0 && sv > m) m = sv;
+  const double lfn = cnew + hself;
+  if (lfn > m) m = lfn;
+  double out = m;
+  if (A.lmv) {
+    // the draw's view term (mvc_par_zdraw_reg_kernel / zview_sum, oracle
+    // eval_view_seq) here, where the lp values are still in the accumulators:
+    // column partials w_j exp(lp_j - m) over ascending dish blocks (lane
+    // column = j & 15), pw16 over the row's 16 lanes, then the new dish and
+    // lm_v.  Same operations in the same order, so the same bits; the draw
+    // then skips its exps and row reads of the view pass.
+    const double sigma = P.hyper[2 * V + v], alpha = P.hyper[V + v];
+    double *w0s = mrest + 16, *Ss = mrest + 32;
+    double w0 = (double)l0p - sigma;
+    if (w0 < 0.0) w0 = 0.0;
+    if (!(l0p > 0)) w0 = -1.0;
+    if (lane < 16) { mrest[col] = m; selfG[col] = sv; w0s[col] = w0; }
+    wave_lds_sync();
+    double mr[4], svr[4], w0r[4], cs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mr[r] = mrest[grp + 4 * r];
+      svr[r] = selfG[grp + 4 * r];
+      w0r[r] = w0s[grp + 4 * r];
+      cs[r] = 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int j = 16 * t + col;
+      const int kc = koff + min(j, K - 1);
+      const double c0j = L.c0[kc], cbj = L.cb[kc];
+      const int lj = L.dl[kc];
+      double wj = (double)lj - sigma;
+      if (wj < 0.0) wj = 0.0;
+      if (!(lj > 0)) wj = -1.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool own = j == j0[r];
+        const double val = own ? svr[r] : __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+        const double term = __builtin_fmax(own ? w0r[r] : wj, 0.0) * mvc_exp_le0(val - mr[r]);
+        if (j < K) cs[r] = cs[r] + term;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {   // pw16 over the row's 16 lanes (oracle pw16 association), lane col 0
+      double x = cs[r];
+      x = x + down_d<1>(x);
+      x = x + down_d<2>(x);
+      x = x + down_d<4>(x);
+      x = x + down_d<8>(x);
+      if (col == 0) Ss[grp + 4 * r] = x;
+    }
+    wave_lds_sync();
+    double S = Ss[col];
+    const int Kact = K - ((l0p == 0) ? 1 : 0);
+    double wn = alpha + (double)Kact * sigma;
+    if (wn < 0.0) wn = 0.0;
+    S = S + wn * mvc_exp_le0(lfn - m);
+    const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
+    out = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
   }
+  double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
+  *dm = out;
   wave_lds_sync();
 }
 
@@ -1650,8 +1711,8 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int
   const int nB = s_boff[V];
   double *Bs = (double *)(smem + 16 * 4);
   double *f_c0 = Bs + nB, *f_cb = f_c0 + sumK, *f_Q = f_cb + sumK;
-  double *wsp = f_Q + sumK + (size_t)w * 48;                   // per wave: y2s, selfG, mrest
-  int *f_dn = (int *)(f_Q + sumK + (size_t)BW * 48), *f_dl = f_dn + sumK;
+  double *wsp = f_Q + sumK + (size_t)w * 80;                   // per wave: y2s, selfG, mrest, w0s, Ss
+  int *f_dn = (int *)(f_Q + sumK + (size_t)BW * 80), *f_dl = f_dn + sumK;
   int *f_tix = f_dl + sumK, *f_nt = f_tix + MVC_FZ_TB * 16 * V;
   int *zs = f_nt + MVC_FZ_TB * 16 + w * 16;
   {
@@ -1875,7 +1936,7 @@ struct MHArgs {
   uint64_t seed;
   uint32_t chain, sweep;
   int do_mh;
-  const Repair *gate;     // non-null: run only once the sweep's repair is done
+  const Repair *gate;     // non-null: run only if the sweep's repair is done with no move
 };
 
 }  // namespace
@@ -1895,7 +1956,10 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
 #else
 #define HYP_MARK(name)
 #endif
-  if (A.gate && !A.gate->done) return;
+  // gated launch (enqueued before the host has read the repair's outcome):
+  // runs only for a finished repair with no move, where nothing (compaction,
+  // relabel, capacity growth) has to come between the repair and the MH
+  if (A.gate && !(A.gate->done && A.gate->moves == 0 && A.gate->overflow == 0 && A.gate->restride == 0)) return;
   const int T = A.status[0];
   // ---- Q = ||S1||^2 per live dish (fma chain in d order), all views at once;
   //      the strided S1 loads are issued 16 ahead of the chain ----
@@ -2206,6 +2270,7 @@ class ParallelSampler : public Sampler {
   double *seq_scr = nullptr;      // repair eval scratch (SeqScratch), kSeqWaves waves
   int64_t seq_stride = 0;
   Repair *rs_host = nullptr;      // pinned copy of a chain's Repair after each batch
+  hipEvent_t rs_ev = nullptr;     // recorded after that copy (the host waits on it, not on the stream)
   double *lpb = nullptr;          // phase-1 lp buffer (lpb_index layout)
   double *vmax = nullptr;         // [V][n] view maxima of the draw (producer -> draw)
   double *zsc = nullptr;          // generic draw: table scores [T][batch] (mvc_par_zdraw_kernel<true>)
@@ -2231,6 +2296,11 @@ class ParallelSampler : public Sampler {
   int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
   int n_cu = 256;
   bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
+  // MVC_LMV=1: the all-views producer forms the view terms lm_v for the
+  // register draw (bitwise the same chain; measured slower at configs[3]:
+  // producer 1.10 -> 1.30 ms, draw 0.44 -> 0.32 ms, profiles/r2t_lmv_ab.json)
+  bool no_lmv = true;
+  bool early_mh_off = false;      // MVC_EARLY_MH=0: the MH launched only after the host has read the repair
   bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
@@ -2372,6 +2442,8 @@ class ParallelSampler : public Sampler {
     }
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     if (const char *e = getenv("MVC_WIDE")) use_wide = e[0] != '0';
+    if (const char *e = getenv("MVC_EARLY_MH")) early_mh_off = e[0] == '0';
+    if (const char *e = getenv("MVC_LMV")) no_lmv = e[0] != '1';
     if (const char *e = getenv("MVC_RUN_LDS")) force_global = e[0] == '0';
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh_in);
@@ -2499,6 +2571,7 @@ class ParallelSampler : public Sampler {
       if (p) hipFree(p);
     if (st_host) hipHostFree(st_host);
     if (rs_host) hipHostFree(rs_host);
+    if (rs_ev) hipEventDestroy(rs_ev);
     if (stream) hipStreamDestroy(stream);
   }
 
@@ -2715,6 +2788,7 @@ class ParallelSampler : public Sampler {
     A.S1t = c.S1t;
     A.SP = SP;
     A.vmax = vmax;
+    A.lmv = 0;
     A.T = c.T;
     A.sumK = sumK(c);
     A.seed = cfg.seed;
@@ -2879,6 +2953,8 @@ class ParallelSampler : public Sampler {
       const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, 8);
       const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                              (spp == 4 || spp == 8 || spp == 16) && lpa_lds <= 160 * 1024;
+      // the view terms in the producer when the register draw follows (A.lmv)
+      A.lmv = (use_lpall && use_zreg && !no_lmv) ? 1 : 0;
       if (use_lpall) {
         const int ntile = (nb + 15) / 16;
         const int grid = std::max(1, std::min(n_cu, (ntile + 7) / 8));
@@ -3040,6 +3116,10 @@ class ParallelSampler : public Sampler {
       hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
     MVC_HIP(hipGetLastError());
     SeqLds L = run_layout(c.T, c.K.data());
+    // the gated early MH (below) only where no per-phase timers bracket the
+    // repair and the MH separately (they would time the MH as repair)
+    const bool early_mh = !early_mh_off && (!timers.on || timers.coarse);
+    if (early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
     int rounds = 1;
     for (;;) {
       for (int r = 0; r < rounds; ++r) {
@@ -3054,7 +3134,17 @@ class ParallelSampler : public Sampler {
       }
       MVC_HIP(hipGetLastError());
       MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
-      MVC_HIP(hipStreamSynchronize(stream));
+      if (early_mh) {
+        // the MH goes into the stream behind the copy, gated on the device by
+        // the repair's outcome (it runs iff the repair is done with no move),
+        // so the GPU runs it while the host waits for the copy and decides the
+        // next launches; it is a no-op in the other cases, which launch it below
+        MVC_HIP(hipEventRecord(rs_ev, stream));
+        launch_hyper(c, 1, s, c.R);
+        MVC_HIP(hipEventSynchronize(rs_ev));
+      } else {
+        MVC_HIP(hipStreamSynchronize(stream));
+      }
       if (rs_host->overflow) {
         grow_capacity(rs_host->overflow);
         Q = make_seq(c, s);
@@ -3087,7 +3177,7 @@ class ParallelSampler : public Sampler {
     c.last[1] = rs_host->births;
     c.last[2] = rs_host->rounds;
     c.last[3] = rs_host->newdish;
-    launch_hyper(c, 1, s);
+    if (!(early_mh && !moved)) launch_hyper(c, 1, s);   // else the gated launch above ran it
     if (moved) {   // new T and dish counts for the next sweep's launch shapes
       MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
       MVC_HIP(hipStreamSynchronize(stream));

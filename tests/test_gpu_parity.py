@@ -341,7 +341,8 @@ def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=
     monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
     monkeypatch.setenv("MVC_FUSED", "1" if draw == "fused" else "0")
     monkeypatch.setenv("MVC_LPALL", "0" if draw.endswith("-perview") else "1")
-    draw = draw.replace("-perview", "")
+    monkeypatch.setenv("MVC_LMV", "1" if draw.endswith("-lmv") else "0")   # view terms in the all-views producer
+    draw = draw.replace("-perview", "").replace("-lmv", "")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
     states = []
@@ -385,7 +386,7 @@ FUSED_SHAPES = {(3001, 4, 64, 16, 16): True, (50, 2, 20, 4, 4): True, (4000, 3, 
                 (4100, 4, 128, 64, 64): True, (777, 1, 32, 16, 16): True}
 
 
-@pytest.mark.parametrize("draw", ["fused", "reg", "lds", "reg-perview"])
+@pytest.mark.parametrize("draw", ["fused", "reg", "lds", "reg-perview", "reg-lmv"])
 @pytest.mark.parametrize("n,V,D,K,T", list(FUSED_SHAPES))
 def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     m = _mvc()
@@ -623,11 +624,15 @@ def test_dish_block_producer(force, monkeypatch):
     s.close()
 
 
-def test_lpall_batches(monkeypatch):
+@pytest.mark.parametrize("lmv", ["0", "1"])
+def test_lpall_batches(lmv, monkeypatch):
     """The all-views producer over customer batches (MVC_LPB_BATCH: the lp
     buffer holds one batch, the draw follows each batch; the last batch
-    ragged): bitwise vs the oracle, warm, V = 4 at D = 32."""
+    ragged): bitwise vs the oracle, warm, V = 4 at D = 32.  lmv = 1: the
+    producer also forms the view terms lm_v for the register draw
+    (MVC_LMV=1, opt-in)."""
     monkeypatch.setenv("MVC_LPB_BATCH", "1024")
+    monkeypatch.setenv("MVC_LMV", lmv)
     m = _mvc()
     from mvc_amd import data
     N, V, D, K = 5000, 4, 32, 16
