@@ -207,16 +207,6 @@ void validate(const mvc_config *c, const double *const *views) {
   if (!views) throw Error(MVC_ERR_ARG, "views is NULL");
   for (int v = 0; v < c->n_views; ++v)
     if (!views[v]) throw Error(MVC_ERR_ARG, "views[v] is NULL");
-  // Concurrent chains (parallel mode: one stream and host thread per chain)
-  // overlap only as far as HIP gives the process hardware queues
-  // (GPU_MAX_HW_QUEUES, default 4, read once at the process's first HIP call):
-  // ask for one per chain, at most 16, unless the caller chose a value.  No
-  // effect once HIP is initialised; never changes results.
-  if (c->mode == MVC_MODE_PARALLEL && c->n_chains > 4) {
-    char q[16];
-    snprintf(q, sizeof q, "%d", std::min(16, c->n_chains));
-    setenv("GPU_MAX_HW_QUEUES", q, 0);
-  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw Error(MVC_ERR_HIP, "no HIP device visible");
   if (c->device < 0 || c->device >= ndev) throw Error(MVC_ERR_ARG, "device ordinal out of range");

@@ -52,6 +52,7 @@ class Config(ctypes.Structure):
 
 
 _lib = None
+HW_QUEUES = 16   # hardware queues requested for concurrent chains (at most 32 on the GPU pool)
 
 
 def lib():
@@ -62,6 +63,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(
             f"{LIB_PATH} not found: build the HIP extension first (make, or __graft_entry__.build())")
+    # Concurrent chains (parallel mode, one stream each) overlap only as far
+    # as HIP gives the process hardware queues: GPU_MAX_HW_QUEUES, 4 by
+    # default, read once when HIP starts (at the latest while this library's
+    # kernels register at load).  Raise it to 16 unless a larger value is set;
+    # a process that started HIP earlier keeps its own.
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u32, u64, sz = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_size_t)
