@@ -175,6 +175,30 @@ def gpu_line(config, seed, device, steps=10, warmup=3):
             "moves_last_sweep": rep["moves"]}
 
 
+def gpu_chains_line(config, seed, device, chains=16, sweeps=1):
+    """Several chains of one config on one GPU at once (parallel-mode ChainSet:
+    one stream and host thread per chain, the data shared), warm
+    start at the generating partition: aggregate chain-sweeps/s.  The loader
+    asks HIP for 16 hardware queues, so 16 chains overlap."""
+    from mvc_amd import data
+    from mvc_amd.sampler import Sampler
+    N, V, D, K, desc = CONFIGS[config]
+    y, z = data.synthetic(N, V, D, K, seed=seed)
+    st = warm_state(z, V, K)
+    s = Sampler(y, seed=seed, mode="parallel", n_chains=chains, device=device)
+    for c in range(chains):
+        s.set_state(*st, chain=c)
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.sweep(sweeps)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    s.close()
+    return {"workload": desc.replace("1 chain/GPU", f"{chains} chains on 1 GPU at once"), "chains": chains,
+            "sweeps": sweeps, "value": round(chains * sweeps / dt, 3), "unit": "chain-sweeps/s",
+            "s_per_sweep_all_chains": round(dt / sweeps, 2)}
+
+
 def gpu_exact_line(seed, device, chains=256, sweeps=200):
     """BASELINE configs[0] (the New_Simulation.R problem, N = 500, V = 2, K = 3,
     200 sweeps) on the exact schedule (mode E: the reference's arithmetic,
@@ -373,6 +397,9 @@ def main():
             # D = 1: ~65% of customers move every sweep (1-D clusters overlap), so
             # the in-order repair dominates; one sweep (~15 s) is timed
             "north_star_literal_gpu": leg("north_star_literal_gpu", gpu_line, "ns", args.seed, local, 1, 0),
+            # the same with 16 chains at once (compare reference_schedule_cpu: one chain per core)
+            "north_star_literal_gpu_16chains": leg("north_star_literal_gpu_16chains", gpu_chains_line, "ns",
+                                                   args.seed, local),
             "configs1_gpu": leg("configs1_gpu", gpu_line, "c2", args.seed, local),
             "exact_schedule_gpu": leg("exact_schedule_gpu", gpu_exact_line, args.seed, local),
             "cold_start_gpu": leg("cold_start_gpu", cold_start, args.seed, local),

@@ -65,7 +65,7 @@ const Api &api() {
   // hardware queues for concurrent chains: HIP reads this once,
   // when it starts, which is while the library loads
   const char *hwq = std::getenv("GPU_MAX_HW_QUEUES");
-  if (!hwq || std::atoi(hwq) < 16) setenv("GPU_MAX_HW_QUEUES", "16", 1);
+  if (!hwq || std::atoi(hwq) < 32) setenv("GPU_MAX_HW_QUEUES", "32", 1);
   void *h = dlopen(path ? path : "libmvc_hip.so", RTLD_NOW | RTLD_LOCAL);
   if (!h) Rcpp::stop(std::string("cannot load libmvc_hip.so: ") + dlerror());
   bind(h, "mvc_config_init", a.config_init);

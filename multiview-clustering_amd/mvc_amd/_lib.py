@@ -52,7 +52,7 @@ class Config(ctypes.Structure):
 
 
 _lib = None
-HW_QUEUES = 16   # hardware queues requested for concurrent chains (at most 32 on the GPU pool)
+HW_QUEUES = 32   # hardware queues requested for concurrent chains (the GPU pool allows at most 32)
 
 
 def lib():
@@ -66,7 +66,7 @@ def lib():
     # Concurrent chains (parallel mode, one stream each) overlap only as far
     # as HIP gives the process hardware queues: GPU_MAX_HW_QUEUES, 4 by
     # default, read once when HIP starts (at the latest while this library's
-    # kernels register at load).  Raise it to 16 unless a larger value is set;
+    # kernels register at load).  Raise it to 32 unless a larger value is set;
     # a process that started HIP earlier keeps its own.
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
         os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
