@@ -8,7 +8,7 @@ HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS := $(EXTRA) -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
             -I$(ROOT)/include -I$(SRC) -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-const-variable
-OBJS := $(PKG)/build/mvc_exact.o $(PKG)/build/mvc_parallel.o $(PKG)/build/mvc_spec.o $(PKG)/build/mvc_ari.o \
+OBJS := $(PKG)/build/mvc_exact.o $(PKG)/build/mvc_parallel.o $(PKG)/build/mvc_spec.o $(PKG)/build/mvc_ari.o $(PKG)/build/mvc_synth.o \
         $(PKG)/build/mvc_api.o
 HDRS := $(ROOT)/include/mvc.h $(ROOT)/include/mvc_pmath.h $(ROOT)/include/mvc_philox.h \
         $(SRC)/mvc_internal.h $(SRC)/mvc_host.h $(SRC)/mvc_repair.h

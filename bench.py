@@ -39,8 +39,8 @@ CONFIGS = {
     "c4": (1_000_000, 4, 128, 64, "BASELINE configs[3] shard: synthetic N=1M V=4 D=128 K=64, 1 chain/GPU"),
     "c2": (100_000, 2, 64, 16, "BASELINE configs[1]: synthetic N=100k V=2 D=64 K=16, 1 chain"),
     "ns": (1_000_000, 4, 1, 64, "north_star literal: synthetic N=1M V=4 D=1 K=64, 1 chain/GPU"),
-    "c5s": (1_000_000, 8, 256, 256, "BASELINE configs[4] shape (V=8 D=256 K=256) at N=1M (N=10M: 164 GB of y, "
-                                    "beyond the box's host-memory cap for the synthetic generator), 1 chain"),
+    "c5": (10_000_000, 8, 256, 256, "BASELINE configs[4]: synthetic N=10M V=8 D=256 K=256 fp64 (y generated on the "
+                                    "device: 164 GB), 1 chain, MFMA dish-block producer"),
 }
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_F64_TFLOPS = 78.6       # fp64 MFMA / vector dense peak (spec)
@@ -218,6 +218,42 @@ def gpu_exact_line(seed, device, chains=256, sweeps=200):
             "unit": "chain-sweeps/s", "per_chain_sweeps_per_s": round(sweeps / dt, 2)}
 
 
+def config5_line(seed, device, steps=3, warmup=1):
+    """BASELINE configs[4] at its full size: N = 10M, V = 8, D = 256, K = 256
+    (164 GB of y, generated on the device by mvc_sampler_create_synthetic;
+    the host never holds it), warm start at the generating partition.
+    sweeps/s plus the z-resample pass against both roofs: MFMA fp64 (2 N D
+    sum K_v flops, AI ~ 64 flop/B: the binding roof) and HBM (the algorithmic
+    N (8 V D + 8) bytes)."""
+    from mvc_amd.sampler import Sampler
+    N, V, D, K, desc = CONFIGS["c5"]
+    t0 = time.perf_counter()
+    s, z = Sampler.synthetic(N, V, D, K, data_seed=seed, seed=seed, device=device, timing="coarse")
+    s.set_state(*warm_state(z, V, K))
+    s.sweep(warmup)
+    s.synchronize()
+    setup = time.perf_counter() - t0
+    s.reset_timers()
+    t1 = time.perf_counter()
+    s.sweep(steps)
+    s.synchronize()
+    dt = time.perf_counter() - t1
+    kms, kcnt = s.kernel_time("zresample")
+    kd = s.dish_counts()
+    rep = s.repair_stats()
+    zp = s.zpath()
+    s.close()
+    pass_s = kms / max(1, kcnt) / 1e3
+    flops = 2.0 * N * D * float(kd.sum())
+    byts = N * (8 * V * D + 8)
+    return {"workload": desc, "value": round(steps / dt, 4), "unit": "sweeps/s", "steps": steps,
+            "ms_per_sweep": round(1e3 * dt / steps, 2), "setup_s": round(setup, 1), "pass_ms": round(pass_s * 1e3, 2),
+            "mfma_tflops": round(flops / pass_s / 1e12, 2), "mfma_frac": round(flops / pass_s / 1e12 / PEAK_F64_TFLOPS, 4),
+            "hbm_gbs": round(byts / pass_s / 1e9, 1), "hbm_frac": round(byts / pass_s / 1e9 / PEAK_HBM_GBS, 4),
+            "bound": "mfma", "dishes": kd.tolist(), "moves_last_sweep": rep["moves"],
+            "producer": "mfma-dish-blocks" if zp & 64 else "other"}
+
+
 def cold_start(seed, device, sweeps=4):
     """BASELINE configs[1] (N = 100k, V = 2, D = 64, K = 16) from the
     reference's initialisation (4 tables, 2 dishes per view,
@@ -266,13 +302,20 @@ def main():
     from mvc_amd.sampler import Sampler
 
     t_gen = time.perf_counter()
-    y, z = data.synthetic(N, V, D, K, seed=args.seed)
+    shard = args.shard and world > 1
+    if args.config == "c5":   # 164 GB of y: generated on the device, never on the host
+        y = None
+        s, z = Sampler.synthetic(N, V, D, K, data_seed=args.seed, seed=args.seed, first_chain=0 if shard else rank,
+                                 device=local, timing="coarse")
+    else:
+        y, z = data.synthetic(N, V, D, K, seed=args.seed)
     t_gen = time.perf_counter() - t_gen
     # coarse timing in the timed region: HIP events around the z-resample pass
     # (the roofline) and the sweep only; the per-phase breakdown is taken on
     # extra sweeps after the timed region (each event pair idles the GPU ~5 us)
-    shard = args.shard and world > 1
-    s = Sampler(y, seed=args.seed, mode="parallel", first_chain=0 if shard else rank, device=local, timing="coarse")
+    if y is not None:
+        s = Sampler(y, seed=args.seed, mode="parallel", first_chain=0 if shard else rank, device=local,
+                    timing="coarse")
     s.set_state(*warm_state(z, V, K))
     if shard:   # every rank holds the whole chain; phase A split, choices all-gathered
         from mvc_amd.dist import ShardExchange
@@ -371,10 +414,10 @@ def main():
                 "mfma_tflops": round(tflops, 3), "mfma_frac": round(tflops / PEAK_F64_TFLOPS, 4),
                 "arith_intensity": round(flops_alg / bytes_alg, 3), "ridge": round(ridge, 3),
                 "bytes_per_launch": bytes_alg, "flops_per_launch": flops_alg, "pass_ms": round(k_avg_s * 1e3, 4),
-                "lp_producer": ("fused" if zpath & 8 else "mfma-all-views" if zpath & 16
+                "lp_producer": ("mfma-all-views" if zpath & 16
                                 else "mfma" if (zpath & 3) == 2 else "mfma-dish-blocks" if zpath & 64
                                 else "generic"),
-                "draw": "fused" if zpath & 8 else "registers" if zpath & 4 else "lds-checkpoints"},
+                "draw": "registers" if zpath & 4 else "lds-checkpoints"},
         "hyper_pooled": {"chains": red["chains"], "draws": red["count"],
                          "alpha_global": round(float(pooled_mean[-2]), 6),
                          "sigma_global": round(float(pooled_mean[-1]), 6),
@@ -401,12 +444,13 @@ def main():
             "north_star_literal_gpu_16chains": leg("north_star_literal_gpu_16chains", gpu_chains_line, "ns",
                                                    args.seed, local),
             "configs1_gpu": leg("configs1_gpu", gpu_line, "c2", args.seed, local),
+            "configs4_full_gpu": leg("configs4_full_gpu", config5_line, args.seed, local),
             "exact_schedule_gpu": leg("exact_schedule_gpu", gpu_exact_line, args.seed, local),
             "cold_start_gpu": leg("cold_start_gpu", cold_start, args.seed, local),
         }
         if not args.no_cpu_baseline:
             out["extra"]["reference_schedule_cpu"] = leg("reference_schedule_cpu", reference_schedule_cpu, args.seed)
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and y is not None:
         out["cpu_baseline"] = leg("cpu_baseline", cpu_baseline, y, z, V, K, D, args.seed)
     print(json.dumps(out), flush=True)
     if dist is not None:

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVC_ABI_VERSION 1
+#define MVC_ABI_VERSION 2
 
 /* status codes */
 #define MVC_OK 0
@@ -47,6 +47,7 @@ extern "C" {
 #define MVC_ERR_HIP 2        /* HIP runtime error (no device, OOM, launch)       */
 #define MVC_ERR_STATE 3      /* sampler state invariant violated (bug)          */
 #define MVC_ERR_UNSUPPORTED 4
+#define MVC_ERR_CALLBACK 5   /* a caller-supplied callback reported failure       */
 
 /* schedules */
 #define MVC_MODE_EXACT 0     /* reference schedule, bit-exact vs. the CPU oracle  */
@@ -68,6 +69,12 @@ typedef struct mvc_config {
   int32_t table_cap;    /* initial table capacity per chain (0 = auto)            */
   int32_t dish_cap;     /* initial dish capacity per view per chain (0 = auto)    */
   int32_t flags;        /* MVC_FLAG_*                                             */
+  /* ABI 2 */
+  int32_t n_devices;    /* mvc_run: chains spread over devices device ..          */
+                        /* device + n_devices - 1, chain c on device + c % n_devices */
+                        /* (one host thread per device); 0 or 1: `device` only    */
+  int32_t chain_stride; /* global id of local chain c = first_chain + c * stride  */
+                        /* (0 = 1); the id keys every Philox counter              */
 } mvc_config;
 
 #define MVC_FLAG_TIMING 1   /* record per-kernel HIP-event times (mvc_sampler_kernel_time) */
@@ -101,6 +108,12 @@ const int32_t *mvc_result_dish_of(const mvc_result *r, int chain, int s);       
 #define MVC_TRACE_ALPHA_GLOBAL 3
 #define MVC_TRACE_SIGMA_GLOBAL 4
 const double *mvc_result_trace(const mvc_result *r, int chain, int which);
+/* Posterior summary over every chain's saved samples (no reference
+ * counterpart: the reference runs one chain).  mean[3V+2] and rhat[3V+2] in
+ * the hyper order tau[V], alpha[V], sigma[V], alpha_g, sigma_g: pooled means
+ * and the Gelman-Rubin potential scale reduction (NaN with fewer than two
+ * chains or two saved samples).  Either pointer may be NULL. */
+int mvc_result_summary(const mvc_result *r, double *mean, double *rhat);
 void mvc_result_free(mvc_result *r);
 
 /* ------------------------------------------------------------------------ */
@@ -168,16 +181,37 @@ int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out);
  * this rank's customers, shard `rank` = [rank S, min(n, (rank+1) S)) with
  * S = mvc_shard_len(n, world).  The handle copies its shard's choices into
  * `exchange` (device memory, world * S int32), synchronises its stream and
- * calls all_gather(user), which must return once every rank's shard is in
- * `exchange` (e.g. an RCCL all-gather in place); then every rank runs the
+ * calls all_gather(user), which must return 0 once every rank's shard is in
+ * `exchange` (e.g. an RCCL all-gather in place).  A nonzero return fails the
+ * sweep with MVC_ERR_CALLBACK before anything reads the exchange buffer: the
+ * chain state is left as it was before the sweep.  Otherwise every rank runs the
  * same in-order repair, compaction and MH on the same state, so the ranks
  * stay identical to each other and to the unsharded chain, bit for bit.
  * world = 1 turns sharding off.  One chain per handle; MVC_ERR_UNSUPPORTED
  * for the exact schedule or several chains.  (No reference counterpart: the
  * reference runs one chain in one process.) */
 int mvc_sampler_set_shard(mvc_sampler *s, int32_t rank, int32_t world, int32_t *exchange,
-                          void (*all_gather)(void *), void *user);
+                          int (*all_gather)(void *), void *user);
 int64_t mvc_shard_len(int64_t n, int32_t world);
+/* Synthetic data generated on the device, no host copy of y (SURVEY.md §8d
+ * recipe): z_i ~ U{0..K-1}, per-view cluster c_v = z mod K_v with K_v =
+ * max(1, K >> v), means mu_v[c] ~ N(0, mu_sd^2 I_D), y_v[i] = mu_v[c_v(i)] +
+ * sd N(0, I_D), drawn from Philox keyed by data_seed (mvc_synth.hip; a
+ * different stream from the Python package's numpy generator).  Creates a
+ * parallel-mode handle on it (cfg->n, n_views, dim as usual; views are not
+ * passed); z_out[n] (host, may be NULL) receives the generating labels.
+ * tau_v's initial value comes from device column sums (one pass, not the
+ * host's two-pass loop bit for bit).  MVC_ERR_UNSUPPORTED for the exact
+ * schedule.  (No reference counterpart: the data source of BASELINE
+ * configs[4], N = 10M x 8 views x 256 dims = 164 GB, which fits the HBM but
+ * not the host.) */
+int mvc_sampler_create_synthetic(const mvc_config *cfg, int32_t K, uint64_t data_seed, double sd, double mu_sd,
+                                 int32_t *z_out, mvc_sampler **out, char *err, size_t errlen);
+/* Rows idx[0..m) of view `view` of the handle's data, m x dim doubles, to
+ * the host (checks against the CPU restatement at sizes the host cannot
+ * hold whole).  Parallel schedule only. */
+int mvc_sampler_copy_rows(mvc_sampler *s, int32_t view, const int32_t *idx, int64_t m, double *out, char *err,
+                          size_t errlen);
 /* Opaque HIP stream the handle launches on (hipStream_t as void*). */
 void *mvc_sampler_stream(mvc_sampler *s);
 void mvc_sampler_destroy(mvc_sampler *s);

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mvc.h"
@@ -18,7 +19,7 @@
 
 namespace mvc {
 
-InitState draw_initial_state(const double *y, int n, int V, int D, uint64_t seed, uint32_t chain) {
+InitState draw_initial_draws(int n, int V, uint64_t seed, uint32_t chain) {
   // multiview_gibbs.cpp:12-62: T0 = 4 tables drawn for i ascending, then per
   // view K0 = 2 dishes for t ascending, all from R::runif(0, K).
   InitState S;
@@ -42,6 +43,12 @@ InitState draw_initial_state(const double *y, int n, int V, int D, uint64_t seed
       if (kk >= 2) kk = 1;
       S.dish_raw[v * 4 + t] = kk;
     }
+  S.draws = k;
+  return S;
+}
+
+InitState draw_initial_state(const double *y, int n, int V, int D, uint64_t seed, uint32_t chain) {
+  InitState S = draw_initial_draws(n, V, seed, chain);
   // tau_v = Var_{n-1}(y_v) * 0.25 * 0.01  (multiview_gibbs.cpp:78-94);
   // for dim > 1 the mean of the per-dimension variances.
   S.tau.resize(V);
@@ -67,7 +74,6 @@ InitState draw_initial_state(const double *y, int n, int V, int D, uint64_t seed
     const double var = vsum / (double)D;
     S.tau[v] = var * 0.25 * 0.01;
   }
-  S.draws = k;
   return S;
 }
 
@@ -169,6 +175,7 @@ Timers::~Timers() {
 // ---------------------------------------------------------------------------
 namespace {
 thread_local std::string g_last_error;
+const double K_dummy = 0.0;   // stands in for host views that a call does not take
 
 int fail(int code, const std::string &msg, char *err, size_t errlen) {
   g_last_error = msg;
@@ -204,12 +211,91 @@ void validate(const mvc_config *c, const double *const *views) {
   if (c->thin < 1) throw Error(MVC_ERR_ARG, "thin must be >= 1");
   if (c->n_chains < 1) throw Error(MVC_ERR_ARG, "n_chains must be >= 1");
   if (c->mode != MVC_MODE_EXACT && c->mode != MVC_MODE_PARALLEL) throw Error(MVC_ERR_ARG, "unknown mode");
+  if (c->n_devices < 0) throw Error(MVC_ERR_ARG, "n_devices must be >= 0");
+  if (c->chain_stride < 0) throw Error(MVC_ERR_ARG, "chain_stride must be >= 0");
   if (!views) throw Error(MVC_ERR_ARG, "views is NULL");
   for (int v = 0; v < c->n_views; ++v)
     if (!views[v]) throw Error(MVC_ERR_ARG, "views[v] is NULL");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw Error(MVC_ERR_HIP, "no HIP device visible");
   if (c->device < 0 || c->device >= ndev) throw Error(MVC_ERR_ARG, "device ordinal out of range");
+  if (c->n_devices > 1 && c->device + std::min(c->n_devices, c->n_chains) > ndev)
+    throw Error(MVC_ERR_ARG, "n_devices: devices device .. device + n_devices - 1 are not all visible");
+}
+
+}  // namespace
+
+namespace {
+
+// One device's share of mvc_run: its chains in one handle, sweeps and the
+// saved samples (multiview_gibbs.cpp:150-210 incl. save_state at :205-206).
+struct RunPart {
+  int S = 0;
+  std::vector<std::vector<std::vector<int32_t>>> table_of, dish_of;   // [chain][s]
+  std::vector<std::vector<int>> T;
+  std::vector<std::vector<std::vector<double>>> traces;               // [chain][which]
+};
+
+void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
+  std::unique_ptr<mvc::Sampler> S(cf.mode == MVC_MODE_EXACT ? mvc::make_exact_sampler(cf, views)
+                                                           : mvc::make_parallel_sampler(cf, views));
+  const int C = cf.n_chains, V = cf.n_views, n = cf.n;
+  R.table_of.resize(C);
+  R.dish_of.resize(C);
+  R.T.resize(C);
+  R.traces.assign(C, std::vector<std::vector<double>>(5));
+  std::vector<std::vector<std::vector<double>>> hv(C);   // [chain][s] hyper vectors
+  std::vector<double> hyper(3 * V + 2);
+  const bool quiet = (cf.flags & MVC_FLAG_QUIET) != 0;
+  const mvc::Sampler::SampleFn save_fn = [&](int c, int T, const int32_t *t, const int32_t *d, const double *h) {
+    R.table_of[c].emplace_back(t, t + n);
+    R.dish_of[c].emplace_back(d, d + (size_t)V * T);
+    R.T[c].push_back(T);
+    hv[c].emplace_back(h, h + 3 * V + 2);
+  };
+  for (int iter = 0; iter < cf.n_iter; ++iter) {
+    if (!quiet && (iter + 1) % 100 == 0)                          // gibbs.cpp:152-155
+      std::fprintf(stderr, "Iteration %d / %d\n", iter + 1, cf.n_iter);
+    S->sweep(1);
+    if (iter >= cf.burn_in && ((iter - cf.burn_in) % cf.thin == 0)) {   // gibbs.cpp:205
+      for (int c = 0; c < C; ++c) {
+        if (S->save_async(c, save_fn)) continue;        // device snapshot + async D2H (f3)
+        std::vector<int32_t> t(n);
+        int32_t T = 0;
+        // first query T, then fetch dish_of with an exact capacity
+        S->get_state(c, t.data(), &T, nullptr, 0, hyper.data());
+        std::vector<int32_t> d((size_t)V * std::max(T, 1));
+        S->get_state(c, nullptr, &T, d.data(), std::max(T, 1), nullptr);
+        d.resize((size_t)V * T);
+        R.table_of[c].push_back(std::move(t));
+        R.dish_of[c].push_back(std::move(d));
+        R.T[c].push_back(T);
+        hv[c].push_back(hyper);
+      }
+      R.S++;
+    }
+  }
+  S->flush_saves();
+  S->synchronize();
+  const int Sn = R.S;
+  for (int c = 0; c < C; ++c) {
+    auto &tr = R.traces[c];
+    tr[MVC_TRACE_ALPHA_V].resize((size_t)V * Sn);
+    tr[MVC_TRACE_SIGMA_V].resize((size_t)V * Sn);
+    tr[MVC_TRACE_TAU_V].resize((size_t)V * Sn);
+    tr[MVC_TRACE_ALPHA_GLOBAL].resize(Sn);
+    tr[MVC_TRACE_SIGMA_GLOBAL].resize(Sn);
+    for (int s = 0; s < Sn; ++s) {
+      const auto &h = hv[c][s];
+      for (int v = 0; v < V; ++v) {
+        tr[MVC_TRACE_TAU_V][(size_t)v * Sn + s] = h[v];
+        tr[MVC_TRACE_ALPHA_V][(size_t)v * Sn + s] = h[V + v];
+        tr[MVC_TRACE_SIGMA_V][(size_t)v * Sn + s] = h[2 * V + v];
+      }
+      tr[MVC_TRACE_ALPHA_GLOBAL][s] = h[3 * V];
+      tr[MVC_TRACE_SIGMA_GLOBAL][s] = h[3 * V + 1];
+    }
+  }
 }
 
 }  // namespace
@@ -256,6 +342,42 @@ int mvc_sampler_create(const mvc_config *cfg, const double *const *views, mvc_sa
       throw;
     }
     *out = h;
+  });
+}
+
+int mvc_sampler_create_synthetic(const mvc_config *cfg, int32_t K, uint64_t data_seed, double sd, double mu_sd,
+                                 int32_t *z_out, mvc_sampler **out, char *err, size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!out) throw mvc::Error(MVC_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (!cfg) throw mvc::Error(MVC_ERR_ARG, "config is NULL");
+    if (cfg->mode != MVC_MODE_PARALLEL)
+      throw mvc::Error(MVC_ERR_UNSUPPORTED, "synthetic device data: parallel schedule only");
+    // validate() checks the views' pointers: hand it V dummies (never read)
+    std::vector<const double *> dummy(std::max(1, cfg->n_views), &K_dummy);
+    validate(cfg, dummy.data());
+    mvc::DeviceData dd = mvc::synth_device_data(cfg->device, cfg->n, cfg->n_views, cfg->dim, K, data_seed, sd, mu_sd,
+                                                z_out);
+    auto *h = new mvc_sampler();
+    try {
+      h->impl.reset(mvc::make_parallel_sampler_device(*cfg, std::move(dd)));
+    } catch (...) {
+      if (dd.y) hipFree(dd.y);
+      if (dd.Y2) hipFree(dd.Y2);
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+int mvc_sampler_copy_rows(mvc_sampler *s, int32_t view, const int32_t *idx, int64_t m, double *out, char *err,
+                          size_t errlen) {
+  return guarded(err, errlen, [&] {
+    if (!s || !s->impl || (m > 0 && (!idx || !out))) throw mvc::Error(MVC_ERR_ARG, "NULL argument");
+    if (m < 0) throw mvc::Error(MVC_ERR_ARG, "m < 0");
+    if (m == 0) return;
+    s->impl->copy_rows(view, idx, m, out);
   });
 }
 
@@ -397,7 +519,7 @@ int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out) {
 }
 
 int mvc_sampler_set_shard(mvc_sampler *s, int32_t rank, int32_t world, int32_t *exchange,
-                          void (*all_gather)(void *), void *user) {
+                          int (*all_gather)(void *), void *user) {
   if (!s || !s->impl) return MVC_ERR_ARG;
   try {
     return s->impl->set_shard(rank, world, exchange, all_gather, user) ? MVC_OK : MVC_ERR_UNSUPPORTED;
@@ -417,71 +539,99 @@ int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out,
     if (!out) throw mvc::Error(MVC_ERR_ARG, "out is NULL");
     *out = nullptr;
     validate(cfg, views);
-    std::unique_ptr<mvc::Sampler> S(cfg->mode == MVC_MODE_EXACT ? mvc::make_exact_sampler(*cfg, views)
-                                                                : mvc::make_parallel_sampler(*cfg, views));
-    auto R = std::make_unique<mvc_result>();
-    const int C = cfg->n_chains, V = cfg->n_views, n = cfg->n;
-    R->C = C;
-    R->n = n;
-    R->V = V;
-    R->table_of.resize(C);
-    R->dish_of.resize(C);
-    R->T.resize(C);
-    R->traces.assign(C, std::vector<std::vector<double>>(5));
-    std::vector<std::vector<std::vector<double>>> hv(C);   // [chain][s] hyper vectors
-    std::vector<double> hyper(3 * V + 2);
-    const bool quiet = (cfg->flags & MVC_FLAG_QUIET) != 0;
-    const mvc::Sampler::SampleFn save_fn = [&](int c, int T, const int32_t *t, const int32_t *d, const double *h) {
-      R->table_of[c].emplace_back(t, t + n);
-      R->dish_of[c].emplace_back(d, d + (size_t)V * T);
-      R->T[c].push_back(T);
-      hv[c].emplace_back(h, h + 3 * V + 2);
+    const int C = cfg->n_chains, V = cfg->n_views;
+    // chain c on device `device + c % nd`, one host thread per device; a
+    // device's chains form one handle with chain ids first_chain + (d + k nd)
+    // * stride, k = 0, 1, ... (the id keys every Philox counter, so a chain
+    // is the same wherever it runs)
+    const int nd = std::max(1, std::min(cfg->n_devices, C));
+    std::vector<RunPart> parts(nd);
+    std::vector<std::exception_ptr> errs(nd);
+    auto one = [&](int d) {
+      try {
+        mvc_config sc = *cfg;
+        sc.device = cfg->device + d;
+        sc.n_devices = 1;
+        sc.first_chain = (int32_t)mvc::chain_gid(*cfg, d);
+        sc.chain_stride = (cfg->chain_stride > 0 ? cfg->chain_stride : 1) * nd;
+        sc.n_chains = (C - d + nd - 1) / nd;
+        if (d > 0) sc.flags |= MVC_FLAG_QUIET;   // one progress line per iteration
+        run_part(sc, views, parts[d]);
+      } catch (...) {
+        errs[d] = std::current_exception();
+      }
     };
-    for (int iter = 0; iter < cfg->n_iter; ++iter) {
-      if (!quiet && (iter + 1) % 100 == 0)                          // gibbs.cpp:152-155
-        std::fprintf(stderr, "Iteration %d / %d\n", iter + 1, cfg->n_iter);
-      S->sweep(1);
-      if (iter >= cfg->burn_in && ((iter - cfg->burn_in) % cfg->thin == 0)) {   // gibbs.cpp:205
-        for (int c = 0; c < C; ++c) {
-          if (S->save_async(c, save_fn)) continue;        // device snapshot + async D2H (f3)
-          std::vector<int32_t> t(n);
-          int32_t T = 0;
-          // first query T, then fetch dish_of with an exact capacity
-          S->get_state(c, t.data(), &T, nullptr, 0, hyper.data());
-          std::vector<int32_t> d((size_t)V * std::max(T, 1));
-          S->get_state(c, nullptr, &T, d.data(), std::max(T, 1), nullptr);
-          d.resize((size_t)V * T);
-          R->table_of[c].push_back(std::move(t));
-          R->dish_of[c].push_back(std::move(d));
-          R->T[c].push_back(T);
-          hv[c].push_back(hyper);
-        }
-        R->S++;
-      }
+    if (nd == 1) {
+      one(0);
+    } else {
+      std::vector<std::thread> ts;
+      for (int d = 0; d < nd; ++d) ts.emplace_back(one, d);
+      for (auto &t : ts) t.join();
     }
-    S->flush_saves();
-    S->synchronize();
-    const int Sn = R->S;
+    for (auto &e : errs)
+      if (e) std::rethrow_exception(e);
+    auto R = std::make_unique<mvc_result>();
+    R->C = C;
+    R->n = cfg->n;
+    R->V = V;
+    R->S = parts[0].S;
     for (int c = 0; c < C; ++c) {
-      auto &tr = R->traces[c];
-      tr[MVC_TRACE_ALPHA_V].resize((size_t)V * Sn);
-      tr[MVC_TRACE_SIGMA_V].resize((size_t)V * Sn);
-      tr[MVC_TRACE_TAU_V].resize((size_t)V * Sn);
-      tr[MVC_TRACE_ALPHA_GLOBAL].resize(Sn);
-      tr[MVC_TRACE_SIGMA_GLOBAL].resize(Sn);
-      for (int s = 0; s < Sn; ++s) {
-        const auto &h = hv[c][s];
-        for (int v = 0; v < V; ++v) {
-          tr[MVC_TRACE_TAU_V][(size_t)v * Sn + s] = h[v];
-          tr[MVC_TRACE_ALPHA_V][(size_t)v * Sn + s] = h[V + v];
-          tr[MVC_TRACE_SIGMA_V][(size_t)v * Sn + s] = h[2 * V + v];
-        }
-        tr[MVC_TRACE_ALPHA_GLOBAL][s] = h[3 * V];
-        tr[MVC_TRACE_SIGMA_GLOBAL][s] = h[3 * V + 1];
-      }
+      RunPart &P = parts[c % nd];
+      const int k = c / nd;
+      R->table_of.push_back(std::move(P.table_of[k]));
+      R->dish_of.push_back(std::move(P.dish_of[k]));
+      R->T.push_back(std::move(P.T[k]));
+      R->traces.push_back(std::move(P.traces[k]));
     }
     *out = R.release();
   });
+}
+
+int mvc_result_summary(const mvc_result *r, double *mean, double *rhat) {
+  if (!r) return MVC_ERR_ARG;
+  const int V = r->V, S = r->S, C = r->C, W = 3 * V + 2;
+  // hyper order tau, alpha, sigma (per view), alpha_g, sigma_g
+  auto draw = [&](int c, int s, int k) -> double {
+    const auto &tr = r->traces[c];
+    if (k < V) return tr[MVC_TRACE_TAU_V][(size_t)k * S + s];
+    if (k < 2 * V) return tr[MVC_TRACE_ALPHA_V][(size_t)(k - V) * S + s];
+    if (k < 3 * V) return tr[MVC_TRACE_SIGMA_V][(size_t)(k - 2 * V) * S + s];
+    return tr[k == 3 * V ? MVC_TRACE_ALPHA_GLOBAL : MVC_TRACE_SIGMA_GLOBAL][s];
+  };
+  const double nan = std::nan("");
+  for (int k = 0; k < W; ++k) {
+    double tot = 0.0;
+    std::vector<double> cm(C, 0.0), cv(C, 0.0);
+    for (int c = 0; c < C; ++c) {
+      double a = 0.0;
+      for (int s = 0; s < S; ++s) a += draw(c, s, k);
+      cm[c] = S > 0 ? a / S : nan;
+      tot += a;
+      if (S > 1) {
+        double q = 0.0;
+        for (int s = 0; s < S; ++s) q += (draw(c, s, k) - cm[c]) * (draw(c, s, k) - cm[c]);
+        cv[c] = q / (S - 1);
+      }
+    }
+    if (mean) mean[k] = (S > 0 && C > 0) ? tot / ((double)S * C) : nan;
+    if (rhat) {
+      // Gelman-Rubin: B = n/(m-1) sum (mean_j - grand)^2, W = mean of the
+      // within-chain variances, var+ = (n-1)/n W + B/n, R = sqrt(var+/W)
+      if (C < 2 || S < 2) {
+        rhat[k] = nan;
+        continue;
+      }
+      double grand = 0.0, Wv = 0.0, B = 0.0;
+      for (int c = 0; c < C; ++c) { grand += cm[c]; Wv += cv[c]; }
+      grand /= C;
+      Wv /= C;
+      for (int c = 0; c < C; ++c) B += (cm[c] - grand) * (cm[c] - grand);
+      B *= (double)S / (C - 1);
+      const double vplus = (S - 1.0) / S * Wv + B / S;
+      rhat[k] = Wv > 0.0 ? std::sqrt(vplus / Wv) : nan;
+    }
+  }
+  return MVC_OK;
 }
 
 int mvc_result_num_saved(const mvc_result *r) { return r ? r->S : -1; }

@@ -804,7 +804,7 @@ class ExactSampler : public Sampler {
     const int KC = std::max(c.dish_cap > 0 ? c.dish_cap : 32, 4);
     chains.resize(c.n_chains);
     for (int ch = 0; ch < c.n_chains; ++ch) {
-      const uint32_t gid = (uint32_t)(c.first_chain + ch);
+      const uint32_t gid = chain_gid(c, ch);
       InitState S = draw_initial_state(y.data(), n, V, 1, c.seed, gid);
       ExactImage I = image_from_init(S, y.data(), TC, KC);
       ExactAlloc &A = chains[ch];

@@ -37,6 +37,23 @@ struct InitState {
 };
 InitState draw_initial_state(const double *y /*[V][n][D]*/, int n, int V, int D, uint64_t seed,
                              uint32_t chain);
+// The table / dish draws of draw_initial_state only (tau left empty).
+InitState draw_initial_draws(int n, int V, uint64_t seed, uint32_t chain);
+
+// Views already on the device (synthetic data generated there): the sampler
+// takes ownership of y and Y2.
+struct DeviceData {
+  double *y = nullptr;              // [V][n][D]
+  double *Y2 = nullptr;             // [V][n], fma chain in ascending d
+  std::vector<double> tau0;         // [V] initial tau_v (multiview_gibbs.cpp:78-94)
+};
+// mvc_synth.hip: the SURVEY §8d synthetic recipe on the device; z_host[n]
+// (optional) receives the generating labels.
+DeviceData synth_device_data(int device, int n, int V, int D, int K, uint64_t seed, double sd, double mu_sd,
+                             int32_t *z_host);
+// Rows idx[0..m) of view `view` of a device y [V][n][D] to the host.
+void gather_rows(const double *y, int n, int D, int view, const int32_t *idx_host, int64_t m, double *out_host,
+                 hipStream_t st);
 
 // Per-kernel HIP-event timers (MVC_FLAG_TIMING).
 struct Timers {
@@ -81,13 +98,18 @@ class Sampler {
   // Device pointer to the chain's table labels [n] (valid until the next
   // sweep; the stream is synchronised), or nullptr when they live on the host.
   virtual const int32_t *device_labels(int chain) { (void)chain; return nullptr; }
+  // Rows idx[0..m) of view `view` of the sampler's data (m x dim doubles).
+  virtual void copy_rows(int view, const int32_t *idx, int64_t m, double *out) {
+    (void)view; (void)idx; (void)m; (void)out;
+    throw Error(MVC_ERR_UNSUPPORTED, "copy_rows: not available for this schedule");
+  }
   // Repair counters of the chain's last parallel sweep:
   // out[0] customers that moved, out[1] births, out[2] repair rounds,
   // out[3] dishes opened.  False for the exact schedule.
   virtual bool repair_stats(int chain, int32_t *out) { (void)chain; (void)out; return false; }
   // Within-chain N-sharding (mvc_sampler_set_shard): false where unsupported
   // (the exact schedule, several chains per handle).
-  virtual bool set_shard(int rank, int world, int32_t *exch, void (*cb)(void *), void *user) {
+  virtual bool set_shard(int rank, int world, int32_t *exch, int (*cb)(void *), void *user) {
     (void)rank; (void)world; (void)exch; (void)cb; (void)user;
     return false;
   }
@@ -117,6 +139,12 @@ class Sampler {
 double ari_device(const int32_t *da, const int32_t *db, int64_t n, hipStream_t stream);
 double ari_from_pairs(uint64_t a, uint64_t sa, uint64_t sb, int64_t n);
 
+// Global id of a handle's local chain c (mvc_config.chain_stride): the id
+// keys every Philox counter of the chain.
+inline uint32_t chain_gid(const mvc_config &c, int local) {
+  return (uint32_t)(c.first_chain + local * (c.chain_stride > 0 ? c.chain_stride : 1));
+}
+
 // Customers per shard of within-chain N-sharding: ceil(n / world) rounded up
 // to 64 (the phase-A batches' alignment); shard r is [r S, min(n, (r+1) S)).
 inline int64_t shard_len(int64_t n, int world) {
@@ -137,5 +165,6 @@ UserState check_user_state(int n, int V, const int32_t *table_of, int32_t T, con
 
 Sampler *make_exact_sampler(const mvc_config &cfg, const double *const *views);
 Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views);
+Sampler *make_parallel_sampler_device(const mvc_config &cfg, DeviceData &&dd);
 
 }  // namespace mvc

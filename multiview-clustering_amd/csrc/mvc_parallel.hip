@@ -52,7 +52,6 @@ struct Sweep {
   const double *S1t;      // MFMA B-fragment layout of S1 (mvc_par_s1tile_kernel)
   int32_t SP;             // k-steps per view in yt/S1t (D/4 rounded up to MVC_ZR)
   double *vmax;           // [V][n] the view maximum m_v of each customer (producer -> draw)
-  int32_t lmv;            // 1: the all-views producer puts the view term lm_v in vmax instead (register draw)
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
@@ -929,7 +928,7 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     int tot = 0;
     for (int v = 0; v < V; ++v) {
       const int K = s_koff[v + 1] - s_koff[v];
-      const bool st = !A.lmv && s_lmin[v] != 0 && K <= 16 && tot + K <= MVC_ZSTAGE;
+      const bool st = s_lmin[v] != 0 && K <= 16 && tot + K <= MVC_ZSTAGE;
       s_soff[v] = st ? tot : -1;
       tot += st ? K : 0;
     }
@@ -944,9 +943,7 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     const bool alive = (P.n_t[p0] - 1) > 0;
     const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
     double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
-    // A.lmv: the producer formed each view's term lm_v (in vmax)
-    for (int v = 0; A.lmv && v < V; ++v) s_new = s_new + A.vmax[(size_t)v * n + i];
-    for (int v = 0; !A.lmv && v < V; ++v) {
+    for (int v = 0; v < V; ++v) {
       const int koff = __builtin_amdgcn_readfirstlane(s_koff[v]);
       const int K = __builtin_amdgcn_readfirstlane(s_koff[v + 1]) - koff;
       const int j0 = s_tix[p0 * V + v] - koff;
@@ -1055,38 +1052,15 @@ __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK
 }
 
 // ---------------------------------------------------------------------------
-// Fused phase 1: lp producer and draw in ONE kernel, no lp
-// buffer.  Applies when T <= 64, every K_v <= 64, V <= MVC_Z_VMAX and every
-// view's S1 B-fragments fit in LDS together (one block per CU, persistent).
-// Each wave owns 16-customer tiles.  Per tile and view: the MFMA tile of
-// lpview_tile_mfma (A-fragments streamed from yt through the register ring,
-// which runs ahead across view and tile boundaries), then the epilogue works
-// in the accumulator layout: customer row = grp + 4 r sits in the 16 lanes
-// of DPP row grp (dish column = lane & 15, dish block t in-register).  So the
-// oracle's per-customer reductions are in-lane over dish blocks plus a 16-lane
-// xor butterfly (row16 max; the pw16 tree of the column partials), and the
-// table scores sp[p] (lane column = table position within a block of 16)
-// gather lp of dish_v(p) from the row's lanes with ds_bpermute.  The draw
-// (block sums pw16, running block totals, pw16 descent) ends with one lane per
-// row set; choices are stored unconditionally (inactive lanes hit a discard
-// slot).  Same arithmetic as oracle eval_view_seq / resample_customer.
+// View patterns (compile-time per-view dish-block counts) of the all-views
+// producer below: bits 0-3 = V, bits 4 + 2 v .. = NT_v - 1 (dish blocks of 16
+// in view v).  Views run in order, unrolled at compile time, so a tile is
+// straight-line code (no joins between views with different NT, which cost
+// the register allocator ~60 VGPRs).  Instances: the bench's K_v = 64, 32,
+// 16, 8 and configs[1]'s 16, 8 shapes, every view count <= 4 with a common
+// dish-block count of 1 or 2, and up to two views of 4 blocks.
 // ---------------------------------------------------------------------------
 #define MVC_FZ_TB 4               // table blocks of 16 (T <= 64)
-#ifndef MVC_FZ_THREADS
-#define MVC_FZ_THREADS 256        // one wave per SIMD: the fused tile needs more than 256 VGPRs
-#endif
-#ifndef MVC_FZ_RP16
-#define MVC_FZ_RP16 8             // A-fragment ring depth (k-step pairs) at D = 128
-#endif
-__host__ __device__ inline size_t fused_shared_bytes(size_t s1t_doubles, int V, int sumK, int waves) {
-  return ((4 * (4 * (size_t)V + 2) + 15) & ~(size_t)15) + 8 * 2 * (size_t)V +
-         8 * (s1t_doubles + 7 * (size_t)sumK + 2 * 16 * MVC_FZ_TB + (size_t)waves * ((V + 1) * 16 + 8)) +
-         4 * ((size_t)sumK + (size_t)16 * MVC_FZ_TB * V + 16 * MVC_FZ_TB) + 64;
-}
-// View patterns with a fused kernel instance (fz_pat_v / fz_pat_nt below):
-// the bench's K_v = 64, 32, 16, 8 and configs[1]'s 16, 8 shapes, every view
-// count <= 4 with a common dish-block count of 1 or 2, and up to two views of
-// 4 blocks (more spill at this register budget).
 #define MVC_FZ_PAT(V, n0, n1, n2, n3) ((V) | (((n0) - 1) << 4) | (((n1) - 1) << 6) | (((n2) - 1) << 8) | (((n3) - 1) << 10))
 #define MVC_FZ_PATS(X)                                                                                     \
   X(MVC_FZ_PAT(4, 4, 2, 1, 1)) X(MVC_FZ_PAT(3, 4, 2, 1, 1)) X(MVC_FZ_PAT(2, 4, 2, 1, 1))                  \
@@ -1094,433 +1068,15 @@ __host__ __device__ inline size_t fused_shared_bytes(size_t s1t_doubles, int V, 
   X(MVC_FZ_PAT(3, 1, 1, 1, 1)) X(MVC_FZ_PAT(4, 1, 1, 1, 1)) X(MVC_FZ_PAT(1, 2, 2, 2, 2))                  \
   X(MVC_FZ_PAT(2, 2, 2, 2, 2)) X(MVC_FZ_PAT(3, 2, 2, 2, 2)) X(MVC_FZ_PAT(4, 2, 2, 2, 2))                  \
   X(MVC_FZ_PAT(1, 4, 4, 4, 4)) X(MVC_FZ_PAT(2, 4, 4, 4, 4)) X(MVC_FZ_PAT(3, 2, 1, 1, 1))
-
-// 16-lane xor butterfly steps on fp64 (DPP within each row): after the steps
-// with masks 1, 2 the 4-groups are uniform, so row_half_mirror / row_mirror
-// deliver the sibling 4- / 8-group exactly as xor 4 / xor 8 would.
-__device__ __forceinline__ double x1_d(double x) { return dpp_d<0xB1>(x); }    // quad_perm [1,0,3,2]
-__device__ __forceinline__ double x2_d(double x) { return dpp_d<0x4E>(x); }    // quad_perm [2,3,0,1]
-__device__ __forceinline__ double x4_d(double x) { return dpp_d<0x141>(x); }   // row_half_mirror
-__device__ __forceinline__ double x8_d(double x) { return dpp_d<0x140>(x); }   // row_mirror
-// pw16 over the row's 16 lanes (lane = column), result in every lane
-__device__ __forceinline__ double row_pw16(double x) {
-  x = x + x1_d(x);
-  x = x + x2_d(x);
-  x = x + x4_d(x);
-  x = x + x8_d(x);
-  return x;
-}
-__device__ __forceinline__ double row_max16(double x) {
-  x = dmax(x, x1_d(x));
-  x = dmax(x, x2_d(x));
-  x = dmax(x, x4_d(x));
-  x = dmax(x, x8_d(x));
-  return x;
-}
-__device__ __forceinline__ int row_max16_i(int x) {
-  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true));
-  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true));
-  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, true));
-  x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, true));
-  return x;
-}
-__device__ __forceinline__ double bperm_d(int addr, double x) {
-  const long long b = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
-  const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-
-struct FzLds {
-  const double *Bs, *c0, *cb, *Q, *w, *sd0, *sden, *scb, *base, *bself, *lden;
-  const int *dl, *tix, *nt, *koff, *boff, *dpos;
-};
-
-// Per-wave row data of the current tile in LDS (row = customer within the
-// tile): Y2 per view, table, uniform.  Lanes read rows grp + 4 r by broadcast.
-struct FzRows {
-  double *y2;     // [V][16]
-  double *u;      // [16]
-  int *p0;        // [16]
-};
-
-// View v of one tile: MFMA, then lp in registers (in place of the
-// accumulators), the view's marginal into s_new and its table contributions
-// into sp.  The four rows a lane holds are processed together (independent
-// chains for the one wave on its SIMD to overlap).  The own dish's coefficients with the
-// customer removed come from per-dish LDS tables (coef() split into its
-// customer-independent parts, same operations), log(denominator) per view
-// likewise, leaving one log, NT + 1 exps and one division per row.
-__device__ __forceinline__ mvc_d4 rot4(mvc_d4 x) { return (mvc_d4){x[1], x[2], x[3], x[0]}; }
-template <int NT, int SPPT, int RP>
-__device__ __forceinline__ void fz_view(const Sweep &A, const FzLds &L, const FzRows &R, int v, int T,
-                                        const mvc_d2 *cur, const mvc_d2 *nxt, mvc_d2 (&ring)[RP], int alive4,
-                                        mvc_d4 &s_new, mvc_d4 (&sp)[MVC_FZ_TB], int oz) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
-  const int V = P.V;
-  mvc_d4 acc[4];                                   // blocks t >= NT unused
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
-  lpview_tile_mfma<NT, SPPT, RP>(cur, nxt, SPPT, L.Bs + L.boff[v] + lane, ring, acc);
-  const int koff = L.koff[v], K = L.koff[v + 1] - koff;
-  const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-  const double cnew = A.cnew[v];
-  // per-dish / per-table LDS reads through an opaque per-tile zero: they are
-  // tile-invariant, and hoisted out of the tile loop they would pin registers
-  const double *Lc0 = L.c0 + oz, *Lcb = L.cb + oz, *Lw = L.w + oz;
-  const int *Ltix = L.tix + oz;
-#ifdef FZ_ABL_EPI
-#pragma unroll
-  for (int t = 0; t < NT; ++t) asm volatile("" : "+v"(acc[t]));
-  if (false)
-#endif
-  {
-  // the four rows of this lane are independent: every step below runs on all
-  // four at once (instruction-level parallelism at one wave per SIMD)
-  double hy[4], hr[4], w0[4], sv[4];
-  int j0[4], l0p[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int row = grp + 4 * r;
-    const double y2 = R.y2[v * 16 + row];
-    const int k0 = Ltix[R.p0[row] * V + v];        // Koff[v] + own dish
-    const bool alive = (alive4 >> r) & 1;
-    hy[r] = 0.5 * y2;
-    hr[r] = (-0.5 * y2) / tau;
-    j0[r] = k0 - koff;
-    l0p[r] = L.dl[k0] - (alive ? 0 : 1);
-    double w = (double)l0p[r] - sigma;
-    if (w < 0.0) w = 0.0;
-    w0[r] = (l0p[r] > 0) ? w : -1.0;
-    // the own dish with the customer removed (computed in every lane; kept
-    // by the lane whose column and block hold j0)
-    double Gs = acc[0][r];
-#pragma unroll
-    for (int t = 1; t < NT; ++t)
-      if ((j0[r] >> 4) == t) Gs = acc[t][r];
-    const double Gp = Gs - y2;
-    const double Qp = (L.Q[k0] - 2.0 * Gs) + y2;
-    const double c0s = L.sd0[k0] - (0.5 * Qp) / L.sden[k0];
-    sv[r] = __builtin_fma(Gp + hy[r], L.scb[k0], c0s) + hr[r];
-  }
-  double wt[NT][4], m[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) m[r] = -MVC_PM_INF;
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-    const int j = 16 * t + col;
-    const int kc = koff + min(j, K - 1);
-    const double cbj = Lcb[kc], c0j = Lc0[kc], wj = j < K ? Lw[kc] : -1.0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double fr = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
-      acc[t][r] = (j == j0[r]) ? sv[r] : fr;       // lp
-      wt[t][r] = (j == j0[r]) ? w0[r] : wj;
-      if (wt[t][r] >= 0.0 && acc[t][r] > m[r]) m[r] = acc[t][r];
-    }
-  }
-  double lfn[4], cs[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = row_max16(m[r]);
-    lfn[r] = cnew + hr[r];
-    if (lfn[r] > m[r]) m[r] = lfn[r];
-    cs[r] = 0.0;
-  }
-#pragma unroll
-  for (int t = 0; t < NT; ++t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double e = mvc_exp_sk(wt[t][r] >= 0.0 ? acc[t][r] - m[r] : 0.0);
-      if (wt[t][r] >= 0.0) cs[r] = cs[r] + wt[t][r] * e;
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    double S = row_pw16(cs[r]);
-    const int Kact = K - ((l0p[r] == 0) ? 1 : 0);
-    double wn = alpha + (double)Kact * sigma;
-    if (wn < 0.0) wn = 0.0;
-    S = S + wn * mvc_exp_sk(lfn[r] - m[r]);
-    const int di = 2 * v + (((alive4 >> r) & 1) ? 0 : 1);
-    const double lm = L.dpos[di] ? (m[r] + mvc_log_nb(S)) - L.lden[di] : lfn[r];
-    s_new[r] = s_new[r] + lm;
-  }
-  }
-  // table scores: sp[tb][r] += lp[row][dish_v(16 tb + col)] (row lanes only).
-  // Branch-free over all MVC_FZ_TB blocks: padding positions p >= T hold
-  // -inf, which the (finite) lp leaves at -inf.
-#ifdef FZ_ABL_GATHER
-#pragma unroll
-  for (int t = 0; t < NT; ++t) asm volatile("" :: "v"(acc[t]));
-  if (false)
-#endif
-#pragma unroll
-  for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
-    const int p = min(16 * tb + col, T - 1);
-    const int jj = Ltix[p * V + v] - koff;
-    const int addr = ((lane & 48) | (jj & 15)) << 2;
-    const int ts = jj >> 4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      double val = bperm_d(addr, acc[0][r]);
-#pragma unroll
-      for (int t = 1; t < NT; ++t) {
-        const double x = bperm_d(addr, acc[t][r]);
-        if (ts == t) val = x;
-      }
-      sp[tb][r] = sp[tb][r] + val;
-    }
-  }
-}
-
-// View pattern of a fused kernel instance: bits 0-3 = V, bits 4 + 2 v .. =
-// NT_v - 1 (dish blocks of 16 in view v).  Views run in order, unrolled at
-// compile time, so the tile is straight-line code (no joins between views
-// with different NT, which cost the register allocator ~60 VGPRs).
 __host__ __device__ constexpr int fz_pat_v(uint32_t pat) { return (int)(pat & 15u); }
 __host__ __device__ constexpr int fz_pat_nt(uint32_t pat, int v) { return (int)((pat >> (4 + 2 * v)) & 3u) + 1; }
-template <int SPPT, int RP, uint32_t PAT, int VI>
-__device__ __forceinline__ void fz_views(const Sweep &A, const FzLds &L, const FzRows &R, int T,
-                                         const mvc_d2 *ybase, size_t vstride, size_t tcur, size_t tnext,
-                                         mvc_d2 (&ring)[RP], int alive4, mvc_d4 &s_new, mvc_d4 (&sp)[MVC_FZ_TB],
-                                         int oz) {
-  if constexpr (VI < fz_pat_v(PAT)) {
-    const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
-    const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
-    fz_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, R, VI, T, cur, nxt, ring, alive4, s_new, sp, oz);
-    fz_views<SPPT, RP, PAT, VI + 1>(A, L, R, T, ybase, vstride, tcur, tnext, ring, alive4, s_new, sp, oz);
-  }
-}
 
-template <int SPPT, int RP, uint32_t PAT>
-__global__ __launch_bounds__(MVC_FZ_THREADS, 1) void mvc_par_zfused_kernel(Sweep A, int *discard) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const ParState &P = A.P;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
-  const int col = lane & 15, grp = lane >> 4;
-  constexpr int V = fz_pat_v(PAT);
-  const int KC = P.KC, TC = P.TC, n = P.n, D = P.D;
-  const int T = __builtin_amdgcn_readfirstlane(A.T);
-  constexpr int SP = 2 * SPPT;
-  // ---- LDS: S1 B-fragments of every view, per-dish and per-table tables,
-  // per-wave row data
-  int *s_koff = (int *)smem;                                   // [V+1]
-  int *s_boff = s_koff + V + 1;                                // [V+1] (doubles)
-  int *s_dpos = s_boff + V + 1;                                // [2V]
-  double *s_lden = (double *)(smem + ((4 * (4 * (size_t)V + 2) + 15) & ~(size_t)15));   // [2V]
-  if (tid <= V) {
-    s_koff[tid] = A.Koff[tid];
-    int acc = 0;
-    for (int u = 0; u < tid; ++u) acc += SP * 64 * fz_pat_nt(PAT, u);
-    s_boff[tid] = acc;
-  }
-  if (tid < 2 * V) {
-    const int v = tid >> 1, dead = tid & 1;
-    const double denom = P.hyper[V + v] + (double)(P.Ltot[v] - dead);
-    s_dpos[tid] = !(denom <= 0.0);
-    s_lden[tid] = !(denom <= 0.0) ? mvc_log(denom) : 0.0;
-  }
-  __syncthreads();
-  const int sumK = s_koff[V];
-  const int nB = s_boff[V];
-  double *Bs = s_lden + 2 * V;                                  // 16 B aligned
-  double *f_c0 = Bs + nB, *f_cb = f_c0 + sumK, *f_Q = f_cb + sumK, *f_w = f_Q + sumK;
-  double *f_sd0 = f_w + sumK, *f_sden = f_sd0 + sumK, *f_scb = f_sden + sumK;
-  double *f_base = f_scb + sumK, *f_bself = f_base + 16 * MVC_FZ_TB;
-  double *f_rows = f_bself + 16 * MVC_FZ_TB;                   // per wave [(V + 1) * 16] doubles + [16] ints
-  constexpr int rows_d = (V + 1) * 16 + 8;
-  int *f_dl = (int *)(f_rows + (size_t)BW * rows_d);
-  int *f_tix = f_dl + sumK, *f_nt = f_tix + 16 * MVC_FZ_TB * V;
-  {
-    const mvc_d2 *src = (const mvc_d2 *)A.S1t;
-    mvc_d2 *dst = (mvc_d2 *)Bs;
-    for (int e = tid; e < nB / 2; e += blockDim.x) dst[e] = src[e];
-  }
-  const double sg = P.hyper[3 * V + 1], ag = P.hyper[3 * V];
-  for (int k = tid; k < sumK; k += blockDim.x) {
-    int v = 0;
-    while (v + 1 < V && s_koff[v + 1] <= k) ++v;
-    const int j = k - s_koff[v];
-    const double tau = P.hyper[v];
-    f_c0[k] = P.c0[v * KC + j];
-    f_cb[k] = P.cb[v * KC + j];
-    f_Q[k] = P.Q[v * KC + j];
-    const int l = P.d_l[v * KC + j];
-    double wl = (double)l - P.hyper[2 * V + v];
-    if (wl < 0.0) wl = 0.0;
-    f_w[k] = l > 0 ? wl : -1.0;
-    f_dl[k] = l;
-    // coef(d_n - 1, Q', tau, L2pt, D) = sd0 - (0.5 Q') / sden, cb = scb
-    const int n_ = P.d_n[v * KC + j] - 1;
-    const double a = tau + (double)n_;
-    const double b = tau + (double)(n_ + 1);
-    f_sd0[k] = (double)D * ((-0.5 * A.L2pt[v]) - 0.5 * mvc_log(b / a));
-    f_sden[k] = (tau * a) * b;
-    f_scb[k] = 1.0 / (tau * b);
-  }
-  for (int p = tid; p < 16 * MVC_FZ_TB; p += blockDim.x) {
-    const int np = p < T ? P.n_t[p] : 0;
-    f_nt[p] = np;
-    f_base[p] = (p < T && np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
-    const int np0 = np - 1;
-    const double m0 = (double)np0 - sg;
-    f_bself[p] = (p < T && np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
-    for (int v = 0; v < V; ++v) f_tix[p * V + v] = s_koff[v] + (p < T ? P.dish[v * TC + p] : 0);
-  }
-  __syncthreads();
-  const FzLds L{Bs, f_c0, f_cb, f_Q, f_w, f_sd0, f_sden, f_scb, f_base, f_bself, s_lden,
-                f_dl, f_tix, f_nt, s_koff, s_boff, s_dpos};
-  double *wrows = f_rows + (size_t)w * rows_d;
-  const FzRows R{wrows, wrows + V * 16, (int *)(wrows + (V + 1) * 16)};
-  const int T_ne = A.status[V + 3];
-  const double snew_alive = mvc_log(ag + sg * (double)T_ne);
-  const double snew_dead = mvc_log(ag + sg * (double)(T_ne - 1));
-
-  const int ntile = (n + 15) >> 4;
-  const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
-  if (gw >= ntile) return;                         // whole wave: no barriers below
-  const int nmy = (ntile - gw + NWT - 1) / NWT;
-  const size_t vstride = (size_t)ntile * SPPT * 64;  // mvc_d2 per view in yt
-  const mvc_d2 *ybase = (const mvc_d2 *)A.yt + lane;
-  auto toff = [&](int m) -> size_t {               // offset of my m-th tile (clamped) within a view
-    return (size_t)(gw + min(m, nmy - 1) * NWT) * SPPT * 64;
-  };
-  mvc_d2 ring[RP];
-  {
-    const mvc_d2 *c0p = ybase + toff(0);
-#pragma unroll
-    for (int u = 0; u < RP; ++u) ring[u] = c0p[u * 64];
-  }
-  // row data (table, Y2 per view) of the tiles, loaded one tile ahead and
-  // unconditionally: a load under a lane-dependent branch makes hipcc wait
-  // vmcnt(0), which would drain the A-fragment ring every tile
-  constexpr int NQ = (V + 3) / 4;
-  auto row_load = [&](int m, int &pz, double (&y2v)[NQ]) {
-    const int ic = min((gw + min(m, nmy - 1) * NWT) * 16 + col, n - 1);
-    pz = P.z[ic];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) y2v[q] = A.Y2[(size_t)min(4 * q + grp, V - 1) * n + ic];
-  };
-  int pz_n;
-  double y2v_n[NQ];
-  row_load(0, pz_n, y2v_n);
-  int *const dslot = discard + lane;
-  for (int m = 0; m < nmy; ++m) {
-    const int li0 = (gw + m * NWT) * 16;
-    {
-      const int pz = pz_n;
-      double y2v[NQ];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) y2v[q] = y2v_n[q];
-      row_load(m + 1, pz_n, y2v_n);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q)
-        if (4 * q + grp < V) R.y2[(4 * q + grp) * 16 + col] = y2v[q];
-      if (grp == 0) R.p0[col] = pz;
-      if (grp == 1) R.u[col] = mvc_uniform(A.seed, (uint32_t)min(li0 + col, n - 1), A.sweep, A.chain, MVC_TAG_Z);
-    }
-    wave_lds_sync();
-    int alive4 = 0;
-    mvc_d4 s_new, sp[MVC_FZ_TB];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int p0 = R.p0[grp + 4 * r];
-      const bool alive = (f_nt[p0] - 1) > 0;
-      alive4 |= alive ? (1 << r) : 0;
-      s_new[r] = alive ? snew_alive : snew_dead;
-#pragma unroll
-      for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
-        const int p = 16 * tb + col;
-        sp[tb][r] = (p == p0) ? f_bself[p] : f_base[p];
-      }
-    }
-    int oz = 0;
-    asm volatile("" : "+v"(oz));
-    fz_views<SPPT, RP, PAT, 0>(A, L, R, T, ybase, vstride, toff(m), toff(m + 1), ring, alive4, s_new, sp, oz);
-    // ---- draw (oracle resample_customer), the four rows at once
-    int pv = -1;
-#ifdef FZ_ABL_DRAW
-#pragma unroll
-    for (int tb = 0; tb < MVC_FZ_TB; ++tb) asm volatile("" :: "v"(sp[tb]), "v"(s_new));
-    pv = R.p0[grp + 4 * col];
-    if (false)
-#endif
-    {
-      double M[4], tot[4], C[MVC_FZ_TB][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double mx = -MVC_PM_INF;
-#pragma unroll
-        for (int tb = 0; tb < MVC_FZ_TB; ++tb)
-          if (16 * tb + col < T && sp[tb][r] > mx) mx = sp[tb][r];
-        M[r] = row_max16(mx);
-        if (s_new[r] > M[r]) M[r] = s_new[r];
-        tot[r] = 0.0;
-      }
-#pragma unroll
-      for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool in = 16 * tb + col < T && sp[tb][r] != -MVC_PM_INF;
-          const double e = mvc_exp_sk(in ? sp[tb][r] - M[r] : 0.0);
-          sp[tb][r] = in ? e : 0.0;                  // weights in place
-        }
-      }
-#pragma unroll
-      for (int tb = 0; tb < MVC_FZ_TB; ++tb) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          tot[r] = tot[r] + row_pw16(sp[tb][r]);     // blocks past T add +0.0: exact
-          C[tb][r] = tot[r];
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double W = mvc_exp_sk(s_new[r] - M[r]) + tot[r];
-        double rr = R.u[grp + 4 * r] * W;
-        const bool birth = !(rr < tot[r]);
-        int bsel = 0;
-        double prev = 0.0, x = sp[0][r];
-#pragma unroll
-        for (int tb = MVC_FZ_TB - 1; tb >= 0; --tb)
-          if (rr < C[tb][r]) { bsel = tb; prev = tb > 0 ? C[tb - 1][r] : 0.0; x = sp[tb][r]; }
-        rr = rr - prev;
-        // pw16 descent: every lane follows the path towards its own column
-        const double t1 = x1_d(x), l1 = x + t1;
-        const double t2 = x2_d(l1), l2 = l1 + t2;
-        const double t4 = x4_d(l2), l4 = l2 + t4;
-        const double t8 = x8_d(l4);
-        bool on = !birth;
-        auto step = [&](double own, double other, int h) {
-          const bool hi = (col & h) != 0;
-          const double Lh = hi ? other : own, Rh = hi ? own : other;
-          const bool right = !(Rh == 0.0 || rr < Lh);
-          if (right != hi) on = false;
-          if (right) rr = rr - Lh;
-        };
-        step(l4, t8, 8);
-        step(l2, t4, 4);
-        step(l1, t2, 2);
-        step(x, t1, 1);
-        const int pk = row_max16_i(on ? 16 * bsel + col : -1);
-        if (col == r) pv = pk;                       // lane (col = r, grp) stores row grp + 4 r
-      }
-    }
-    const int li = li0 + grp + 4 * col;
-    int *dst = (col < 4 && li < n) ? A.choice + li : dslot;
-    *dst = pv;
-    wave_lds_sync();                               // row data reused by the next tile
-  }
-}
 
 // ---------------------------------------------------------------------------
 // All-views lp producer: the per-view producers' work in ONE launch.  Every
 // view's S1 B-fragments sit in LDS (one block per CU); each wave takes a
 // 16-customer tile through all views in order (view pattern PAT fixed at
-// compile time, as the fused kernel), so MFMA-heavy views (K_v = 64) and
+// compile time, see MVC_FZ_PATS), so MFMA-heavy views (K_v = 64) and
 // stream-heavy ones (K_v <= 16) alternate inside each wave and the two waves
 // of a SIMD overlap them; one launch instead of V removes V - 1 prologues and
 // tails.  Same outputs and arithmetic as mvc_par_lpview_kernel (lp rows and
@@ -1609,66 +1165,8 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
   if (l0p > 0 && sv > m) m = sv;
   const double lfn = cnew + hself;
   if (lfn > m) m = lfn;
-  double out = m;
-  if (A.lmv) {
-    // the draw's view term (mvc_par_zdraw_reg_kernel / zview_sum, oracle
-    // eval_view_seq) here, where the lp values are still in the accumulators:
-    // column partials w_j exp(lp_j - m) over ascending dish blocks (lane
-    // column = j & 15), pw16 over the row's 16 lanes, then the new dish and
-    // lm_v.  Same operations in the same order, so the same bits; the draw
-    // then skips its exps and row reads of the view pass.
-    const double sigma = P.hyper[2 * V + v], alpha = P.hyper[V + v];
-    double *w0s = mrest + 16, *Ss = mrest + 32;
-    double w0 = (double)l0p - sigma;
-    if (w0 < 0.0) w0 = 0.0;
-    if (!(l0p > 0)) w0 = -1.0;
-    if (lane < 16) { mrest[col] = m; selfG[col] = sv; w0s[col] = w0; }
-    wave_lds_sync();
-    double mr[4], svr[4], w0r[4], cs[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      mr[r] = mrest[grp + 4 * r];
-      svr[r] = selfG[grp + 4 * r];
-      w0r[r] = w0s[grp + 4 * r];
-      cs[r] = 0.0;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int j = 16 * t + col;
-      const int kc = koff + min(j, K - 1);
-      const double c0j = L.c0[kc], cbj = L.cb[kc];
-      const int lj = L.dl[kc];
-      double wj = (double)lj - sigma;
-      if (wj < 0.0) wj = 0.0;
-      if (!(lj > 0)) wj = -1.0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const bool own = j == j0[r];
-        const double val = own ? svr[r] : __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
-        const double term = __builtin_fmax(own ? w0r[r] : wj, 0.0) * mvc_exp_le0(val - mr[r]);
-        if (j < K) cs[r] = cs[r] + term;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {   // pw16 over the row's 16 lanes (oracle pw16 association), lane col 0
-      double x = cs[r];
-      x = x + down_d<1>(x);
-      x = x + down_d<2>(x);
-      x = x + down_d<4>(x);
-      x = x + down_d<8>(x);
-      if (col == 0) Ss[grp + 4 * r] = x;
-    }
-    wave_lds_sync();
-    double S = Ss[col];
-    const int Kact = K - ((l0p == 0) ? 1 : 0);
-    double wn = alpha + (double)Kact * sigma;
-    if (wn < 0.0) wn = 0.0;
-    S = S + wn * mvc_exp_le0(lfn - m);
-    const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
-    out = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
-  }
   double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
-  *dm = out;
+  *dm = m;
   wave_lds_sync();
 }
 
@@ -2283,32 +1781,24 @@ class ParallelSampler : public Sampler {
   bool force_generic = false;
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
-  size_t lpb_batch = 0;           // MVC_LPB_BATCH: customers per phase-1 batch (0: kLpbBudget)
-  bool no_fused = true;           // MVC_FUSED=1: the fused phase-1 kernel where it applies (experimental: slower today)
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
   int shard_rank = 0, shard_world = 1;
   int32_t *shard_exch = nullptr;
-  void (*shard_cb)(void *) = nullptr;
+  int (*shard_cb)(void *) = nullptr;
   void *shard_user = nullptr;
   bool no_lpall = false;          // MVC_LPALL=0: per-view producer launches even where the all-views producer applies
-  int fz_waves = MVC_FZ_THREADS / 64;   // waves per block of the fused kernel (MVC_FZ_WAVES: fewer)
-  int *fz_discard = nullptr;      // [64] the fused kernel's per-lane discard slots
   int n_cu = 256;
   bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
-  // MVC_LMV=1: the all-views producer forms the view terms lm_v for the
-  // register draw (bitwise the same chain; measured slower at configs[3]:
-  // producer 1.10 -> 1.30 ms, draw 0.44 -> 0.32 ms, profiles/r2t_lmv_ab.json)
-  bool no_lmv = true;
   bool early_mh_off = false;      // MVC_EARLY_MH=0: the MH launched only after the host has read the repair
   bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
   int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
-  int team_w = 1;                 // waves per customer in the run kernel (MVC_TEAM; default by V)
   bool use_wide = true;           // MVC_WIDE=0: global-scratch run kernel speculates one customer per wave
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
+  bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
 
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
@@ -2327,9 +1817,18 @@ class ParallelSampler : public Sampler {
   // sampler on the same device and data whose device copies of y, Y2 and the
   // MFMA tiling this one reads instead of making its own (ChainSet).
   ParallelSampler(const mvc_config &cf, const double *yh, const ParallelSampler *share) { init(cf, yh, share); }
+  // data already on the device (mvc_sampler_create_synthetic): takes ownership
+  ParallelSampler(const mvc_config &cf, DeviceData &&dd) {
+    y = dd.y;
+    Y2 = dd.Y2;
+    dd.y = dd.Y2 = nullptr;
+    tau0 = dd.tau0;
+    init(cf, nullptr, nullptr, true);
+  }
 
   bool owns_y = true;
-  void init(const mvc_config &cf, const double *yh_in, const ParallelSampler *share) {
+  std::vector<double> tau0;        // device data: initial tau_v per view (host data: from the views)
+  void init(const mvc_config &cf, const double *yh_in, const ParallelSampler *share, bool dev_data = false) {
     cfg = cf;
     n = cf.n; V = cf.n_views; D = cf.dim;
     // initial capacities (mvc_config.table_cap / dish_cap); a birth beyond
@@ -2357,6 +1856,9 @@ class ParallelSampler : public Sampler {
       Y2 = share->Y2;
       yt = share->yt;
       SP = share->SP;
+      tau0 = share->tau0;
+    } else if (dev_data) {
+      // y and Y2 were made on the device (owned from here on)
     } else {
       y = dmalloc<double>((size_t)V * n * D);
       Y2 = dmalloc<double>((size_t)V * n);
@@ -2394,11 +1896,7 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_LPV_BPC")) lpv_bpc = std::max(0, std::min(8, atoi(e)));
     const char *zl = getenv("MVC_ZDRAW_LDS");
     force_zdraw_lds = zl && zl[0] == '1';
-    if (const char *e = getenv("MVC_LPB_BATCH")) lpb_batch = (size_t)std::max(0L, atol(e)) / 64 * 64;
-    if (const char *e = getenv("MVC_FUSED")) no_fused = e[0] != '1';
     if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
-    if (const char *e = getenv("MVC_FZ_WAVES")) fz_waves = std::max(1, std::min(MVC_FZ_THREADS / 64, atoi(e)));
-    fz_discard = dmalloc<int>(64);
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
@@ -2415,11 +1913,8 @@ class ParallelSampler : public Sampler {
     lpall_attr<4, 4>();
     lpall_attr<8, 8>();
     lpall_attr<16, 8>();
-    fused_attr<4, 4>();
-    fused_attr<8, 8>();
-    fused_attr<16, MVC_FZ_RP16>();
     // (instance 2 runs the global-scratch layout only: no dynamic LDS)
-  for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<1>})
+    for (const void *f : {(const void *)mvc_seq_run_kernel<0>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {
@@ -2431,22 +1926,13 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
-    // MVC_TEAM=2/4: a customer's views split over a team of waves (fewer
-    // customers per step, each evaluated with more lanes).  Measured slower
-    // than one wave per customer at configs[1] and configs[3] cold starts and
-    // 4 % faster on the D = 1 literal, so off by default.
-    team_w = 1;
-    if (const char *e = getenv("MVC_TEAM")) {
-      const int t = atoi(e);
-      team_w = (t >= 4 && V >= 4) ? 4 : (t >= 2 && V >= 2) ? 2 : 1;
-    }
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
+    if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
     if (const char *e = getenv("MVC_WIDE")) use_wide = e[0] != '0';
     if (const char *e = getenv("MVC_EARLY_MH")) early_mh_off = e[0] == '0';
-    if (const char *e = getenv("MVC_LMV")) no_lmv = e[0] != '1';
     if (const char *e = getenv("MVC_RUN_LDS")) force_global = e[0] == '0';
     chains.resize(cf.n_chains);
-    for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], (uint32_t)(cf.first_chain + c), yh_in);
+    for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], chain_gid(cf, c), yh_in);
     MVC_HIP(hipStreamSynchronize(stream));
   }
 
@@ -2566,7 +2052,7 @@ class ParallelSampler : public Sampler {
     if (owns_y)
       for (void *p : {(void *)y, (void *)Y2, (void *)yt})
         if (p) hipFree(p);
-    for (void *p : {(void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2, (void *)fz_discard, (void *)vmax,
+    for (void *p : {(void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2, (void *)vmax,
                     (void *)zsc})
       if (p) hipFree(p);
     if (st_host) hipHostFree(st_host);
@@ -2615,7 +2101,13 @@ class ParallelSampler : public Sampler {
   void init_chain(Chain &c, uint32_t gid, const double *yh) {
     c.gid = gid;
     alloc_chain(c);
-    const InitState S = draw_initial_state(yh, n, V, D, cfg.seed, gid);
+    InitState S;
+    if (yh) {
+      S = draw_initial_state(yh, n, V, D, cfg.seed, gid);
+    } else {   // device data: the same draws, tau_v from the device's column sums
+      S = draw_initial_draws(n, V, cfg.seed, gid);
+      S.tau = tau0;
+    }
     // multiview_gibbs.cpp:12-98 in dense-position / live-list form
     std::vector<int32_t> nt(4, 0);
     for (int i = 0; i < n; ++i) nt[S.table[i]]++;
@@ -2788,7 +2280,6 @@ class ParallelSampler : public Sampler {
     A.S1t = c.S1t;
     A.SP = SP;
     A.vmax = vmax;
-    A.lmv = 0;
     A.T = c.T;
     A.sumK = sumK(c);
     A.seed = cfg.seed;
@@ -2829,18 +2320,6 @@ class ParallelSampler : public Sampler {
   }
 
   template <int SPPT, int RP>
-  void launch_fused(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A) {
-    switch (pat) {
-#define X(p)                                                                                             \
-  case p:                                                                                                \
-    hipLaunchKernelGGL((mvc_par_zfused_kernel<SPPT, RP, p>), grid, block, lds, stream, A, fz_discard); \
-    break;
-      MVC_FZ_PATS(X)
-#undef X
-      default: throw Error(MVC_ERR_STATE, "fused kernel: no instance for this view pattern");
-    }
-  }
-  template <int SPPT, int RP>
   void launch_lpall(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A, int b0, int nb) {
     double *disc = lpb + lpb_cap;
     switch (pat) {
@@ -2861,15 +2340,6 @@ class ParallelSampler : public Sampler {
     MVC_FZ_PATS(X)
 #undef X
   }
-  template <int SPPT, int RP>
-  static void fused_attr() {
-#define X(p)                                                                                              \
-  MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_zfused_kernel<SPPT, RP, p>,                           \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    MVC_FZ_PATS(X)
-#undef X
-  }
-
   void sweep_chain(Chain &c, uint32_t s) {
     Sweep A = make_sweep(c, s);
     const SeqArgs Q0 = make_seq(c, s);
@@ -2897,7 +2367,6 @@ class ParallelSampler : public Sampler {
     // batch: multiple of 64 customers, lp buffer <= kLpbBudget doubles
     const size_t per64 = (size_t)std::max(1, sk) * 64;
     size_t nb_max = std::max<size_t>(64, (kLpbBudget / per64) * 64);
-    if (lpb_batch) nb_max = std::min(nb_max, lpb_batch);
     const size_t nb_full = ((size_t)n + 63) / 64 * 64;
     const size_t nbatch_sz = std::min(nb_max, nb_full);
     const size_t need = (nbatch_sz / 64) * per64;
@@ -2906,11 +2375,10 @@ class ParallelSampler : public Sampler {
     // phase A on the two-kernel path needs the draw's LDS tables; beyond them
     // the repair's eval kernel evaluates the sweep from customer 0 instead
     const bool phaseA = use_zreg || zdraw_shared_bytes(V, c.T, sk) <= 160 * 1024;
-    // fused phase 1 (lp never leaves registers): T <= 64, K_v <= 64, every
-    // view's S1 B-fragments in LDS at once, fully unrolled k-step pairs
+    // the all-views producer: T <= 64, K_v <= 64, every view's S1
+    // B-fragments in LDS at once, fully unrolled k-step pairs
     size_t s1t_d = 0;
     for (int v = 0; v < V; ++v) s1t_d += (size_t)SP * 64 * ((c.K[v] + 15) / 16);
-    const size_t fz_lds = fused_shared_bytes(s1t_d, V, sk, fz_waves);
     const int spp = SP / 2;
     uint32_t fz_pat = (uint32_t)V;
     for (int v = 0; v < V && v < 4; ++v) fz_pat |= (uint32_t)(std::min(4, (c.K[v] + 15) / 16) - 1) << (4 + 2 * v);
@@ -2922,39 +2390,23 @@ class ParallelSampler : public Sampler {
       break;
       default: pat_ok = false;
     }
-    const bool use_fused = !no_fused && shard_world == 1 && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
-                           (spp == 4 || spp == 8 || spp == 16) && fz_lds <= 160 * 1024;
-    if (phaseA && !use_fused && need > lpb_cap) {   // the lp buffer only exists for the two-kernel path
+    if (phaseA && need > lpb_cap) {
       retire(lpb, sizeof(double) * (lpb_cap + 64));
       lpb_cap = need;
       lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
     }
     bool zpath_lpall = false;
     timers.begin("zresample", &e0);
-    if (phaseA && use_fused) {
-      const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / fz_lds));
-      const int ntile = (n + 15) / 16;
-      const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + fz_waves - 1) / fz_waves));
-      const dim3 blk(64 * fz_waves);
-      switch (spp) {
-        case 4: launch_fused<4, 4>(fz_pat, dim3(grid), blk, fz_lds, A); break;
-        case 8: launch_fused<8, 8>(fz_pat, dim3(grid), blk, fz_lds, A); break;
-        default: launch_fused<16, MVC_FZ_RP16>(fz_pat, dim3(grid), blk, fz_lds, A); break;
-      }
-      MVC_HIP(hipGetLastError());
-    }
     // this rank's customers [lo, hi) (the whole chain unless sharded)
     const size_t S = (size_t)shard_len(n, shard_world);
     const size_t lo = std::min((size_t)n, (size_t)shard_rank * S), hi = std::min((size_t)n, lo + S);
-    for (size_t b0 = lo; phaseA && !use_fused && b0 < hi; b0 += nbatch_sz) {
+    for (size_t b0 = lo; phaseA && b0 < hi; b0 += nbatch_sz) {
       const int nb = (int)std::min(nbatch_sz, hi - b0);
       hipEvent_t el = nullptr, ed = nullptr;
       timers.begin("lp", &el);
       const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, 8);
       const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                              (spp == 4 || spp == 8 || spp == 16) && lpa_lds <= 160 * 1024;
-      // the view terms in the producer when the register draw follows (A.lmv)
-      A.lmv = (use_lpall && use_zreg && !no_lmv) ? 1 : 0;
       if (use_lpall) {
         const int ntile = (nb + 15) / 16;
         const int grid = std::max(1, std::min(n_cu, (ntile + 7) / 8));
@@ -3039,10 +2491,13 @@ class ParallelSampler : public Sampler {
         MVC_HIP(hipMemcpyAsync(shard_exch + lo, c.choice + lo, (hi - lo) * sizeof(int32_t), hipMemcpyDeviceToDevice,
                                stream));
       MVC_HIP(hipStreamSynchronize(stream));
-      shard_cb(shard_user);
+      // a failed exchange stops the sweep here: nothing has read the buffer
+      // and phase A changed no chain state (only choice / lp / vmax)
+      if (shard_cb(shard_user) != 0)
+        throw Error(MVC_ERR_CALLBACK, "set_shard: the all_gather callback reported failure; the sweep was not run");
       MVC_HIP(hipMemcpyAsync(c.choice, shard_exch, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, stream));
     }
-    zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (use_fused ? 8 : 0) | (zpath_lpall ? 16 : 0) |
+    zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) |
                       (use_big ? 64 : 0)) : 32;
     repair(c, s, phaseA);
   }
@@ -3063,16 +2518,17 @@ class ParallelSampler : public Sampler {
       const int kgrow = attempt < 2 ? std::max(8, kmax / 2) : 4;
       const int tgrow = attempt < 2 ? std::max(64, T / 2) : 16;
       L.ks = (kmax + kgrow + 7) / 8 * 8;
-      L.ts = (T + tgrow + 15) / 16 * 16;
+      L.ts = (T + tgrow + 63) / 64 * 64;   // whole 64-table chunks (the lane-column evaluation's e[] scratch)
       L.s1 = s1 ? 1 : 0;
       L.cache_dbl = seq_lds_cache(V, D, L.ks, L.ts, s1);
       L.stride = seq_lds_stride(V, D, L.ks, L.ts);
       const int64_t room = (int64_t)kSeqLdsBudget / 8 - L.cache_dbl;
-      const int cap = std::min(run_waves, kSeqRunWaves / team_w);   // customers per step
+      const int cap = run_waves;   // customers per step
       L.nws = room > 0 ? (int)std::min<int64_t>(cap, room / L.stride) : 0;
       if (L.nws >= std::min(cap, s1 ? 4 : 2)) {
         L.lds = 1;
-        L.tw = team_w;
+        L.tw = 1;
+        L.lc = (use_lc && s1 && L.ts <= 64 * kLcChunks) ? 1 : 0;
         // the staged-row ring in what is left: a power of two >= 2 nws customers
         const int64_t slot = seq_ring_slot(V, D);
         const int64_t left = room - (int64_t)L.nws * L.stride;
@@ -3086,6 +2542,7 @@ class ParallelSampler : public Sampler {
       }
     }
     L.lds = 0;   // per-wave global scratch (SeqScratch(A, w)): capacity-sized, never restrides
+    L.lc = 0;
     // the whole block on one customer (seq_resample_wide): the dish / table
     // lists are long here, and where the state outgrows the LDS nearly every
     // customer moves (cold-start transients), so speculation buys little
@@ -3126,7 +2583,7 @@ class ParallelSampler : public Sampler {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
         else
-          hipLaunchKernelGGL(L.tw == 1 ? mvc_seq_run_kernel<0> : L.lds ? mvc_seq_run_kernel<1> : mvc_seq_run_kernel<2>,
+          hipLaunchKernelGGL(L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
                              dim3(1), dim3(kSeqRunThreads),
                              L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
                              stream, Q, L);
@@ -3167,7 +2624,7 @@ class ParallelSampler : public Sampler {
     }
     timers.end("repair", e1);
 #ifdef MVC_RUN_PROF
-    fprintf(stderr, "runprof moves %d iters %llu | view %.1f tables %.1f exp+blocks %.1f select %.1f | commit %.1f spec %.1f decide %.1f (us per iter)\n",
+    fprintf(stderr, "runprof moves %d iters %llu | lc: views %.2f tables %.2f weights+draw %.2f | commit %.2f check %.2f spec %.2f decide %.2f (us per iter)\n",
             rs_host->moves, rs_host->prof[7], rs_host->prof[0] * 0.01 / std::max(1ull, rs_host->prof[7]),
             rs_host->prof[1] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[2] * 0.01 / std::max(1ull, rs_host->prof[7]),
             rs_host->prof[3] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[4] * 0.01 / std::max(1ull, rs_host->prof[7]),
@@ -3254,7 +2711,8 @@ class ParallelSampler : public Sampler {
 
   void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
 
-  bool set_shard(int rank, int world, int32_t *exch, void (*cb)(void *), void *user) override {
+  bool set_shard(int rank, int world, int32_t *exch, int (*cb)(void *), void *user) override {
+    if (chains.size() > 1) return false;   // one chain per sharded handle (mvc.h)
     if (world < 1 || rank < 0 || rank >= world || (world > 1 && (!exch || !cb)))
       throw Error(MVC_ERR_ARG, "set_shard: rank / world / exchange");
     synchronize();
@@ -3275,6 +2733,14 @@ class ParallelSampler : public Sampler {
     if (chain < 0 || chain >= (int)chains.size()) throw Error(MVC_ERR_ARG, "chain out of range");
     MVC_HIP(hipStreamSynchronize(stream));
     return chains[chain].P.z;
+  }
+
+  void copy_rows(int view, const int32_t *idx, int64_t m, double *out) override {
+    if (view < 0 || view >= V) throw Error(MVC_ERR_ARG, "copy_rows: view out of range");
+    for (int64_t r = 0; r < m; ++r)
+      if (idx[r] < 0 || idx[r] >= n) throw Error(MVC_ERR_ARG, "copy_rows: row index out of range");
+    MVC_HIP(hipStreamSynchronize(stream));
+    gather_rows(y, n, D, view, idx, m, out, stream);
   }
 
   void get_state(int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of, int32_t dish_cap,
@@ -3372,7 +2838,7 @@ class ParallelSampler : public Sampler {
 // its own stream, phase-A buffers and repair state, sharing the device copy
 // of the data; sweep() drives them from one host thread per chain, so one
 // chain's latency-bound repair (one CU) overlaps the others' work.  Chain c
-// keeps its global id first_chain + c, so every draw is the one the serial
+// keeps its global id chain_gid(cfg, c), so every draw is the one the serial
 // loop would make: the chains are bitwise the same.
 class ChainSet : public Sampler {
  public:
@@ -3385,8 +2851,21 @@ class ChainSet : public Sampler {
     for (int c = 0; c < cf.n_chains; ++c) {
       mvc_config one = cf;
       one.n_chains = 1;
-      one.first_chain = cf.first_chain + c;
+      one.first_chain = (int32_t)chain_gid(cf, c);
+      one.chain_stride = 1;
       subs.emplace_back(new ParallelSampler(one, yh.data(), c == 0 ? nullptr : subs[0].get()));
+    }
+    stream = subs[0]->stream;
+  }
+  ChainSet(const mvc_config &cf, DeviceData &&dd) {
+    cfg = cf;
+    for (int c = 0; c < cf.n_chains; ++c) {
+      mvc_config one = cf;
+      one.n_chains = 1;
+      one.first_chain = (int32_t)chain_gid(cf, c);
+      one.chain_stride = 1;
+      if (c == 0) subs.emplace_back(new ParallelSampler(one, std::move(dd)));
+      else subs.emplace_back(new ParallelSampler(one, nullptr, subs[0].get()));
     }
     stream = subs[0]->stream;
   }
@@ -3445,6 +2924,7 @@ class ChainSet : public Sampler {
     for (auto &s : subs) s->flush_saves();
   }
   const int32_t *device_labels(int chain) override { return at(chain).device_labels(0); }
+  void copy_rows(int view, const int32_t *idx, int64_t m, double *out) override { subs[0]->copy_rows(view, idx, m, out); }
   bool repair_stats(int chain, int32_t *out) override { return at(chain).repair_stats(0, out); }
   // timing: chain 0's timers (every chain runs the same kernels)
   void set_timing(bool on, bool coarse) override {
@@ -3459,6 +2939,12 @@ class ChainSet : public Sampler {
     return subs[0]->kernel_time(name, ms, launches);
   }
 };
+
+Sampler *make_parallel_sampler_device(const mvc_config &cfg, DeviceData &&dd) {
+  const char *e = getenv("MVC_CHAIN_THREADS");
+  if (cfg.n_chains > 1 && !(e && e[0] == '0')) return new ChainSet(cfg, std::move(dd));
+  return new ParallelSampler(cfg, std::move(dd));
+}
 
 Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views) {
   const char *e = getenv("MVC_CHAIN_THREADS");   // =0: one handle runs its chains one after another

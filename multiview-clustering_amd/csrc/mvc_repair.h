@@ -74,18 +74,19 @@ struct SeqLds {
   int64_t stride;       // doubles per wave
   int32_t ring;         // customers in the staged-row ring (power of 2, after the per-wave scratch; 0: none)
   int32_t pfn;          // customers prefetched into the ring per step
-  int32_t tw;           // waves per customer (1: seq_resample; 2, 4: seq_resample_team); nws customers per step
+  int32_t tw;           // waves per customer (1: seq_resample; kSeqRunWaves: seq_resample_wide); nws customers per step
+  int32_t lc;           // 1: the lane-column evaluation (seq_resample_lc; LDS layout with S1 cached, ts <= 512)
 };
 // ring slot: y rows [V][D], Y2 [V], z (as a double)
 __host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
 
 __host__ __device__ inline int64_t seq_lds_stride(int V, int D, int ks, int ts) {
-  // ... + ys [V][D] + Y2 [V] + (teams) lm_v [V] + member maxima [4]
+  // ... + ys [V][D] + Y2 [V] + lm_v [V] + member maxima [4] (unused by seq_resample)
   return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + V + 4;
 }
 __host__ __device__ inline int64_t seq_lds_cache(int V, int D, int ks, int ts, bool s1) {
   const int64_t ints = (int64_t)ts + (int64_t)V * ts + 2 * (int64_t)V * ks + 2 * V + 2;
-  return (ints + 1) / 2 + 6 * (int64_t)V * ks + ts + (s1 ? (int64_t)V * D * ks : 0);
+  return (ints + 1) / 2 + 7 * (int64_t)V * ks + ts + (s1 ? (int64_t)V * D * ks : 0);
 }
 
 struct SeqArgs {
@@ -205,18 +206,19 @@ __device__ __forceinline__ int pw16_select_seq(const double *x, double r) {
   return idx;
 }
 
-// pw16_select across a wave: lane l < 16 holds element l; r wave-uniform.
-// Levels by DPP row shifts (node c at offset h = x[c] + x[c + h], the pw16
-// association), descent left iff R == 0 || r < L.
-__device__ __forceinline__ int pw16_select_wave(double x, double r) {
+// pw16_select across a wave: lane base + l (l < 16, base a multiple of 16)
+// holds element l; r wave-uniform.  Levels by DPP row shifts (node c at
+// offset h = x[c] + x[c + h], the pw16 association), descent left iff R == 0
+// || r < L.
+__device__ __forceinline__ int pw16_select_wave(double x, double r, int base = 0) {
   const double l1 = x + down_d<1>(x);
   const double l2 = l1 + down_d<2>(l1);
   const double l3 = l2 + down_d<4>(l2);
   int lo = 0;
 #define MVC_PW16_DESCEND(VAL, H)                              \
   {                                                           \
-    const double a = readlane_d((VAL), lo);                   \
-    const double b = readlane_d((VAL), lo + (H));             \
+    const double a = readlane_d((VAL), base + lo);            \
+    const double b = readlane_d((VAL), base + lo + (H));      \
     if (!(b == 0.0 || r < a)) { r = r - a; lo = lo + (H); }   \
   }
   MVC_PW16_DESCEND(l3, 8)
@@ -602,244 +604,6 @@ __device__ int seq_resample(const SeqArgs &A, const SView &W, const Cust &C, int
     r = r - cprev;
     const double x = lane < 16 ? S.e[bsel * 16 + lane] : 0.0;
     pick = bsel * 16 + pw16_select_wave(x, r);
-  }
-  RUN_MARK(3);
-  return pick;
-}
-
-// seq_resample by a team of tw waves (run kernel, tw = 2 or 4): member r owns
-// views r, r + tw, ... (their lp, terms, marginals) and the 64-table chunks
-// q = r mod tw (scores, weights, block sums); member 0 draws.  The team
-// shares S (lp / aux / e / B per view / table; mv, K_act, lm_v, member
-// maxima).  Every quantity is the same operations in the same order as in
-// seq_resample, so the same bits.  Block-wide: every wave of the block calls
-// it (act = false: no customer, barriers only); three __syncthreads.
-// Returns the pick on member 0.
-__device__ int seq_resample_team(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
-                                 int r, int tw, bool act) {
-  const ParState &P = A.P;
-  const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
-  const int V = P.V, D = P.D, ts = W.ts, ks = W.ks, lps = S.lps;
-  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
-  double *lmv = S.ys + (size_t)V * D + V, *mxr = lmv + V;
-  int32_t *kact = S.koff + V + 1;
-  int np0 = 0, Tne_i = 0;
-  bool alive = false;
-  double lmass0 = 0.0;
-  RUN_T0();
-  if (act) {
-    np0 = W.n_t[p0] - 1;
-    alive = np0 > 0;
-    Tne_i = *W.T_ne - (alive ? 0 : 1);
-    const double mass0 = (double)np0 - sg;
-    lmass0 = (np0 >= 1 && mass0 > 0.0) ? mvc_log(mass0) : 0.0;
-    const int nvr = r < V ? (V - r + tw - 1) / tw : 0;   // views of this member
-    int NK = 0;
-    for (int q = 0; q < nvr; ++q) NK += W.Klist[r + q * tw];
-    // pass 1: lp of the member's listed dishes (concatenated in view order)
-    for (int g0 = 0; g0 < NK; g0 += 64) {
-      const int g = g0 + lane;
-      if (g < NK) {
-        int v = r, off = 0;
-        while (g >= off + W.Klist[v]) { off += W.Klist[v]; v += tw; }
-        const int j = g - off;
-        const double tau = P.hyper[v];
-        const double Y2i = C.Y2[(size_t)v * C.y2stride];
-        const double hy = 0.5 * Y2i;
-        const double h = (-0.5 * Y2i) / tau;
-        const double G = fma_dot_strided(C.y + (size_t)v * C.ystride, W.S1T + (size_t)v * D * W.s1s + j, (size_t)W.s1s, D, 0.0);
-        double val;
-        if (j == W.dish[v * ts + p0]) {
-          const double Gp = G - Y2i;
-          const double Qp = (W.Q[v * ks + j] - 2.0 * G) + Y2i;
-          double c0, cb;
-          if (W.xm) {
-            c0 = W.xm[v * ks + j] - (0.5 * Qp) / W.ym[v * ks + j];
-            cb = W.cbm[v * ks + j];
-          } else {
-            const Coef c = coef(W.d_n[v * ks + j] - 1, Qp, tau, A.L2pt[v], D);
-            c0 = c.c0;
-            cb = c.cb;
-          }
-          val = __builtin_fma(Gp + hy, cb, c0) + h;
-        } else {
-          val = __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
-        }
-        S.lp[v * lps + j] = val;
-      }
-    }
-    __threadfence_block();
-    // max / K_act of four member views at once (one per row)
-    for (int q0 = 0; q0 < nvr; q0 += 4) {
-      const int v = r + (q0 + row) * tw;
-      double mx = -MVC_PM_INF;
-      int cnt = 0;
-      if (q0 + row < nvr) {
-        const int K = W.Klist[v];
-        const int j0 = W.dish[v * ts + p0];
-        for (int j = col; j < K; j += 16) {
-          const int l = W.d_l[v * ks + j] - ((j == j0 && !alive) ? 1 : 0);
-          if (l > 0) {
-            ++cnt;
-            const double x = S.lp[v * lps + j];
-            if (x > mx) mx = x;
-          }
-        }
-      }
-      mx = row16_max(mx);
-      cnt = row16_isum(cnt);
-      if (q0 + row < nvr && col == 0) {
-        const double Y2i = C.Y2[(size_t)v * C.y2stride];
-        const double lfn = A.cnew[v] + (-0.5 * Y2i) / P.hyper[v];
-        S.mv[v] = lfn > mx ? lfn : mx;
-        kact[v] = cnt;
-      }
-    }
-    __threadfence_block();
-    // pass 2: weighted terms of the member's included dishes
-    for (int g0 = 0; g0 < NK; g0 += 64) {
-      const int g = g0 + lane;
-      if (g < NK) {
-        int v = r, off = 0;
-        while (g >= off + W.Klist[v]) { off += W.Klist[v]; v += tw; }
-        const int j = g - off;
-        const int l = W.d_l[v * ks + j] - ((j == W.dish[v * ts + p0] && !alive) ? 1 : 0);
-        double t = 0.0;
-        if (l > 0) {
-          double w = (double)l - P.hyper[2 * V + v];
-          if (w < 0.0) w = 0.0;
-          t = w * mvc_exp(S.lp[v * lps + j] - S.mv[v]);
-        }
-        S.aux[v * lps + j] = t;
-      }
-    }
-    __threadfence_block();
-    // column partials / pw16 / new dish / lm_v of four member views at once
-    for (int q0 = 0; q0 < nvr; q0 += 4) {
-      const int v = r + (q0 + row) * tw;
-      double cs = 0.0;
-      if (q0 + row < nvr) {
-        const int K = W.Klist[v];
-        for (int j = col; j < K; j += 16) cs = cs + S.aux[v * lps + j];
-      }
-      double Sv = row_pw16(cs);
-      if (q0 + row < nvr && col == 0) {
-        const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-        const double Y2i = C.Y2[(size_t)v * C.y2stride];
-        const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
-        const double m = S.mv[v];
-        double wn = alpha + (double)kact[v] * sigma;
-        if (wn < 0.0) wn = 0.0;
-        Sv = Sv + wn * mvc_exp(lfn - m);
-        const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
-        lmv[v] = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - mvc_log(denom);
-      }
-    }
-  }
-  __syncthreads();
-  RUN_MARK(0);
-  // s_new in view order (every member); table scores of the member's chunks
-  double s_new = 0.0, M = -MVC_PM_INF;
-  const int T = *W.T;
-  const int TB = (T + 15) / 16;
-  if (act) {
-    s_new = mvc_log(ag + sg * (double)Tne_i);
-    for (int v = 0; v < V; ++v) s_new = s_new + lmv[v];
-    constexpr int kU = 4;
-    const int nch = TB * 16;   // padded table slots; chunk c covers [64 c, 64 c + 64)
-    for (int c0 = r; c0 * 64 < nch; c0 += tw * kU) {
-      int np[kU];
-      double lm[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int p = (c0 + u * tw) * 64 + lane;
-        np[u] = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
-        lm[u] = p < T ? ((p == p0) ? lmass0 : W.lmass[p]) : 0.0;
-      }
-      double sp[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int p = (c0 + u * tw) * 64 + lane;
-        const double mass = (double)np[u] - sg;
-        sp[u] = (p < T && np[u] >= 1 && mass > 0.0) ? lm[u] : -MVC_PM_INF;
-      }
-      for (int v = 0; v < V; ++v) {
-        int dj[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const int p = (c0 + u * tw) * 64 + lane;
-          dj[u] = (sp[u] != -MVC_PM_INF) ? W.dish[v * ts + p] : 0;
-        }
-        double lv[kU];
-#pragma unroll
-        for (int u = 0; u < kU; ++u) lv[u] = S.lp[v * lps + dj[u]];
-#pragma unroll
-        for (int u = 0; u < kU; ++u)
-          if (sp[u] != -MVC_PM_INF) sp[u] = sp[u] + lv[u];
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int p = (c0 + u * tw) * 64 + lane;
-        if (p < nch) S.e[p] = sp[u];
-        if (sp[u] > M) M = sp[u];
-      }
-    }
-    M = wave_max(M);
-    if (lane == 0) mxr[r] = M;
-  }
-  __syncthreads();
-  RUN_MARK(1);
-  if (act) {
-    for (int k = 0; k < tw; ++k) M = mxr[k] > M ? mxr[k] : M;
-    if (s_new > M) M = s_new;
-    // weights and block sums of the member's chunks
-    for (int c0 = r; c0 * 64 < TB * 16; c0 += tw) {
-      const int p = c0 * 64 + lane;
-      double wgt = 0.0;
-      if (p < TB * 16) {
-        const double x = S.e[p];
-        wgt = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
-        S.e[p] = wgt;
-      }
-      const double Bv = row_pw16(wgt);
-      const int b = c0 * 4 + row;
-      if (col == 0 && b < TB) S.B[b] = Bv;
-    }
-  }
-  __syncthreads();
-  RUN_MARK(2);
-  int pick = -1;
-  if (act && r == 0) {
-    double tot = 0.0;
-    for (int b0 = 0; b0 < TB; b0 += 64) {
-      const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
-      const int nb = min(64, TB - b0);
-      for (int k = 0; k < nb; ++k) tot = tot + readlane_d(Bl, k);
-    }
-    const double Wt = mvc_exp(s_new - M) + tot;
-    double u = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
-    if (u < tot) {
-      double c = 0.0, cprev = 0.0;
-      int bsel = TB - 1;
-      bool found = false;
-      for (int b0 = 0; b0 < TB && !found; b0 += 64) {
-        const double Bl = (b0 + lane < TB) ? S.B[b0 + lane] : 0.0;
-        const int nb = min(64, TB - b0);
-        for (int k = 0; k < nb; ++k) {
-          const double c2 = c + readlane_d(Bl, k);
-          if (u < c2) {
-            bsel = b0 + k;
-            cprev = c;
-            found = true;
-            break;
-          }
-          c = c2;
-        }
-      }
-      u = u - cprev;
-      const double x = lane < 16 ? S.e[bsel * 16 + lane] : 0.0;
-      pick = bsel * 16 + pw16_select_wave(x, u);
-    }
   }
   RUN_MARK(3);
   return pick;
@@ -1250,6 +1014,176 @@ __device__ int seq_tree_select(const double *lv, int m, int nlev, double r) {
   return idx;
 }
 
+// Exact integer sum over each 16-lane row, every lane of the row gets it
+// (xor butterfly by DPP: quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror; after the first two steps the 4-groups are uniform, so the
+// mirrors deliver the sibling 4- and 8-groups).
+__device__ __forceinline__ int row16_isum_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, true);
+  return x;
+}
+// lane k of each 16-lane row broadcast to the row (DPP row_newbcast:k)
+template <int k>
+__device__ __forceinline__ double row_bcast_d(double x) { return dpp_d<0x150 + k>(x); }
+
+// seq_resample shaped for latency on the run kernel's LDS state ("lane
+// columns"): the same decision, bit for bit, with every reduction either
+// in-lane or a 16-lane row tree.  Lane (row r, column c) owns view v = g + r
+// of view group g (views g .. g + 3) and that view's dishes j = c, c + 16,
+// c + 32, ... in ascending order, so the spec's column partial col_c (the
+// sequential sum over j = c mod 16) is this lane's running
+// sum and pw16 over the columns is the row's DPP tree; the view maximum and
+// K_act are row reductions.  The per-view logs (log S_v, log of the
+// denominator) of four views, the new-table log and the own table's log mass
+// share one log evaluation (one lane each).  Tables: lane p of 64-table
+// chunks (T <= 64 kLcChunks), the lp rows gathered from the wave's LDS
+// scratch, block sums by row pw16, running block totals in lane b (b < 64)
+// so the draw finds its block with one ballot.  hyp / cnewv: the sweep's
+// hyperparameters and new-dish constants, staged in LDS at kernel launch.
+constexpr int kLcChunks = 8;   // tables <= 512 (block totals in lanes b < 64 need TB <= 64)
+__device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
+                               const double *hyp, const double *cnewv) {
+  const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
+  const int V = A.P.V, D = A.P.D, ts = W.ts, ks = W.ks, lps = S.lps, s1s = W.s1s;
+  const double ag = hyp[3 * V], sg = hyp[3 * V + 1];
+  const int np0 = W.n_t[p0] - 1;
+  const bool alive = np0 > 0;
+  const int Tne_i = *W.T_ne - (alive ? 0 : 1);
+  const double mass0 = (double)np0 - sg;
+  double s_new = 0.0, lmass0 = 0.0;
+  RUN_T0();
+  for (int g = 0; g < V; g += 4) {
+    const int v = g + row;
+    const bool vok = v < V;
+    const int vv = vok ? v : V - 1;   // rows past the last view mirror it (their results are not used)
+    const int K = vok ? W.Klist[vv] : 0;
+    const double tau = hyp[vv], alpha = hyp[V + vv], sigma = hyp[2 * V + vv];
+    const double Y2i = C.Y2[(size_t)vv * C.y2stride];
+    const double hy = 0.5 * Y2i;
+    const double h = (-0.5 * Y2i) / tau;
+    const double lfn = cnewv[vv] + h;
+    const int j0 = W.dish[vv * ts + p0];
+    const double *yv = C.y + (size_t)vv * C.ystride;
+    const double *S1v = W.S1T + (size_t)vv * D * s1s;
+    const int *dl = W.d_l + vv * ks;
+    double *lpv = S.lp + (size_t)vv * lps;
+    // the own dish with the customer removed, every lane of the row
+    double self;
+    {
+      double G = 0.0;
+      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[(size_t)d * s1s + j0], G);
+      const double Gp = G - Y2i;
+      const double Qp = (W.Q[vv * ks + j0] - 2.0 * G) + Y2i;
+      const double c0 = W.xm[vv * ks + j0] - (0.5 * Qp) / W.ym[vv * ks + j0];
+      self = __builtin_fma(Gp + hy, W.cbm[vv * ks + j0], c0) + h;
+    }
+    const int l0p = dl[j0] - (alive ? 0 : 1);
+    // lp of this lane's dishes (to the scratch for the table gathers), their
+    // max over the included ones (l' > 0) and K_act
+    double mx = -MVC_PM_INF;
+    int cnt = 0;
+    for (int j = col; j < K; j += 16) {
+      double G = 0.0;
+      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[(size_t)d * s1s + j], G);
+      const double fr = __builtin_fma(G + hy, W.cb[vv * ks + j], W.c0[vv * ks + j]) + h;
+      const bool own = j == j0;
+      const double val = own ? self : fr;
+      const int l = own ? l0p : dl[j];
+      lpv[j] = val;
+      if (l > 0) {
+        ++cnt;
+        if (val > mx) mx = val;
+      }
+    }
+    mx = row16_max(mx);
+    cnt = row16_isum_dpp(cnt);
+    const double m = lfn > mx ? lfn : mx;
+    // column partial: w_j exp(lp_j - m) in ascending j (excluded dishes add +0)
+    double cs = 0.0;
+    for (int j = col; j < K; j += 16) {
+      const bool own = j == j0;
+      const int l = own ? l0p : dl[j];
+      double w = (double)l - sigma;
+      if (w < 0.0) w = 0.0;
+      const double x = lpv[j];
+      cs = cs + w * mvc_exp_le0(l > 0 ? x - m : -MVC_PM_INF);
+    }
+    double Sv = row_pw16(cs);
+    double wn = alpha + (double)cnt * sigma;
+    if (wn < 0.0) wn = 0.0;
+    Sv = Sv + wn * mvc_exp_le0(lfn - m);
+    const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
+    // one log for the group: column 0 log S_v, column 1 log(denominator);
+    // group 0, row 0 also the new-table mass (column 2) and the own table's
+    // mass without the customer (column 3)
+    double arg = col == 0 ? Sv : (col == 1 ? denom : 1.0);
+    if (g == 0 && row == 0 && col == 2) arg = ag + sg * (double)Tne_i;
+    if (g == 0 && row == 0 && col == 3) arg = mass0;
+    const double Lg = mvc_log(arg);
+    const double logS = row_bcast_d<0>(Lg), logden = row_bcast_d<1>(Lg);
+    const double lm = (denom <= 0.0) ? lfn : (m + logS) - logden;
+    if (g == 0) {
+      s_new = readlane_d(Lg, 2);
+      lmass0 = readlane_d(Lg, 3);
+    }
+    for (int r = 0; r < 4 && g + r < V; ++r) s_new = s_new + readlane_d(lm, 16 * r);   // view order
+  }
+  RUN_MARK(0);
+  // table scores log(n_p' - sigma_g) + sum_v lp_{v, dish_v(p)} (view order),
+  // -inf when excluded; to the wave's scratch e[]
+  const int T = *W.T, TB = (T + 15) >> 4, nch = (T + 63) >> 6;
+  double M = -MVC_PM_INF;
+  for (int q = 0; q < nch; ++q) {
+    const int p = 64 * q + lane;
+    const int np = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+    const double mass = (double)np - sg;
+    const bool inc = p < T && np >= 1 && mass > 0.0;
+    double x = inc ? (p == p0 ? lmass0 : W.lmass[p]) : -MVC_PM_INF;
+    for (int v = 0; v < V; ++v) {
+      const double lv = S.lp[(size_t)v * lps + (inc ? W.dish[v * ts + p] : 0)];
+      if (inc) x = x + lv;
+    }
+    S.e[p] = x;
+    if (x > M) M = x;
+  }
+  M = wave_max(M);
+  if (s_new > M) M = s_new;
+  RUN_MARK(1);
+  // weights exp(sp - M) (0 where excluded or past T), block sums pw16 per
+  // row, running block totals C_b kept in lane b
+  double tot = 0.0, Cb = 0.0;
+  for (int q = 0; q < nch; ++q) {
+    const int p = 64 * q + lane;
+    const double e = mvc_exp_le0(S.e[p] - M);
+    S.e[p] = e;
+    const double B = row_pw16(e);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = 4 * q + r;
+      if (b < TB) {
+        tot = tot + readlane_d(B, 16 * r);
+        if (lane == b) Cb = tot;
+      }
+    }
+  }
+  const double Wt = mvc_exp_le0(s_new - M) + tot;
+  double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
+  if (!(r < tot)) {
+    RUN_MARK(2);
+    return -1;
+  }
+  const uint64_t hit = __ballot(lane < TB && r < Cb);
+  const int bsel = (int)__ffsll((long long)hit) - 1;
+  r = r - (bsel > 0 ? readlane_d(Cb, bsel - 1) : 0.0);
+  const double x = S.e[16 * (bsel & ~3) + lane];   // the block's row of its 64-table chunk
+  const int pick = 16 * bsel + pw16_select_wave(x, r, 16 * (bsel & 3));
+  RUN_MARK(2);
+  return pick;
+}
+
 // Dish of a birth in view v (oracle SeqSampler::draw_dish): leaves w_j
 // exp(lp_j - m) of the included dishes, the new dish last; tree64; r = u S.
 // lp: [K] scratch, tree: the tree64 levels' scratch.  Returns a list index;
@@ -1353,7 +1287,9 @@ namespace {
 struct SCache {
   int32_t *n_t, *dish, *d_l, *d_n, *Klist, *Ltot, *T, *T_ne;
   double *c0, *cb, *Q, *xm, *ym, *cbm, *lmass;
+  double *S2;                  // [V][ks]: the commit's S2 read-modify-writes stay in LDS (stores to HBM only)
   double *S1T;   // nullptr: S1 is read from global memory
+  const double *hyp, *L2pt;    // the sweep's hyperparameters [3V+2] and log(2 pi tau) [V], staged at launch
   int ts, ks;
 };
 __device__ __forceinline__ SView cache_view(const SCache &c, const SeqArgs &A) {
@@ -1379,6 +1315,16 @@ __device__ __forceinline__ void self_coef_parts(int n_, double tau, double L2pt,
   cbm = 1.0 / (tau * b);
 }
 
+// Block barrier.  lds_only: the waves hand each other only LDS data (the run
+// kernel with its whole state cached in LDS, S1 included): wait for this
+// wave's LDS operations, not for its global stores -- __syncthreads' release
+// fence waits for every outstanding store (vmcnt), i.e. an L2 round trip per
+// barrier after the commits' write-through stores.
+__device__ __forceinline__ void seq_bar(bool lds_only) {
+  if (lds_only) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else __syncthreads();
+}
+
 // Commit customer i's exact choice c (a table position, or -1 = birth) to the
 // state (oracle SeqSampler::sweep_once body + move); p0 = z[i].  The state is
 // read through W (global or the LDS cache cc) and written to the global
@@ -1391,7 +1337,8 @@ __device__ __forceinline__ void self_coef_parts(int n_, double tau, double L2pt,
 // cnt: the moves / births / new-dish counters (R->moves... or the run
 // kernel's LDS copies).
 __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const Cust &Ci, int i, int p0, int c,
-                           double *lpw, double *treew, int32_t *cnt, int nwd, const SeqScratch *pre = nullptr) {
+                           double *lpw, double *treew, int32_t *cnt, int nwd, const SeqScratch *pre = nullptr,
+                           bool lds_only = false) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1399,6 +1346,10 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
   const int ks = W.ks, ts = W.ts;
   __shared__ int s_ovf, s_c, s_dies, s_born;
   __shared__ int s_tup[MVC_MAXV], s_j0[MVC_MAXV], s_j1[MVC_MAXV];
+  // constants from LDS when the run kernel staged them (a global load here
+  // would wait for every store the commits have issued: vmcnt is in order)
+  const double *hyp = (cc && cc->hyp) ? cc->hyp : P.hyper;
+  const double *l2pt = (cc && cc->L2pt) ? cc->L2pt : A.L2pt;
   if (c < 0) {
     // a birth: dishes drawn against the current state, then the table
     const bool alive = (W.n_t[p0] - 1) > 0;
@@ -1437,6 +1388,7 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
           P.d_l[v * KC + j] = 0;
           P.S2[v * KC + j] = 0.0;
           P.Q[v * KC + j] = 0.0;
+          if (cc) cc->S2[v * ks + j] = 0.0;
           R->Klist[v] = j + 1;
           if (cc) {
             cc->d_n[v * ks + j] = 0;
@@ -1469,7 +1421,7 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
     s_born = ntc == 0;
     P.n_t[p0] = nt0;
     P.n_t[c] = ntc + 1;
-    const double sg = P.hyper[3 * V + 1];
+    const double sg = hyp[3 * V + 1];
     const double lm0 = mvc_log((double)nt0 - sg), lmc = mvc_log((double)(ntc + 1) - sg);
     P.lmass[p0] = lm0;
     P.lmass[c] = lmc;
@@ -1490,7 +1442,7 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
     if (cc) *cc->T_ne = Tne;
     P.z[i] = c;
   }
-  __syncthreads();
+  seq_bar(lds_only);
   if (tid < V && (s_dies || s_born)) {   // table counts of the two tables' dishes
     const int v = tid;
     int L = W.Ltot[v];
@@ -1531,8 +1483,14 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
     const int v = tid, j0 = s_j0[v], j1 = s_j1[v];
     if (j0 != j1) {
       const double y2 = Ci.Y2[(size_t)v * Ci.y2stride];
-      P.S2[v * KC + j0] = P.S2[v * KC + j0] - y2;
-      P.S2[v * KC + j1] = P.S2[v * KC + j1] + y2;
+      const double a0 = (cc ? cc->S2[v * ks + j0] : P.S2[v * KC + j0]) - y2;
+      const double a1 = (cc ? cc->S2[v * ks + j1] : P.S2[v * KC + j1]) + y2;
+      P.S2[v * KC + j0] = a0;
+      P.S2[v * KC + j1] = a1;
+      if (cc) {
+        cc->S2[v * ks + j0] = a0;
+        cc->S2[v * ks + j1] = a1;
+      }
       const int n0 = W.d_n[v * ks + j0] - 1, n1 = W.d_n[v * ks + j1] + 1;
       P.d_n[v * KC + j0] = n0;
       P.d_n[v * KC + j1] = n1;
@@ -1542,12 +1500,12 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
       }
     }
   }
-  __syncthreads();
+  seq_bar(lds_only);
   if (tid < 2 * V) {   // Q and the coefficients of the two dishes (oracle refresh_dish)
     const int v = tid >> 1, j = (tid & 1) ? s_j1[v] : s_j0[v];
     if (s_j0[v] != s_j1[v]) {
       const double q = fma_sq_strided(W.S1T + (size_t)v * D * W.s1s + j, (size_t)W.s1s, D);
-      const Coef cf = coef(W.d_n[v * ks + j], q, P.hyper[v], A.L2pt[v], D);
+      const Coef cf = coef(W.d_n[v * ks + j], q, hyp[v], l2pt[v], D);
       P.Q[v * KC + j] = q;
       P.c0[v * KC + j] = cf.c0;
       P.cb[v * KC + j] = cf.cb;
@@ -1555,13 +1513,13 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
         cc->Q[v * ks + j] = q;
         cc->c0[v * ks + j] = cf.c0;
         cc->cb[v * ks + j] = cf.cb;
-        self_coef_parts(W.d_n[v * ks + j], P.hyper[v], A.L2pt[v], D, cc->xm[v * ks + j], cc->ym[v * ks + j],
+        self_coef_parts(W.d_n[v * ks + j], hyp[v], l2pt[v], D, cc->xm[v * ks + j], cc->ym[v * ks + j],
                         cc->cbm[v * ks + j]);
       }
     }
   }
   if (tid == 0) cnt[0] += 1;
-  __syncthreads();
+  seq_bar(lds_only);
   return true;
 }
 
@@ -1628,7 +1586,8 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A
 // runs; read from R at entry and written back at exit).
 struct RunCursor {
   int go, stop, cur, pend, pc, pp0, mode, streak, done, i;
-  int fill;                       // ring: customers [.., fill) are staged (slot = customer % ring)
+  int fill;                       // ring: customers [.., fill) are requested (slot = customer % ring)
+  int landed;                     // ring: customers [.., landed) are in LDS (every request before them waited for)
   int lpc;                        // wide evaluation: the customer whose lp rows wave 0's scratch holds (-1: none)
   int32_t cnt[3];                 // moves, births, new dishes
   int ch[kSeqRunWaves], p0[kSeqRunWaves];
@@ -1695,30 +1654,32 @@ __device__ __forceinline__ int ring_z(const Ring &G, int c, int V, int D) {
 
 // The run kernel's loop, for state read through the LDS cache (kLds) or the
 // global arrays.  Returns through ovf / restride why it stopped early.
-template <bool kLds, bool kTeam>
+template <bool kLds, bool kWide>
 __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
-                             const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride) {
+                             const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride,
+                             const double *hypc = nullptr, const double *cnewc = nullptr) {
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
   const bool ring = kLds && G.n > 0;
+  const bool lsync = kLds && ccp && ccp->S1T;   // every state read is an LDS read: LDS-only barriers
   for (;;) {
     // invariant here: U.mode == kSeqRun || U.pend, not done
     RUN_T0();
     if (U.pend) {
-      const bool staged = ring && U.cur < U.fill && U.cur >= U.fill - G.n;
+      const bool staged = ring && U.cur < U.landed && U.cur >= U.fill - G.n;
       const Cust Ci = staged ? G.cust(U.cur, V, D) : global_cust(A, U.cur);
-      // dish draws of a birth: wave w < nwd, lp scratch = its slice of its team's lp
-      const int tw = (kTeam && kLds) ? L.tw : 1;   // LDS teams share a scratch; global scratch is per wave
+      // dish draws of a birth: wave w < nwd, each with its own lp scratch
       // wide evaluation of this very customer against this state: its lp rows are reused by the dish draws
       const SeqScratch S0(A, 0);
-      const bool reuse = kTeam && !kLds && U.lpc == U.cur;
-      if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp + (size_t)(w % tw) * L.ks, tree, U.cnt,
-                      kLds ? L.nws * tw : (int)(blockDim.x >> 6), reuse ? &S0 : nullptr)) {
+      const bool reuse = kWide && !kLds && U.lpc == U.cur;
+      if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt,
+                      kLds ? L.nws : (int)(blockDim.x >> 6), reuse ? &S0 : nullptr, lsync)) {
         // overflow: the host grows and relaunches
         ovf = 1;
         return;
       }
+      RUN_MARK(3);
       if (tid == 0) {
         U.cur = U.cur + 1;
         U.pend = 0;
@@ -1737,7 +1698,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       }
       U.i = U.cur;
     }
-    __syncthreads();
+    seq_bar(lsync);
     RUN_MARK(4);
     if (U.stop) {
       restride = U.stop == 2;
@@ -1745,23 +1706,30 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
     }
     const int i0 = U.i;
     const int need = min(n, i0 + L.nws);
-    int fill_next = 0;
+    int fill_next = 0, landed_next = 0;
     if (ring) {
-      // this step's customers must be staged: a synchronous fill when the
-      // ring fell behind (kernel start, after a window jump)
-      const int f0 = max(U.fill, i0);
-      if (f0 < need) {
-        ring_fill_async(A, G, f0, need);
+      // The rows arrive in batches, requested half a ring ahead, so a step
+      // waits for memory only when its customers are beyond what has landed
+      // (once per batch; by then the batch was requested tens of steps ago).
+      // Every wait is s_waitcnt(0): vmcnt also counts the commits' stores.
+      fill_next = max(U.fill, i0);
+      landed_next = U.landed;
+      if (need > U.landed) {
+        if (fill_next < need) {
+          ring_fill_async(A, G, fill_next, need);
+          fill_next = need;
+        }
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
+        landed_next = fill_next;
       }
-      // prefetch the customers after them, up to a ring ahead; they land
-      // while this step evaluates (waited for before the decision barrier)
-      const int p0c = max(f0, need), p1c = min(n, min(i0 + G.n, p0c + L.pfn));
-      if (p1c > p0c) ring_fill_async(A, G, p0c, p1c);
-      fill_next = max(p1c, need);   // U.fill is written after the decision barrier (every wave read it above)
+      if (fill_next - i0 <= G.n / 2 && fill_next < n) {   // keep the next batch in flight
+        const int f1 = min(n, i0 + G.n);
+        ring_fill_async(A, G, fill_next, f1);
+        fill_next = f1;
+      }
     }
-    if constexpr (kTeam && !kLds) {   // global scratch: the whole block on one customer
+    if constexpr (kWide && !kLds) {   // global scratch: the whole block on one customer
       const int i = i0;
       const bool act = i < n;
       const int p0 = act ? P.z[i] : 0;
@@ -1771,29 +1739,8 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         U.p0[0] = p0;
       }
     }
-    if constexpr (kTeam && kLds) {   // teams of tw waves, one customer each
-      const int team = w / L.tw, r = w % L.tw;
-      const int i = i0 + team;
-      const bool act = team < L.nws && i < n;
-      int p0 = 0;
-      Cust C{};
-      if (act) {
-        if (ring) {
-          C = G.cust(i, V, D);
-          p0 = ring_z(G, i, V, D);
-        } else {
-          p0 = P.z[i];
-          C = global_cust(A, i);
-        }
-      }
-      const int c = seq_resample_team(A, Wv, C, i, p0, S, r, L.tw, act);
-      if (act && r == 0 && lane == 0) {
-        U.ch[team] = c;
-        U.p0[team] = p0;
-      }
-    }
     const int i = i0 + w;
-    if (!kTeam && w < L.nws && i < n) {
+    if (!kWide && w < L.nws && i < n) {
       int p0;
       Cust C;
       if (ring) {
@@ -1815,17 +1762,19 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         p0 = P.z[i];
         C = global_cust(A, i);
       }
-      const int c = seq_resample(A, Wv, C, i, p0, S);
+      const int c = (kLds && L.lc) ? seq_resample_lc(A, Wv, C, i, p0, S, hypc, cnewc) : seq_resample(A, Wv, C, i, p0, S);
       if (lane == 0) {
         U.ch[w] = c;
         U.p0[w] = p0;
       }
     }
-    if (ring) __builtin_amdgcn_s_waitcnt(0);   // this wave's prefetch has landed
-    __syncthreads();
+    seq_bar(lsync);
     RUN_MARK(5);
     if (tid == 0) {
-      if (ring) U.fill = fill_next;
+      if (ring) {
+        U.fill = fill_next;
+        U.landed = landed_next;
+      }
       int f = -1;
       const int m = min(L.nws, n - U.i);
       for (int k = 0; k < m; ++k)
@@ -1835,7 +1784,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         U.pend = 1;
         U.pc = U.ch[f];
         U.pp0 = U.p0[f];
-        U.lpc = (kTeam && !kLds) ? U.cur : -1;
+        U.lpc = (kWide && !kLds) ? U.cur : -1;
       } else {
         U.cur = U.i + m;
         U.streak += m;
@@ -1844,7 +1793,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       }
       U.go = !U.done && (U.mode == kSeqRun || U.pend);
     }
-    __syncthreads();
+    seq_bar(lsync);
     RUN_MARK(6);
 #ifdef MVC_RUN_PROF
     if (tid == 0) A.R->prof[7] += 1;
@@ -1867,7 +1816,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 // window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
 // One instance per evaluation shape, compiled separately so each keeps its
 // own register allocation.
-template <int kMode>   // 0: one wave per customer; 1: LDS teams (L.tw > 1, LDS layout); 2: wide (L.tw > 1, global layout)
+template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout)
 __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
   extern __shared__ double seq_sm[];
   Repair *R = A.R;
@@ -1894,6 +1843,7 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     U.streak = R->streak;
     U.done = R->done;
     U.fill = U.cur;   // nothing staged yet
+    U.landed = U.cur;
     U.lpc = -1;
     U.cnt[0] = R->moves;
     U.cnt[1] = R->births;
@@ -1936,7 +1886,18 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     cc.ym = dp; dp += V * ks;
     cc.cbm = dp; dp += V * ks;
     cc.lmass = dp; dp += ts;
+    cc.S2 = dp; dp += V * ks;
     cc.S1T = L.s1 ? dp : nullptr;
+    // the sweep's hyperparameters and per-view constants (the evaluation and
+    // the commits read them from LDS; the MH changes them only after the repair)
+    __shared__ double s_hyp[3 * MVC_MAXV + 2], s_cnew[MVC_MAXV], s_l2pt[MVC_MAXV];
+    for (int k = tid; k < 3 * V + 2; k += nt) s_hyp[k] = P.hyper[k];
+    for (int k = tid; k < V; k += nt) {
+      s_cnew[k] = A.cnew[k];
+      s_l2pt[k] = A.L2pt[k];
+    }
+    cc.hyp = s_hyp;
+    cc.L2pt = s_l2pt;
     const int T = R->T;
     for (int k = tid; k < T; k += nt) {
       cc.n_t[k] = P.n_t[k];
@@ -1954,6 +1915,7 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
         cc.c0[k] = P.c0[v * KC + j];
         cc.cb[k] = P.cb[v * KC + j];
         cc.Q[k] = P.Q[v * KC + j];
+        cc.S2[k] = P.S2[v * KC + j];
         self_coef_parts(cc.d_n[k], P.hyper[v], A.L2pt[v], D, cc.xm[k], cc.ym[k], cc.cbm[k]);
       }
     }
@@ -1976,9 +1938,10 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     G.n = L.ring;
     G.slot = (int)seq_ring_slot(V, D);
     G.base = seq_sm + L.cache_dbl + (int64_t)L.nws * L.stride;
-    seq_run_loop<true, kMode == 1>(A, L, cache_view(cc, A), &cc,
-                              SeqScratch(seq_sm + L.cache_dbl + (int64_t)(w / L.tw) * L.stride, V, L.ks, L.ts), G,
-                              tree, U, ovf, restride);
+    seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
+                              SeqScratch(seq_sm + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts), G,
+                              tree, U, ovf, restride, s_hyp, s_cnew);
+    __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
   } else {
     Ring G{nullptr, 0, 0};
     seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);

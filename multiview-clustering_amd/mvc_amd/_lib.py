@@ -20,8 +20,11 @@ FLAG_TIMING_COARSE = 4
 TRACE_ALPHA_V, TRACE_SIGMA_V, TRACE_TAU_V, TRACE_ALPHA_GLOBAL, TRACE_SIGMA_GLOBAL = range(5)
 
 
-# all_gather callback of mvc_sampler_set_shard: void (*)(void *user)
-SHARD_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+ABI_VERSION = 2
+MVC_ERR_CALLBACK = 5
+
+# all_gather callback of mvc_sampler_set_shard: int (*)(void *user), 0 = done
+SHARD_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 
 
 class MvcError(RuntimeError):
@@ -48,11 +51,22 @@ class Config(ctypes.Structure):
         ("table_cap", ctypes.c_int32),
         ("dish_cap", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+        ("n_devices", ctypes.c_int32),      # ABI 2
+        ("chain_stride", ctypes.c_int32),
     ]
 
 
 _lib = None
 HW_QUEUES = 32   # hardware queues requested for concurrent chains (the GPU pool allows at most 32)
+
+
+def hw_queues(value):
+    """GPU_MAX_HW_QUEUES to run with: the user's value when it is an integer,
+    else HW_QUEUES (unset, empty or unparsable counts as unset)."""
+    try:
+        return int(str(value).strip()) if value is not None else HW_QUEUES
+    except ValueError:
+        return HW_QUEUES
 
 
 def lib():
@@ -66,10 +80,10 @@ def lib():
     # Concurrent chains (parallel mode, one stream each) overlap only as far
     # as HIP gives the process hardware queues: GPU_MAX_HW_QUEUES, 4 by
     # default, read once when HIP starts (at the latest while this library's
-    # kernels register at load).  Raise it to 32 unless a larger value is set;
-    # a process that started HIP earlier keeps its own.
-    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES:
-        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+    # kernels register at load).  Ask for 32 only when the variable is unset
+    # (or not an integer): a value the user chose is kept; a process that
+    # started HIP earlier keeps its own.
+    os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues(os.environ.get("GPU_MAX_HW_QUEUES")))
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u32, u64, sz = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_size_t)
@@ -90,6 +104,7 @@ def lib():
         "mvc_result_table_of": (ip, [vp, i32, i32]),
         "mvc_result_dish_of": (ip, [vp, i32, i32]),
         "mvc_result_trace": (dp, [vp, i32, i32]),
+        "mvc_result_summary": (i32, [vp, dp, dp]),
         "mvc_result_free": (None, [vp]),
         "mvc_sampler_create": (i32, [cfgp, ctypes.POINTER(dp), vpp, cp, sz]),
         "mvc_sampler_sweep": (i32, [vp, i32, cp, sz]),
@@ -107,6 +122,9 @@ def lib():
         "mvc_sampler_ari": (i32, [vp, i32, ip, dp, cp, sz]),
         "mvc_ari": (i32, [i32, ip, ip, i64, dp, cp, sz]),
         "mvc_sampler_stream": (vp, [vp]),
+        "mvc_sampler_create_synthetic": (i32, [cfgp, ctypes.c_int32, u64, ctypes.c_double, ctypes.c_double, ip, vpp,
+                                               cp, sz]),
+        "mvc_sampler_copy_rows": (i32, [vp, ctypes.c_int32, ip, i64, dp, cp, sz]),
         "mvc_sampler_set_shard": (i32, [vp, i32, i32, vp, vp, vp]),
         "mvc_shard_len": (i64, [i64, i32]),
         "mvc_sampler_destroy": (None, [vp]),
@@ -119,6 +137,8 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if L.mvc_abi_version() != ABI_VERSION:
+        raise OSError(f"{LIB_PATH}: ABI version {L.mvc_abi_version()}, this binding needs {ABI_VERSION}")
     _lib = L
     return L
 

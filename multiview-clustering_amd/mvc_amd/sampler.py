@@ -52,7 +52,7 @@ def _timing_flags(timing):
 
 
 def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_chain=0, device=0,
-                mode="exact", table_cap=0, dish_cap=0, timing=False, quiet=True):
+                mode="exact", table_cap=0, dish_cap=0, timing=False, quiet=True, n_devices=1, chain_stride=1):
     cfg = L.Config()
     L.lib().mvc_config_init(ctypes.byref(cfg))
     cfg.n, cfg.n_views, cfg.dim = n, V, D
@@ -62,6 +62,7 @@ def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_ch
     cfg.mode = {"exact": L.MODE_EXACT, "parallel": L.MODE_PARALLEL}[mode]
     cfg.table_cap, cfg.dish_cap = table_cap, dish_cap
     cfg.flags = _timing_flags(timing) | (L.FLAG_QUIET if quiet else 0)
+    cfg.n_devices, cfg.chain_stride = n_devices, chain_stride
     return cfg
 
 
@@ -74,20 +75,31 @@ def _view_ptrs(y):
 
 
 def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chains=1, device=0,
-                  first_chain=0, quiet=False):
+                  first_chain=0, quiet=False, n_devices=1, summary=None):
     """Drop-in for the reference's ``run_gibbs_cpp`` (see module docstring).
 
-    With ``n_chains > 1`` a list of per-chain result dicts is returned.
+    With ``n_chains > 1`` a list of per-chain result dicts is returned; the
+    chains run on ``n_devices`` GPUs (chain c on device ``device + c %
+    n_devices``, one host thread per device).  ``summary`` (a dict) receives
+    the pooled posterior means and Gelman-Rubin R-hat of the hyperparameters
+    (mvc_result_summary: keys ``mean`` and ``rhat``, float64[3V+2] in the
+    order tau_v, alpha_v, sigma_v, alpha_global, sigma_global).
     """
     y = _views_to_array(data_views)
     V, n, D = y.shape
-    cfg = make_config(n, V, D, M, burn_in, thin, seed, n_chains, first_chain, device, mode, quiet=quiet)
+    cfg = make_config(n, V, D, M, burn_in, thin, seed, n_chains, first_chain, device, mode, quiet=quiet,
+                      n_devices=n_devices)
     lib = L.lib()
     res = ctypes.c_void_p()
     buf = L.errbuf()
     L.check(lib.mvc_run(ctypes.byref(cfg), _view_ptrs(y), ctypes.byref(res), buf, len(buf)), buf)
     try:
         S = lib.mvc_result_num_saved(res)
+        if summary is not None:
+            mean, rhat = np.empty(3 * V + 2), np.empty(3 * V + 2)
+            dp = ctypes.POINTER(ctypes.c_double)
+            lib.mvc_result_summary(res, mean.ctypes.data_as(dp), rhat.ctypes.data_as(dp))
+            summary["mean"], summary["rhat"] = mean, rhat
         outs = []
         for c in range(n_chains):
             table_of, dish_of = [], []
@@ -144,12 +156,47 @@ class Sampler:
         L.check(self._lib.mvc_sampler_create(ctypes.byref(cfg), _view_ptrs(self.y), ctypes.byref(self._h), buf,
                                              len(buf)), buf)
 
+    @classmethod
+    def synthetic(cls, N, V, D, K, data_seed=1999, sd=1.3, mu_sd=3.0, seed=1999, n_chains=1, first_chain=0,
+                  device=0, table_cap=0, dish_cap=0, timing=False):
+        """A parallel-mode handle on synthetic data generated ON THE DEVICE
+        (mvc_sampler_create_synthetic: the SURVEY §8d recipe from a Philox
+        stream keyed by ``data_seed``; y never exists on the host, so N x V x D
+        may exceed host memory, e.g. BASELINE configs[4] at 164 GB).  Returns
+        (sampler, z) with z the generating labels (int32[N])."""
+        self = cls.__new__(cls)
+        self.y = None
+        self.V, self.n, self.D = V, N, D
+        self.n_chains = n_chains
+        cfg = make_config(N, V, D, 0, 0, 1, seed, n_chains, first_chain, device, "parallel", table_cap, dish_cap,
+                          timing)
+        self._lib = L.lib()
+        self._h = ctypes.c_void_p()
+        z = np.empty(N, dtype=np.int32)
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_create_synthetic(ctypes.byref(cfg), K, ctypes.c_uint64(data_seed), sd, mu_sd,
+                                                       z.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                       ctypes.byref(self._h), buf, len(buf)), buf)
+        return self, z
+
+    def rows(self, view, idx):
+        """Rows idx of view ``view`` of the handle's data (float64 [m][D]),
+        read from the device (mvc_sampler_copy_rows)."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        out = np.empty((idx.size, self.D))
+        buf = L.errbuf()
+        L.check(self._lib.mvc_sampler_copy_rows(self._h, view, idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                                idx.size, out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), buf,
+                                                len(buf)), buf)
+        return out
+
     def sweep(self, n_sweeps=1):
         buf = L.errbuf()
-        L.check(self._lib.mvc_sampler_sweep(self._h, n_sweeps, buf, len(buf)), buf)
+        st = self._lib.mvc_sampler_sweep(self._h, n_sweeps, buf, len(buf))
         err, self._shard_err = getattr(self, "_shard_err", None), None
-        if err is not None:
+        if err is not None:   # the exchange raised: the library stopped the sweep (MVC_ERR_CALLBACK)
             raise RuntimeError("shard exchange failed") from err
+        L.check(st, buf)
 
     def synchronize(self):
         buf = L.errbuf()
@@ -268,8 +315,10 @@ class Sampler:
             def _cb(_user):
                 try:
                     exchange.all_gather()
+                    return 0
                 except BaseException as e:   # an exception cannot cross the C frame: re-raised by sweep()
                     self._shard_err = e
+                    return 1
             self._shard_cb = L.SHARD_CB(_cb)   # kept alive with the handle
             ptr = ctypes.c_void_p(exchange.ptr)
         self._shard_ex = exchange

@@ -34,6 +34,7 @@
 //
 // Build: oracle/Makefile  (g++ -O2 -ffp-contract=off, no fast-math).
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 #include <math.h>
 #include <algorithm>
@@ -96,6 +97,13 @@ struct Result {
   std::vector<int> trace_T;                // per sweep: T after the sweep
   std::vector<uint64_t> trace_draws;       // per sweep: sequential draws used so far
   std::vector<int64_t> trace_moves, trace_births, trace_newdish;  // SeqSampler, per sweep
+  // ExactSampler, per sweep: the reference's linear-space underflow
+  // (multiview_utils.cpp:107,114,124-135; multiview_gibbs.cpp:169-176):
+  // customers whose sum_p <= 0 took the table-0 fallback; tables with
+  // n_t - sigma_g > 0 whose probability underflowed to 0 (summed over
+  // customers); customers with at least one such table; customers whose
+  // new-table probability underflowed with a positive mass
+  std::vector<int64_t> trace_fallback, trace_uf_tables, trace_uf_customers, trace_uf_new;
   // final sufficient statistics (parallel sampler): per view, live dishes in
   // ascending raw id; S1 [K][D], S2 [K], n_vk [K]
   std::vector<std::vector<double>> fS1, fS2;
@@ -292,8 +300,10 @@ struct ExactSampler {
     }
     return cache_val[v][k];
   }
+  int64_t uf_tables = 0, uf_customers = 0, uf_new = 0, fallback = 0;   // underflow counters (Result traces)
   void table_probs(int i, std::vector<double> &p, double &p_new) {
     ++stamp;
+    int64_t uf_here = 0;
     if ((int)cache_val.size() != d) { cache_val.assign(d, {}); cache_stamp.assign(d, {}); }
     for (int t = 0; t < T; ++t) {
       if (n_t[t] == 0) { p[t] = 0.0; continue; }
@@ -301,7 +311,10 @@ struct ExactSampler {
       for (int v = 0; v < d; ++v) lpt += Math::log(cached_f(v, dish_of[v][t], i));
       const double mass = n_t[t] - sigma_global;
       p[t] = (mass <= 0.0) ? 0.0 : mass * Math::exp(lpt);
+      if (mass > 0.0 && p[t] == 0.0) ++uf_here;
     }
+    uf_tables += uf_here;
+    uf_customers += uf_here > 0 ? 1 : 0;
     double lnew = 0.0;
     for (int v = 0; v < d; ++v) lnew += Math::log(marg_new_table(v, i));
     int T_ne = 0;
@@ -309,6 +322,7 @@ struct ExactSampler {
       if (n_t[t] > 0) ++T_ne;
     const double mass_new = alpha_global + sigma_global * T_ne;
     p_new = (mass_new <= 0.0) ? 0.0 : mass_new * Math::exp(lnew);
+    if (mass_new > 0.0 && p_new == 0.0) ++uf_new;
   }
 
   // ---- multiview_utils.cpp:138-192 remove_customer ----
@@ -606,7 +620,7 @@ struct ExactSampler {
         table_probs(i, p, p_new);
         double sum_p = p_new;
         for (int t = 0; t < T; ++t) sum_p += p[t];
-        if (sum_p <= 0.0) { add_existing(i, 0); continue; }
+        if (sum_p <= 0.0) { ++fallback; add_existing(i, 0); continue; }
         for (int t = 0; t < T; ++t) p[t] /= sum_p;
         p_new /= sum_p;
         const double u = rng.unif_rand();
@@ -627,6 +641,11 @@ struct ExactSampler {
       update_hyper();
       R.trace_T.push_back(T);
       R.trace_draws.push_back(rng.draws);
+      R.trace_fallback.push_back(fallback);
+      R.trace_uf_tables.push_back(uf_tables);
+      R.trace_uf_customers.push_back(uf_customers);
+      R.trace_uf_new.push_back(uf_new);
+      fallback = uf_tables = uf_customers = uf_new = 0;
       if (iter >= burn_in && ((iter - burn_in) % thin == 0)) save(R);
     }
   }
@@ -860,6 +879,12 @@ struct ParallelSampler {
         const double *r = y + ((size_t)v * n + i) * D;
         Y2[(size_t)v * n + i] = fma_dot(r, r, D);
       }
+    load_partition(tab, T_, dish_raw, hyper);
+    rebuild_stats();
+  }
+
+  // the partition and hyperparameters of load_state (no statistics)
+  void load_partition(const int *tab, int T_, const int *dish_raw, const double *hyper) {
     T = T_;
     z.assign(tab, tab + n);
     n_t.assign(T, 0);
@@ -888,7 +913,6 @@ struct ParallelSampler {
     }
     ag = hyper[3 * V];
     sg = hyper[3 * V + 1];
-    rebuild_stats();
   }
 
   struct Coef { double c0, cb; };
@@ -1022,11 +1046,13 @@ struct ParallelSampler {
   // dish order, so one GPU lane can own one customer.  lp of every dish goes
   // to lp_out[0..K); returns lm_v.
   double eval_view_seq(int i, int v, bool alive, int j0, double *lp_out) const {
+    return eval_view_seq_r(y + ((size_t)v * n + i) * D, Y2[(size_t)v * n + i], v, alive, j0, lp_out);
+  }
+  // the same for a customer whose view-v row is yi with sum of squares Y2i
+  double eval_view_seq_r(const double *yi, double Y2i, int v, bool alive, int j0, double *lp_out) const {
     const int K = (int)ids[v].size();
-    const double Y2i = Y2[(size_t)v * n + i];
     const double hy = 0.5 * Y2i;
     const double h = (-0.5 * Y2i) / tau[v];
-    const double *yi = y + ((size_t)v * n + i) * D;
     int l0p = 0;
     for (int j = 0; j < K; ++j) {
       const double G = fma_dot(yi, &S1[v][(size_t)j * D], D);
@@ -1082,6 +1108,17 @@ struct ParallelSampler {
   // first block with r < C_b is entered with r - C_{b-1} and the leaf is the
   // pw16 descent (pw16_select) inside it.
   int resample_customer(int i, int s) const {
+    std::vector<const double *> rows(V);
+    std::vector<double> y2(V);
+    for (int v = 0; v < V; ++v) {
+      rows[v] = y + ((size_t)v * n + i) * D;
+      y2[v] = Y2[(size_t)v * n + i];
+    }
+    return resample_rows(i, s, rows.data(), y2.data());
+  }
+  // resample_customer for customer i with view rows rows[v] (D doubles) and
+  // their sums of squares y2[v] (checks at sizes where y is not on the host)
+  int resample_rows(int i, int s, const double *const *rows, const double *y2) const {
     const int p0 = z[i];
     const bool alive = (n_t[p0] - 1) > 0;
     std::vector<std::vector<double>> lp(V);
@@ -1089,7 +1126,7 @@ struct ParallelSampler {
     double s_new = mvc_log(ag + sg * (double)Tne_i);
     for (int v = 0; v < V; ++v) {
       lp[v].resize(ids[v].size());
-      s_new = s_new + eval_view_seq(i, v, alive, dish[v][p0], lp[v].data());
+      s_new = s_new + eval_view_seq_r(rows[v], y2[v], v, alive, dish[v][p0], lp[v].data());
     }
     const int TB = (T + 15) / 16;
     std::vector<double> sc((size_t)TB * 16, -MVC_PM_INF);
@@ -1753,6 +1790,49 @@ void *mvo_run_from(const double *y, int n, int V, int D, int M, int burn_in, int
   return R;
 }
 
+// Phase-A table draw (ParallelSampler::resample_customer against the
+// sweep-start state) of customers idx[0..m) in sweep `sweep`, given the state
+// as a partition (table_of[n], dish_raw[V][T], hyper[3V+2]) and the per-view
+// statistics in ascending raw-id order (S1 [K_v][D], S2 [K_v], nk [K_v],
+// concatenated over views), and only the sampled customers' rows
+// rows[m][V][D]: checks the device's full-size conditional where y itself
+// does not fit on the host (BASELINE configs[4]).  Returns 0, or -1 with the
+// message in err.
+int mvo_phase_a(int n, int V, int D, const int *table_of, int T, const int *dish_raw, const double *hyper,
+                const int *K, const double *S1, const double *S2, const int *nk, uint64_t seed, int chain, int sweep,
+                int m, const int *idx, const double *rows, int *out, char *err, int errlen) {
+  try {
+    ParallelSampler P;
+    P.n = n; P.V = V; P.D = D; P.y = nullptr;
+    P.seed = seed; P.chain = (uint32_t)chain;
+    P.load_partition(table_of, T, dish_raw, hyper);
+    P.nk.assign(V, {}); P.S1.assign(V, {}); P.S2.assign(V, {});
+    size_t o1 = 0, o2 = 0;
+    for (int v = 0; v < V; ++v) {
+      if (K[v] != (int)P.ids[v].size()) throw std::runtime_error("K_v does not match the partition's dishes");
+      P.nk[v].assign(nk + o2, nk + o2 + K[v]);
+      P.S2[v].assign(S2 + o2, S2 + o2 + K[v]);
+      P.S1[v].assign(S1 + o1, S1 + o1 + (size_t)K[v] * D);
+      o1 += (size_t)K[v] * D;
+      o2 += K[v];
+    }
+    P.sweep_constants();
+    std::vector<const double *> rp(V);
+    std::vector<double> y2(V);
+    for (int k = 0; k < m; ++k) {
+      for (int v = 0; v < V; ++v) {
+        rp[v] = rows + ((size_t)k * V + v) * D;
+        y2[v] = ParallelSampler::fma_dot(rp[v], rp[v], D);
+      }
+      out[k] = P.resample_rows(idx[k], sweep, rp.data(), y2.data());
+    }
+    return 0;
+  } catch (const std::exception &e) {
+    if (err && errlen > 0) snprintf(err, errlen, "%s", e.what());
+    return -1;
+  }
+}
+
 int mvo_stats_K(void *h, int v) {
   Result *R = (Result *)h;
   return v < (int)R->fnk.size() ? (int)R->fnk[v].size() : 0;
@@ -1804,6 +1884,20 @@ void mvo_copy_trace_moves(void *h, int64_t *moves, int64_t *births, int64_t *new
     newdish[s] = s < m ? R->trace_newdish[s] : -1;
   }
 }
+// ExactSampler's per-sweep underflow counters (zeros for the other samplers)
+void mvo_copy_trace_underflow(void *h, int64_t *fallback, int64_t *uf_tables, int64_t *uf_customers,
+                              int64_t *uf_new) {
+  Result *R = (Result *)h;
+  const size_t S = R->trace_T.size();
+  for (size_t s = 0; s < S; ++s) {
+    const bool have = s < R->trace_fallback.size();
+    fallback[s] = have ? R->trace_fallback[s] : 0;
+    uf_tables[s] = have ? R->trace_uf_tables[s] : 0;
+    uf_customers[s] = have ? R->trace_uf_customers[s] : 0;
+    uf_new[s] = have ? R->trace_uf_new[s] : 0;
+  }
+}
+
 void mvo_free(void *h) { delete (Result *)h; }
 
 // ---- spec primitives, exposed so tests can check the GPU against them ----

@@ -56,6 +56,7 @@ def lib():
         L.mvo_copy_trace.argtypes = [vp, ip, ctypes.POINTER(ctypes.c_uint64)]
         L.mvo_copy_trace_moves.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                                            ctypes.POINTER(ctypes.c_int64)]
+        L.mvo_copy_trace_underflow.argtypes = [vp] + [ctypes.POINTER(ctypes.c_int64)] * 4
         L.mvo_free.argtypes = [vp]
         L.mvo_stats_K.restype = i32
         L.mvo_stats_K.argtypes = [vp, i32]
@@ -67,6 +68,9 @@ def lib():
         L.mvo_seq_uniforms.argtypes = [u64, ctypes.c_uint32, u64, dp, i64]
         L.mvo_tree64_sum.restype = ctypes.c_double
         L.mvo_tree64_sum.argtypes = [dp, i64]
+        L.mvo_phase_a.restype = i32
+        L.mvo_phase_a.argtypes = [i32, i32, i32, ip, i32, ip, dp, ip, dp, dp, ip, u64, i32, i32, i32, ip, dp, ip,
+                                  ctypes.c_char_p, i32]
         L.mvo_tree64_select.restype = i64
         L.mvo_tree64_select.argtypes = [dp, i64, ctypes.c_double]
         _lib = L
@@ -133,6 +137,8 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=Non
         tm, tb, tn = (np.empty(nsw, dtype=np.int64) for _ in range(3))
         i64p = ctypes.POINTER(ctypes.c_int64)
         L.mvo_copy_trace_moves(h, tm.ctypes.data_as(i64p), tb.ctypes.data_as(i64p), tn.ctypes.data_as(i64p))
+        uf = [np.empty(nsw, dtype=np.int64) for _ in range(4)]
+        L.mvo_copy_trace_underflow(h, *(a.ctypes.data_as(i64p) for a in uf))
         return {
             "table_of": table_of,
             "dish_of": dish_of,
@@ -146,10 +152,42 @@ def run(y, M, burn_in, thin, seed, chain=0, mode=EXACT, math=PORTABLE, state=Non
             "trace_moves": tm,         # PARALLEL mode: customers that changed table, per sweep (else -1)
             "trace_births": tb,
             "trace_newdish": tn,
+            # EXACT mode, per sweep: the reference's linear-space underflow
+            # (table-0 fallbacks, underflowed tables summed over customers,
+            # customers with one, underflowed new-table probabilities)
+            "trace_fallback": uf[0], "trace_uf_tables": uf[1], "trace_uf_customers": uf[2], "trace_uf_new": uf[3],
             "stats": stats,            # parallel mode: final S1 [K][D], S2, n per view
         }
     finally:
         L.mvo_free(h)
+
+
+def phase_a(table_of, dish_of, hyper, stats, seed, chain, sweep, idx, rows):
+    """Phase-A draws (the sweep-start conditional, ParallelSampler::
+    resample_customer) of customers idx given the state as a partition
+    (table_of[n], dish_of[V][T] raw ids, hyper[3V+2]) plus per-view stats
+    (list of dicts S1 [K][D], S2 [K], n [K] in ascending raw id, as
+    Sampler.stats returns them) and only those customers' rows
+    rows[m][V][D].  For checks at sizes where y is not on the host."""
+    tab = np.ascontiguousarray(table_of, dtype=np.int32)
+    dsh = np.ascontiguousarray(dish_of, dtype=np.int32)
+    hyp = np.ascontiguousarray(hyper, dtype=np.float64)
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    rows = np.ascontiguousarray(rows, dtype=np.float64)
+    m, V, D = rows.shape
+    K = np.array([st["n"].size for st in stats], dtype=np.int32)
+    S1 = np.ascontiguousarray(np.concatenate([np.asarray(st["S1"], dtype=np.float64).ravel() for st in stats]))
+    S2 = np.ascontiguousarray(np.concatenate([np.asarray(st["S2"], dtype=np.float64) for st in stats]))
+    nk = np.ascontiguousarray(np.concatenate([np.asarray(st["n"], dtype=np.int32) for st in stats]))
+    out = np.empty(m, dtype=np.int32)
+    err = ctypes.create_string_buffer(512)
+    ipt = ctypes.POINTER(ctypes.c_int)
+    rc = lib().mvo_phase_a(tab.size, V, D, tab.ctypes.data_as(ipt), dsh.shape[1], dsh.ctypes.data_as(ipt), _dp(hyp),
+                           K.ctypes.data_as(ipt), _dp(S1), _dp(S2), nk.ctypes.data_as(ipt), ctypes.c_uint64(seed),
+                           chain, sweep, m, idx.ctypes.data_as(ipt), _dp(rows), out.ctypes.data_as(ipt), err, 512)
+    if rc != 0:
+        raise RuntimeError(err.value.decode())
+    return out
 
 
 def _vec(fn, x):

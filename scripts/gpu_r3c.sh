@@ -1,0 +1,13 @@
+#!/bin/bash
+# run kernel: parity of the repair paths, timings, then the phase profile
+# (MVC_RUN_PROF variant) at the north-star literal warm + configs[1] cold
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 --timeout-method thread \
+    -k "repair or capacity or config2 or chains or golden or live_oracle or multichunk or warm_start or mfma_path" \
+    > gpurun_out/pytest_r3c.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/pytest_r3c.log; exit 1; }
+tail -2 gpurun_out/pytest_r3c.log
+timeout -k 10 200 python -u scripts/r3_probe.py shapes > gpurun_out/r3c_shapes.log 2>&1 || { echo "shapes failed"; cat gpurun_out/r3c_shapes.log; exit 1; }
+cat gpurun_out/r3c_shapes.log
+MVC_HIP_LIB=$GRAFT_REPO_ROOT/build_variants/prof/libmvc_hip.so timeout -k 10 200 python -u scripts/r3_probe.py shapes \
+    > gpurun_out/r3c_prof.log 2>&1 || { echo "prof failed"; tail gpurun_out/r3c_prof.log; exit 1; }
+cat gpurun_out/r3c_prof.log

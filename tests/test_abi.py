@@ -43,10 +43,39 @@ def test_library_exports_every_declared_symbol(lib):
 
 def test_abi_version_and_defaults(lib):
     L = lib.lib()
-    assert L.mvc_abi_version() == 1
+    assert L.mvc_abi_version() == 2
     cfg = lib.Config()
     L.mvc_config_init(ctypes.byref(cfg))
     assert cfg.thin >= 1 and cfg.n_chains == 1 and cfg.mode == lib.MODE_EXACT
+    assert cfg.n_devices == 0 and cfg.chain_stride == 0   # one device; chain ids first_chain + c
+
+
+def test_config_layout_matches_header(lib, tmp_path):
+    """The ctypes mirror of mvc_config has the C header's size and offsets
+    (the Rcpp drop-in carries the same layout)."""
+    fields = [f for f, _ in lib.Config._fields_]
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mvc.h"\nint main(void){printf("%zu",'
+                   'sizeof(mvc_config));' + "".join(f'printf(" %zu", offsetof(mvc_config, {f}));' for f in fields) +
+                   "return 0;}\n")
+    exe = tmp_path / "lay"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got[0] == ctypes.sizeof(lib.Config)
+    assert got[1:] == [getattr(lib.Config, f).offset for f in fields]
+
+
+def test_shard_callback_returns_a_status(lib):
+    """mvc_sampler_set_shard's all_gather returns int (0 = done; nonzero fails
+    the sweep with MVC_ERR_CALLBACK before the exchange buffer is read)."""
+    assert lib.SHARD_CB._restype_ is ctypes.c_int
+    assert "int (*all_gather)(void *)" in open(HEADER).read()
+
+
+def test_hw_queue_request_keeps_a_user_setting(lib):
+    assert lib.hw_queues(None) == lib.HW_QUEUES
+    assert lib.hw_queues("4") == 4 and lib.hw_queues(" 8 ") == 8
+    assert lib.hw_queues("") == lib.HW_QUEUES and lib.hw_queues("many") == lib.HW_QUEUES
 
 
 def _call_run(lib, cfg, y):
@@ -60,6 +89,7 @@ def _call_run(lib, cfg, y):
 @pytest.mark.parametrize("field,value,needle", [
     ("n", 1, "n must be"), ("n_views", 0, "n_views"), ("dim", 0, "dim"), ("thin", 0, "thin"),
     ("n_chains", 0, "n_chains"), ("mode", 7, "mode"), ("n_iter", -1, "n_iter"),
+    ("n_devices", -1, "n_devices"), ("chain_stride", -2, "chain_stride"),
 ])
 def test_invalid_config_is_rejected_before_touching_a_device(lib, field, value, needle):
     from mvc_amd.sampler import make_config

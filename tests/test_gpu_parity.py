@@ -332,17 +332,15 @@ def test_parallel_warm_start(D):
     s.close()
 
 
-def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=None, expect_fused=None):
+def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=None):
     """Run `sweeps` warm-started sweeps forcing the lp producer (0 generic,
-    2 MFMA) and the phase-1 kernels ("fused" the one-pass MFMA + draw kernel,
-    "reg" lp buffer + register draw, "lds" lp buffer + checkpoint draw); check
-    the path taken on the first sweep."""
+    2 MFMA) and the phase-1 kernels ("reg" lp buffer + register draw, "lds"
+    lp buffer + checkpoint draw; "-perview" one producer launch per view);
+    check the path taken on the first sweep."""
     monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
     monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
-    monkeypatch.setenv("MVC_FUSED", "1" if draw == "fused" else "0")
     monkeypatch.setenv("MVC_LPALL", "0" if draw.endswith("-perview") else "1")
-    monkeypatch.setenv("MVC_LMV", "1" if draw.endswith("-lmv") else "0")   # view terms in the all-views producer
-    draw = draw.replace("-perview", "").replace("-lmv", "")
+    draw = draw.replace("-perview", "")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
     states = []
@@ -351,11 +349,7 @@ def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=
         if it == 0:          # later sweeps may leave the path's limits (births)
             zp = s.zpath()
             assert zp & 3 == path
-            if draw == "fused":
-                assert bool(zp & 8) == (True if expect_fused is None else expect_fused)
-            else:
-                assert not zp & 8
-                assert bool(zp & 4) == ((draw == "reg") if expect_reg is None else expect_reg)
+            assert bool(zp & 4) == ((draw == "reg") if expect_reg is None else expect_reg)
         states.append(s.state())
     s.close()
     return states
@@ -368,7 +362,6 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
     y, z = data.synthetic(2000, V, D, K, seed=5)
     st = _warm_state(z, V, K)
     out = [_run_path(m, y, st, 9, 3, p, monkeypatch) for p in (0, 2)]
-    out.append(_run_path(m, y, st, 9, 3, 2, monkeypatch, draw="fused"))
     for a in out[1:]:
         for sa, sb in zip(out[0], a):
             assert np.array_equal(sa[0], sb[0])
@@ -378,20 +371,17 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
 
 # MFMA lp producer (path 2): ragged tiles (n % 16 != 0), fewer tiles than
 # waves, D not a multiple of 16 (zero-padded k-steps), T > 64, K_v of 64;
-# phase 1 as the fused kernel (T <= 64 and an instantiated view pattern,
-# else the two-kernel path), or lp buffer + register draw (T <= 64, K_v <= 64)
-# or lp buffer + LDS checkpoint draw (any T)
-FUSED_SHAPES = {(3001, 4, 64, 16, 16): True, (50, 2, 20, 4, 4): True, (4000, 3, 32, 64, 96): False,
-                (2500, 2, 128, 64, 64): True, (1500, 3, 16, 32, 40): True, (2000, 2, 24, 8, 24): True,
-                (4100, 4, 128, 64, 64): True, (777, 1, 32, 16, 16): True}
+# phase 1 as lp buffer + register draw (T <= 64, K_v <= 64) or lp buffer +
+# LDS checkpoint draw (any T), the all-views producer or one launch per view
+ZPATH_SHAPES = [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96), (2500, 2, 128, 64, 64),
+                (1500, 3, 16, 32, 40), (2000, 2, 24, 8, 24), (4100, 4, 128, 64, 64), (777, 1, 32, 16, 16)]
 
 
-@pytest.mark.parametrize("draw", ["fused", "reg", "lds", "reg-perview", "reg-lmv"])
-@pytest.mark.parametrize("n,V,D,K,T", list(FUSED_SHAPES))
+@pytest.mark.parametrize("draw", ["reg", "lds", "reg-perview"])
+@pytest.mark.parametrize("n,V,D,K,T", ZPATH_SHAPES)
 def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     m = _mvc()
     from mvc_amd import data
-    T_gen = T
     y, z = data.synthetic(n, V, D, T, seed=n + D)
     uniq, table_of = np.unique(z, return_inverse=True)   # generating partition
     table_of = table_of.astype(np.int32)
@@ -399,8 +389,7 @@ def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
     hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
     st = (table_of, dish, hyper)
-    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw.startswith("reg") and T <= 64),
-                    expect_fused=FUSED_SHAPES[(n, V, D, K, T_gen)])
+    gpu = _run_path(m, y, st, 31, 3, 2, monkeypatch, draw=draw, expect_reg=(draw.startswith("reg") and T <= 64))
     ref = O.run(y, 3, 0, 1, seed=31, mode=O.PARALLEL, state=st)
     for it in range(3):
         t, d, h = gpu[it]
@@ -537,15 +526,18 @@ def test_timing_levels_do_not_change_the_chain():
     ref.close()
 
 
-@pytest.mark.parametrize("waves,repair", [("1", "run"), ("3", "run"), ("8", "grid")])
-def test_repair_shapes_same_chain(waves, repair, monkeypatch):
+@pytest.mark.parametrize("waves,repair,lc", [("1", "run", "1"), ("3", "run", "1"), ("8", "grid", "1"),
+                                             ("8", "run", "0"), ("3", "run", "0")])
+def test_repair_shapes_same_chain(waves, repair, lc, monkeypatch):
     """The repair's execution shape does not change the chain: the run kernel
-    evaluating 1 or 3 customers per step (fewer waves than the V = 5 views,
-    so birth dish draws wrap over the waves), and the grid-window path alone
-    (MVC_REPAIR=grid), all bitwise vs oracle SeqSampler through the births of
-    a cold start."""
+    evaluating 1, 3 or 8 customers per step (fewer waves than the V = 5
+    views, so birth dish draws wrap over the waves; the lane-column
+    evaluation, or MVC_LC=0 the one-wave-per-pass form), and the grid-window
+    path alone (MVC_REPAIR=grid), all bitwise vs oracle SeqSampler through the
+    births of a cold start."""
     monkeypatch.setenv("MVC_RUN_WAVES", waves)
     monkeypatch.setenv("MVC_REPAIR", repair)
+    monkeypatch.setenv("MVC_LC", lc)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.new_simulation(1999)
@@ -556,14 +548,11 @@ def test_repair_shapes_same_chain(waves, repair, monkeypatch):
     s.close()
 
 
-@pytest.mark.parametrize("team,waves,V", [("1", "8", 5), ("2", "8", 5), ("4", "8", 5), ("4", "1", 5),
-                                          ("2", "3", 3), ("4", "8", 4)])
-def test_repair_team_shapes(team, waves, V, monkeypatch):
-    """The run kernel evaluating each customer with a team of 1, 2 or 4 waves
-    (views split unevenly over the members when V = 3 or 5; one customer per
-    step with MVC_RUN_WAVES=1) gives the oracle SeqSampler chain bit for bit,
-    through the births of a cold start (D = 16: S1 in the LDS cache)."""
-    monkeypatch.setenv("MVC_TEAM", team)
+@pytest.mark.parametrize("waves,V", [("8", 5), ("1", 5), ("3", 3), ("8", 4)])
+def test_repair_run_shapes_d16(waves, V, monkeypatch):
+    """The run kernel evaluating 8, 3 or 1 customers per step (one wave each)
+    gives the oracle SeqSampler chain bit for bit, through the births of a
+    cold start (D = 16: S1 in the LDS cache)."""
     monkeypatch.setenv("MVC_RUN_WAVES", waves)
     m = _mvc()
     from mvc_amd import data
@@ -621,28 +610,6 @@ def test_dish_block_producer(force, monkeypatch):
     ref = O.run(y, 3, 0, 1, seed=5, mode=O.PARALLEL, state=st)
     _check_sweeps(s, ref, 3)
     assert s.zpath() & 64   # the dish-block producer ran
-    s.close()
-
-
-@pytest.mark.parametrize("lmv", ["0", "1"])
-def test_lpall_batches(lmv, monkeypatch):
-    """The all-views producer over customer batches (MVC_LPB_BATCH: the lp
-    buffer holds one batch, the draw follows each batch; the last batch
-    ragged): bitwise vs the oracle, warm, V = 4 at D = 32.  lmv = 1: the
-    producer also forms the view terms lm_v for the register draw
-    (MVC_LMV=1, opt-in)."""
-    monkeypatch.setenv("MVC_LPB_BATCH", "1024")
-    monkeypatch.setenv("MVC_LMV", lmv)
-    m = _mvc()
-    from mvc_amd import data
-    N, V, D, K = 5000, 4, 32, 16
-    y, z = data.synthetic(N, V, D, K, seed=23)
-    st = _warm_state(z, V, K)
-    s = m.Sampler(y, seed=9, mode="parallel")
-    s.set_state(*st)
-    ref = O.run(y, 3, 0, 1, seed=9, mode=O.PARALLEL, state=st)
-    _check_sweeps(s, ref, 3)
-    assert s.zpath() & 16   # the all-views producer ran
     s.close()
 
 

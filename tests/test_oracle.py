@@ -181,3 +181,29 @@ def test_warm_start_is_a_pure_function_of_the_state():
     b = O.run(y, 4, 0, 1, 11, mode=O.PARALLEL, state=(z.astype(np.int32), dish, hyper))
     assert all(np.array_equal(s, t) for s, t in zip(a["table_of"], b["table_of"]))
     _check_state(a["table_of"][-1], a["dish_of"][-1], 800)
+
+
+def test_phase_a_from_statistics_matches_the_sequential_sweep():
+    """oracle.phase_a (the sweep-start conditional from given statistics and
+    only the sampled rows; the CPU check of configs[4] at N = 10M) agrees
+    with the oracle's own sweep: on a state with movers, every customer
+    before the first mover draws its own table and the first mover does not."""
+    from mvc_amd import data
+    N, V, D, K = 2500, 3, 8, 6
+    y, z = data.synthetic(N, V, D, K, seed=12)
+    rng = np.random.default_rng(0)
+    z = z.copy()
+    flip = rng.choice(N, 200, replace=False)
+    z[flip] = rng.integers(0, K, 200)              # a perturbed partition: customers move
+    T = K
+    dish = np.stack([np.arange(T) % max(1, K >> v) for v in range(V)]).astype(np.int32)
+    hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
+    st = (z.astype(np.int32), dish, hyper)
+    stats = O.run(y, 0, 0, 1, seed=3, mode=O.PARALLEL, state=st)["stats"]
+    after = O.run(y, 1, 0, 1, seed=3, mode=O.PARALLEL, state=st)
+    moved = np.flatnonzero(after["table_of"][0] != z)
+    assert after["trace_moves"][0] > 0 and moved.size > 0
+    first = int(moved[0])
+    idx = np.arange(first + 1, dtype=np.int32)
+    ch = O.phase_a(z, dish, hyper, stats, 3, 0, 0, idx, np.stack([y[:, i, :] for i in idx]))
+    assert np.array_equal(ch[:first], z[:first]) and ch[first] != z[first]

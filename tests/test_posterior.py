@@ -14,6 +14,19 @@ Quantities: alpha_g, sigma_g, the number of tables, alpha_v, sigma_v, tau_v
 ~10^4 correlated entries, so at 4 sigma a few may exceed by chance: every
 entry must be within 6 sigma and at most 0.1 % of them beyond 4 sigma.
 
+test_underflow_divergence_is_confined_to_sweep0 pins where the parallel
+mode's conditional is NOT the reference's Markov kernel: the reference forms
+p[t] = (n_t - sigma_g) exp(sum_v log f_vk) in linear space, so a table whose
+probability underflows is excluded and a customer whose every probability
+underflows goes to table 0 with no draw (multiview_gibbs.cpp:169-176,
+multiview_utils.cpp:107,114); the parallel mode normalises by the maximum in
+log space and has neither effect.  Counted on cold starts (tau_v starts at
+0.0025 Var(y), multiview_gibbs.cpp:94): every fallback happens in sweep 0
+(New_Simulation.R's shape: ~15 of 200 customers per chain), the table count
+after sweep 0 differs (fewer tables in the reference), and from sweep 1 on
+the transient (mean T and sigma_g per sweep over 32 chains) agrees within 4
+MCSE.  DESIGN.md §2 states this divergence with these numbers.
+
 test_jacobi_schedule_is_biased keeps round 1's schedule (every customer
 against the sweep-start state) as a documented negative result: on the
 configs[0] shape it drifts to sigma_g ~ 0.9 and ~300 tables (the reference:
@@ -88,6 +101,33 @@ def test_parallel_schedule_matches_reference_posterior(name, M, burn):
     zc = _zscores(ce[:, iu[0], iu[1]], cp[:, iu[0], iu[1]])
     assert zc.max() < 6.0, f"co-clustering entry at {zc.max():.2f} MCSE"
     assert (zc > 4.0).mean() <= 1e-3, f"{(zc > 4.0).mean():.4%} of co-clustering entries beyond 4 MCSE"
+
+
+def _trace_chain(args):
+    name, mode, chain, M = args
+    r = O.run(_shape(name), M, 0, 1, seed=2024, chain=chain, mode=mode, math=O.LIBM)
+    return (r["trace_T"].astype(np.float64), np.asarray(r["sigma_global"]), r["trace_fallback"],
+            r["trace_uf_customers"])
+
+
+@pytest.mark.parametrize("name", ["newsim", "config1"])
+def test_underflow_divergence_is_confined_to_sweep0(name):
+    M, C = 30, 32
+    with get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
+        ex = pool.map(_trace_chain, [(name, O.EXACT, c, M) for c in range(C)])
+        pa = pool.map(_trace_chain, [(name, O.PARALLEL, c, M) for c in range(C)])
+    fallback = np.sum([e[2] for e in ex], axis=0)
+    assert fallback[0] > 0, "the reference's sum_p <= 0 fallback happens in the cold sweep"
+    assert fallback[1:].sum() == 0, f"fallbacks after sweep 0: {fallback[1:]}"
+    pa_fallback = np.sum([p_[2] for p_ in pa], axis=0)
+    assert pa_fallback.sum() == 0   # the parallel mode has no fallback (log space)
+    for k, lab in ((0, "T"), (1, "sigma_g")):
+        a = np.stack([e[k] for e in ex])
+        b = np.stack([p_[k] for p_ in pa])
+        z = _zscores(a[:, 1:], b[:, 1:])
+        assert z.max() < 4.0, f"{lab}: sweeps 1..{M - 1} differ at {z.max():.2f} MCSE (sweep {1 + z.argmax()})"
+    print(f"{name}: reference fallbacks in sweep 0 = {fallback[0] / C:.1f} per chain; tables after sweep 0: "
+          f"reference {np.mean([e[0][0] for e in ex]):.1f}, parallel mode {np.mean([p_[0][0] for p_ in pa]):.1f}")
 
 
 def test_jacobi_schedule_is_biased():
