@@ -179,7 +179,8 @@ def gpu_chains_line(config, seed, device, chains=16, sweeps=1):
     """Several chains of one config on one GPU at once (parallel-mode ChainSet:
     one stream and host thread per chain, the data shared), warm
     start at the generating partition: aggregate chain-sweeps/s.  The loader
-    asks HIP for 16 hardware queues, so 16 chains overlap."""
+    asks HIP for _lib.HW_QUEUES (32) hardware queues unless the user set
+    GPU_MAX_HW_QUEUES, so 16 chains overlap."""
     from mvc_amd import data
     from mvc_amd.sampler import Sampler
     N, V, D, K, desc = CONFIGS[config]
@@ -252,6 +253,44 @@ def config5_line(seed, device, steps=3, warmup=1):
             "hbm_gbs": round(byts / pass_s / 1e9, 1), "hbm_frac": round(byts / pass_s / 1e9 / PEAK_HBM_GBS, 4),
             "bound": "mfma", "dishes": kd.tolist(), "moves_last_sweep": rep["moves"],
             "producer": "mfma-dish-blocks" if zp & 64 else "other"}
+
+
+def newsim_call_line(seed, device, M=10000, M_short=2000):
+    """The reference's own caller (New_Simulation.R:123-133: N = 200, V = 5,
+    M = 10,000, burn-in 9,000, thin 1, the data of :47-60) through the
+    drop-in entry point mvc_run, in both schedules, against the reference's
+    algorithm on one host core (oracle ExactSampler<LibmMath>).  The parallel
+    schedule (the drop-in's default) runs the whole call; the exact schedule
+    and the host run M_short sweeps (their per-sweep cost is flat after the
+    first few hundred sweeps) and are reported as sweeps/s."""
+    import mvc_amd
+    from mvc_amd import data
+    y, _ = data.new_simulation(seed)
+    out = {"workload": "New_Simulation.R call: N=200 V=5 M=10000 burn_in=9000 thin=1, one chain"}
+    t0 = time.perf_counter()
+    mvc_amd.run_gibbs_cpp(y, M, M - 1000, 1, seed=seed, mode="parallel", device=device, quiet=True)
+    dt = time.perf_counter() - t0
+    out["parallel_gpu"] = {"sweeps": M, "s": round(dt, 2), "sweeps_per_s": round(M / dt, 1)}
+    t0 = time.perf_counter()
+    mvc_amd.run_gibbs_cpp(y, M_short, M_short - 200, 1, seed=seed, mode="exact", device=device, quiet=True)
+    dt = time.perf_counter() - t0
+    out["exact_gpu"] = {"sweeps": M_short, "s": round(dt, 2), "sweeps_per_s": round(M_short / dt, 1)}
+    out["default_mode"] = "parallel"
+    return out
+
+
+def newsim_call_cpu(seed, M_short=2000):
+    """CPU baseline of newsim_call_line: the reference's algorithm (oracle
+    ExactSampler<LibmMath>, the line-by-line restatement) on one host core,
+    M_short sweeps of the same call."""
+    from mvc_amd import data
+    from oracle import oracle as O
+    y, _ = data.new_simulation(seed)
+    t0 = time.perf_counter()
+    O.run(y, M_short, M_short - 200, 1, seed=seed, mode=O.EXACT, math=O.LIBM)
+    dt = time.perf_counter() - t0
+    return {"sweeps": M_short, "s": round(dt, 2), "sweeps_per_s": round(M_short / dt, 1), "cores": 1,
+            "kind": "reference-algorithm restatement (oracle ExactSampler<LibmMath>)", "host": host_cpu()}
 
 
 def cold_start(seed, device, sweeps=4):
@@ -446,10 +485,19 @@ def main():
             "configs1_gpu": leg("configs1_gpu", gpu_line, "c2", args.seed, local),
             "configs4_full_gpu": leg("configs4_full_gpu", config5_line, args.seed, local),
             "exact_schedule_gpu": leg("exact_schedule_gpu", gpu_exact_line, args.seed, local),
+            "newsim_call": leg("newsim_call", newsim_call_line, args.seed, local),
             "cold_start_gpu": leg("cold_start_gpu", cold_start, args.seed, local),
         }
         if not args.no_cpu_baseline:
             out["extra"]["reference_schedule_cpu"] = leg("reference_schedule_cpu", reference_schedule_cpu, args.seed)
+            out["extra"]["newsim_call"]["reference_cpu_1core"] = leg("newsim_call_cpu", newsim_call_cpu, args.seed)
+            # the chains' comparator: min(chains, nproc) host cores, one chain each
+            ch = out["extra"]["north_star_literal_gpu_16chains"]
+            cores = min(ch["chains"], os.cpu_count() or 1)
+            ref1 = out["extra"]["reference_schedule_cpu"]["value"]
+            ch["cpu_cores_compared"] = cores
+            ch["reference_cpu_same_cores"] = round(cores * ref1, 3)
+            ch["vs_reference_cpu_same_cores"] = round(ch["value"] / (cores * ref1), 3)
     if world == 1 and not args.no_cpu_baseline and y is not None:
         out["cpu_baseline"] = leg("cpu_baseline", cpu_baseline, y, z, V, K, D, args.seed)
     print(json.dumps(out), flush=True)

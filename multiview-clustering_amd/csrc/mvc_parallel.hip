@@ -1794,7 +1794,10 @@ class ParallelSampler : public Sampler {
   bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
-  int run_waves = kSeqRunWaves;   // MVC_RUN_WAVES: customers the run kernel evaluates per step (tuning)
+  // MVC_RUN_WAVES: customers the run kernel evaluates per step.  4 by default:
+  // one evaluating wave per SIMD (a second wave on a SIMD halves the first
+  // customer's issue rate, and with dense movers the first customer decides)
+  int run_waves = 4;
   bool use_wide = true;           // MVC_WIDE=0: global-scratch run kernel speculates one customer per wave
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
@@ -1914,7 +1917,7 @@ class ParallelSampler : public Sampler {
     lpall_attr<8, 8>();
     lpall_attr<16, 8>();
     // (instance 2 runs the global-scratch layout only: no dynamic LDS)
-    for (const void *f : {(const void *)mvc_seq_run_kernel<0>})
+    for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {
@@ -2528,7 +2531,7 @@ class ParallelSampler : public Sampler {
       if (L.nws >= std::min(cap, s1 ? 4 : 2)) {
         L.lds = 1;
         L.tw = 1;
-        L.lc = (use_lc && s1 && L.ts <= 64 * kLcChunks) ? 1 : 0;
+        L.lc = 0;   // the lane-column kernel needs the ring (set below)
         // the staged-row ring in what is left: a power of two >= 2 nws customers
         const int64_t slot = seq_ring_slot(V, D);
         const int64_t left = room - (int64_t)L.nws * L.stride;
@@ -2538,6 +2541,8 @@ class ParallelSampler : public Sampler {
             if ((int64_t)r * slot <= left) { rn = r; break; }
         L.ring = rn;
         L.pfn = rn ? std::max(1, rn / 2) : 0;
+        L.lc = (use_lc && s1 && rn > 0 && L.ts <= 64 * kLcChunks) ? 1 : 0;
+        if (L.lc) L.nws = std::min(L.nws, kSeqLcThreads / 64);   // its block has 4 waves
         return L;
       }
     }
@@ -2583,8 +2588,8 @@ class ParallelSampler : public Sampler {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
         else
-          hipLaunchKernelGGL(L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
-                             dim3(1), dim3(kSeqRunThreads),
+          hipLaunchKernelGGL(L.lc ? mvc_seq_run_kernel<3> : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
+                             dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads),
                              L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
                              stream, Q, L);
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
@@ -2649,10 +2654,16 @@ class ParallelSampler : public Sampler {
   // 209-216, 251-258).  The repair step that overflowed changed nothing and
   // is redone.
   void grow_capacity(int flags) {
-    const int TC2 = (flags & 1) ? std::min(kParTC, 2 * TC) : TC;
+    // the table limit: the MH's three-level tree64 over the table sizes
+    // (64^3 = 262,144); MVC_MAX_TABLES lowers it (tests of the limit's error)
+    int max_tc = kParTC;
+    if (const char *e = getenv("MVC_MAX_TABLES")) max_tc = std::max(16, std::min(kParTC, atoi(e)));
+    const int TC2 = (flags & 1) ? std::min(max_tc, 2 * TC) : TC;
     const int KC2 = (flags & 2) ? std::min(kParKC, 2 * KC + 1) : KC;
     if (TC2 == TC && KC2 == KC)
-      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: more than 262144 tables or 262143 dishes per view");
+      throw Error(MVC_ERR_UNSUPPORTED, "parallel mode: a birth needs table " + std::to_string(TC + 1) + " (limit " +
+                                           std::to_string(max_tc) + " tables, " + std::to_string(kParKC) +
+                                           " dishes per view); the sweep stopped at that customer, so the handle cannot continue");
     flush_saves();
     for (SaveSlot &q : saves) {   // the ring slots are capacity-sized
       for (void *p : {(void *)q.dz, (void *)q.ddish, (void *)q.ddid, (void *)q.dhyp}) retire(p);

@@ -45,13 +45,15 @@ struct Repair {
 
 constexpr int32_t kSeqScan = 0, kSeqRun = 1;
 
-// MVC_RUN_PROF builds (scripts/build_variant.sh NAME -DMVC_RUN_PROF): wave 0
-// of the run kernel accumulates wall-clock ticks (100 MHz) per phase; thread 0
-// prints them when the kernel exits.  Tuning aid only.
+// MVC_RUN_PROF builds (scripts/build_variant.sh NAME -DMVC_RUN_PROF): thread 0
+// of the run kernel accumulates wall-clock ticks (100 MHz) per phase in LDS
+// (no global read-modify-write inside the timed phases) and adds them to
+// R->prof when the kernel exits; the host prints them per sweep.  Tuning aid only.
 #ifdef MVC_RUN_PROF
+__shared__ unsigned long long mvc_prof_lds[8];
 #define RUN_T0() uint64_t _rt = wall_clock64()
 #define RUN_MARK(k) do { const uint64_t _n = wall_clock64(); \
-    if (threadIdx.x == 0 && blockDim.x == kSeqRunThreads) A.R->prof[k] += _n - _rt; _rt = _n; } while (0)
+    if (threadIdx.x == 0) mvc_prof_lds[k] += _n - _rt; _rt = _n; } while (0)
 #else
 #define RUN_T0() do {} while (0)
 #define RUN_MARK(k) do {} while (0)
@@ -59,6 +61,9 @@ constexpr int32_t kSeqScan = 0, kSeqRun = 1;
 // run kernel block: 8 waves (256 VGPRs each: the per-customer evaluation
 // spills at the 128 VGPRs of a 16-wave block)
 constexpr int kSeqRunThreads = 512, kSeqRunWaves = kSeqRunThreads / 64;
+// the lane-column run kernel: 4 waves, one per SIMD (its evaluation is issue-
+// bound; a second wave per SIMD would halve the first customer's rate)
+constexpr int kSeqLcThreads = 256;
 
 // LDS layout of the run kernel's per-wave scratch (host-chosen at launch):
 // lp [V][ks] | e [ts + 16] | B, C [ts/16 + 2]; nws waves speculate.
@@ -1054,6 +1059,7 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
   const int Tne_i = *W.T_ne - (alive ? 0 : 1);
   const double mass0 = (double)np0 - sg;
   double s_new = 0.0, lmass0 = 0.0;
+  const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);   // independent of the rest
   RUN_T0();
   for (int g = 0; g < V; g += 4) {
     const int v = g + row;
@@ -1061,20 +1067,20 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     const int vv = vok ? v : V - 1;   // rows past the last view mirror it (their results are not used)
     const int K = vok ? W.Klist[vv] : 0;
     const double tau = hyp[vv], alpha = hyp[V + vv], sigma = hyp[2 * V + vv];
-    const double Y2i = C.Y2[(size_t)vv * C.y2stride];
+    const double Y2i = C.Y2[vv * (int)C.y2stride];
     const double hy = 0.5 * Y2i;
     const double h = (-0.5 * Y2i) / tau;
     const double lfn = cnewv[vv] + h;
     const int j0 = W.dish[vv * ts + p0];
-    const double *yv = C.y + (size_t)vv * C.ystride;
-    const double *S1v = W.S1T + (size_t)vv * D * s1s;
+    const double *yv = C.y + vv * (int)C.ystride;
+    const double *S1v = W.S1T + vv * D * s1s;
     const int *dl = W.d_l + vv * ks;
-    double *lpv = S.lp + (size_t)vv * lps;
+    double *lpv = S.lp + vv * lps;
     // the own dish with the customer removed, every lane of the row
     double self;
     {
       double G = 0.0;
-      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[(size_t)d * s1s + j0], G);
+      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j0], G);
       const double Gp = G - Y2i;
       const double Qp = (W.Q[vv * ks + j0] - 2.0 * G) + Y2i;
       const double c0 = W.xm[vv * ks + j0] - (0.5 * Qp) / W.ym[vv * ks + j0];
@@ -1087,7 +1093,7 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     int cnt = 0;
     for (int j = col; j < K; j += 16) {
       double G = 0.0;
-      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[(size_t)d * s1s + j], G);
+      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j], G);
       const double fr = __builtin_fma(G + hy, W.cb[vv * ks + j], W.c0[vv * ks + j]) + h;
       const bool own = j == j0;
       const double val = own ? self : fr;
@@ -1104,12 +1110,10 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     // column partial: w_j exp(lp_j - m) in ascending j (excluded dishes add +0)
     double cs = 0.0;
     for (int j = col; j < K; j += 16) {
-      const bool own = j == j0;
-      const int l = own ? l0p : dl[j];
+      const int l = (j == j0) ? l0p : dl[j];
       double w = (double)l - sigma;
       if (w < 0.0) w = 0.0;
-      const double x = lpv[j];
-      cs = cs + w * mvc_exp_le0(l > 0 ? x - m : -MVC_PM_INF);
+      cs = cs + w * mvc_exp_le0(l > 0 ? lpv[j] - m : -MVC_PM_INF);
     }
     double Sv = row_pw16(cs);
     double wn = alpha + (double)cnt * sigma;
@@ -1136,18 +1140,46 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
   // -inf when excluded; to the wave's scratch e[]
   const int T = *W.T, TB = (T + 15) >> 4, nch = (T + 63) >> 6;
   double M = -MVC_PM_INF;
-  for (int q = 0; q < nch; ++q) {
-    const int p = 64 * q + lane;
-    const int np = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
-    const double mass = (double)np - sg;
-    const bool inc = p < T && np >= 1 && mass > 0.0;
-    double x = inc ? (p == p0 ? lmass0 : W.lmass[p]) : -MVC_PM_INF;
-    for (int v = 0; v < V; ++v) {
-      const double lv = S.lp[(size_t)v * lps + (inc ? W.dish[v * ts + p] : 0)];
-      if (inc) x = x + lv;
+  // two 64-table chunks per step, every view's dish index loaded before the
+  // gathers (4 views at a time): two dependent LDS latencies per step, not 2 V
+  for (int q0 = 0; q0 < nch; q0 += 2) {
+    double x[2];
+    bool inc[2];
+    int pp[2];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int p = 64 * (q0 + h2) + lane;
+      pp[h2] = p;
+      const int np = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+      const double mass = (double)np - sg;
+      inc[h2] = p < T && np >= 1 && mass > 0.0;
+      x[h2] = inc[h2] ? (p == p0 ? lmass0 : W.lmass[p]) : -MVC_PM_INF;
     }
-    S.e[p] = x;
-    if (x > M) M = x;
+    for (int v0 = 0; v0 < V; v0 += 4) {
+      int dj[2][4];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          dj[h2][u] = (inc[h2] && v0 + u < V) ? W.dish[(v0 + u) * ts + pp[h2]] : 0;
+      double lv[2][4];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + dj[h2][u]];
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (inc[h2] && v0 + u < V) x[h2] = x[h2] + lv[h2][u];   // view order
+    }
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      if (q0 + h2 < nch) {
+        S.e[pp[h2]] = x[h2];
+        if (x[h2] > M) M = x[h2];
+      }
+    }
   }
   M = wave_max(M);
   if (s_new > M) M = s_new;
@@ -1155,22 +1187,31 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
   // weights exp(sp - M) (0 where excluded or past T), block sums pw16 per
   // row, running block totals C_b kept in lane b
   double tot = 0.0, Cb = 0.0;
-  for (int q = 0; q < nch; ++q) {
-    const int p = 64 * q + lane;
-    const double e = mvc_exp_le0(S.e[p] - M);
-    S.e[p] = e;
-    const double B = row_pw16(e);
+  for (int q0 = 0; q0 < nch; q0 += 2) {
+    double e[2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int b = 4 * q + r;
-      if (b < TB) {
-        tot = tot + readlane_d(B, 16 * r);
-        if (lane == b) Cb = tot;
+    for (int h2 = 0; h2 < 2; ++h2) e[h2] = S.e[64 * min(q0 + h2, nch - 1) + lane];
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) e[h2] = mvc_exp_le0(e[h2] - M);
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int q = q0 + h2;
+      if (q < nch) {
+        S.e[64 * q + lane] = e[h2];
+        const double B = row_pw16(e[h2]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int b = 4 * q + r;
+          if (b < TB) {
+            tot = tot + readlane_d(B, 16 * r);
+            if (lane == b) Cb = tot;
+          }
+        }
       }
     }
   }
   const double Wt = mvc_exp_le0(s_new - M) + tot;
-  double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * Wt;
+  double r = u_i * Wt;
   if (!(r < tot)) {
     RUN_MARK(2);
     return -1;
@@ -1290,6 +1331,7 @@ struct SCache {
   double *S2;                  // [V][ks]: the commit's S2 read-modify-writes stay in LDS (stores to HBM only)
   double *S1T;   // nullptr: S1 is read from global memory
   const double *hyp, *L2pt;    // the sweep's hyperparameters [3V+2] and log(2 pi tau) [V], staged at launch
+  const double *cnew;          // [V] D (-1/2 log(2 pi tau)), staged at launch
   int ts, ks;
 };
 __device__ __forceinline__ SView cache_view(const SCache &c, const SeqArgs &A) {
@@ -1302,6 +1344,43 @@ __device__ __forceinline__ SView cache_view(const SCache &c, const SeqArgs &A) {
   W.Klist = c.Klist; W.Ltot = c.Ltot; W.T = c.T; W.T_ne = c.T_ne;
   W.ts = c.ts; W.ks = c.ks;
   return W;
+}
+
+// The run kernel's dynamic LDS (the state cache, per-wave scratch, ring) and
+// its per-sweep constants (hyper [3V+2] | cnew [V] | L2pt [V]).  Every
+// pointer into them is derived here from the symbols themselves, never
+// loaded from memory, so the compiler keeps LDS accesses as ds_* (a pointer
+// that went through a struct in memory would be a flat access, which also
+// waits on every outstanding global store).
+extern __shared__ double mvc_seq_lds[];
+__shared__ double mvc_seq_const[5 * MVC_MAXV + 2];
+__device__ __forceinline__ SCache lds_cache(int V, int D, int ts, int ks, int s1) {
+  SCache cc{};
+  int32_t *ip = (int32_t *)mvc_seq_lds;
+  cc.ts = ts;
+  cc.ks = ks;
+  cc.n_t = ip; ip += ts;
+  cc.dish = ip; ip += V * ts;
+  cc.d_l = ip; ip += V * ks;
+  cc.d_n = ip; ip += V * ks;
+  cc.Klist = ip; ip += V;
+  cc.Ltot = ip; ip += V;
+  cc.T = ip++;
+  cc.T_ne = ip++;
+  double *dp = mvc_seq_lds + (ip - (int32_t *)mvc_seq_lds + 1) / 2;
+  cc.c0 = dp; dp += V * ks;
+  cc.cb = dp; dp += V * ks;
+  cc.Q = dp; dp += V * ks;
+  cc.xm = dp; dp += V * ks;
+  cc.ym = dp; dp += V * ks;
+  cc.cbm = dp; dp += V * ks;
+  cc.lmass = dp; dp += ts;
+  cc.S2 = dp; dp += V * ks;
+  cc.S1T = s1 ? dp : nullptr;
+  cc.hyp = mvc_seq_const;
+  cc.cnew = mvc_seq_const + 3 * MVC_MAXV + 2;
+  cc.L2pt = mvc_seq_const + 4 * MVC_MAXV + 2;
+  return cc;
 }
 
 // The parts of coef(n - 1, Qp) that do not depend on the customer (the own
@@ -1523,6 +1602,111 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
   return true;
 }
 
+// A move p0 -> c (c >= 0) committed by ONE wave, for the run kernel with its
+// whole state in LDS (S1 included): the updates of seq_commit (oracle
+// SeqSampler::move) in the same operations and order per quantity, lane-
+// parallel, with no block barrier inside (one wave's LDS operations execute
+// in order; the caller's next block barrier publishes them).  Global arrays
+// are written through (store only) for the kernels after this one.
+__device__ void seq_commit_move_wave(SeqArgs &A, const SCache &cc, const Cust &Ci, int i, int p0, int c,
+                                     int32_t *cnt) {
+  ParState &P = A.P;
+  Repair *R = A.R;
+  const int lane = threadIdx.x & 63;
+  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, ks = cc.ks, ts = cc.ts;
+  const double *hyp = cc.hyp, *l2pt = cc.L2pt;
+  const double sg = hyp[3 * V + 1];
+  // every read of the old state first
+  const int nt0 = cc.n_t[p0] - 1, ntc = cc.n_t[c];
+  const bool dies = nt0 == 0, born = ntc == 0;
+  const int Tne = *cc.T_ne - (dies ? 1 : 0) + (born ? 1 : 0);
+  // the two tables' log masses, one log per lane (lanes 0, 1)
+  const double lmv = mvc_log((double)(lane == 0 ? nt0 : ntc + 1) - sg);
+  if (lane == 0) {
+    cc.n_t[p0] = nt0;
+    cc.n_t[c] = ntc + 1;
+    cc.lmass[p0] = lmv;
+    *cc.T_ne = Tne;
+    P.n_t[p0] = nt0;
+    P.n_t[c] = ntc + 1;
+    P.lmass[p0] = lmv;
+    R->T_ne = Tne;
+    P.z[i] = c;
+    cnt[0] += 1;
+  }
+  if (lane == 1) {
+    cc.lmass[c] = lmv;
+    P.lmass[c] = lmv;
+  }
+  // per view (lane v): table counts of the two dishes, S2, n
+  if (lane < V) {
+    const int v = lane;
+    const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+    if (dies || born) {
+      int L = cc.Ltot[v];
+      if (dies) {
+        const int l = cc.d_l[v * ks + j0] - 1;
+        cc.d_l[v * ks + j0] = l;
+        P.d_l[v * KC + j0] = l;
+        --L;
+      }
+      if (born) {
+        const int l = cc.d_l[v * ks + j1] + 1;   // after the decrement above when j1 == j0
+        cc.d_l[v * ks + j1] = l;
+        P.d_l[v * KC + j1] = l;
+        ++L;
+      }
+      cc.Ltot[v] = L;
+      P.Ltot[v] = L;
+    }
+    if (j0 != j1) {
+      const double y2 = Ci.Y2[(size_t)v * Ci.y2stride];
+      const double a0 = cc.S2[v * ks + j0] - y2, a1 = cc.S2[v * ks + j1] + y2;
+      cc.S2[v * ks + j0] = a0;
+      cc.S2[v * ks + j1] = a1;
+      P.S2[v * KC + j0] = a0;
+      P.S2[v * KC + j1] = a1;
+      const int n0 = cc.d_n[v * ks + j0] - 1, n1 = cc.d_n[v * ks + j1] + 1;
+      cc.d_n[v * ks + j0] = n0;
+      cc.d_n[v * ks + j1] = n1;
+      P.d_n[v * KC + j0] = n0;
+      P.d_n[v * KC + j1] = n1;
+    }
+  }
+  // S1 of the two dishes of every view that changed dish (lanes over (v, d))
+  for (int e = lane; e < V * D; e += 64) {
+    const int v = e / D, d = e - v * D;
+    const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+    if (j0 == j1) continue;
+    const double yd = Ci.y[(size_t)v * Ci.ystride + d];
+    double *cl = cc.S1T + ((size_t)v * D + d) * ks;
+    const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
+    cl[j0] = a0;
+    cl[j1] = a1;
+    double *col = P.S1T + ((size_t)v * D + d) * KC;
+    col[j0] = a0;
+    col[j1] = a1;
+  }
+  // Q and the coefficients of the two dishes (oracle refresh_dish), lanes over (v, which)
+  if (lane < 2 * V) {
+    const int v = lane >> 1;
+    const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+    const int j = (lane & 1) ? j1 : j0;
+    if (j0 != j1) {
+      const double q = fma_sq_strided(cc.S1T + (size_t)v * D * ks + j, (size_t)ks, D);
+      const int nj = cc.d_n[v * ks + j];
+      const Coef cf = coef(nj, q, hyp[v], l2pt[v], D);
+      cc.Q[v * ks + j] = q;
+      cc.c0[v * ks + j] = cf.c0;
+      cc.cb[v * ks + j] = cf.cb;
+      self_coef_parts(nj, hyp[v], l2pt[v], D, cc.xm[v * ks + j], cc.ym[v * ks + j], cc.cbm[v * ks + j]);
+      P.Q[v * KC + j] = q;
+      P.c0[v * KC + j] = cf.c0;
+      P.cb[v * KC + j] = cf.cb;
+    }
+  }
+}
+
 // Resolve the grid window evaluated by the last mvc_seq_eval_kernel (thread 0).
 __device__ void seq_resolve_window(const SeqArgs &A, Repair *R) {
   const int n = A.P.n;
@@ -1656,8 +1840,7 @@ __device__ __forceinline__ int ring_z(const Ring &G, int c, int V, int D) {
 // global arrays.  Returns through ovf / restride why it stopped early.
 template <bool kLds, bool kWide>
 __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
-                             const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride,
-                             const double *hypc = nullptr, const double *cnewc = nullptr) {
+                             const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride) {
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
@@ -1674,7 +1857,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       const SeqScratch S0(A, 0);
       const bool reuse = kWide && !kLds && U.lpc == U.cur;
       if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt,
-                      kLds ? L.nws : (int)(blockDim.x >> 6), reuse ? &S0 : nullptr, lsync)) {
+                             kLds ? L.nws : (int)(blockDim.x >> 6), reuse ? &S0 : nullptr, lsync)) {
         // overflow: the host grows and relaunches
         ovf = 1;
         return;
@@ -1762,7 +1945,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         p0 = P.z[i];
         C = global_cust(A, i);
       }
-      const int c = (kLds && L.lc) ? seq_resample_lc(A, Wv, C, i, p0, S, hypc, cnewc) : seq_resample(A, Wv, C, i, p0, S);
+      const int c = seq_resample(A, Wv, C, i, p0, S);
       if (lane == 0) {
         U.ch[w] = c;
         U.p0[w] = p0;
@@ -1796,7 +1979,142 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
     seq_bar(lsync);
     RUN_MARK(6);
 #ifdef MVC_RUN_PROF
-    if (tid == 0) A.R->prof[7] += 1;
+    if (tid == 0) mvc_prof_lds[7] += 1;
+#endif
+    if (!U.go) return;
+  }
+}
+
+// The birth commit of the lane-column run kernel, out of line: births are
+// rare, and inlined the general commit (dish draws, tree64, capacity checks)
+// would raise the register pressure of the whole loop.
+__device__ __attribute__((noinline)) bool seq_commit_birth(SeqArgs &A, const SeqLds &L, const Cust &Ci, int i, int p0,
+                                                           double *lpw, double *treew, int32_t *cnt, int nwd) {
+  const SCache cc = lds_cache(A.P.V, A.P.D, L.ts, L.ks, 1);
+  return seq_commit(A, cache_view(cc, A), &cc, Ci, i, p0, -1, lpw, treew, cnt, nwd, nullptr, false);
+}
+
+// seq_run_loop for the lane-column evaluation (L.lc: the whole state in LDS,
+// S1 included, the staged-row ring): moves committed by wave 0
+// (seq_commit_move_wave), births out of line, LDS-only barriers.  Compiled as
+// its own kernel instance so nothing of the other evaluation shapes sits in
+// its registers.
+__device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, double *tree, RunCursor &U, int &ovf,
+                                int &restride) {
+  const ParState &P = A.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int V = P.V, D = P.D, n = P.n;
+  const SCache cc = lds_cache(V, D, L.ts, L.ks, 1);   // L.lc implies S1 in LDS
+  SView Wv = cache_view(cc, A);
+  Wv.S1T = cc.S1T;                                      // no select against the global copy: LDS for sure
+  Wv.s1s = cc.ks;
+  const SeqScratch S(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts);
+  if (U.pend) {   // a mover carried over from the previous launch (a resolved window): stage its row first
+    ring_fill_async(A, G, U.cur, U.cur + 1);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+      U.fill = U.cur + 1;
+      U.landed = U.cur + 1;
+    }
+    __syncthreads();
+  }
+  for (;;) {
+    RUN_T0();
+    if (U.pend) {
+      // the mover was evaluated in the previous step (or staged above), so its
+      // row is in the ring (landed, not yet reused: requests stop a ring ahead of it)
+      const Cust Ci = G.cust(U.cur, V, D);
+      if (U.pc >= 0) {
+        if (w == 0) seq_commit_move_wave(A, cc, Ci, U.cur, U.pp0, U.pc, U.cnt);
+      } else {
+        __syncthreads();
+        const bool ok = seq_commit_birth(A, L, Ci, U.cur, U.pp0, S.lp, tree, U.cnt, L.nws);
+        __syncthreads();
+        if (!ok) {
+          ovf = 1;
+          return;
+        }
+      }
+      RUN_MARK(3);
+      if (tid == 0) {
+        U.cur = U.cur + 1;
+        U.pend = 0;
+        U.streak = 0;
+      }
+    }
+    if (tid == 0) {
+      U.stop = 0;
+      if (U.cur >= n) {
+        U.done = 1;
+        U.stop = 1;
+      } else {   // the LDS layout must hold the current lists plus one birth
+        int bad = *cc.T >= L.ts ? 1 : 0;
+        for (int v = 0; v < V; ++v) bad |= cc.Klist[v] >= L.ks ? 1 : 0;
+        if (bad) U.stop = 2;
+      }
+      U.i = U.cur;
+    }
+    seq_bar(true);
+    RUN_MARK(4);
+    if (U.stop) {
+      restride = U.stop == 2;
+      return;
+    }
+    const int i0 = U.i;
+    const int need = min(n, i0 + L.nws);
+    // rows in batches half a ring ahead; a step waits only beyond what has landed
+    int fill_next = max(U.fill, i0), landed_next = U.landed;
+    if (need > U.landed) {
+      if (fill_next < need) {
+        ring_fill_async(A, G, fill_next, need);
+        fill_next = need;
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      landed_next = fill_next;
+    }
+    if (fill_next - i0 <= G.n / 2 && fill_next < n) {
+      const int f1 = min(n, i0 + G.n);
+      ring_fill_async(A, G, fill_next, f1);
+      fill_next = f1;
+    }
+    const int i = i0 + w;
+    if (w < L.nws && i < n) {
+      const int p0 = ring_z(G, i, V, D);
+      const int c = seq_resample_lc(A, Wv, G.cust(i, V, D), i, p0, S, cc.hyp, cc.cnew);
+      if (lane == 0) {
+        U.ch[w] = c;
+        U.p0[w] = p0;
+      }
+    }
+    seq_bar(true);
+    RUN_MARK(5);
+    if (tid == 0) {
+      U.fill = fill_next;
+      U.landed = landed_next;
+      int f = -1;
+      const int m = min(L.nws, n - U.i);
+      for (int k = 0; k < m; ++k)
+        if (U.ch[k] != U.p0[k]) { f = k; break; }
+      if (f >= 0) {
+        U.cur = U.i + f;
+        U.pend = 1;
+        U.pc = U.ch[f];
+        U.pp0 = U.p0[f];
+        U.lpc = -1;
+      } else {
+        U.cur = U.i + m;
+        U.streak += m;
+        if (U.streak >= L.limit) U.mode = kSeqScan;
+        if (U.cur >= n) U.done = 1;
+      }
+      U.go = !U.done && (U.mode == kSeqRun || U.pend);
+    }
+    seq_bar(true);
+    RUN_MARK(6);
+#ifdef MVC_RUN_PROF
+    if (tid == 0) mvc_prof_lds[7] += 1;
 #endif
     if (!U.go) return;
   }
@@ -1816,14 +2134,16 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 // window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
 // One instance per evaluation shape, compiled separately so each keeps its
 // own register allocation.
-template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout)
-__global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
-  extern __shared__ double seq_sm[];
+template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc)
+__global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, w = tid >> 6, nt = blockDim.x;
   const int V = P.V, D = P.D, n = P.n, KC = P.KC, TC = P.TC;
   __shared__ RunCursor U;
+#ifdef MVC_RUN_PROF
+  if (tid < 8) mvc_prof_lds[tid] = 0;
+#endif
   if (tid == 0) {
     const int go = !(R->done || R->overflow || R->restride);
     if (go && R->win1 > R->win0) {
@@ -1865,39 +2185,15 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
   int ovf = 0, restride = 0;
   double *tree = SeqScratch(A, w).tree;   // global per-wave scratch: the dish draws' tree64 levels
   if (L.lds) {   // the state cache, from the global state at launch
-    SCache cc{};
     const int ts = L.ts, ks = L.ks;
-    int32_t *ip = (int32_t *)seq_sm;
-    cc.ts = ts;
-    cc.ks = ks;
-    cc.n_t = ip; ip += ts;
-    cc.dish = ip; ip += V * ts;
-    cc.d_l = ip; ip += V * ks;
-    cc.d_n = ip; ip += V * ks;
-    cc.Klist = ip; ip += V;
-    cc.Ltot = ip; ip += V;
-    cc.T = ip++;
-    cc.T_ne = ip++;
-    double *dp = seq_sm + (ip - (int32_t *)seq_sm + 1) / 2;
-    cc.c0 = dp; dp += V * ks;
-    cc.cb = dp; dp += V * ks;
-    cc.Q = dp; dp += V * ks;
-    cc.xm = dp; dp += V * ks;
-    cc.ym = dp; dp += V * ks;
-    cc.cbm = dp; dp += V * ks;
-    cc.lmass = dp; dp += ts;
-    cc.S2 = dp; dp += V * ks;
-    cc.S1T = L.s1 ? dp : nullptr;
+    const SCache cc = lds_cache(V, D, ts, ks, L.s1);
     // the sweep's hyperparameters and per-view constants (the evaluation and
     // the commits read them from LDS; the MH changes them only after the repair)
-    __shared__ double s_hyp[3 * MVC_MAXV + 2], s_cnew[MVC_MAXV], s_l2pt[MVC_MAXV];
-    for (int k = tid; k < 3 * V + 2; k += nt) s_hyp[k] = P.hyper[k];
+    for (int k = tid; k < 3 * V + 2; k += nt) mvc_seq_const[k] = P.hyper[k];
     for (int k = tid; k < V; k += nt) {
-      s_cnew[k] = A.cnew[k];
-      s_l2pt[k] = A.L2pt[k];
+      mvc_seq_const[3 * MVC_MAXV + 2 + k] = A.cnew[k];
+      mvc_seq_const[4 * MVC_MAXV + 2 + k] = A.L2pt[k];
     }
-    cc.hyp = s_hyp;
-    cc.L2pt = s_l2pt;
     const int T = R->T;
     for (int k = tid; k < T; k += nt) {
       cc.n_t[k] = P.n_t[k];
@@ -1937,16 +2233,22 @@ __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, 
     Ring G;
     G.n = L.ring;
     G.slot = (int)seq_ring_slot(V, D);
-    G.base = seq_sm + L.cache_dbl + (int64_t)L.nws * L.stride;
-    seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
-                              SeqScratch(seq_sm + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts), G,
-                              tree, U, ovf, restride, s_hyp, s_cnew);
+    G.base = mvc_seq_lds + L.cache_dbl + (int64_t)L.nws * L.stride;
+    if constexpr (kMode == 3)
+      seq_run_loop_lc(A, L, G, tree, U, ovf, restride);
+    else
+      seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
+                                SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts), G,
+                                tree, U, ovf, restride);
     __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
-  } else {
+  } else if constexpr (kMode != 3) {   // (the lane-column kernel always has the LDS layout)
     Ring G{nullptr, 0, 0};
     seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
+#ifdef MVC_RUN_PROF
+    for (int k = 0; k < 8; ++k) R->prof[k] += mvc_prof_lds[k];
+#endif
     R->cur = U.cur;
     R->pend = U.pend;
     R->pchoice = U.pc;

@@ -13,6 +13,13 @@ The clustering is scored (mcclust::arandi, as New_Simulation.R:189 scores
 its clusters) against the 6 most frequent TOPICS labels: documents whose
 TOPICS hold exactly one of them; the other documents are clustered but not
 scored.
+
+Label leak: the reference's third view holds every <D> value of a document
+(pre-process.R:88-102), and the TOPICS values (the ARI truth) are <D> values
+too -- 120 of its 445 columns.  views(..., drop_topics=True) zeroes those 120
+columns (the random projection then never sees them), so an ARI computed on
+it measures clustering from the other fields (body, title, PLACES, PEOPLE,
+ORGS, EXCHANGES) alone.  The default keeps the reference's view.
 """
 import os
 
@@ -37,12 +44,24 @@ def counts():
                 _csr(z, "topics", z["topics_terms"]))
 
 
-def views(D=64, seed=2026):
-    """float64 [3][N][D]: log1p(counts) @ R_v per view, R_v ~ N(0, 1/D)."""
+def topics_columns():
+    """Column indices of the third view whose <D> value is a TOPICS value."""
+    with np.load(COUNTS) as z:
+        names, topics = z["topics_names"], set(z["label_names"].tolist())
+    return np.array([j for j, x in enumerate(names.tolist()) if x in topics], np.int64)
+
+
+def views(D=64, seed=2026, drop_topics=False):
+    """float64 [3][N][D]: log1p(counts) @ R_v per view, R_v ~ N(0, 1/D).
+    drop_topics: zero the third view's TOPICS columns (the ARI truth) first."""
     out = []
     for v, X in enumerate(counts()):
         X = X.copy()
         X.data = np.log1p(X.data)
+        if v == 2 and drop_topics:
+            keep = np.ones(X.shape[1])
+            keep[topics_columns()] = 0.0
+            X = X.multiply(keep[None, :]).tocsr()
         R = np.random.default_rng([seed, v]).standard_normal((X.shape[1], D)) / np.sqrt(D)
         out.append(np.ascontiguousarray(X @ R))
     return np.stack(out)

@@ -133,7 +133,7 @@ def main():
         title_indptr=tp, title_indices=ti, title_data=td, title_terms=np.array(len(tv)),
         topics_indptr=np.array(kp, np.int64), topics_indices=np.array(ki, np.int32), topics_terms=np.array(len(dvocab)),
         label_indptr=np.array(lp, np.int64), label_indices=np.array(li, np.int32),
-        label_names=np.array(tvocab))
+        label_names=np.array(tvocab), topics_names=np.array(dvocab))
     print(f"{len(docs)} documents; body {len(bv)} terms ({bi.size} nonzeros), title {len(tv)} terms, "
           f"<D> values {len(dvocab)}, TOPICS values {len(tvocab)} -> {a.out} ({os.path.getsize(a.out) / 1e6:.1f} MB)")
 

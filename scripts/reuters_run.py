@@ -28,8 +28,10 @@ def main():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--ari-every", type=int, default=5)
     ap.add_argument("--budget-s", type=float, default=150.0)
+    ap.add_argument("--drop-topics", action="store_true",
+                    help="zero the TOPICS columns of the third view (the ARI truth; mvc_amd.reuters)")
     a = ap.parse_args()
-    y = reuters.views()
+    y = reuters.views(drop_topics=a.drop_topics)
     lab, names, _ = reuters.topic_truth()
     sel = lab >= 0
     s = mvc_amd.Sampler(y, seed=a.seed, mode="parallel", n_chains=a.chains)
@@ -40,7 +42,7 @@ def main():
         s.sweep(1)
         s.synchronize()
         dt = time.perf_counter() - t0
-        rec = {"sweep": it, "s": round(dt, 4)}
+        rec = {"sweep": it, "s": round(dt, 4), "drop_topics": a.drop_topics}
         Ts, aris, moves = [], [], []
         for c in range(a.chains):
             t, d, h = s.state(chain=c)

@@ -668,3 +668,107 @@ def test_repair_global_wide(wide, V, monkeypatch):
     _check_sweeps(s, ref, 5)
     assert sum(ref["trace_births"]) > 0 and s.repair_stats()["moves"] == ref["trace_moves"][-1]
     s.close()
+
+
+@pytest.mark.parametrize("mode", ["parallel", "exact"])
+def test_run_chain_ids_and_pooled_summary(mode):
+    """mvc_run's chain ids (first_chain + c * chain_stride: the layout the
+    multi-device split uses, chain c of n_devices on device c % n_devices)
+    give every chain the chain a one-chain call with that id gives, bit for
+    bit; mvc_result_summary's pooled means and R-hat equal a host
+    computation over the saved draws."""
+    m = _mvc()
+    from mvc_amd import data
+    from mvc_amd import _lib as L
+    from mvc_amd.sampler import make_config, _view_ptrs, _views_to_array
+    import ctypes
+    y, _ = data.new_simulation(3)
+    M, burn = 30, 10
+    V = y.shape[0]
+    summ = {}
+    multi = m.run_gibbs_cpp(y, M, burn, 1, seed=99, mode=mode, n_chains=3, n_devices=1, summary=summ)
+    for c, res in enumerate(multi):
+        one = m.run_gibbs_cpp(y, M, burn, 1, seed=99, mode=mode, first_chain=c)
+        _compare(res, one)
+    # chain_stride: ids 1, 3, 5
+    yy = _views_to_array(y)
+    cfg = make_config(yy.shape[1], V, 1, M, burn, 1, 99, 3, 1, 0, mode, n_devices=1, chain_stride=2)
+    lib = L.lib()
+    r = ctypes.c_void_p()
+    buf = L.errbuf()
+    L.check(lib.mvc_run(ctypes.byref(cfg), _view_ptrs(yy), ctypes.byref(r), buf, len(buf)), buf)
+    try:
+        for c, gid in enumerate((1, 3, 5)):
+            one = m.run_gibbs_cpp(y, M, burn, 1, seed=99, mode=mode, first_chain=gid)
+            t = np.ctypeslib.as_array(lib.mvc_result_table_of(r, c, M - burn - 1), shape=(yy.shape[1],))
+            assert np.array_equal(t, one["table_of"][-1]), gid
+    finally:
+        lib.mvc_result_free(r)
+    H = np.stack([np.concatenate([np.stack(res["tau_v"]).T, np.stack(res["alpha_v"]).T, np.stack(res["sigma_v"]).T,
+                                  res["alpha_global"][:, None], res["sigma_global"][:, None]], axis=1)
+                  for res in multi])                                       # [C][S][3V+2]
+    assert np.allclose(summ["mean"], H.mean(axis=(0, 1)), rtol=1e-12, atol=0)
+    C, S = H.shape[0], H.shape[1]
+    cm, cv = H.mean(1), H.var(1, ddof=1)
+    B = S * cm.var(0, ddof=1)
+    W = cv.mean(0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        rh = np.sqrt(((S - 1) / S * W + B / S) / W)
+    assert np.allclose(summ["rhat"], rh, rtol=1e-10, equal_nan=True)
+
+
+def test_shard_exchange_failure_leaves_the_chain_unchanged():
+    """A failing all_gather (the callback returns nonzero) stops the sweep
+    with MVC_ERR_CALLBACK before the exchange buffer is read: the state is
+    the state before the sweep, and the handle sweeps on normally after a
+    working exchange is installed."""
+    m = _mvc()
+    from mvc_amd import data
+    import torch
+
+    from mvc_amd.dist import shard_len
+
+    class Failing:
+        def __init__(self, n):
+            self.buf = torch.zeros(2 * shard_len(n, 2), dtype=torch.int32, device="cuda")
+            self.ptr = self.buf.data_ptr()
+
+        def all_gather(self):
+            raise RuntimeError("exchange down")
+
+    y, _ = data.synthetic(4000, 2, 16, 6, seed=3)
+    s = m.Sampler(y, seed=5, mode="parallel")
+    s.sweep(1)
+    before = s.state()
+    s.set_shard(0, 2, Failing(4000))
+    with pytest.raises(RuntimeError, match="shard exchange failed"):
+        s.sweep(1)
+    after = s.state()
+    assert np.array_equal(before[0], after[0]) and np.array_equal(before[1], after[1])
+    assert before[2]["sigma_global"] == after[2]["sigma_global"]
+    assert s.sweeps_done == 1
+    s.set_shard(0, 1)
+    s.sweep(1)
+    ref = m.Sampler(y, seed=5, mode="parallel")
+    ref.sweep(2)
+    assert np.array_equal(s.state()[0], ref.state()[0])
+    s.close()
+    ref.close()
+
+
+def test_table_limit_is_a_clean_error(monkeypatch):
+    """A cold start that needs more tables than the parallel mode's limit
+    (262,144 = 64^3, the MH's three-level tree64; lowered here with
+    MVC_MAX_TABLES) fails with MVC_ERR_UNSUPPORTED and a message naming the
+    limit, not a wrong answer (configs[3] at N = 1M from the
+    reference initialisation would reach it: nearly every customer opens a
+    table in sweep 0, multiview_gibbs.cpp:94)."""
+    monkeypatch.setenv("MVC_MAX_TABLES", "32")
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(1999)          # opens ~70 tables in sweep 0
+    s = m.Sampler(y, seed=5, mode="parallel", table_cap=16)
+    with pytest.raises(m.MvcError, match="limit 32 tables") as e:
+        s.sweep(3)
+    assert e.value.code == 4                  # MVC_ERR_UNSUPPORTED
+    s.close()
