@@ -2592,6 +2592,8 @@ class ParallelSampler : public Sampler {
                              dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads),
                              L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
                              stream, Q, L);
+        if (L.lc && !repair_grid_only)   // its loop leaves births pending
+          hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, Q);
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
       }
       MVC_HIP(hipGetLastError());

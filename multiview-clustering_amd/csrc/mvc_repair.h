@@ -1034,6 +1034,121 @@ __device__ __forceinline__ int row16_isum_dpp(int x) {
 template <int k>
 __device__ __forceinline__ double row_bcast_d(double x) { return dpp_d<0x150 + k>(x); }
 
+// The own dish's value with the customer removed from its
+// dot product G = y . S1[:, j0].
+__device__ __forceinline__ double lc_self(const SView &W, int vv, int ks, int j0, double G, double Y2i, double hy,
+                                          double h) {
+  const double Gp = G - Y2i;
+  const double Qp = (W.Q[vv * ks + j0] - 2.0 * G) + Y2i;
+  const double c0 = W.xm[vv * ks + j0] - (0.5 * Qp) / W.ym[vv * ks + j0];
+  return __builtin_fma(Gp + hy, W.cbm[vv * ks + j0], c0) + h;
+}
+// One view's terms for the lane-column evaluation, NU dishes per lane
+// (j = col + 16 u, K <= 16 NU): the NU dot products run as interleaved fma
+// chains, each in ascending d (the own dish's chain is the one its self-
+// removed value starts from: the same operations as a separate chain), every
+// LDS load of a step issued before its first use; the lp values and counts
+// stay in registers for the column partial.  Lanes past K load a clamped
+// column and contribute nothing (w = 0, exp(-inf) = 0: cs + 0 = cs).
+template <int NU>
+__device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, const double *S1v, int s1s, int D,
+                                              int vv, int ks, int col, int K, int j0, int l0p, double hy, double h,
+                                              double Y2i, double lfn, double sigma, const int *dl, double *lpv,
+                                              double &mx, int &cnt, double &cs) {
+  int jc[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) jc[u] = min(col + 16 * u, ks - 1);
+  double G[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) G[u] = 0.0;
+  int d = 0;
+  for (; d + 4 <= D; d += 4) {
+    double yd[4], sd[4][NU];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      yd[k] = yv[d + k];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) sd[k][u] = S1v[(d + k) * s1s + jc[u]];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int u = 0; u < NU; ++u) G[u] = __builtin_fma(yd[k], sd[k][u], G[u]);
+  }
+  for (; d < D; ++d) {
+    const double yd = yv[d];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) G[u] = __builtin_fma(yd, S1v[d * s1s + jc[u]], G[u]);
+  }
+  double Gown = 0.0;
+#pragma unroll
+  for (int u = 0; u < NU; ++u)
+    if (col + 16 * u == j0) Gown = G[u];
+  const double self = lc_self(W, vv, ks, j0, Gown, Y2i, hy, h);
+  double lp[NU];
+  int lj[NU];
+  mx = -MVC_PM_INF;
+  cnt = 0;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int j = col + 16 * u;
+    const bool valid = j < K, own = j == j0;
+    const double fr = __builtin_fma(G[u] + hy, W.cb[vv * ks + jc[u]], W.c0[vv * ks + jc[u]]) + h;
+    const int dlj = dl[jc[u]];
+    lp[u] = own ? self : fr;
+    lj[u] = valid ? (own ? l0p : dlj) : 0;
+    if (valid) lpv[j] = lp[u];
+    if (lj[u] > 0) {
+      ++cnt;
+      if (lp[u] > mx) mx = lp[u];
+    }
+  }
+  mx = row16_max(mx);
+  cnt = row16_isum_dpp(cnt);
+  const double m = lfn > mx ? lfn : mx;
+  cs = 0.0;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    double w = (double)lj[u] - sigma;
+    if (w < 0.0) w = 0.0;
+    cs = cs + w * mvc_exp_le0(lj[u] > 0 ? lp[u] - m : -MVC_PM_INF);
+  }
+}
+// The same for any K (more than 8 dishes per lane): one dish at a time.
+__device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double *yv, const double *S1v, int s1s, int D,
+                                                int vv, int ks, int col, int K, int j0, int l0p, double hy, double h,
+                                                double Y2i, double lfn, double sigma, const int *dl, double *lpv,
+                                                double &mx, int &cnt, double &cs) {
+  double Gs = 0.0;
+  for (int d = 0; d < D; ++d) Gs = __builtin_fma(yv[d], S1v[d * s1s + j0], Gs);
+  const double self = lc_self(W, vv, ks, j0, Gs, Y2i, hy, h);
+  mx = -MVC_PM_INF;
+  cnt = 0;
+  for (int j = col; j < K; j += 16) {
+    double G = 0.0;
+    for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j], G);
+    const double fr = __builtin_fma(G + hy, W.cb[vv * ks + j], W.c0[vv * ks + j]) + h;
+    const bool own = j == j0;
+    const double val = own ? self : fr;
+    const int l = own ? l0p : dl[j];
+    lpv[j] = val;
+    if (l > 0) {
+      ++cnt;
+      if (val > mx) mx = val;
+    }
+  }
+  mx = row16_max(mx);
+  cnt = row16_isum_dpp(cnt);
+  const double m = lfn > mx ? lfn : mx;
+  cs = 0.0;
+  for (int j = col; j < K; j += 16) {
+    const int l = (j == j0) ? l0p : dl[j];
+    double w = (double)l - sigma;
+    if (w < 0.0) w = 0.0;
+    cs = cs + w * mvc_exp_le0(l > 0 ? lpv[j] - m : -MVC_PM_INF);
+  }
+}
+
 // seq_resample shaped for latency on the run kernel's LDS state ("lane
 // columns"): the same decision, bit for bit, with every reduction either
 // in-lane or a 16-lane row tree.  Lane (row r, column c) owns view v = g + r
@@ -1076,45 +1191,24 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     const double *S1v = W.S1T + vv * D * s1s;
     const int *dl = W.d_l + vv * ks;
     double *lpv = S.lp + vv * lps;
-    // the own dish with the customer removed, every lane of the row
-    double self;
-    {
-      double G = 0.0;
-      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j0], G);
-      const double Gp = G - Y2i;
-      const double Qp = (W.Q[vv * ks + j0] - 2.0 * G) + Y2i;
-      const double c0 = W.xm[vv * ks + j0] - (0.5 * Qp) / W.ym[vv * ks + j0];
-      self = __builtin_fma(Gp + hy, W.cbm[vv * ks + j0], c0) + h;
-    }
     const int l0p = dl[j0] - (alive ? 0 : 1);
     // lp of this lane's dishes (to the scratch for the table gathers), their
-    // max over the included ones (l' > 0) and K_act
-    double mx = -MVC_PM_INF;
-    int cnt = 0;
-    for (int j = col; j < K; j += 16) {
-      double G = 0.0;
-      for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j], G);
-      const double fr = __builtin_fma(G + hy, W.cb[vv * ks + j], W.c0[vv * ks + j]) + h;
-      const bool own = j == j0;
-      const double val = own ? self : fr;
-      const int l = own ? l0p : dl[j];
-      lpv[j] = val;
-      if (l > 0) {
-        ++cnt;
-        if (val > mx) mx = val;
-      }
-    }
-    mx = row16_max(mx);
-    cnt = row16_isum_dpp(cnt);
+    // max over the included ones (l' > 0), K_act, and the column partial
+    // w_j exp(lp_j - m) in ascending j (excluded dishes add +0)
+    double mx, cs;
+    int cnt;
+    const int nu = (max(max(readlane_i(K, 0), readlane_i(K, 16)), max(readlane_i(K, 32), readlane_i(K, 48))) + 15) >> 4;
+    if (nu <= 1)
+      lc_view_terms<1>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+    else if (nu <= 2)
+      lc_view_terms<2>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+    else if (nu <= 4)
+      lc_view_terms<4>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+    else if (nu <= 8)
+      lc_view_terms<8>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+    else
+      lc_view_terms_loop(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
     const double m = lfn > mx ? lfn : mx;
-    // column partial: w_j exp(lp_j - m) in ascending j (excluded dishes add +0)
-    double cs = 0.0;
-    for (int j = col; j < K; j += 16) {
-      const int l = (j == j0) ? l0p : dl[j];
-      double w = (double)l - sigma;
-      if (w < 0.0) w = 0.0;
-      cs = cs + w * mvc_exp_le0(l > 0 ? lpv[j] - m : -MVC_PM_INF);
-    }
     double Sv = row_pw16(cs);
     double wn = alpha + (double)cnt * sigma;
     if (wn < 0.0) wn = 0.0;
@@ -1602,107 +1696,140 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
   return true;
 }
 
-// A move p0 -> c (c >= 0) committed by ONE wave, for the run kernel with its
-// whole state in LDS (S1 included): the updates of seq_commit (oracle
-// SeqSampler::move) in the same operations and order per quantity, lane-
-// parallel, with no block barrier inside (one wave's LDS operations execute
-// in order; the caller's next block barrier publishes them).  Global arrays
-// are written through (store only) for the kernels after this one.
-__device__ void seq_commit_move_wave(SeqArgs &A, const SCache &cc, const Cust &Ci, int i, int p0, int c,
-                                     int32_t *cnt) {
+// A store to global memory as a global_store (not flat: a flat store also
+// counts on lgkmcnt, so every LDS-only barrier after it would wait for HBM).
+template <class T>
+__device__ __forceinline__ void gst(T *p, T v) {
+  *(__attribute__((address_space(1))) T *)p = v;
+}
+
+// A move p0 -> c (c >= 0) for the run kernel with its whole state in LDS
+// (S1 included): the updates of seq_commit (oracle SeqSampler::move) in the
+// same operations and order per quantity, split over the block's waves by
+// what they write, so no wave reads what another writes in the same commit:
+//   wave 0: the two tables (n_t, log mass, T_ne, z, the move count);
+//   wave 1: table counts of the dishes (d_l, L_v) and S2;
+//   wave 2: S1 of the two dishes of every view that changed dish, then d_n,
+//           Q and the coefficients (lanes < 2V: coef; lanes 2V.. 4V: the
+//           self-removed parts), all from its own writes (in order within a wave);
+//   wave 3: nothing.
+// nt0 / ntc: n_t[p0] and n_t[c] before the move, read by the evaluating wave
+// when it drew c (the tables' counts are wave 0's to write).  No block
+// barrier inside: the caller's next barrier publishes the LDS writes; global
+// arrays are written through (store only) for the kernels after this one.
+__device__ void seq_commit_move_split(SeqArgs &A, const SCache &cc, const Cust &Ci, int i, int p0, int c, int nt0,
+                                      int ntc, int32_t *cnt) {
   ParState &P = A.P;
   Repair *R = A.R;
-  const int lane = threadIdx.x & 63;
-  const int V = P.V, D = P.D, KC = P.KC, TC = P.TC, ks = cc.ks, ts = cc.ts;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int V = P.V, D = P.D, KC = P.KC, ks = cc.ks, ts = cc.ts;
   const double *hyp = cc.hyp, *l2pt = cc.L2pt;
-  const double sg = hyp[3 * V + 1];
-  // every read of the old state first
-  const int nt0 = cc.n_t[p0] - 1, ntc = cc.n_t[c];
-  const bool dies = nt0 == 0, born = ntc == 0;
-  const int Tne = *cc.T_ne - (dies ? 1 : 0) + (born ? 1 : 0);
-  // the two tables' log masses, one log per lane (lanes 0, 1)
-  const double lmv = mvc_log((double)(lane == 0 ? nt0 : ntc + 1) - sg);
-  if (lane == 0) {
-    cc.n_t[p0] = nt0;
-    cc.n_t[c] = ntc + 1;
-    cc.lmass[p0] = lmv;
-    *cc.T_ne = Tne;
-    P.n_t[p0] = nt0;
-    P.n_t[c] = ntc + 1;
-    P.lmass[p0] = lmv;
-    R->T_ne = Tne;
-    P.z[i] = c;
-    cnt[0] += 1;
-  }
-  if (lane == 1) {
-    cc.lmass[c] = lmv;
-    P.lmass[c] = lmv;
-  }
-  // per view (lane v): table counts of the two dishes, S2, n
-  if (lane < V) {
-    const int v = lane;
-    const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
-    if (dies || born) {
-      int L = cc.Ltot[v];
-      if (dies) {
-        const int l = cc.d_l[v * ks + j0] - 1;
-        cc.d_l[v * ks + j0] = l;
-        P.d_l[v * KC + j0] = l;
-        --L;
-      }
-      if (born) {
-        const int l = cc.d_l[v * ks + j1] + 1;   // after the decrement above when j1 == j0
-        cc.d_l[v * ks + j1] = l;
-        P.d_l[v * KC + j1] = l;
-        ++L;
-      }
-      cc.Ltot[v] = L;
-      P.Ltot[v] = L;
+  const bool dies = nt0 == 1, born = ntc == 0;
+  if (w == 0) {
+    const double sg = hyp[3 * V + 1];
+    const double lmv = mvc_log((double)(lane == 0 ? nt0 - 1 : ntc + 1) - sg);   // lanes 0, 1
+    if (lane == 0) {
+      const int Tne = *cc.T_ne - (dies ? 1 : 0) + (born ? 1 : 0);
+      cc.n_t[p0] = nt0 - 1;
+      cc.n_t[c] = ntc + 1;
+      cc.lmass[p0] = lmv;
+      *cc.T_ne = Tne;
+      cnt[0] += 1;
+      gst(&P.n_t[p0], nt0 - 1);
+      gst(&P.n_t[c], ntc + 1);
+      gst(&P.lmass[p0], lmv);
+      gst(&R->T_ne, Tne);
+      gst(&P.z[i], c);
     }
-    if (j0 != j1) {
-      const double y2 = Ci.Y2[(size_t)v * Ci.y2stride];
-      const double a0 = cc.S2[v * ks + j0] - y2, a1 = cc.S2[v * ks + j1] + y2;
-      cc.S2[v * ks + j0] = a0;
-      cc.S2[v * ks + j1] = a1;
-      P.S2[v * KC + j0] = a0;
-      P.S2[v * KC + j1] = a1;
-      const int n0 = cc.d_n[v * ks + j0] - 1, n1 = cc.d_n[v * ks + j1] + 1;
-      cc.d_n[v * ks + j0] = n0;
-      cc.d_n[v * ks + j1] = n1;
-      P.d_n[v * KC + j0] = n0;
-      P.d_n[v * KC + j1] = n1;
+    if (lane == 1) {
+      cc.lmass[c] = lmv;
+      gst(&P.lmass[c], lmv);
     }
-  }
-  // S1 of the two dishes of every view that changed dish (lanes over (v, d))
-  for (int e = lane; e < V * D; e += 64) {
-    const int v = e / D, d = e - v * D;
-    const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
-    if (j0 == j1) continue;
-    const double yd = Ci.y[(size_t)v * Ci.ystride + d];
-    double *cl = cc.S1T + ((size_t)v * D + d) * ks;
-    const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
-    cl[j0] = a0;
-    cl[j1] = a1;
-    double *col = P.S1T + ((size_t)v * D + d) * KC;
-    col[j0] = a0;
-    col[j1] = a1;
-  }
-  // Q and the coefficients of the two dishes (oracle refresh_dish), lanes over (v, which)
-  if (lane < 2 * V) {
-    const int v = lane >> 1;
-    const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
-    const int j = (lane & 1) ? j1 : j0;
-    if (j0 != j1) {
-      const double q = fma_sq_strided(cc.S1T + (size_t)v * D * ks + j, (size_t)ks, D);
-      const int nj = cc.d_n[v * ks + j];
-      const Coef cf = coef(nj, q, hyp[v], l2pt[v], D);
-      cc.Q[v * ks + j] = q;
-      cc.c0[v * ks + j] = cf.c0;
-      cc.cb[v * ks + j] = cf.cb;
-      self_coef_parts(nj, hyp[v], l2pt[v], D, cc.xm[v * ks + j], cc.ym[v * ks + j], cc.cbm[v * ks + j]);
-      P.Q[v * KC + j] = q;
-      P.c0[v * KC + j] = cf.c0;
-      P.cb[v * KC + j] = cf.cb;
+  } else if (w == 1) {
+    for (int v = lane; v < V; v += 64) {
+      const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+      if (dies || born) {
+        int L = cc.Ltot[v];
+        if (dies) {
+          const int l = cc.d_l[v * ks + j0] - 1;
+          cc.d_l[v * ks + j0] = l;
+          gst(&P.d_l[v * KC + j0], l);
+          --L;
+        }
+        if (born) {
+          const int l = cc.d_l[v * ks + j1] + 1;   // after the decrement above when j1 == j0
+          cc.d_l[v * ks + j1] = l;
+          gst(&P.d_l[v * KC + j1], l);
+          ++L;
+        }
+        cc.Ltot[v] = L;
+        gst(&P.Ltot[v], L);
+      }
+      if (j0 != j1) {
+        const double y2 = Ci.Y2[(size_t)v * Ci.y2stride];
+        const double a0 = cc.S2[v * ks + j0] - y2, a1 = cc.S2[v * ks + j1] + y2;
+        cc.S2[v * ks + j0] = a0;
+        cc.S2[v * ks + j1] = a1;
+        gst(&P.S2[v * KC + j0], a0);
+        gst(&P.S2[v * KC + j1], a1);
+      }
+    }
+  } else if (w == 2) {
+    // S1 of the two dishes of every view that changed dish (lanes over (v, d))
+    for (int e = lane; e < V * D; e += 64) {
+      const int v = e / D, d = e - v * D;
+      const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+      if (j0 == j1) continue;
+      const double yd = Ci.y[(size_t)v * Ci.ystride + d];
+      double *cl = cc.S1T + ((size_t)v * D + d) * ks;
+      const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
+      cl[j0] = a0;
+      cl[j1] = a1;
+      double *col = P.S1T + ((size_t)v * D + d) * KC;
+      gst(&col[j0], a0);
+      gst(&col[j1], a1);
+    }
+    // d_n, Q and the coefficients of the two dishes (oracle refresh_dish):
+    // lane k < 2V: (v, which) = (k / 2, k & 1) coef; 2V <= k < 4V the same
+    // dish's self-removed parts
+    for (int k0 = 0; k0 < 4 * V; k0 += 64) {
+      const int k = k0 + lane;
+      const bool act = k < 4 * V;
+      const bool part = k >= 2 * V;
+      const int kk = part ? k - 2 * V : k;
+      const int v = act ? kk >> 1 : 0;
+      const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+      const bool which = kk & 1;
+      const int j = which ? j1 : j0;
+      const bool go = act && j0 != j1;
+      const int nj = cc.d_n[v * ks + j] + (which ? 1 : -1);
+      const double q = go && !part ? fma_sq_strided(cc.S1T + (size_t)v * D * ks + j, (size_t)ks, D) : 0.0;
+      if (go && !part) {
+        const Coef cf = coef(nj, q, hyp[v], l2pt[v], D);
+        cc.Q[v * ks + j] = q;
+        cc.c0[v * ks + j] = cf.c0;
+        cc.cb[v * ks + j] = cf.cb;
+        gst(&P.Q[v * KC + j], q);
+        gst(&P.c0[v * KC + j], cf.c0);
+        gst(&P.cb[v * KC + j], cf.cb);
+      }
+      if (go && part) {
+        double xm, ym, cbm;
+        self_coef_parts(nj, hyp[v], l2pt[v], D, xm, ym, cbm);
+        cc.xm[v * ks + j] = xm;
+        cc.ym[v * ks + j] = ym;
+        cc.cbm[v * ks + j] = cbm;
+      }
+    }
+    // d_n last: the loop above read the counts before the move
+    for (int k = lane; k < 2 * V; k += 64) {
+      const int v = k >> 1;
+      const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+      if (j0 == j1) continue;
+      const int j = (k & 1) ? j1 : j0;
+      const int nj = cc.d_n[v * ks + j] + ((k & 1) ? 1 : -1);
+      cc.d_n[v * ks + j] = nj;
+      gst(&P.d_n[v * KC + j], nj);
     }
   }
 }
@@ -1766,6 +1893,31 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_apply_kernel(SeqArgs A
   }
 }
 
+// The birth left pending by the lane-column run kernel (its loop stops at a
+// birth): the block-cooperative commit on the global state (dish draws on the
+// 8 waves), then the next run launch resumes at the following customer and
+// re-stages its LDS cache.  A no-op unless a birth is pending.
+extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_birth_kernel(SeqArgs A) {
+  Repair *R = A.R;
+  const int tid = threadIdx.x;
+  __shared__ int s_go, s_i;
+  if (tid == 0) {
+    s_go = !(R->done || R->overflow || R->restride) && R->pend && R->pchoice < 0;
+    s_i = R->cur;
+  }
+  __syncthreads();
+  if (!s_go) return;
+  const SeqScratch S(A, tid >> 6);
+  if (!seq_commit(A, global_view(A), nullptr, global_cust(A, s_i), s_i, A.P.z[s_i], -1, S.lp, S.tree, &R->moves,
+                  blockDim.x >> 6))
+    return;   // overflow: the host grows and relaunches this step
+  if (tid == 0) {
+    R->cur = s_i + 1;
+    R->pend = 0;
+    R->streak = 0;
+  }
+}
+
 // The run kernel's repair cursor (LDS, owned by thread 0 while the kernel
 // runs; read from R at entry and written back at exit).
 struct RunCursor {
@@ -1775,6 +1927,8 @@ struct RunCursor {
   int lpc;                        // wide evaluation: the customer whose lp rows wave 0's scratch holds (-1: none)
   int32_t cnt[3];                 // moves, births, new dishes
   int ch[kSeqRunWaves], p0[kSeqRunWaves];
+  int chb[2][kSeqLcThreads / 64], p0b[2][kSeqLcThreads / 64];   // the lane-column loop's, by step parity
+  int ntb[2][kSeqLcThreads / 64][2];   // ... and n_t of the mover's two tables before its move
 };
 
 namespace {
@@ -1802,9 +1956,12 @@ struct Ring {
 // range of the slots split over the waves, 64 dwords per instruction.  The
 // caller waits (s_waitcnt + barrier) before anyone reads the slots.  Slot
 // dwords: y rows [V][D] (2 per double), Y2 [V], then z (int) twice.
+// nwc: the block's waves when known at compile time (blockDim.x is a load
+// from the dispatch packet, and that load waits for every outstanding store).
+template <int nwc = 0>
 __device__ __forceinline__ void ring_fill_async(const SeqArgs &A, const Ring &G, int c0, int c1) {
   const int V = A.P.V, D = A.P.D, n = A.P.n;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = nwc ? nwc : (int)(blockDim.x >> 6);
   const int sdw = 2 * G.slot;
   int c = c0;
   while (c < c1) {   // contiguous runs of slots (split at the ring's end)
@@ -1985,22 +2142,21 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
   }
 }
 
-// The birth commit of the lane-column run kernel, out of line: births are
-// rare, and inlined the general commit (dish draws, tree64, capacity checks)
-// would raise the register pressure of the whole loop.
-__device__ __attribute__((noinline)) bool seq_commit_birth(SeqArgs &A, const SeqLds &L, const Cust &Ci, int i, int p0,
-                                                           double *lpw, double *treew, int32_t *cnt, int nwd) {
-  const SCache cc = lds_cache(A.P.V, A.P.D, L.ts, L.ks, 1);
-  return seq_commit(A, cache_view(cc, A), &cc, Ci, i, p0, -1, lpw, treew, cnt, nwd, nullptr, false);
-}
-
 // seq_run_loop for the lane-column evaluation (L.lc: the whole state in LDS,
-// S1 included, the staged-row ring): moves committed by wave 0
-// (seq_commit_move_wave), births out of line, LDS-only barriers.  Compiled as
-// its own kernel instance so nothing of the other evaluation shapes sits in
-// its registers.
-__device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, double *tree, RunCursor &U, int &ovf,
-                                int &restride) {
+// S1 included, the staged-row ring), compiled as its own kernel instance so
+// nothing of the other evaluation shapes sits in its registers.
+//   * moves are committed by wave 0 alone (seq_commit_move_wave); a birth
+//     ends the loop with the birth pending, and mvc_seq_birth_kernel commits
+//     it on the global state before the next launch (births are rare here,
+//     and the general commit inlined would raise the loop's register pressure);
+//   * the cursor lives in registers, the same in every wave: each wave
+//     derives it from the same LDS values after the same barriers, so a step
+//     is {commit; barrier; evaluate; barrier} with no single-thread decision
+//     section; the speculated choices are double-buffered by step parity (a
+//     step without a commit has only one barrier, so a fast wave may write
+//     the next step's choices while a slow one still reads this step's);
+//   * every barrier waits for LDS operations only.
+__device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U, int &restride) {
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
@@ -2009,114 +2165,120 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, doub
   Wv.S1T = cc.S1T;                                      // no select against the global copy: LDS for sure
   Wv.s1s = cc.ks;
   const SeqScratch S(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts);
-  if (U.pend) {   // a mover carried over from the previous launch (a resolved window): stage its row first
-    ring_fill_async(A, G, U.cur, U.cur + 1);
+  int cur = U.cur, pend = U.pend, pc = U.pc, pp0 = U.pp0, mode = U.mode, streak = U.streak, done = U.done;
+  int fill = U.fill, landed = U.landed, par = 0;
+  int pnt0 = 0, pntc = 0;   // n_t of the pending mover's two tables before its move
+  if (pend && pc >= 0) {    // a mover carried over from the previous launch
+    pnt0 = cc.n_t[pp0];
+    pntc = cc.n_t[pc];
+  }
+  if (pend && pc >= 0) {   // a mover carried over from the previous launch (a resolved window): stage its row
+    ring_fill_async<kSeqLcThreads / 64>(A, G, cur, cur + 1);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (tid == 0) {
-      U.fill = U.cur + 1;
-      U.landed = U.cur + 1;
-    }
-    __syncthreads();
+    fill = landed = cur + 1;
   }
   for (;;) {
     RUN_T0();
-    if (U.pend) {
+    if (pend) {
+      if (pc < 0) break;   // a birth: left pending for mvc_seq_birth_kernel
       // the mover was evaluated in the previous step (or staged above), so its
       // row is in the ring (landed, not yet reused: requests stop a ring ahead of it)
-      const Cust Ci = G.cust(U.cur, V, D);
-      if (U.pc >= 0) {
-        if (w == 0) seq_commit_move_wave(A, cc, Ci, U.cur, U.pp0, U.pc, U.cnt);
-      } else {
-        __syncthreads();
-        const bool ok = seq_commit_birth(A, L, Ci, U.cur, U.pp0, S.lp, tree, U.cnt, L.nws);
-        __syncthreads();
-        if (!ok) {
-          ovf = 1;
-          return;
-        }
-      }
+      seq_commit_move_split(A, cc, G.cust(cur, V, D), cur, pp0, pc, pnt0, pntc, U.cnt);
+      cur = cur + 1;
+      pend = 0;
+      streak = 0;
       RUN_MARK(3);
-      if (tid == 0) {
-        U.cur = U.cur + 1;
-        U.pend = 0;
-        U.streak = 0;
+      if (cur >= n) {
+        done = 1;
+        break;
+      }
+      seq_bar(true);   // the commit, visible to every wave
+    }
+    {   // the LDS layout must hold the current lists plus one birth
+      bool bad = *cc.T >= L.ts;
+      for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks;
+      if (bad) {
+        restride = 1;
+        break;
       }
     }
-    if (tid == 0) {
-      U.stop = 0;
-      if (U.cur >= n) {
-        U.done = 1;
-        U.stop = 1;
-      } else {   // the LDS layout must hold the current lists plus one birth
-        int bad = *cc.T >= L.ts ? 1 : 0;
-        for (int v = 0; v < V; ++v) bad |= cc.Klist[v] >= L.ks ? 1 : 0;
-        if (bad) U.stop = 2;
-      }
-      U.i = U.cur;
-    }
-    seq_bar(true);
     RUN_MARK(4);
-    if (U.stop) {
-      restride = U.stop == 2;
-      return;
-    }
-    const int i0 = U.i;
+    const int i0 = cur;
     const int need = min(n, i0 + L.nws);
-    // rows in batches half a ring ahead; a step waits only beyond what has landed
-    int fill_next = max(U.fill, i0), landed_next = U.landed;
-    if (need > U.landed) {
-      if (fill_next < need) {
-        ring_fill_async(A, G, fill_next, need);
-        fill_next = need;
+    // rows in batches half a ring ahead; a step waits only beyond what has
+    // landed (slots being refilled belong to customers before cur: final)
+    if (need > landed) {
+      if (fill < need) {
+        ring_fill_async<kSeqLcThreads / 64>(A, G, max(fill, i0), need);
+        fill = need;
       }
       __builtin_amdgcn_s_waitcnt(0);
       __syncthreads();
-      landed_next = fill_next;
+      landed = fill;
     }
-    if (fill_next - i0 <= G.n / 2 && fill_next < n) {
+    if (fill - i0 <= G.n / 2 && fill < n) {
       const int f1 = min(n, i0 + G.n);
-      ring_fill_async(A, G, fill_next, f1);
-      fill_next = f1;
+      ring_fill_async<kSeqLcThreads / 64>(A, G, max(fill, i0), f1);
+      fill = f1;
     }
     const int i = i0 + w;
     if (w < L.nws && i < n) {
       const int p0 = ring_z(G, i, V, D);
       const int c = seq_resample_lc(A, Wv, G.cust(i, V, D), i, p0, S, cc.hyp, cc.cnew);
       if (lane == 0) {
-        U.ch[w] = c;
-        U.p0[w] = p0;
+        U.chb[par][w] = c;
+        U.p0b[par][w] = p0;
+        if (c != p0 && c >= 0) {
+          U.ntb[par][w][0] = cc.n_t[p0];
+          U.ntb[par][w][1] = cc.n_t[c];
+        }
       }
     }
     seq_bar(true);
     RUN_MARK(5);
-    if (tid == 0) {
-      U.fill = fill_next;
-      U.landed = landed_next;
-      int f = -1;
-      const int m = min(L.nws, n - U.i);
-      for (int k = 0; k < m; ++k)
-        if (U.ch[k] != U.p0[k]) { f = k; break; }
-      if (f >= 0) {
-        U.cur = U.i + f;
-        U.pend = 1;
-        U.pc = U.ch[f];
-        U.pp0 = U.p0[f];
-        U.lpc = -1;
-      } else {
-        U.cur = U.i + m;
-        U.streak += m;
-        if (U.streak >= L.limit) U.mode = kSeqScan;
-        if (U.cur >= n) U.done = 1;
+    // every wave: the first customer whose choice is not its table
+    const int m = min(L.nws, n - i0);
+    int f = -1;
+    for (int k = 0; k < m; ++k)
+      if (U.chb[par][k] != U.p0b[par][k]) {
+        f = k;
+        break;
       }
-      U.go = !U.done && (U.mode == kSeqRun || U.pend);
+    if (f >= 0) {
+      cur = i0 + f;
+      pend = 1;
+      pc = U.chb[par][f];
+      pp0 = U.p0b[par][f];
+      if (pc >= 0) {
+        pnt0 = U.ntb[par][f][0];
+        pntc = U.ntb[par][f][1];
+      }
+    } else {
+      cur = i0 + m;
+      streak += m;
+      if (streak >= L.limit) mode = kSeqScan;
+      if (cur >= n) done = 1;
     }
-    seq_bar(true);
+    par ^= 1;
     RUN_MARK(6);
 #ifdef MVC_RUN_PROF
     if (tid == 0) mvc_prof_lds[7] += 1;
 #endif
-    if (!U.go) return;
+    if (done || !(mode == kSeqRun || pend)) break;
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
+  __syncthreads();                 // every wave out of the loop before thread 0 writes the cursor back
+  if (tid == 0) {
+    U.cur = cur;
+    U.pend = pend;
+    U.pc = pc;
+    U.pp0 = pp0;
+    U.mode = mode;
+    U.streak = streak;
+    U.done = done;
+    U.fill = fill;
+    U.landed = landed;
   }
 }
 
@@ -2235,7 +2397,7 @@ __global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void m
     G.slot = (int)seq_ring_slot(V, D);
     G.base = mvc_seq_lds + L.cache_dbl + (int64_t)L.nws * L.stride;
     if constexpr (kMode == 3)
-      seq_run_loop_lc(A, L, G, tree, U, ovf, restride);
+      seq_run_loop_lc(A, L, G, U, restride);
     else
       seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
                                 SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts), G,
