@@ -2631,7 +2631,7 @@ class ParallelSampler : public Sampler {
     }
     timers.end("repair", e1);
 #ifdef MVC_RUN_PROF
-    fprintf(stderr, "runprof moves %d iters %llu | lc: views %.2f tables %.2f weights+draw %.2f | commit %.2f check %.2f spec %.2f decide %.2f (us per iter)\n",
+    fprintf(stderr, "runprof moves %d iters %llu | lc: views %.2f tables+weights %.2f draw %.2f | commit %.2f check %.2f spec %.2f decide %.2f (us per iter)\n",
             rs_host->moves, rs_host->prof[7], rs_host->prof[0] * 0.01 / std::max(1ull, rs_host->prof[7]),
             rs_host->prof[1] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[2] * 0.01 / std::max(1ull, rs_host->prof[7]),
             rs_host->prof[3] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[4] * 0.01 / std::max(1ull, rs_host->prof[7]),

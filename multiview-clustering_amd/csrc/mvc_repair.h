@@ -1061,17 +1061,19 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
   double G[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) G[u] = 0.0;
+  // d in blocks of DB, every load of a block issued before its fmas
+  constexpr int DB = NU <= 2 ? 16 : 4;
   int d = 0;
-  for (; d + 4 <= D; d += 4) {
-    double yd[4], sd[4][NU];
+  for (; d + DB <= D; d += DB) {
+    double yd[DB], sd[DB][NU];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < DB; ++k) {
       yd[k] = yv[d + k];
 #pragma unroll
       for (int u = 0; u < NU; ++u) sd[k][u] = S1v[(d + k) * s1s + jc[u]];
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
+    for (int k = 0; k < DB; ++k)
 #pragma unroll
       for (int u = 0; u < NU; ++u) G[u] = __builtin_fma(yd[k], sd[k][u], G[u]);
   }
@@ -1146,6 +1148,92 @@ __device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double 
     double w = (double)l - sigma;
     if (w < 0.0) w = 0.0;
     cs = cs + w * mvc_exp_le0(l > 0 ? lpv[j] - m : -MVC_PM_INF);
+  }
+}
+
+// The table part of the lane-column evaluation: scores log(n_p' - sigma_g) +
+// sum_v lp_{v, dish_v(p)} (view order; -inf when excluded) of QB 64-table
+// chunks per step, every view's dish index loaded before the gathers (4 views
+// at a time); their max M (with s_new); weights exp(score - M) to the wave's
+// scratch e[]; block sums pw16 per row and running block totals C_b kept in
+// lane b.  kOne: one step covers every table (nch <= QB), so the scores stay
+// in registers between the two passes.  Same operations and order for every QB.
+template <int QB, bool kOne>
+__device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScratch &S, int V, int ts, int lps, int p0,
+                                                  int T, double sg, double lmass0, double s_new, double &M,
+                                                  double &tot, double &Cb) {
+  const int lane = threadIdx.x & 63;
+  const int TB = (T + 15) >> 4, nch = (T + 63) >> 6;
+  double xk[QB];
+  M = -MVC_PM_INF;
+  for (int q0 = 0; q0 < nch; q0 += QB) {
+    double x[QB];
+    bool inc[QB];
+    int pp[QB];
+#pragma unroll
+    for (int h2 = 0; h2 < QB; ++h2) {
+      const int p = 64 * (q0 + h2) + lane;
+      pp[h2] = p;
+      const int np = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+      const double mass = (double)np - sg;
+      inc[h2] = p < T && np >= 1 && mass > 0.0;
+      x[h2] = inc[h2] ? (p == p0 ? lmass0 : W.lmass[p]) : -MVC_PM_INF;
+    }
+    for (int v0 = 0; v0 < V; v0 += 4) {
+      int dj[QB][4];
+#pragma unroll
+      for (int h2 = 0; h2 < QB; ++h2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          dj[h2][u] = (inc[h2] && v0 + u < V) ? W.dish[(v0 + u) * ts + pp[h2]] : 0;
+      double lv[QB][4];
+#pragma unroll
+      for (int h2 = 0; h2 < QB; ++h2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + dj[h2][u]];
+#pragma unroll
+      for (int h2 = 0; h2 < QB; ++h2)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (inc[h2] && v0 + u < V) x[h2] = x[h2] + lv[h2][u];   // view order
+    }
+#pragma unroll
+    for (int h2 = 0; h2 < QB; ++h2) {
+      if (q0 + h2 < nch) {
+        if (kOne)
+          xk[h2] = x[h2];
+        else
+          S.e[pp[h2]] = x[h2];
+        if (x[h2] > M) M = x[h2];
+      }
+    }
+  }
+  M = wave_max(M);
+  if (s_new > M) M = s_new;
+  tot = 0.0;
+  Cb = 0.0;
+  for (int q0 = 0; q0 < nch; q0 += QB) {
+    double e[QB];
+#pragma unroll
+    for (int h2 = 0; h2 < QB; ++h2) e[h2] = kOne ? xk[h2] : S.e[64 * min(q0 + h2, nch - 1) + lane];
+#pragma unroll
+    for (int h2 = 0; h2 < QB; ++h2) e[h2] = mvc_exp_le0(e[h2] - M);
+#pragma unroll
+    for (int h2 = 0; h2 < QB; ++h2) {
+      const int q = q0 + h2;
+      if (q < nch) {
+        S.e[64 * q + lane] = e[h2];
+        const double B = row_pw16(e[h2]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int b = 4 * q + r;
+          if (b < TB) {
+            tot = tot + readlane_d(B, 16 * r);
+            if (lane == b) Cb = tot;
+          }
+        }
+      }
+    }
   }
 }
 
@@ -1233,77 +1321,14 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
   // table scores log(n_p' - sigma_g) + sum_v lp_{v, dish_v(p)} (view order),
   // -inf when excluded; to the wave's scratch e[]
   const int T = *W.T, TB = (T + 15) >> 4, nch = (T + 63) >> 6;
-  double M = -MVC_PM_INF;
-  // two 64-table chunks per step, every view's dish index loaded before the
-  // gathers (4 views at a time): two dependent LDS latencies per step, not 2 V
-  for (int q0 = 0; q0 < nch; q0 += 2) {
-    double x[2];
-    bool inc[2];
-    int pp[2];
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int p = 64 * (q0 + h2) + lane;
-      pp[h2] = p;
-      const int np = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
-      const double mass = (double)np - sg;
-      inc[h2] = p < T && np >= 1 && mass > 0.0;
-      x[h2] = inc[h2] ? (p == p0 ? lmass0 : W.lmass[p]) : -MVC_PM_INF;
-    }
-    for (int v0 = 0; v0 < V; v0 += 4) {
-      int dj[2][4];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          dj[h2][u] = (inc[h2] && v0 + u < V) ? W.dish[(v0 + u) * ts + pp[h2]] : 0;
-      double lv[2][4];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + dj[h2][u]];
-#pragma unroll
-      for (int h2 = 0; h2 < 2; ++h2)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (inc[h2] && v0 + u < V) x[h2] = x[h2] + lv[h2][u];   // view order
-    }
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      if (q0 + h2 < nch) {
-        S.e[pp[h2]] = x[h2];
-        if (x[h2] > M) M = x[h2];
-      }
-    }
-  }
-  M = wave_max(M);
-  if (s_new > M) M = s_new;
+  double M, tot, Cb;
+  if (nch <= 2)
+    lc_scores_weights<2, true>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb);
+  else if (nch <= 4)
+    lc_scores_weights<4, true>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb);
+  else
+    lc_scores_weights<4, false>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb);
   RUN_MARK(1);
-  // weights exp(sp - M) (0 where excluded or past T), block sums pw16 per
-  // row, running block totals C_b kept in lane b
-  double tot = 0.0, Cb = 0.0;
-  for (int q0 = 0; q0 < nch; q0 += 2) {
-    double e[2];
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) e[h2] = S.e[64 * min(q0 + h2, nch - 1) + lane];
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) e[h2] = mvc_exp_le0(e[h2] - M);
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      const int q = q0 + h2;
-      if (q < nch) {
-        S.e[64 * q + lane] = e[h2];
-        const double B = row_pw16(e[h2]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = 4 * q + r;
-          if (b < TB) {
-            tot = tot + readlane_d(B, 16 * r);
-            if (lane == b) Cb = tot;
-          }
-        }
-      }
-    }
-  }
   const double Wt = mvc_exp_le0(s_new - M) + tot;
   double r = u_i * Wt;
   if (!(r < tot)) {
@@ -1709,10 +1734,9 @@ __device__ __forceinline__ void gst(T *p, T v) {
 // what they write, so no wave reads what another writes in the same commit:
 //   wave 0: the two tables (n_t, log mass, T_ne, z, the move count);
 //   wave 1: table counts of the dishes (d_l, L_v) and S2;
-//   wave 2: S1 of the two dishes of every view that changed dish, then d_n,
-//           Q and the coefficients (lanes < 2V: coef; lanes 2V.. 4V: the
-//           self-removed parts), all from its own writes (in order within a wave);
-//   wave 3: nothing.
+//   waves 2 / 3: the dish left / joined in every view that changed dish: S1,
+//           then Q and the coefficients, then d_n, each from its own writes
+//           (in order within a wave; the two dishes differ).
 // nt0 / ntc: n_t[p0] and n_t[c] before the move, read by the evaluating wave
 // when it drew c (the tables' counts are wave 0's to write).  No block
 // barrier inside: the caller's next barrier publishes the LDS writes; global
@@ -1774,60 +1798,63 @@ __device__ void seq_commit_move_split(SeqArgs &A, const SCache &cc, const Cust &
         gst(&P.S2[v * KC + j1], a1);
       }
     }
-  } else if (w == 2) {
-    // S1 of the two dishes of every view that changed dish (lanes over (v, d))
+  } else {
+    // wave 2: the dish the customer leaves (j0), wave 3: the one it joins (j1),
+    // in every view where they differ: S1 (lanes over d), then Q and the
+    // coefficients (lanes < V: coef; V <= lane < 2V: the self-removed parts),
+    // then d_n (oracle refresh_dish; the two waves touch different dishes)
+    const bool join = w == 3;
     for (int e = lane; e < V * D; e += 64) {
       const int v = e / D, d = e - v * D;
       const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
       if (j0 == j1) continue;
+      const int j = join ? j1 : j0;
       const double yd = Ci.y[(size_t)v * Ci.ystride + d];
       double *cl = cc.S1T + ((size_t)v * D + d) * ks;
-      const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
-      cl[j0] = a0;
-      cl[j1] = a1;
-      double *col = P.S1T + ((size_t)v * D + d) * KC;
-      gst(&col[j0], a0);
-      gst(&col[j1], a1);
+      const double a = join ? cl[j] + yd : cl[j] - yd;
+      cl[j] = a;
+      gst(&P.S1T[((size_t)v * D + d) * KC + j], a);
     }
-    // d_n, Q and the coefficients of the two dishes (oracle refresh_dish):
-    // lane k < 2V: (v, which) = (k / 2, k & 1) coef; 2V <= k < 4V the same
-    // dish's self-removed parts
-    for (int k0 = 0; k0 < 4 * V; k0 += 64) {
+    for (int k0 = 0; k0 < 2 * V; k0 += 64) {
+      // coef(n', Q) (lanes k < V) and self_coef_parts(n') (V <= k < 2V) share
+      // their operations: D (-L2pt / 2 - log(b / a) / 2), (tau a) b and
+      // 1 / (tau b) with (a, b) = (tau + n', tau + n' + 1), resp. (tau + n' - 1,
+      // tau + n'); one instruction stream for both kinds of lane
       const int k = k0 + lane;
-      const bool act = k < 4 * V;
-      const bool part = k >= 2 * V;
-      const int kk = part ? k - 2 * V : k;
-      const int v = act ? kk >> 1 : 0;
+      const bool act = k < 2 * V, part = k >= V;
+      const int v = act ? (part ? k - V : k) : 0;
       const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
-      const bool which = kk & 1;
-      const int j = which ? j1 : j0;
+      const int j = join ? j1 : j0;
       const bool go = act && j0 != j1;
-      const int nj = cc.d_n[v * ks + j] + (which ? 1 : -1);
-      const double q = go && !part ? fma_sq_strided(cc.S1T + (size_t)v * D * ks + j, (size_t)ks, D) : 0.0;
+      const int nj = cc.d_n[v * ks + j] + (join ? 1 : -1);
+      const double q = fma_sq_strided(cc.S1T + (size_t)v * D * ks + j, (size_t)ks, D);
+      const double tau = hyp[v];
+      const double a = tau + (double)(part ? nj - 1 : nj);
+      const double b = tau + (double)(part ? nj : nj + 1);
+      const double X = (double)D * ((-0.5 * l2pt[v]) - 0.5 * mvc_log_nb(b / a));
+      const double Y = (tau * a) * b;
+      const double Z = 1.0 / (tau * b);
+      const double c0 = X - (0.5 * q) / Y;
       if (go && !part) {
-        const Coef cf = coef(nj, q, hyp[v], l2pt[v], D);
         cc.Q[v * ks + j] = q;
-        cc.c0[v * ks + j] = cf.c0;
-        cc.cb[v * ks + j] = cf.cb;
+        cc.c0[v * ks + j] = c0;
+        cc.cb[v * ks + j] = Z;
         gst(&P.Q[v * KC + j], q);
-        gst(&P.c0[v * KC + j], cf.c0);
-        gst(&P.cb[v * KC + j], cf.cb);
+        gst(&P.c0[v * KC + j], c0);
+        gst(&P.cb[v * KC + j], Z);
       }
       if (go && part) {
-        double xm, ym, cbm;
-        self_coef_parts(nj, hyp[v], l2pt[v], D, xm, ym, cbm);
-        cc.xm[v * ks + j] = xm;
-        cc.ym[v * ks + j] = ym;
-        cc.cbm[v * ks + j] = cbm;
+        cc.xm[v * ks + j] = X;
+        cc.ym[v * ks + j] = Y;
+        cc.cbm[v * ks + j] = Z;
       }
     }
     // d_n last: the loop above read the counts before the move
-    for (int k = lane; k < 2 * V; k += 64) {
-      const int v = k >> 1;
+    for (int v = lane; v < V; v += 64) {
       const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
       if (j0 == j1) continue;
-      const int j = (k & 1) ? j1 : j0;
-      const int nj = cc.d_n[v * ks + j] + ((k & 1) ? 1 : -1);
+      const int j = join ? j1 : j0;
+      const int nj = cc.d_n[v * ks + j] + (join ? 1 : -1);
       cc.d_n[v * ks + j] = nj;
       gst(&P.d_n[v * KC + j], nj);
     }
