@@ -32,6 +32,14 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
 
+# The 16-chain leg runs 16 chains in this process, one HIP stream each; HIP
+# maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
+# default, and the GPU pool's environment sets 4), and beyond that streams
+# share queues and their kernels serialise.  The library
+# leaves the caller's setting alone, so the bench, which is the caller here,
+# asks for 32 before anything starts HIP.
+os.environ["GPU_MAX_HW_QUEUES"] = "32"
+
 import numpy as np  # noqa: E402
 
 CONFIGS = {
@@ -179,8 +187,8 @@ def gpu_chains_line(config, seed, device, chains=16, sweeps=1):
     """Several chains of one config on one GPU at once (parallel-mode ChainSet:
     one stream and host thread per chain, the data shared), warm
     start at the generating partition: aggregate chain-sweeps/s.  The loader
-    asks HIP for _lib.HW_QUEUES (32) hardware queues unless the user set
-    GPU_MAX_HW_QUEUES, so 16 chains overlap."""
+    runs with 32 hardware queues (set at the top of this file), so 16 chains
+    overlap."""
     from mvc_amd import data
     from mvc_amd.sampler import Sampler
     N, V, D, K, desc = CONFIGS[config]

@@ -20,8 +20,7 @@ def main():
     y, z = data.synthetic(N, V, D, K, seed=1999)
     st = bench.warm_state(z, V, K)
     for C in [int(a) for a in sys.argv[1:]] or [8]:
-        # the library asks HIP for _lib.HW_QUEUES (32) hardware queues (unless set) at
-        # the process's first HIP call, so nothing here touches the GPU before
+        # importing bench set GPU_MAX_HW_QUEUES=32 for this process before HIP started
         s = Sampler(y, seed=1999, mode="parallel", n_chains=C, device=0)
         for c in range(C):
             s.set_state(*st, chain=c)
