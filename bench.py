@@ -284,6 +284,13 @@ def newsim_call_line(seed, device, M=10000, M_short=2000):
     dt = time.perf_counter() - t0
     out["exact_gpu"] = {"sweeps": M_short, "s": round(dt, 2), "sweeps_per_s": round(M_short / dt, 1)}
     out["default_mode"] = "parallel"
+    # several chains per call (MVC_CHAINS in the drop-in): aggregate chain-sweeps/s
+    for mode, C, Mc in (("parallel", 16, 1000), ("exact", 256, 500)):
+        t0 = time.perf_counter()
+        mvc_amd.run_gibbs_cpp(y, Mc, Mc // 2, 1, seed=seed, mode=mode, n_chains=C, device=device, quiet=True)
+        dt = time.perf_counter() - t0
+        out[f"{mode}_gpu_{C}chains"] = {"chains": C, "sweeps": Mc, "s": round(dt, 2),
+                                        "chain_sweeps_per_s": round(C * Mc / dt, 1)}
     return out
 
 
@@ -506,6 +513,13 @@ def main():
             ch["cpu_cores_compared"] = cores
             ch["reference_cpu_same_cores"] = round(cores * ref1, 3)
             ch["vs_reference_cpu_same_cores"] = round(ch["value"] / (cores * ref1), 3)
+            ns = out["extra"]["newsim_call"]
+            r1 = ns["reference_cpu_1core"]["sweeps_per_s"]
+            for key in ("parallel_gpu_16chains", "exact_gpu_256chains"):
+                if key in ns:
+                    cores = min(ns[key]["chains"], os.cpu_count() or 1)
+                    ns[key]["cpu_cores_compared"] = cores
+                    ns[key]["vs_reference_cpu_same_cores"] = round(ns[key]["chain_sweeps_per_s"] / (cores * r1), 3)
     if world == 1 and not args.no_cpu_baseline and y is not None:
         out["cpu_baseline"] = leg("cpu_baseline", cpu_baseline, y, z, V, K, D, args.seed)
     print(json.dumps(out), flush=True)

@@ -39,6 +39,7 @@ struct Repair {
   int32_t streak;     // consecutive stays seen by the run kernel since its last mover
   int32_t restride;   // 1: the run kernel's LDS layout is too small for T / the dish lists (host relaunches)
   int32_t moves, births, newdish, rounds;
+  int32_t lastm, gapq;  // the last mover, and the moving average (x16) of the gaps between movers
   int32_t Klist[MVC_MAXV];
   unsigned long long prof[8];   // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz)   // dish list length per view (dishes that died this sweep stay, l = 0)
 };
@@ -1412,6 +1413,8 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->win1 = n;
   R->fmin = n;
   R->W = A.Wmin;
+  R->lastm = 0;
+  R->gapq = 0;
   R->done = 0;
   R->overflow = 0;
   R->mode = kSeqScan;
@@ -1861,6 +1864,24 @@ __device__ void seq_commit_move_split(SeqArgs &A, const SCache &cc, const Cust &
   }
 }
 
+// The run kernel's stay limit adapts to how sparse the movers are: after
+// L.limit stays in a row it hands over to grid windows, but where the gaps
+// between movers average more than kSparseGap customers a window (one
+// customer per wavefront over the grid, ~the latency of one evaluation) finds
+// the next mover sooner than run steps of a few customers each, so the limit
+// drops to kSparseLimit (measured: configs[3] after its cold transient, gaps
+// ~160: 1.36 s per sweep at 64, 0.40 at 8; configs[1], gaps ~5: 0.35 s at 64,
+// 0.45 at 8).  Only the schedule of the work changes, not any decision.
+constexpr int kSparseGap = 32, kSparseLimit = 8;
+__device__ __forceinline__ void note_mover(int32_t &lastm, int32_t &gapq, int f) {
+  const int gap = min(f - lastm, 1 << 20);
+  gapq = (3 * gapq + 16 * gap) >> 2;
+  lastm = f;
+}
+__device__ __forceinline__ int stay_limit(int limit, int gapq) {
+  return gapq > 16 * kSparseGap ? min(limit, kSparseLimit) : limit;
+}
+
 // Resolve the grid window evaluated by the last mvc_seq_eval_kernel (thread 0).
 __device__ void seq_resolve_window(const SeqArgs &A, Repair *R) {
   const int n = A.P.n;
@@ -1871,6 +1892,7 @@ __device__ void seq_resolve_window(const SeqArgs &A, Repair *R) {
     R->pend = 1;
     R->pchoice = A.choice[f];
     R->W = A.Wmin;
+    note_mover(R->lastm, R->gapq, f);
   } else {             // a mover-free window: every customer in it is final
     R->cur = R->win1;
     R->W = min(2 * R->W, A.Wmax);
@@ -1953,6 +1975,7 @@ struct RunCursor {
   int landed;                     // ring: customers [.., landed) are in LDS (every request before them waited for)
   int lpc;                        // wide evaluation: the customer whose lp rows wave 0's scratch holds (-1: none)
   int32_t cnt[3];                 // moves, births, new dishes
+  int32_t lastm, gapq;            // Repair::lastm / gapq
   int ch[kSeqRunWaves], p0[kSeqRunWaves];
   int chb[2][kSeqLcThreads / 64], p0b[2][kSeqLcThreads / 64];   // the lane-column loop's, by step parity
   int ntb[2][kSeqLcThreads / 64][2];   // ... and n_t of the mover's two tables before its move
@@ -2152,10 +2175,11 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
         U.pc = U.ch[f];
         U.pp0 = U.p0[f];
         U.lpc = (kWide && !kLds) ? U.cur : -1;
+        note_mover(U.lastm, U.gapq, U.cur);
       } else {
         U.cur = U.i + m;
         U.streak += m;
-        if (U.streak >= L.limit) U.mode = kSeqScan;
+        if (U.streak >= stay_limit(L.limit, U.gapq)) U.mode = kSeqScan;
         if (U.cur >= n) U.done = 1;
       }
       U.go = !U.done && (U.mode == kSeqRun || U.pend);
@@ -2195,6 +2219,7 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
   int cur = U.cur, pend = U.pend, pc = U.pc, pp0 = U.pp0, mode = U.mode, streak = U.streak, done = U.done;
   int fill = U.fill, landed = U.landed, par = 0;
   int pnt0 = 0, pntc = 0;   // n_t of the pending mover's two tables before its move
+  int lastm = U.lastm, gapq = U.gapq;
   if (pend && pc >= 0) {    // a mover carried over from the previous launch
     pnt0 = cc.n_t[pp0];
     pntc = cc.n_t[pc];
@@ -2208,7 +2233,8 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
   for (;;) {
     RUN_T0();
     if (pend) {
-      if (pc < 0) break;   // a birth: left pending for mvc_seq_birth_kernel
+      if (pc < 0) break;   // a birth: left pending for mvc_seq_birth_kernel (inlined here, the
+                           // general commit costs the loop 184 B of scratch and flat accesses)
       // the mover was evaluated in the previous step (or staged above), so its
       // row is in the ring (landed, not yet reused: requests stop a ring ahead of it)
       seq_commit_move_split(A, cc, G.cust(cur, V, D), cur, pp0, pc, pnt0, pntc, U.cnt);
@@ -2281,10 +2307,11 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
         pnt0 = U.ntb[par][f][0];
         pntc = U.ntb[par][f][1];
       }
+      note_mover(lastm, gapq, cur);
     } else {
       cur = i0 + m;
       streak += m;
-      if (streak >= L.limit) mode = kSeqScan;
+      if (streak >= stay_limit(L.limit, gapq)) mode = kSeqScan;
       if (cur >= n) done = 1;
     }
     par ^= 1;
@@ -2306,6 +2333,8 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
     U.done = done;
     U.fill = fill;
     U.landed = landed;
+    U.lastm = lastm;
+    U.gapq = gapq;
   }
 }
 
@@ -2357,6 +2386,8 @@ __global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void m
     U.cnt[0] = R->moves;
     U.cnt[1] = R->births;
     U.cnt[2] = R->newdish;
+    U.lastm = R->lastm;
+    U.gapq = R->gapq;
   }
   __syncthreads();
   if (!U.go || !(U.mode == kSeqRun || U.pend)) {
@@ -2446,6 +2477,8 @@ __global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void m
     R->moves = U.cnt[0];
     R->births = U.cnt[1];
     R->newdish = U.cnt[2];
+    R->lastm = U.lastm;
+    R->gapq = U.gapq;
     if (restride) R->restride = 1;
     if (U.done && !U.pend) {
       R->done = 1;
