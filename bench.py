@@ -32,13 +32,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
 
-# The 16-chain leg runs 16 chains in this process, one HIP stream each; HIP
-# maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by
-# default, and the GPU pool's environment sets 4), and beyond that streams
-# share queues and their kernels serialise.  The library
-# leaves the caller's setting alone, so the bench, which is the caller here,
-# asks for 32 before anything starts HIP.
-os.environ["GPU_MAX_HW_QUEUES"] = "32"
+# The legs that run many chains at once (one HIP stream each) run in a child
+# process with GPU_MAX_HW_QUEUES = 32 (child_leg): HIP maps a process's
+# streams onto that many hardware queues (4 by default, and the GPU pool's
+# environment sets 4), beyond which streams share queues and their kernels
+# serialise.  Not in this process: once many queues are live,
+# every later launch-heavy leg runs slower (configs[1] cold sweep 0: 0.97 s
+# alone, 1.44 s after a 16-stream run, r3r), so the headline and the
+# single-chain legs keep the caller's setting.
+HW_QUEUES_MULTI = "32"
 
 import numpy as np  # noqa: E402
 
@@ -65,6 +67,8 @@ def parse():
     ap.add_argument("--shard", action="store_true",
                     help="N > 1: ONE chain split over the N GPUs (within-chain N-sharding of phase A, an RCCL "
                          "all-gather of the choices per sweep; strong scaling) instead of one chain per GPU")
+    ap.add_argument("--leg", default=None, help=argparse.SUPPRESS)   # child_leg: run one multi-chain leg, print it
+    ap.add_argument("--leg-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra lines (other configs, exact schedule, cold start, reference CPU)")
     return ap.parse_args()
@@ -186,9 +190,8 @@ def gpu_line(config, seed, device, steps=10, warmup=3):
 def gpu_chains_line(config, seed, device, chains=16, sweeps=1):
     """Several chains of one config on one GPU at once (parallel-mode ChainSet:
     one stream and host thread per chain, the data shared), warm
-    start at the generating partition: aggregate chain-sweeps/s.  The loader
-    runs with 32 hardware queues (set at the top of this file), so 16 chains
-    overlap."""
+    start at the generating partition: aggregate chain-sweeps/s.  Run through
+    child_leg (a process with 32 hardware queues), so the 16 chains overlap."""
     from mvc_amd import data
     from mvc_amd.sampler import Sampler
     N, V, D, K, desc = CONFIGS[config]
@@ -284,7 +287,16 @@ def newsim_call_line(seed, device, M=10000, M_short=2000):
     dt = time.perf_counter() - t0
     out["exact_gpu"] = {"sweeps": M_short, "s": round(dt, 2), "sweeps_per_s": round(M_short / dt, 1)}
     out["default_mode"] = "parallel"
-    # several chains per call (MVC_CHAINS in the drop-in): aggregate chain-sweeps/s
+    return out
+
+
+def newsim_chains_line(seed, device):
+    """The same call with several chains per call (MVC_CHAINS in the drop-in):
+    aggregate chain-sweeps/s, parallel schedule 16 chains, exact 256."""
+    import mvc_amd
+    from mvc_amd import data
+    y, _ = data.new_simulation(seed)
+    out = {}
     for mode, C, Mc in (("parallel", 16, 1000), ("exact", 256, 500)):
         t0 = time.perf_counter()
         mvc_amd.run_gibbs_cpp(y, Mc, Mc // 2, 1, seed=seed, mode=mode, n_chains=C, device=device, quiet=True)
@@ -292,6 +304,20 @@ def newsim_call_line(seed, device, M=10000, M_short=2000):
         out[f"{mode}_gpu_{C}chains"] = {"chains": C, "sweeps": Mc, "s": round(dt, 2),
                                         "chain_sweeps_per_s": round(C * Mc / dt, 1)}
     return out
+
+
+CHILD_LEGS = {"ns16": lambda seed, dev: gpu_chains_line("ns", seed, dev), "newsim_chains": newsim_chains_line}
+
+
+def child_leg(name, seed, device, timeout=600):
+    """Run CHILD_LEGS[name] in a child process (its own HIP runtime, 32 hardware queues)."""
+    import subprocess
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=HW_QUEUES_MULTI)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--leg", name, "--seed", str(seed),
+                        "--leg-device", str(device)], env=env, capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"bench leg {name} failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def newsim_call_cpu(seed, M_short=2000):
@@ -333,6 +359,9 @@ def cold_start(seed, device, sweeps=4):
 
 def main():
     args = parse()
+    if args.leg:   # a child_leg process: one multi-chain leg, one JSON line
+        print(json.dumps(CHILD_LEGS[args.leg](args.seed, args.leg_device)), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -495,12 +524,13 @@ def main():
             # the in-order repair dominates; one sweep (~15 s) is timed
             "north_star_literal_gpu": leg("north_star_literal_gpu", gpu_line, "ns", args.seed, local, 1, 0),
             # the same with 16 chains at once (compare reference_schedule_cpu: one chain per core)
-            "north_star_literal_gpu_16chains": leg("north_star_literal_gpu_16chains", gpu_chains_line, "ns",
+            "north_star_literal_gpu_16chains": leg("north_star_literal_gpu_16chains", child_leg, "ns16",
                                                    args.seed, local),
             "configs1_gpu": leg("configs1_gpu", gpu_line, "c2", args.seed, local),
             "configs4_full_gpu": leg("configs4_full_gpu", config5_line, args.seed, local),
             "exact_schedule_gpu": leg("exact_schedule_gpu", gpu_exact_line, args.seed, local),
-            "newsim_call": leg("newsim_call", newsim_call_line, args.seed, local),
+            "newsim_call": {**leg("newsim_call", newsim_call_line, args.seed, local),
+                            **leg("newsim_chains", child_leg, "newsim_chains", args.seed, local)},
             "cold_start_gpu": leg("cold_start_gpu", cold_start, args.seed, local),
         }
         if not args.no_cpu_baseline:

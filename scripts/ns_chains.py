@@ -8,6 +8,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["GPU_MAX_HW_QUEUES"] = "32"   # C concurrent chains, one stream each; before HIP starts
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
 
 import bench  # noqa: E402
@@ -20,7 +21,6 @@ def main():
     y, z = data.synthetic(N, V, D, K, seed=1999)
     st = bench.warm_state(z, V, K)
     for C in [int(a) for a in sys.argv[1:]] or [8]:
-        # importing bench set GPU_MAX_HW_QUEUES=32 for this process before HIP started
         s = Sampler(y, seed=1999, mode="parallel", n_chains=C, device=0)
         for c in range(C):
             s.set_state(*st, chain=c)
