@@ -1802,6 +1802,8 @@ class ParallelSampler : public Sampler {
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
   bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
+  bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
+  bool vp_stats = false;          // MVC_VP_STATS=1
 
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
@@ -1917,7 +1919,8 @@ class ParallelSampler : public Sampler {
     lpall_attr<8, 8>();
     lpall_attr<16, 8>();
     // (instance 2 runs the global-scratch layout only: no dynamic LDS)
-    for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>})
+    for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>,
+                          (const void *)mvc_seq_run_kernel<4>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {
@@ -1931,6 +1934,8 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
+    if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
+    if (const char *e = getenv("MVC_VP_STATS")) vp_stats = e[0] == '1';
     if (const char *e = getenv("MVC_WIDE")) use_wide = e[0] != '0';
     if (const char *e = getenv("MVC_EARLY_MH")) early_mh_off = e[0] == '0';
     if (const char *e = getenv("MVC_RUN_LDS")) force_global = e[0] == '0';
@@ -2509,7 +2514,7 @@ class ParallelSampler : public Sampler {
   // lists Klist, with room for growth (a birth past it makes the kernel exit
   // with R->restride; the host then relaunches with a new layout).  Falls back
   // to the per-wave global scratch when even a few waves do not fit.
-  SeqLds run_layout(int T, const int32_t *Klist) const {
+  SeqLds run_layout(int T, const int32_t *Klist, bool vp_ok = true) const {
     int kmax = 1;
     for (int v = 0; v < V; ++v) kmax = std::max(kmax, (int)Klist[v]);
     SeqLds L{};
@@ -2543,6 +2548,12 @@ class ParallelSampler : public Sampler {
         L.pfn = rn ? std::max(1, rn / 2) : 0;
         L.lc = (use_lc && s1 && rn > 0 && L.ts <= 64 * kLcChunks) ? 1 : 0;
         if (L.lc) L.nws = std::min(L.nws, kSeqLcThreads / 64);   // its block has 4 waves
+        // value prediction (lc == 2) where its overlay fits: V <= kVpV, every dish list <= 128, and the
+        // overlay's S1 columns [kVpE][D] after the ring (which follows the clamped nws scratches)
+        L.vpo = L.cache_dbl + (int64_t)L.nws * L.stride + (int64_t)rn * slot;
+        if (L.lc && use_vp && vp_ok && V <= kVpV && kmax <= 128 && L.nws >= kSeqLcThreads / 64 &&
+            left - (int64_t)rn * slot >= (int64_t)kVpE * D)
+          L.lc = 2;
         return L;
       }
     }
@@ -2577,7 +2588,8 @@ class ParallelSampler : public Sampler {
     else
       hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
     MVC_HIP(hipGetLastError());
-    SeqLds L = run_layout(c.T, c.K.data());
+    bool vp_ok = true;   // value prediction until it stops itself in this sweep (R->vpoff)
+    SeqLds L = run_layout(c.T, c.K.data(), vp_ok);
     // the gated early MH (below) only where no per-phase timers bracket the
     // repair and the MH separately (they would time the MH as repair)
     const bool early_mh = !early_mh_off && (!timers.on || timers.coarse);
@@ -2588,9 +2600,12 @@ class ParallelSampler : public Sampler {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
         else
-          hipLaunchKernelGGL(L.lc ? mvc_seq_run_kernel<3> : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
+          hipLaunchKernelGGL(L.lc ? (L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
+                                  : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
                              dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads),
-                             L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D))) : 0,
+                             L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D) +
+                                                   (L.lc == 2 ? (int64_t)kVpE * D : 0)))
+                                   : 0,
                              stream, Q, L);
         if (L.lc && !repair_grid_only)   // its loop leaves births pending
           hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, Q);
@@ -2614,8 +2629,12 @@ class ParallelSampler : public Sampler {
         Q = make_seq(c, s);
         continue;
       }
+      if (rs_host->vpoff && vp_ok) {   // predictions missed (or a dish list outgrew them): plain lane columns
+        vp_ok = false;
+        if (L.lc == 2) L.lc = 1;
+      }
       if (rs_host->restride) {
-        L = run_layout(rs_host->T, rs_host->Klist);
+        L = run_layout(rs_host->T, rs_host->Klist, vp_ok);
         MVC_HIP(hipMemsetAsync(&c.R->restride, 0, sizeof(int32_t), stream));
         continue;
       }
@@ -2636,7 +2655,11 @@ class ParallelSampler : public Sampler {
             rs_host->prof[1] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[2] * 0.01 / std::max(1ull, rs_host->prof[7]),
             rs_host->prof[3] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[4] * 0.01 / std::max(1ull, rs_host->prof[7]),
             rs_host->prof[5] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[6] * 0.01 / std::max(1ull, rs_host->prof[7]));
+    fprintf(stderr, "runprof decided %llu same-as-phase-A %llu | movers %llu same-as-phase-A %llu\n", rs_host->prof[8],
+            rs_host->prof[9], rs_host->prof[10], rs_host->prof[11]);
 #endif
+    if (vp_stats)   // MVC_VP_STATS=1: value prediction's steps and full hits of this sweep, on stderr
+      fprintf(stderr, "mvc vp steps %d hits %d off %d\n", rs_host->vpsteps, rs_host->vphits, rs_host->vpoff);
     c.last[0] = rs_host->moves;
     c.last[1] = rs_host->births;
     c.last[2] = rs_host->rounds;

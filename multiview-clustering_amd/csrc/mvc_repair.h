@@ -40,8 +40,10 @@ struct Repair {
   int32_t restride;   // 1: the run kernel's LDS layout is too small for T / the dish lists (host relaunches)
   int32_t moves, births, newdish, rounds;
   int32_t lastm, gapq;  // the last mover, and the moving average (x16) of the gaps between movers
+  int32_t vpoff;        // 1: value prediction stopped for this sweep (predictions miss, or a dish list > 128)
+  int32_t vpsteps, vphits;   // vp steps, and those whose predictions all held
   int32_t Klist[MVC_MAXV];
-  unsigned long long prof[8];   // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz)   // dish list length per view (dishes that died this sweep stay, l = 0)
+  unsigned long long prof[12];  // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz), steps, decided customers, phase-A hits
 };
 
 constexpr int32_t kSeqScan = 0, kSeqRun = 1;
@@ -51,7 +53,7 @@ constexpr int32_t kSeqScan = 0, kSeqRun = 1;
 // (no global read-modify-write inside the timed phases) and adds them to
 // R->prof when the kernel exits; the host prints them per sweep.  Tuning aid only.
 #ifdef MVC_RUN_PROF
-__shared__ unsigned long long mvc_prof_lds[8];
+__shared__ unsigned long long mvc_prof_lds[12];
 #define RUN_T0() uint64_t _rt = wall_clock64()
 #define RUN_MARK(k) do { const uint64_t _n = wall_clock64(); \
     if (threadIdx.x == 0) mvc_prof_lds[k] += _n - _rt; _rt = _n; } while (0)
@@ -81,7 +83,8 @@ struct SeqLds {
   int32_t ring;         // customers in the staged-row ring (power of 2, after the per-wave scratch; 0: none)
   int32_t pfn;          // customers prefetched into the ring per step
   int32_t tw;           // waves per customer (1: seq_resample; kSeqRunWaves: seq_resample_wide); nws customers per step
-  int32_t lc;           // 1: the lane-column evaluation (seq_resample_lc; LDS layout with S1 cached, ts <= 512)
+  int32_t lc;           // 1: the lane-column evaluation (seq_resample_lc; LDS layout with S1 cached, ts <= 512); 2: + value prediction
+  int64_t vpo;          // lc == 2: offset (doubles) of the overlay's S1 columns [kVpE][D] in the dynamic LDS
 };
 // ring slot: y rows [V][D], Y2 [V], z (as a double)
 __host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
@@ -1035,14 +1038,100 @@ __device__ __forceinline__ int row16_isum_dpp(int x) {
 template <int k>
 __device__ __forceinline__ double row_bcast_d(double x) { return dpp_d<0x150 + k>(x); }
 
+// Value prediction (vp, the lane-column kernel's second instance): the repair
+// draws customer i with the same uniform as phase A, so its decision nearly
+// always equals its phase-A choice (98 % at the literal and at configs[1]
+// steady state).  A vp step evaluates customers i .. i+3 at once, customer
+// i + w against the state with the PREDICTED decisions (phase-A choices) of
+// i .. i+w-1 applied.  That state is the current one plus an overlay of what
+// the predicted moves touch (their tables' counts and log masses, T_ne, L_v,
+// and per view the left / joined dishes' counts, coefficients and S1 columns),
+// built at the start of the step with the commit's own arithmetic.  The step
+// then decides customers up to the first whose decision differs from its
+// prediction: every one of them was evaluated against the state the
+// sequential schedule has at its turn.
+constexpr int kVpMoves = 4, kVpV = 8, kVpE = kVpMoves * kVpV * 2;
+struct VpOv {
+  int nm;                                      // predicted customers in the overlay (i .. i+nm-1)
+  int mv[kVpMoves], p0[kVpMoves], c[kVpMoves]; // mv: customer i+m is a predicted move p0 -> c
+  int dies[kVpMoves], born[kVpMoves];          // its table p0 dies, its table c is born (with the earlier moves applied)
+  int pz[kVpMoves], pcs[kVpMoves];             // the step's customers' tables and predictions
+  int ntp0[kVpMoves], ntc[kVpMoves], tne[kVpMoves];   // after move m
+  int ltot[kVpMoves * kVpV];                   // L_v after move m
+  int chg[kVpMoves * kVpV];                    // move m changes the dish of view v (S1 deltas)
+  int j[kVpE], dn[kVpE], dl[kVpE];             // dish entry e = (m kVpV + v) 2 + (0 left | 1 joined), values after m
+  int s1x[kVpE];                               // 1: the entry's S1 column differs from the state's (in the LDS area vpo)
+  double lmp0[kVpMoves], lmc[kVpMoves];
+  double Q[kVpE], c0[kVpE], cb[kVpE], xm[kVpE], ym[kVpE], cbm[kVpE];
+};
+__shared__ VpOv mvc_vp_ov;
+// one wave's view of the overlay: the moves m < nw apply
+struct VpCtx {
+  int nw;                          // moves of the overlay this wave's customer sees
+  int tne;                         // T_ne with them applied
+  const double *s1;                // the overlay's S1 columns [kVpE][D] (LDS)
+};
+// the overlay entry of dish j of view v (the latest move m < nw touching it), or -1
+template <bool kVp>
+__device__ __forceinline__ int vp_de(const VpCtx &X, int v, int j) {
+  int e = -1;
+  if constexpr (kVp) {
+#pragma unroll
+    for (int m = 0; m < kVpMoves; ++m)
+      if (m < X.nw) {
+        const int e0 = (m * kVpV + v) * 2;
+        if (mvc_vp_ov.j[e0] == j) e = e0;
+        if (mvc_vp_ov.j[e0 + 1] == j) e = e0 + 1;
+      }
+  }
+  return e;
+}
+// n_t and log mass of table p with the moves m < nw applied
+template <bool kVp>
+__device__ __forceinline__ void vp_table(const VpCtx &X, int p, int &nt, double &lm) {
+  if constexpr (kVp) {
+#pragma unroll
+    for (int m = 0; m < kVpMoves; ++m)
+      if (m < X.nw && mvc_vp_ov.mv[m]) {
+        if (p == mvc_vp_ov.p0[m]) {
+          nt = mvc_vp_ov.ntp0[m];
+          lm = mvc_vp_ov.lmp0[m];
+        }
+        if (p == mvc_vp_ov.c[m]) {
+          nt = mvc_vp_ov.ntc[m];
+          lm = mvc_vp_ov.lmc[m];
+        }
+      }
+  }
+}
+// L_v with the moves m < nw applied
+template <bool kVp>
+__device__ __forceinline__ int vp_ltot(const VpCtx &X, int v, int base) {
+  int L = base;
+  if constexpr (kVp) {
+#pragma unroll
+    for (int m = 0; m < kVpMoves; ++m)
+      if (m < X.nw && mvc_vp_ov.mv[m]) L = mvc_vp_ov.ltot[m * kVpV + v];
+  }
+  return L;
+}
+
 // The own dish's value with the customer removed from its
 // dot product G = y . S1[:, j0].
+template <bool kVp = false>
 __device__ __forceinline__ double lc_self(const SView &W, int vv, int ks, int j0, double G, double Y2i, double hy,
-                                          double h) {
+                                          double h, int eown = -1) {
+  double Q = W.Q[vv * ks + j0], xm = W.xm[vv * ks + j0], ym = W.ym[vv * ks + j0], cbm = W.cbm[vv * ks + j0];
+  if (kVp && eown >= 0) {
+    Q = mvc_vp_ov.Q[eown];
+    xm = mvc_vp_ov.xm[eown];
+    ym = mvc_vp_ov.ym[eown];
+    cbm = mvc_vp_ov.cbm[eown];
+  }
   const double Gp = G - Y2i;
-  const double Qp = (W.Q[vv * ks + j0] - 2.0 * G) + Y2i;
-  const double c0 = W.xm[vv * ks + j0] - (0.5 * Qp) / W.ym[vv * ks + j0];
-  return __builtin_fma(Gp + hy, W.cbm[vv * ks + j0], c0) + h;
+  const double Qp = (Q - 2.0 * G) + Y2i;
+  const double c0 = xm - (0.5 * Qp) / ym;
+  return __builtin_fma(Gp + hy, cbm, c0) + h;
 }
 // One view's terms for the lane-column evaluation, NU dishes per lane
 // (j = col + 16 u, K <= 16 NU): the NU dot products run as interleaved fma
@@ -1051,14 +1140,30 @@ __device__ __forceinline__ double lc_self(const SView &W, int vv, int ks, int j0
 // LDS load of a step issued before its first use; the lp values and counts
 // stay in registers for the column partial.  Lanes past K load a clamped
 // column and contribute nothing (w = 0, exp(-inf) = 0: cs + 0 = cs).
-template <int NU>
+template <int NU, bool kVp = false>
 __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, const double *S1v, int s1s, int D,
                                               int vv, int ks, int col, int K, int j0, int l0p, double hy, double h,
                                               double Y2i, double lfn, double sigma, const int *dl, double *lpv,
-                                              double &mx, int &cnt, double &cs) {
+                                              double &mx, int &cnt, double &cs, const VpCtx &X) {
   int jc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) jc[u] = min(col + 16 * u, ks - 1);
+  // vp: a dish whose S1 column an earlier predicted move changed is read from
+  // the overlay's copy of that column (stride 1) instead of the state's
+  const double *colp[NU];
+  int cst[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    colp[u] = S1v + jc[u];
+    cst[u] = s1s;
+    if constexpr (kVp) {
+      const int e = vp_de<kVp>(X, vv, col + 16 * u);
+      if (e >= 0 && mvc_vp_ov.s1x[e]) {
+        colp[u] = X.s1 + (size_t)e * D;
+        cst[u] = 1;
+      }
+    }
+  }
   double G[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) G[u] = 0.0;
@@ -1071,7 +1176,7 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
     for (int k = 0; k < DB; ++k) {
       yd[k] = yv[d + k];
 #pragma unroll
-      for (int u = 0; u < NU; ++u) sd[k][u] = S1v[(d + k) * s1s + jc[u]];
+      for (int u = 0; u < NU; ++u) sd[k][u] = kVp ? colp[u][(d + k) * cst[u]] : S1v[(d + k) * s1s + jc[u]];
     }
 #pragma unroll
     for (int k = 0; k < DB; ++k)
@@ -1081,13 +1186,13 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
   for (; d < D; ++d) {
     const double yd = yv[d];
 #pragma unroll
-    for (int u = 0; u < NU; ++u) G[u] = __builtin_fma(yd, S1v[d * s1s + jc[u]], G[u]);
+    for (int u = 0; u < NU; ++u) G[u] = __builtin_fma(yd, kVp ? colp[u][d * cst[u]] : S1v[d * s1s + jc[u]], G[u]);
   }
   double Gown = 0.0;
 #pragma unroll
   for (int u = 0; u < NU; ++u)
     if (col + 16 * u == j0) Gown = G[u];
-  const double self = lc_self(W, vv, ks, j0, Gown, Y2i, hy, h);
+  const double self = lc_self<kVp>(W, vv, ks, j0, Gown, Y2i, hy, h, vp_de<kVp>(X, vv, j0));
   double lp[NU];
   int lj[NU];
   mx = -MVC_PM_INF;
@@ -1096,8 +1201,17 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
   for (int u = 0; u < NU; ++u) {
     const int j = col + 16 * u;
     const bool valid = j < K, own = j == j0;
-    const double fr = __builtin_fma(G[u] + hy, W.cb[vv * ks + jc[u]], W.c0[vv * ks + jc[u]]) + h;
-    const int dlj = dl[jc[u]];
+    double cbj = W.cb[vv * ks + jc[u]], c0j = W.c0[vv * ks + jc[u]];
+    int dlj = dl[jc[u]];
+    if constexpr (kVp) {
+      const int e = vp_de<kVp>(X, vv, j);
+      if (e >= 0) {
+        cbj = mvc_vp_ov.cb[e];
+        c0j = mvc_vp_ov.c0[e];
+        dlj = mvc_vp_ov.dl[e];
+      }
+    }
+    const double fr = __builtin_fma(G[u] + hy, cbj, c0j) + h;
     lp[u] = own ? self : fr;
     lj[u] = valid ? (own ? l0p : dlj) : 0;
     if (valid) lpv[j] = lp[u];
@@ -1159,10 +1273,10 @@ __device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double 
 // scratch e[]; block sums pw16 per row and running block totals C_b kept in
 // lane b.  kOne: one step covers every table (nch <= QB), so the scores stay
 // in registers between the two passes.  Same operations and order for every QB.
-template <int QB, bool kOne>
+template <int QB, bool kOne, bool kVp = false>
 __device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScratch &S, int V, int ts, int lps, int p0,
                                                   int T, double sg, double lmass0, double s_new, double &M,
-                                                  double &tot, double &Cb) {
+                                                  double &tot, double &Cb, const VpCtx &X) {
   const int lane = threadIdx.x & 63;
   const int TB = (T + 15) >> 4, nch = (T + 63) >> 6;
   double xk[QB];
@@ -1175,10 +1289,13 @@ __device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScrat
     for (int h2 = 0; h2 < QB; ++h2) {
       const int p = 64 * (q0 + h2) + lane;
       pp[h2] = p;
-      const int np = p < T ? W.n_t[p] - (p == p0 ? 1 : 0) : 0;
+      int ntp = p < T ? W.n_t[p] : 0;
+      double lmp = p < T ? W.lmass[p] : 0.0;
+      vp_table<kVp>(X, p, ntp, lmp);
+      const int np = p < T ? ntp - (p == p0 ? 1 : 0) : 0;
       const double mass = (double)np - sg;
       inc[h2] = p < T && np >= 1 && mass > 0.0;
-      x[h2] = inc[h2] ? (p == p0 ? lmass0 : W.lmass[p]) : -MVC_PM_INF;
+      x[h2] = inc[h2] ? (p == p0 ? lmass0 : lmp) : -MVC_PM_INF;
     }
     for (int v0 = 0; v0 < V; v0 += 4) {
       int dj[QB][4];
@@ -1253,14 +1370,18 @@ __device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScrat
 // so the draw finds its block with one ballot.  hyp / cnewv: the sweep's
 // hyperparameters and new-dish constants, staged in LDS at kernel launch.
 constexpr int kLcChunks = 8;   // tables <= 512 (block totals in lanes b < 64 need TB <= 64)
-__device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
-                               const double *hyp, const double *cnewv) {
+template <bool kVp = false>
+__device__ __forceinline__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
+                               const double *hyp, const double *cnewv, const VpCtx &X = VpCtx{}) {
   const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
   const int V = A.P.V, D = A.P.D, ts = W.ts, ks = W.ks, lps = S.lps, s1s = W.s1s;
   const double ag = hyp[3 * V], sg = hyp[3 * V + 1];
-  const int np0 = W.n_t[p0] - 1;
+  int nt0 = W.n_t[p0];
+  double lm_unused = 0.0;
+  vp_table<kVp>(X, p0, nt0, lm_unused);
+  const int np0 = nt0 - 1;
   const bool alive = np0 > 0;
-  const int Tne_i = *W.T_ne - (alive ? 0 : 1);
+  const int Tne_i = (kVp ? X.tne : *W.T_ne) - (alive ? 0 : 1);
   const double mass0 = (double)np0 - sg;
   double s_new = 0.0, lmass0 = 0.0;
   const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);   // independent of the rest
@@ -1280,7 +1401,12 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     const double *S1v = W.S1T + vv * D * s1s;
     const int *dl = W.d_l + vv * ks;
     double *lpv = S.lp + vv * lps;
-    const int l0p = dl[j0] - (alive ? 0 : 1);
+    int dl0 = dl[j0];
+    if constexpr (kVp) {
+      const int e = vp_de<kVp>(X, vv, j0);
+      if (e >= 0) dl0 = mvc_vp_ov.dl[e];
+    }
+    const int l0p = dl0 - (alive ? 0 : 1);
     // lp of this lane's dishes (to the scratch for the table gathers), their
     // max over the included ones (l' > 0), K_act, and the column partial
     // w_j exp(lp_j - m) in ascending j (excluded dishes add +0)
@@ -1288,13 +1414,13 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     int cnt;
     const int nu = (max(max(readlane_i(K, 0), readlane_i(K, 16)), max(readlane_i(K, 32), readlane_i(K, 48))) + 15) >> 4;
     if (nu <= 1)
-      lc_view_terms<1>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+      lc_view_terms<1, kVp>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs, X);
     else if (nu <= 2)
-      lc_view_terms<2>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+      lc_view_terms<2, kVp>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs, X);
     else if (nu <= 4)
-      lc_view_terms<4>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
-    else if (nu <= 8)
-      lc_view_terms<8>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
+      lc_view_terms<4, kVp>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs, X);
+    else if (kVp || nu <= 8)   // (the vp kernel runs only while every K_v <= 128)
+      lc_view_terms<8, kVp>(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs, X);
     else
       lc_view_terms_loop(W, yv, S1v, s1s, D, vv, ks, col, K, j0, l0p, hy, h, Y2i, lfn, sigma, dl, lpv, mx, cnt, cs);
     const double m = lfn > mx ? lfn : mx;
@@ -1302,7 +1428,7 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
     double wn = alpha + (double)cnt * sigma;
     if (wn < 0.0) wn = 0.0;
     Sv = Sv + wn * mvc_exp_le0(lfn - m);
-    const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
+    const double denom = alpha + (double)(vp_ltot<kVp>(X, vv, W.Ltot[vv]) - (alive ? 0 : 1));
     // one log for the group: column 0 log S_v, column 1 log(denominator);
     // group 0, row 0 also the new-table mass (column 2) and the own table's
     // mass without the customer (column 3)
@@ -1324,11 +1450,11 @@ __device__ int seq_resample_lc(const SeqArgs &A, const SView &W, const Cust &C, 
   const int T = *W.T, TB = (T + 15) >> 4, nch = (T + 63) >> 6;
   double M, tot, Cb;
   if (nch <= 2)
-    lc_scores_weights<2, true>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb);
+    lc_scores_weights<2, true, kVp>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb, X);
   else if (nch <= 4)
-    lc_scores_weights<4, true>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb);
+    lc_scores_weights<4, true, kVp>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb, X);
   else
-    lc_scores_weights<4, false>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb);
+    lc_scores_weights<4, false, kVp>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb, X);
   RUN_MARK(1);
   const double Wt = mvc_exp_le0(s_new - M) + tot;
   double r = u_i * Wt;
@@ -1415,6 +1541,9 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->W = A.Wmin;
   R->lastm = 0;
   R->gapq = 0;
+  R->vpoff = 0;
+  R->vpsteps = 0;
+  R->vphits = 0;
   R->done = 0;
   R->overflow = 0;
   R->mode = kSeqScan;
@@ -1424,7 +1553,7 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->T = A.status[0];
   R->T_ne = A.status[V + 3];
   R->moves = R->births = R->newdish = R->rounds = 0;
-  for (int k = 0; k < 8; ++k) R->prof[k] = 0;
+  for (int k = 0; k < 12; ++k) R->prof[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
 }
 
@@ -1744,7 +1873,7 @@ __device__ __forceinline__ void gst(T *p, T v) {
 // when it drew c (the tables' counts are wave 0's to write).  No block
 // barrier inside: the caller's next barrier publishes the LDS writes; global
 // arrays are written through (store only) for the kernels after this one.
-__device__ void seq_commit_move_split(SeqArgs &A, const SCache &cc, const Cust &Ci, int i, int p0, int c, int nt0,
+__device__ __forceinline__ void seq_commit_move_split(SeqArgs &A, const SCache &cc, const Cust &Ci, int i, int p0, int c, int nt0,
                                       int ntc, int32_t *cnt) {
   ParState &P = A.P;
   Repair *R = A.R;
@@ -1883,7 +2012,7 @@ __device__ __forceinline__ int stay_limit(int limit, int gapq) {
 }
 
 // Resolve the grid window evaluated by the last mvc_seq_eval_kernel (thread 0).
-__device__ void seq_resolve_window(const SeqArgs &A, Repair *R) {
+__device__ __forceinline__ void seq_resolve_window(const SeqArgs &A, Repair *R) {
   const int n = A.P.n;
   if (R->done || R->overflow || !(R->win1 > R->win0)) return;
   const int f = R->fmin;
@@ -2029,8 +2158,8 @@ __device__ __forceinline__ void ring_fill_async(const SeqArgs &A, const Ring &G,
           src = (const int32_t *)(A.y + ((size_t)v * n + cc) * D + d) + half;
         } else if (e < V * D + V) {
           src = (const int32_t *)(A.Y2 + (size_t)(e - V * D) * n + cc) + half;
-        } else {
-          src = A.P.z + cc;
+        } else {   // z, then the phase-A choice (value prediction's guess)
+          src = half ? A.choice + cc : A.P.z + cc;
         }
         __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                          (__attribute__((address_space(3))) void *)(dst0 + (int64_t)q * 256), 4, 0, 0);
@@ -2041,6 +2170,9 @@ __device__ __forceinline__ void ring_fill_async(const SeqArgs &A, const Ring &G,
 }
 __device__ __forceinline__ int ring_z(const Ring &G, int c, int V, int D) {
   return ((const int32_t *)(G.at(c) + (size_t)V * D + V))[0];
+}
+__device__ __forceinline__ int ring_pred(const Ring &G, int c, int V, int D) {
+  return ((const int32_t *)(G.at(c) + (size_t)V * D + V))[1];
 }
 
 // The run kernel's loop, for state read through the LDS cache (kLds) or the
@@ -2207,7 +2339,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 //     step without a commit has only one barrier, so a fast wave may write
 //     the next step's choices while a slow one still reads this step's);
 //   * every barrier waits for LDS operations only.
-__device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U, int &restride) {
+__device__ __forceinline__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U, int &restride) {
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
@@ -2314,6 +2446,20 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
       if (streak >= stay_limit(L.limit, gapq)) mode = kSeqScan;
       if (cur >= n) done = 1;
     }
+#ifdef MVC_RUN_PROF
+    if (tid == 0) {   // how often the sequential decision equals the phase-A choice (A.choice)
+      const int nd = f >= 0 ? f + 1 : m;
+      for (int k = 0; k < nd; ++k) {
+        const int ck = U.chb[par][k];
+        mvc_prof_lds[8] += 1;
+        if (A.choice[i0 + k] == ck) mvc_prof_lds[9] += 1;
+        if (k == f) {
+          mvc_prof_lds[10] += 1;
+          if (A.choice[i0 + k] == ck) mvc_prof_lds[11] += 1;
+        }
+      }
+    }
+#endif
     par ^= 1;
     RUN_MARK(6);
 #ifdef MVC_RUN_PROF
@@ -2338,6 +2484,490 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
   }
 }
 
+// ---- value prediction: the overlay, its commit, the loop ----
+
+// The step's predicted moves (uniform, every thread the same): customer
+// i0 + m moves p0 -> c when its phase-A choice c >= 0 differs from its table
+// p0; dies / born from the table counts with the earlier predicted moves applied.
+struct VpMoves {
+  int mv[kVpMoves], p0[kVpMoves], c[kVpMoves], dies[kVpMoves], born[kVpMoves];
+};
+// a[i] for a runtime i without indexing a register array (which would go to scratch)
+template <class T>
+__device__ __forceinline__ T vsel(const T (&a)[kVpMoves], int i) {
+  T r = a[0];
+#pragma unroll
+  for (int k = 1; k < kVpMoves; ++k)
+    if (i == k) r = a[k];
+  return r;
+}
+__device__ __forceinline__ VpMoves vp_moves(const SCache &cc, int nm, const int (&pz)[kVpMoves],
+                                            const int (&pcs)[kVpMoves]) {
+  VpMoves M;
+#pragma unroll
+  for (int m = 0; m < kVpMoves; ++m) {
+    M.mv[m] = m < nm && pcs[m] >= 0 && pcs[m] != pz[m];
+    M.p0[m] = pz[m];
+    M.c[m] = pcs[m];
+    M.dies[m] = M.born[m] = 0;
+    if (M.mv[m]) {
+      int a = cc.n_t[M.p0[m]], b = cc.n_t[M.c[m]];
+#pragma unroll
+      for (int m2 = 0; m2 < m; ++m2)
+        if (M.mv[m2]) {
+          a += (M.p0[m] == M.c[m2] ? 1 : 0) - (M.p0[m] == M.p0[m2] ? 1 : 0);
+          b += (M.c[m] == M.c[m2] ? 1 : 0) - (M.c[m] == M.p0[m2] ? 1 : 0);
+        }
+      M.dies[m] = a == 1;
+      M.born[m] = b == 0;
+    }
+  }
+  return M;
+}
+
+// The step's predicted moves into the overlay header (thread 0; a barrier
+// before vp_build): per-lane indexing by move reads them from LDS (indexing a
+// register array by a per-lane value would put it in scratch).
+__device__ __forceinline__ void vp_publish(const VpMoves &M, const int (&pz)[kVpMoves], const int (&pcs)[kVpMoves]) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int m = 0; m < kVpMoves; ++m) {
+      mvc_vp_ov.pz[m] = pz[m];
+      mvc_vp_ov.pcs[m] = pcs[m];
+      mvc_vp_ov.mv[m] = M.mv[m];
+      mvc_vp_ov.p0[m] = M.p0[m];
+      mvc_vp_ov.c[m] = M.c[m];
+      mvc_vp_ov.dies[m] = M.dies[m];
+      mvc_vp_ov.born[m] = M.born[m];
+    }
+  }
+}
+
+// Build the overlay (mvc_vp_ov) of the predicted moves of customers
+// i0 .. i0 + nm - 1 on the current LDS state: every value with the
+// arithmetic its commit would use (seq_commit_move_split), for the state
+// after moves 0 .. m.  yr[m]: customer i0 + m's staged row.  Block-wide; the
+// caller's barrier publishes it.
+__device__ __forceinline__ void vp_build(const SeqArgs &A, const SCache &cc, const VpMoves &M, int nm,
+                                         const double *const (&yr)[kVpMoves], double *ovs1) {
+  const int tid = threadIdx.x;
+  const int V = A.P.V, D = A.P.D, ks = cc.ks, ts = cc.ts;
+  const double *hyp = cc.hyp, *l2pt = cc.L2pt;
+  const double sg = hyp[3 * V + 1];
+  if (tid < 2 * kVpMoves) {   // the two tables of move m
+    const int m = tid >> 1, which = tid & 1;
+    if (mvc_vp_ov.mv[m]) {
+      const int p = which ? mvc_vp_ov.c[m] : mvc_vp_ov.p0[m];
+      int n_ = cc.n_t[p];
+#pragma unroll
+      for (int m2 = 0; m2 < kVpMoves; ++m2)
+        if (m2 <= m && M.mv[m2]) n_ += (p == M.c[m2] ? 1 : 0) - (p == M.p0[m2] ? 1 : 0);
+      const double lm = mvc_log((double)n_ - sg);
+      if (which) {
+        mvc_vp_ov.ntc[m] = n_;
+        mvc_vp_ov.lmc[m] = lm;
+      } else {
+        mvc_vp_ov.ntp0[m] = n_;
+        mvc_vp_ov.lmp0[m] = lm;
+      }
+    }
+    if (which == 0) {
+      int tne = *cc.T_ne;
+#pragma unroll
+      for (int m2 = 0; m2 < kVpMoves; ++m2)
+        if (m2 <= m && M.mv[m2]) tne += (M.born[m2] ? 1 : 0) - (M.dies[m2] ? 1 : 0);
+      mvc_vp_ov.tne[m] = tne;
+    }
+  } else if (tid >= 64 && tid < 64 + kVpMoves * kVpV) {   // L_v after move m (the commit's order of updates)
+    const int t = tid - 64, m = t / kVpV, v = t - m * kVpV;
+    if (v < V) {
+      int L = cc.Ltot[v];
+#pragma unroll
+      for (int m2 = 0; m2 < kVpMoves; ++m2)
+        if (m2 <= m && M.mv[m2] && (M.dies[m2] || M.born[m2])) {
+          if (M.dies[m2]) --L;
+          if (M.born[m2]) ++L;
+        }
+      mvc_vp_ov.ltot[m * kVpV + v] = L;
+    }
+  } else if (tid >= 128 && tid < 128 + 2 * kVpE) {   // dish entries (m, v, left | joined) x (coef | self parts)
+    const int t = tid - 128, part = t & 1, e = t >> 1, which = e & 1, mvv = e >> 1;
+    const int m = mvv / kVpV, v = mvv - m * kVpV;
+    const bool act = mvc_vp_ov.mv[m] && v < V;
+    const int vs = act ? v : 0;
+    const int pm0 = mvc_vp_ov.p0[m], pmc = mvc_vp_ov.c[m];
+    const int j0 = cc.dish[vs * ts + pm0], j1 = cc.dish[vs * ts + (act ? pmc : pm0)];
+    const int j = which ? j1 : j0;
+    // the moves 0 .. m that change this dish's statistics (dish of view v changed, j left or joined)
+    int n_ = cc.d_n[vs * ks + j], dl = cc.d_l[vs * ks + j];
+    bool touched = false;
+    int jl[kVpMoves], jj[kVpMoves], ch[kVpMoves];
+#pragma unroll
+    for (int m2 = 0; m2 < kVpMoves; ++m2) {
+      jl[m2] = cc.dish[vs * ts + M.p0[m2]];
+      jj[m2] = M.mv[m2] ? cc.dish[vs * ts + M.c[m2]] : jl[m2];
+      ch[m2] = m2 <= m && M.mv[m2] && jl[m2] != jj[m2];
+      if (ch[m2]) {
+        if (j == jl[m2]) { --n_; touched = true; }
+        if (j == jj[m2]) { ++n_; touched = true; }
+      }
+      if (m2 <= m && M.mv[m2]) {
+        if (M.dies[m2] && j == jl[m2]) --dl;
+        if (M.born[m2] && j == jj[m2]) ++dl;
+      }
+    }
+    double Q = cc.Q[vs * ks + j], c0 = cc.c0[vs * ks + j], cb = cc.cb[vs * ks + j];
+    double xm = cc.xm[vs * ks + j], ym = cc.ym[vs * ks + j], cbm = cc.cbm[vs * ks + j];
+    const int eo = (m * kVpV + v) * 2 + which;
+    if (act && touched) {   // the commit's refresh of this dish, after moves 0 .. m
+      double q = 0.0;
+      for (int d = 0; d < D; ++d) {
+        double x = cc.S1T[((size_t)vs * D + d) * ks + j];
+#pragma unroll
+        for (int m2 = 0; m2 < kVpMoves; ++m2)
+          if (ch[m2]) {
+            if (j == jl[m2]) x = x - yr[m2][vs * D + d];
+            if (j == jj[m2]) x = x + yr[m2][vs * D + d];
+          }
+        q = __builtin_fma(x, x, q);
+        if (part == 0) ovs1[(size_t)eo * D + d] = x;
+      }
+      const double tau = hyp[vs];
+      const double a = tau + (double)(part ? n_ - 1 : n_);
+      const double b = tau + (double)(part ? n_ : n_ + 1);
+      const double Xc = (double)D * ((-0.5 * l2pt[vs]) - 0.5 * mvc_log_nb(b / a));
+      const double Yc = (tau * a) * b;
+      const double Zc = 1.0 / (tau * b);
+      if (part) {
+        xm = Xc;
+        ym = Yc;
+        cbm = Zc;
+      } else {
+        Q = q;
+        c0 = Xc - (0.5 * q) / Yc;
+        cb = Zc;
+      }
+    }
+    if (part == 0) {
+      mvc_vp_ov.j[eo] = act ? j : -1;
+      mvc_vp_ov.s1x[eo] = act && touched;
+      mvc_vp_ov.dn[eo] = n_;
+      mvc_vp_ov.dl[eo] = dl;
+      mvc_vp_ov.Q[eo] = Q;
+      mvc_vp_ov.c0[eo] = c0;
+      mvc_vp_ov.cb[eo] = cb;
+      if (which == 0) mvc_vp_ov.chg[m * kVpV + v] = act && j0 != j1;
+    } else {
+      mvc_vp_ov.xm[eo] = xm;
+      mvc_vp_ov.ym[eo] = ym;
+      mvc_vp_ov.cbm[eo] = cbm;
+    }
+  }
+}
+
+// Commit the predicted moves of customers i0 .. i0 + nc - 1 (they held): the
+// overlay's values after the last of them into the LDS state and HBM, S1 and
+// S2 updated in move order (one thread per element).  Block-wide.
+__device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const VpMoves &M, int i0, int nc,
+                                          const double *const (&yr)[kVpMoves], int32_t *cnt) {
+  ParState &P = A.P;
+  Repair *R = A.R;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int V = P.V, D = P.D, KC = P.KC, ks = cc.ks, ts = cc.ts;
+  int last = -1, nmv = 0;
+#pragma unroll
+  for (int m = 0; m < kVpMoves; ++m)
+    if (m < nc && M.mv[m]) {
+      last = m;
+      ++nmv;
+    }
+  if (last < 0) return;
+  // S1 (threads over (v, d)) and S2 (threads over v), in move order
+  for (int e = tid; e < V * D; e += nt) {
+    const int v = e / D, d = e - v * D;
+    double *cl = cc.S1T + ((size_t)v * D + d) * ks;
+    double *col = P.S1T + ((size_t)v * D + d) * KC;
+#pragma unroll
+    for (int m = 0; m < kVpMoves; ++m)
+      if (m < nc && M.mv[m]) {
+        const int j0 = cc.dish[v * ts + M.p0[m]], j1 = cc.dish[v * ts + M.c[m]];
+        if (j0 != j1) {
+          const double yd = yr[m][v * D + d];
+          const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
+          cl[j0] = a0;
+          cl[j1] = a1;
+          gst(&col[j0], a0);
+          gst(&col[j1], a1);
+        }
+      }
+  }
+  if (tid >= 64 && tid < 64 + V) {
+    const int v = tid - 64;
+#pragma unroll
+    for (int m = 0; m < kVpMoves; ++m)
+      if (m < nc && M.mv[m]) {
+        const int j0 = cc.dish[v * ts + M.p0[m]], j1 = cc.dish[v * ts + M.c[m]];
+        if (j0 != j1) {
+          const double y2 = yr[m][V * D + v];
+          const double a0 = cc.S2[v * ks + j0] - y2, a1 = cc.S2[v * ks + j1] + y2;
+          cc.S2[v * ks + j0] = a0;
+          cc.S2[v * ks + j1] = a1;
+          gst(&P.S2[v * KC + j0], a0);
+          gst(&P.S2[v * KC + j1], a1);
+        }
+      }
+    cc.Ltot[v] = mvc_vp_ov.ltot[last * kVpV + v];
+    gst(&P.Ltot[v], mvc_vp_ov.ltot[last * kVpV + v]);
+  }
+  // dish entries whose dish no later committed move touches: their final values
+  if (tid >= 128 && tid < 128 + kVpE) {
+    const int e = tid - 128, mvv = e >> 1, m = mvv / kVpV, v = mvv - m * kVpV;
+    const int j = mvc_vp_ov.j[e];
+    if (m < nc && v < V && j >= 0) {
+      bool fin = !((e & 1) == 0 && mvc_vp_ov.j[e + 1] == j);   // j0 == j1: the joined entry writes
+#pragma unroll
+      for (int m2 = 0; m2 < kVpMoves; ++m2)
+        if (m2 > m && m2 < nc) {
+          const int e2 = (m2 * kVpV + v) * 2;
+          if (mvc_vp_ov.j[e2] == j || mvc_vp_ov.j[e2 + 1] == j) fin = false;
+        }
+      if (fin) {
+        cc.d_n[v * ks + j] = mvc_vp_ov.dn[e];
+        cc.d_l[v * ks + j] = mvc_vp_ov.dl[e];
+        cc.Q[v * ks + j] = mvc_vp_ov.Q[e];
+        cc.c0[v * ks + j] = mvc_vp_ov.c0[e];
+        cc.cb[v * ks + j] = mvc_vp_ov.cb[e];
+        cc.xm[v * ks + j] = mvc_vp_ov.xm[e];
+        cc.ym[v * ks + j] = mvc_vp_ov.ym[e];
+        cc.cbm[v * ks + j] = mvc_vp_ov.cbm[e];
+        gst(&P.d_n[v * KC + j], mvc_vp_ov.dn[e]);
+        gst(&P.d_l[v * KC + j], mvc_vp_ov.dl[e]);
+        gst(&P.Q[v * KC + j], mvc_vp_ov.Q[e]);
+        gst(&P.c0[v * KC + j], mvc_vp_ov.c0[e]);
+        gst(&P.cb[v * KC + j], mvc_vp_ov.cb[e]);
+      }
+    }
+  }
+  // the tables (last touch), T_ne, z and the move count
+  if (tid < 2 * kVpMoves) {
+    const int m = tid >> 1, which = tid & 1;
+    if (m < nc && mvc_vp_ov.mv[m]) {
+      const int p = which ? mvc_vp_ov.c[m] : mvc_vp_ov.p0[m];
+      bool fin = true;
+#pragma unroll
+      for (int m2 = 0; m2 < kVpMoves; ++m2)
+        if (m2 > m && m2 < nc && M.mv[m2] && (M.p0[m2] == p || M.c[m2] == p)) fin = false;
+      if (fin) {
+        const int n_ = which ? mvc_vp_ov.ntc[m] : mvc_vp_ov.ntp0[m];
+        const double lm = which ? mvc_vp_ov.lmc[m] : mvc_vp_ov.lmp0[m];
+        cc.n_t[p] = n_;
+        cc.lmass[p] = lm;
+        gst(&P.n_t[p], n_);
+        gst(&P.lmass[p], lm);
+      }
+      if (which == 0) gst(&P.z[i0 + m], mvc_vp_ov.c[m]);
+    }
+    if (tid == 0) {
+      *cc.T_ne = mvc_vp_ov.tne[last];
+      gst(&R->T_ne, mvc_vp_ov.tne[last]);
+      cnt[0] += nmv;
+    }
+  }
+}
+
+// The value-prediction loop (L.vp; the lane-column state, V <= kVpV, every
+// dish list <= 128): a step builds the overlay of customers i .. i+3's
+// predicted moves, evaluates the four customers at once (customer i + w
+// against the overlay of the moves before it), keeps the decisions up to and
+// including the first that differs from its prediction, commits the held
+// predictions from the overlay and a differing move the ordinary way.  Births
+// end the loop (mvc_seq_birth_kernel); so does a low hit rate (R->vpoff: the
+// lane-column loop takes the rest of the sweep).
+__device__ __forceinline__ void seq_run_loop_vp(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U, int &restride,
+                                int &vpoff) {
+  const ParState &P = A.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int V = P.V, D = P.D, n = P.n;
+  const SCache cc = lds_cache(V, D, L.ts, L.ks, 1);
+  SView Wv = cache_view(cc, A);
+  Wv.S1T = cc.S1T;
+  Wv.s1s = cc.ks;
+  const SeqScratch S(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts);
+  int cur = U.cur, pend = U.pend, pc = U.pc, pp0 = U.pp0, mode = U.mode, streak = U.streak, done = U.done;
+  int fill = U.fill, landed = U.landed, par = 0;
+  int lastm = U.lastm, gapq = U.gapq;
+  int steps = 0, hits = 0;
+  // a move to commit the ordinary way at the top of the next step (customer rci: rp0 -> rc)
+  int rci = -1, rp0 = 0, rc = 0;
+  bool skip = false;
+  if (A.R->vpoff) {   // stopped earlier in this sweep (later rounds of the batch): nothing to do
+    vpoff = 1;
+    skip = true;
+  } else if (pend && pc < 0) {   // a birth: mvc_seq_birth_kernel
+    skip = true;
+  } else if (pend) {   // a mover carried over from the previous launch
+    ring_fill_async<kSeqLcThreads / 64>(A, G, cur, cur + 1);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    fill = landed = cur + 1;
+    rci = cur;
+    rp0 = pp0;
+    rc = pc;
+    cur = cur + 1;
+    pend = 0;
+    streak = 0;
+    if (cur >= n) done = 1;
+  }
+  while (!skip) {
+    RUN_T0();
+    if (rci >= 0) {   // (its row is in the ring: landed, and requests stop a ring ahead)
+      const int nt0 = cc.n_t[rp0], ntc = cc.n_t[rc];
+      seq_bar(true);
+      seq_commit_move_split(A, cc, G.cust(rci, V, D), rci, rp0, rc, nt0, ntc, U.cnt);
+      rci = -1;
+      seq_bar(true);
+    }
+    if (done || mode != kSeqRun) break;
+    {   // the LDS layout must hold the lists plus one birth; the vp evaluation needs K_v <= 128
+      bool bad = *cc.T >= L.ts, big = false;
+      for (int v = 0; v < V; ++v) {
+        bad = bad || cc.Klist[v] >= L.ks;
+        big = big || cc.Klist[v] > 128;
+      }
+      if (bad) {
+        restride = 1;
+        break;
+      }
+      if (big || (steps >= 128 && 2 * hits < steps)) {
+        vpoff = 1;
+        break;
+      }
+    }
+    const int i0 = cur;
+    const int need = min(n, i0 + kSeqLcThreads / 64);
+    if (need > landed) {
+      if (fill < need) {
+        ring_fill_async<kSeqLcThreads / 64>(A, G, max(fill, i0), need);
+        fill = need;
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+      landed = fill;
+    }
+    if (fill - i0 <= G.n / 2 && fill < n) {
+      const int f1 = min(n, i0 + G.n);
+      ring_fill_async<kSeqLcThreads / 64>(A, G, max(fill, i0), f1);
+      fill = f1;
+    }
+    // the predictions; a predicted birth ends the step's depth (its new table is unknown)
+    const int nav = min(kVpMoves, n - i0);
+    int pz[kVpMoves], pcs[kVpMoves];
+    const double *yr[kVpMoves];
+    int depth = nav;
+#pragma unroll
+    for (int k = 0; k < kVpMoves; ++k) {
+      const int ik = min(i0 + k, n - 1);
+      pz[k] = ring_z(G, ik, V, D);
+      pcs[k] = ring_pred(G, ik, V, D);
+      yr[k] = G.at(ik);
+      if (k < depth && pcs[k] < 0) depth = k + 1;
+    }
+    const VpMoves M = vp_moves(cc, depth, pz, pcs);
+    vp_publish(M, pz, pcs);
+    seq_bar(true);
+    double *const ovs1 = mvc_seq_lds + L.vpo;
+    vp_build(A, cc, M, depth, yr, ovs1);
+    seq_bar(true);
+    RUN_MARK(4);
+    if (w < depth) {
+      VpCtx X;
+      X.nw = w;
+      X.tne = *cc.T_ne;
+      X.s1 = ovs1;
+#pragma unroll
+      for (int m = 0; m < kVpMoves; ++m)
+        if (m < w && M.mv[m]) X.tne = mvc_vp_ov.tne[m];
+      const int c = seq_resample_lc<true>(A, Wv, G.cust(i0 + w, V, D), i0 + w,
+                                          mvc_vp_ov.pz[w], S, cc.hyp, cc.cnew, X);
+      if (lane == 0) U.chb[par][w] = c;
+    }
+    seq_bar(true);
+    RUN_MARK(5);
+    // keep the decisions up to the first that differs from its prediction
+    int a = depth;
+#pragma unroll
+    for (int k = kVpMoves - 1; k >= 0; --k)
+      if (k < depth && U.chb[par][k] != pcs[k]) a = k;
+    ++steps;
+    if (a == depth) ++hits;
+    // a held predicted birth is the step's last customer (depth was cut there)
+    const bool pbirth = a == depth && mvc_vp_ov.pcs[depth - 1] < 0;
+    const int nc = pbirth ? depth - 1 : a;   // customers whose held predictions commit from the overlay
+    vp_commit(A, cc, M, i0, nc, yr, U.cnt);
+    int mlast = -1;   // the last mover decided in this step
+#pragma unroll
+    for (int k = 0; k < kVpMoves; ++k)
+      if (k < nc && M.mv[k]) mlast = i0 + k;
+    int decided = nc;
+    bool stop = false;
+    const int kx = pbirth ? depth - 1 : a;   // the customer after the held predictions, if any
+    if (kx < depth) {
+      const int ck = U.chb[par][kx], zk = mvc_vp_ov.pz[kx];
+      decided = kx + 1;
+      if (ck != zk) {
+        mlast = i0 + kx;
+        if (ck < 0) {   // a birth: pending for mvc_seq_birth_kernel
+          cur = i0 + kx;
+          pend = 1;
+          pc = -1;
+          pp0 = zk;
+          stop = true;
+        } else {        // an unpredicted move: the ordinary commit (next step's top), on the state with the held ones
+          rci = i0 + kx;
+          rp0 = zk;
+          rc = ck;
+        }
+      }
+    }
+    if (stop) {
+      if (mlast >= 0) note_mover(lastm, gapq, mlast);
+      break;
+    }
+    cur = i0 + decided;
+    if (mlast >= 0) {
+      note_mover(lastm, gapq, mlast);
+      streak = cur - 1 - mlast;
+    } else {
+      streak += decided;
+    }
+    if (streak >= stay_limit(L.limit, gapq)) mode = kSeqScan;
+    if (cur >= n) done = 1;
+    par ^= 1;
+    seq_bar(true);
+    RUN_MARK(6);
+#ifdef MVC_RUN_PROF
+    if (tid == 0) mvc_prof_lds[7] += 1;
+#endif
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) {
+    U.cur = cur;
+    U.pend = pend;
+    U.pc = pc;
+    U.pp0 = pp0;
+    U.mode = mode;
+    U.streak = streak;
+    U.done = done;
+    U.fill = fill;
+    U.landed = landed;
+    U.lastm = lastm;
+    U.gapq = gapq;
+    A.R->vpsteps += steps;
+    A.R->vphits += hits;
+  }
+}
+
 }  // namespace
 
 // The run kernel (one block of kSeqRunThreads = 8 waves): the
@@ -2352,15 +2982,15 @@ __device__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunC
 // window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
 // One instance per evaluation shape, compiled separately so each keeps its
 // own register allocation.
-template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc)
-__global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
+template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc); 4: + value prediction
+__global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, w = tid >> 6, nt = blockDim.x;
   const int V = P.V, D = P.D, n = P.n, KC = P.KC, TC = P.TC;
   __shared__ RunCursor U;
 #ifdef MVC_RUN_PROF
-  if (tid < 8) mvc_prof_lds[tid] = 0;
+  if (tid < 12) mvc_prof_lds[tid] = 0;
 #endif
   if (tid == 0) {
     const int go = !(R->done || R->overflow || R->restride);
@@ -2402,7 +3032,7 @@ __global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void m
     }
     return;
   }
-  int ovf = 0, restride = 0;
+  int ovf = 0, restride = 0, vpoff = 0;
   double *tree = SeqScratch(A, w).tree;   // global per-wave scratch: the dish draws' tree64 levels
   if (L.lds) {   // the state cache, from the global state at launch
     const int ts = L.ts, ks = L.ks;
@@ -2456,18 +3086,20 @@ __global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void m
     G.base = mvc_seq_lds + L.cache_dbl + (int64_t)L.nws * L.stride;
     if constexpr (kMode == 3)
       seq_run_loop_lc(A, L, G, U, restride);
+    else if constexpr (kMode == 4)
+      seq_run_loop_vp(A, L, G, U, restride, vpoff);
     else
       seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
                                 SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts), G,
                                 tree, U, ovf, restride);
     __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
-  } else if constexpr (kMode != 3) {   // (the lane-column kernel always has the LDS layout)
+  } else if constexpr (kMode < 3) {   // (the lane-column kernels always have the LDS layout)
     Ring G{nullptr, 0, 0};
     seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
 #ifdef MVC_RUN_PROF
-    for (int k = 0; k < 8; ++k) R->prof[k] += mvc_prof_lds[k];
+    for (int k = 0; k < 12; ++k) R->prof[k] += mvc_prof_lds[k];
 #endif
     R->cur = U.cur;
     R->pend = U.pend;
@@ -2480,6 +3112,7 @@ __global__ __launch_bounds__(kMode == 3 ? kSeqLcThreads : kSeqRunThreads) void m
     R->lastm = U.lastm;
     R->gapq = U.gapq;
     if (restride) R->restride = 1;
+    if (vpoff) R->vpoff = 1;
     if (U.done && !U.pend) {
       R->done = 1;
     } else if (!ovf && !restride && U.mode == kSeqScan && !U.pend) {

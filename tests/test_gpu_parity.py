@@ -772,3 +772,37 @@ def test_table_limit_is_a_clean_error(monkeypatch):
         s.sweep(3)
     assert e.value.code == 4                  # MVC_ERR_UNSUPPORTED
     s.close()
+
+
+@pytest.mark.parametrize("V,D,K,vp", [(4, 1, 16, "1"), (4, 1, 16, "0"), (2, 16, 8, "1"), (5, 4, 12, "1")])
+def test_value_prediction_same_chain(V, D, K, vp, monkeypatch, capfd):
+    """Value prediction (the lane-column run kernel evaluating customers i ..
+    i+3 against the state with the phase-A choices of the ones before applied,
+    mvc_repair.h seq_run_loop_vp) gives the oracle SeqSampler chain bit for
+    bit from a warm state where most customers move (overlapping clusters) and
+    through births; MVC_VP=0 is the plain lane-column loop on the same chain."""
+    monkeypatch.setenv("MVC_VP", vp)
+    monkeypatch.setenv("MVC_VP_STATS", "1")
+    m = _mvc()
+    import bench
+    from mvc_amd import data
+    y, z = data.synthetic(20_000, V, D, K, seed=70 + V + D, sd=1.3 if D == 1 else 4.0)
+    st = bench.warm_state(z, V, K)
+    s = m.Sampler(y, seed=21, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 3, 0, 1, seed=21, mode=O.PARALLEL, state=st)
+    for it in range(3):
+        s.sweep(1)
+        t, d, h = s.state()
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+        assert np.array_equal(h["tau_v"], ref["tau_v"][:, it]), it
+    rep = s.repair_stats()
+    s.close()
+    err = capfd.readouterr().err
+    steps = sum(int(l.split()[3]) for l in err.splitlines() if l.startswith("mvc vp steps"))
+    assert rep["moves"] > 0
+    if vp == "1":
+        assert steps > 0, "value prediction did not run"
+    else:
+        assert steps == 0
