@@ -175,6 +175,13 @@ int mvc_sampler_zpath(mvc_sampler *s);
  * out[3] dishes opened.  MVC_ERR_UNSUPPORTED for the exact schedule.  (No
  * reference counterpart: diagnostics of this implementation.) */
 int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out);
+/* Phase A alone: the data-parallel pass of the next parallel sweep (every
+ * customer evaluated against the current state with that sweep's uniforms,
+ * DESIGN.md §4.8) into choice[n] (table position, -1 = a new table); the
+ * chain's state and sweep count are unchanged.  MVC_ERR_UNSUPPORTED for the
+ * exact schedule and for handles with several chains.  (No reference
+ * counterpart: a diagnostic that lets tests check the pass directly.) */
+int mvc_sampler_phase_a(mvc_sampler *s, int chain, int32_t *choice);
 /* Within-chain N-sharding (one chain split over `world` processes, one GPU
  * each, every rank holding the whole data and state).  Phase A of each sweep
  * (the data-parallel evaluation against the sweep-start state) covers only

@@ -47,6 +47,38 @@ MVC_PM double mvc_u2d(uint64_t u) { double x; __builtin_memcpy(&x, &u, 8); retur
 #define MVC_HALF_LOG_2PI 0.9189385332046728
 #define MVC_PI 3.14159265358979323846          /* M_PI as used by the reference */
 
+#if defined(__HIPCC__)
+/* The exp's Horner steps from 1/14! down to 1/2! as ONE inline-asm block of
+ * three-operand v_fma_f64 (coefficients in VGPRs or SGPRs): the same
+ * instructions on the same values as the host's __builtin_fma chain, without
+ * the compiler's v_mov_b64 + v_fmac_f64 pairs and without the s_nop it puts
+ * after every separate asm statement.  Consecutive dependent v_fma_f64 need
+ * no wait states on gfx950 (the compiler emits them back to back itself). */
+#if !defined(MVC_PM_NO_ASM_FMA)
+#define MVC_HORNER12(p, r, K0, K)                                                                   \
+  asm("v_fma_f64 %0, %2, %1, %3\n\tv_fma_f64 %0, %0, %1, %4\n\tv_fma_f64 %0, %0, %1, %5\n\t"         \
+      "v_fma_f64 %0, %0, %1, %6\n\tv_fma_f64 %0, %0, %1, %7\n\tv_fma_f64 %0, %0, %1, %8\n\t"          \
+      "v_fma_f64 %0, %0, %1, %9\n\tv_fma_f64 %0, %0, %1, %10\n\tv_fma_f64 %0, %0, %1, %11\n\t"        \
+      "v_fma_f64 %0, %0, %1, %12\n\tv_fma_f64 %0, %0, %1, %13"                                     \
+      : "=&v"(p)                                                                                   \
+      : "v"(r), K0(1.1470745597729725e-11), K(1.6059043836821613e-10), K(2.08767569878681e-09),     \
+        K(2.505210838544172e-08), K(2.755731922398589e-07), K(2.7557319223985893e-06),             \
+        K(2.48015873015873e-05), K(0.0001984126984126984), K(0.001388888888888889),                \
+        K(0.008333333333333333), K(0.041666666666666664), K(0.16666666666666666))
+#else
+#define MVC_HORNER12(p, r, K0, K)                                                                   \
+  do {                                                                                              \
+    p = __builtin_fma(1.1470745597729725e-11, r, 1.6059043836821613e-10);                           \
+    p = __builtin_fma(p, r, 2.08767569878681e-09);                                                  \
+    p = __builtin_fma(p, r, 2.505210838544172e-08); p = __builtin_fma(p, r, 2.755731922398589e-07); \
+    p = __builtin_fma(p, r, 2.7557319223985893e-06); p = __builtin_fma(p, r, 2.48015873015873e-05); \
+    p = __builtin_fma(p, r, 0.0001984126984126984); p = __builtin_fma(p, r, 0.001388888888888889);  \
+    p = __builtin_fma(p, r, 0.008333333333333333); p = __builtin_fma(p, r, 0.041666666666666664);   \
+    p = __builtin_fma(p, r, 0.16666666666666666);                                                   \
+  } while (0)
+#endif
+#endif
+
 MVC_PM double mvc_exp(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   /* Device: the same value without branches (divergence-free; 64 unrolled
@@ -62,27 +94,9 @@ MVC_PM double mvc_exp(double x) {
     const int k = (int)kd;
     double r = __builtin_fma(-kd, MVC_LN2_HI, x);
     r = __builtin_fma(-kd, MVC_LN2_LO, r);
-    /* Horner steps as one three-operand v_fma_f64 each (coefficients in
-     * VGPRs, hoisted by the compiler); left to itself the compiler emits
-     * v_mov_b64 + v_fmac_f64, two instructions per step. */
-#if !defined(MVC_PM_NO_ASM_FMA)
-#define MVC_DFMA_S(p, r, c) asm("v_fma_f64 %0, %1, %2, %3" : "=v"(p) : "v"(p), "v"(r), "v"((double)(c)))
-#else
-#define MVC_DFMA_S(p, r, c) p = __builtin_fma(p, r, c)
-#endif
-    double p = 1.1470745597729725e-11;
-    MVC_DFMA_S(p, r, 1.6059043836821613e-10);
-    MVC_DFMA_S(p, r, 2.08767569878681e-09);
-    MVC_DFMA_S(p, r, 2.505210838544172e-08);
-    MVC_DFMA_S(p, r, 2.755731922398589e-07);
-    MVC_DFMA_S(p, r, 2.7557319223985893e-06);
-    MVC_DFMA_S(p, r, 2.48015873015873e-05);
-    MVC_DFMA_S(p, r, 0.0001984126984126984);
-    MVC_DFMA_S(p, r, 0.001388888888888889);
-    MVC_DFMA_S(p, r, 0.008333333333333333);
-    MVC_DFMA_S(p, r, 0.041666666666666664);
-    MVC_DFMA_S(p, r, 0.16666666666666666);
-#undef MVC_DFMA_S
+    /* the Horner steps to 1/2!: one asm block (MVC_HORNER12) */
+    double p;
+    MVC_HORNER12(p, r, "v", "v");
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     const double e = __builtin_fma(p, r, 1.0);
@@ -142,27 +156,9 @@ static __device__ __forceinline__ double mvc_exp_sk(double x) {
     const int k = (int)kd;
     double r = __builtin_fma(-kd, MVC_LN2_HI, x);
     r = __builtin_fma(-kd, MVC_LN2_LO, r);
-    /* Horner steps as one three-operand v_fma_f64 each (coefficients in
-     * VGPRs, hoisted by the compiler); left to itself the compiler emits
-     * v_mov_b64 + v_fmac_f64, two instructions per step. */
-#if !defined(MVC_PM_NO_ASM_FMA)
-#define MVC_DFMA_S(p, r, c) asm("v_fma_f64 %0, %1, %2, %3" : "=v"(p) : "v"(p), "v"(r), "s"((double)(c)))
-#else
-#define MVC_DFMA_S(p, r, c) p = __builtin_fma(p, r, c)
-#endif
-    double p = 1.1470745597729725e-11;
-    MVC_DFMA_S(p, r, 1.6059043836821613e-10);
-    MVC_DFMA_S(p, r, 2.08767569878681e-09);
-    MVC_DFMA_S(p, r, 2.505210838544172e-08);
-    MVC_DFMA_S(p, r, 2.755731922398589e-07);
-    MVC_DFMA_S(p, r, 2.7557319223985893e-06);
-    MVC_DFMA_S(p, r, 2.48015873015873e-05);
-    MVC_DFMA_S(p, r, 0.0001984126984126984);
-    MVC_DFMA_S(p, r, 0.001388888888888889);
-    MVC_DFMA_S(p, r, 0.008333333333333333);
-    MVC_DFMA_S(p, r, 0.041666666666666664);
-    MVC_DFMA_S(p, r, 0.16666666666666666);
-#undef MVC_DFMA_S
+    /* the Horner steps to 1/2!: one asm block (MVC_HORNER12) */
+    double p;
+    MVC_HORNER12(p, r, "v", "s");   /* one SGPR operand per VOP3 */
     p = __builtin_fma(p, r, 0.5);
     p = __builtin_fma(p, r, 1.0);
     const double e = __builtin_fma(p, r, 1.0);
@@ -190,24 +186,8 @@ static __device__ __forceinline__ double mvc_exp_le0(double x) {
   const int k = (int)kd;
   double r = __builtin_fma(-kd, MVC_LN2_HI, x);
   r = __builtin_fma(-kd, MVC_LN2_LO, r);
-#if !defined(MVC_PM_NO_ASM_FMA)
-#define MVC_DFMA_S(p, r, c) asm("v_fma_f64 %0, %1, %2, %3" : "=v"(p) : "v"(p), "v"(r), "v"((double)(c)))
-#else
-#define MVC_DFMA_S(p, r, c) p = __builtin_fma(p, r, c)
-#endif
-  double p = 1.1470745597729725e-11;
-  MVC_DFMA_S(p, r, 1.6059043836821613e-10);
-  MVC_DFMA_S(p, r, 2.08767569878681e-09);
-  MVC_DFMA_S(p, r, 2.505210838544172e-08);
-  MVC_DFMA_S(p, r, 2.755731922398589e-07);
-  MVC_DFMA_S(p, r, 2.7557319223985893e-06);
-  MVC_DFMA_S(p, r, 2.48015873015873e-05);
-  MVC_DFMA_S(p, r, 0.0001984126984126984);
-  MVC_DFMA_S(p, r, 0.001388888888888889);
-  MVC_DFMA_S(p, r, 0.008333333333333333);
-  MVC_DFMA_S(p, r, 0.041666666666666664);
-  MVC_DFMA_S(p, r, 0.16666666666666666);
-#undef MVC_DFMA_S
+  double p;
+  MVC_HORNER12(p, r, "v", "v");
   p = __builtin_fma(p, r, 0.5);
   p = __builtin_fma(p, r, 1.0);
   const double e = __builtin_fma(p, r, 1.0);

@@ -258,6 +258,10 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
       std::fprintf(stderr, "Iteration %d / %d\n", iter + 1, cf.n_iter);
     S->sweep(1);
     if (iter >= cf.burn_in && ((iter - cf.burn_in) % cf.thin == 0)) {   // gibbs.cpp:205
+      if (S->save_all_async(save_fn)) {                   // all chains in one snapshot (exact schedule)
+        R.S++;
+        continue;
+      }
       for (int c = 0; c < C; ++c) {
         if (S->save_async(c, save_fn)) continue;        // device snapshot + async D2H (f3)
         std::vector<int32_t> t(n);
@@ -508,6 +512,15 @@ int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags) {
 }
 
 int mvc_sampler_zpath(mvc_sampler *s) { return (s && s->impl) ? s->impl->zpath : -1; }
+
+int mvc_sampler_phase_a(mvc_sampler *s, int chain, int32_t *choice) {
+  if (!s || !s->impl || !choice) return MVC_ERR_ARG;
+  try {
+    return s->impl->phase_a(chain, choice) ? MVC_OK : MVC_ERR_UNSUPPORTED;
+  } catch (const mvc::Error &e) {
+    return e.code;
+  }
+}
 
 int mvc_sampler_repair_stats(mvc_sampler *s, int chain, int32_t *out) {
   if (!s || !s->impl || !out) return MVC_ERR_ARG;

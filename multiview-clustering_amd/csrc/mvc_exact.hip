@@ -296,15 +296,38 @@ struct MH {
 
 // ---------------------------------------------------------------------------
 // One sweep (or the rest of one) for every chain: grid = chains, block = 64.
+// The chain's capacity-sized arrays (n_t .. P, and z when it fits) are one
+// contiguous range of its allocation (carve); when the range fits in the
+// lds_bytes of dynamic LDS it is copied in at the start, the kernel works on
+// the copy (every dependent access an LDS round trip instead of an L2 one)
+// and it is written back at the end.  Same operations, same order: the bits
+// do not depend on where the arrays live.
 // ---------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
-    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed) {
+    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, int lds_bytes) {
   __shared__ Shared sh;
+  extern __shared__ __attribute__((aligned(16))) char ex_lds[];
   ExactChain &Cg = chains[blockIdx.x];
   ExactChain C = Cg;               // pointers + scalars in registers
   const int lane = threadIdx.x;
   if (C.status == MVC_ST_DONE || C.status == MVC_ST_ERROR) return;
   const int TC = C.TC, KC = C.KC;
+  char *gbeg = nullptr;
+  size_t nbytes = 0;
+  {
+    const size_t full = (size_t)((char *)C.mhbuf - (char *)C.z), part = (size_t)((char *)C.mhbuf - (char *)C.n_t);
+    if (full <= (size_t)lds_bytes) { gbeg = (char *)C.z; nbytes = full; }
+    else if (part <= (size_t)lds_bytes) { gbeg = (char *)C.n_t; nbytes = part; }
+  }
+  if (gbeg) {
+    const uint4 *src = (const uint4 *)gbeg;   // 256-byte granules (carve)
+    uint4 *dst = (uint4 *)ex_lds;
+    for (size_t e = lane; e < nbytes / 16; e += MVC_WAVE) dst[e] = src[e];
+    auto re = [&](auto *&ptr) { ptr = (std::remove_reference_t<decltype(ptr)>)(ex_lds + ((char *)ptr - gbeg)); };
+    if (gbeg == (char *)C.z) re(C.z);
+    re(C.n_t); re(C.pos_of_slot); re(C.slot_at_pos); re(C.free_slots); re(C.dish);
+    re(C.d_id); re(C.d_n); re(C.d_l); re(C.d_S1); re(C.d_S2); re(C.f); re(C.logf); re(C.P);
+  }
 
   for (int v = lane; v < V; v += MVC_WAVE) {
     sh.Kact[v] = C.Kact[v];
@@ -601,6 +624,12 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     Cg.resume_i = i;
     Cg.status = status;
   }
+  if (gbeg) {                      // the LDS copy back to the chain's allocation
+    __syncthreads();
+    const uint4 *src = (const uint4 *)ex_lds;
+    uint4 *dst = (uint4 *)gbeg;
+    for (size_t e = lane; e < nbytes / 16; e += MVC_WAVE) dst[e] = src[e];
+  }
 }
 
 // Snapshot of one chain in reference output form (utils.cpp:291-303):
@@ -616,6 +645,28 @@ extern "C" __global__ void mvc_exact_snapshot_kernel(int n, int V, const ExactCh
     const int v = e / T, p = e % T;
     if (p < dish_cap) dish_of[v * dish_cap + p] = C.d_id[v * C.KC + C.dish[v * C.TC + C.slot_at_pos[p]]];
   }
+}
+
+// Snapshot of every chain at once (mvc_run's saved samples): chain c =
+// blockIdx.y writes table_of[c][n], dish_of[c][V][dcap] (positions < T), T[c]
+// and hyper[c][3V+2] into one save slot, read back asynchronously.
+extern "C" __global__ void mvc_exact_snapshot_all_kernel(int n, int V, const ExactChain *chains, int dcap,
+                                                         int32_t *table_of, int32_t *dish_of, int32_t *T_out,
+                                                         double *hyper) {
+  const int c = blockIdx.y;
+  const ExactChain &C = chains[c];
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int stride = gridDim.x * blockDim.x;
+  int32_t *tz = table_of + (size_t)c * n;
+  for (int i = tid; i < n; i += stride) tz[i] = C.pos_of_slot[C.z[i]];
+  const int T = C.T;
+  int32_t *dd = dish_of + (size_t)c * V * dcap;
+  for (int e = tid; e < V * T; e += stride) {
+    const int v = e / T, p = e % T;
+    if (p < dcap) dd[v * dcap + p] = C.d_id[v * C.KC + C.dish[v * C.TC + C.slot_at_pos[p]]];
+  }
+  if (tid == 0) T_out[c] = T;
+  for (int e = tid; e < 3 * V + 2; e += stride) hyper[(size_t)c * (3 * V + 2) + e] = C.hyper[e];
 }
 
 // ===========================================================================
@@ -822,8 +873,101 @@ class ExactSampler : public Sampler {
     MVC_HIP(hipStreamSynchronize(stream));
   }
 
+  // save slots of save_all_async (every chain's sample in one snapshot)
+  struct SaveSlot {
+    int32_t *dz = nullptr, *ddish = nullptr, *dT = nullptr;
+    double *dhyp = nullptr;
+    int32_t *hz = nullptr, *hdish = nullptr, *hT = nullptr;
+    double *hhyp = nullptr;
+    int dcap = 0;
+    hipEvent_t snap = nullptr, done = nullptr;
+    bool busy = false;
+    SampleFn fn;
+  };
+  static constexpr int kSaveSlots = 4;
+  SaveSlot saves[kSaveSlots];
+  int save_next = 0;
+  hipStream_t cstream = nullptr;
+
+  void free_slot(SaveSlot &q) {
+    hipFree(q.dz); hipFree(q.ddish); hipFree(q.dT); hipFree(q.dhyp);
+    hipHostFree(q.hz); hipHostFree(q.hdish); hipHostFree(q.hT); hipHostFree(q.hhyp);
+    q.dz = q.ddish = q.dT = nullptr; q.dhyp = nullptr;
+    q.hz = q.hdish = q.hT = nullptr; q.hhyp = nullptr;
+    q.dcap = 0;
+  }
+  void finish_slot(SaveSlot &q) {
+    MVC_HIP(hipEventSynchronize(q.done));
+    const int C = (int)chains.size(), H = 3 * V + 2;
+    std::vector<int32_t> d;
+    for (int c = 0; c < C; ++c) {
+      const int T = q.hT[c];
+      d.assign((size_t)V * T, 0);
+      for (int v = 0; v < V; ++v)
+        std::copy(q.hdish + ((size_t)c * V + v) * q.dcap, q.hdish + ((size_t)c * V + v) * q.dcap + T,
+                  d.begin() + (size_t)v * T);
+      q.fn(c, T, q.hz + (size_t)c * n, d.data(), q.hhyp + (size_t)c * H);
+    }
+    q.busy = false;
+  }
+  // One snapshot kernel for all chains into a device slot, read back on a
+  // second stream; the samples reach fn (chain by chain, in order) when the
+  // slot is reused or at flush_saves.  Replaces two get_state calls per chain
+  // and sample, each of which synchronised the device.
+  bool save_all_async(const SampleFn &fn) override {
+    if (!cstream) MVC_HIP(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+    SaveSlot &q = saves[save_next];
+    if (q.busy) finish_slot(q);
+    const int C = (int)chains.size(), H = 3 * V + 2;
+    int dcap = 1;
+    for (auto &A : chains) dcap = std::max(dcap, A.h.TC);
+    if (q.dcap < dcap) {
+      if (q.dz) free_slot(q);
+      MVC_HIP(hipMalloc(&q.dz, sizeof(int32_t) * (size_t)C * std::max(n, 1)));
+      MVC_HIP(hipMalloc(&q.ddish, sizeof(int32_t) * (size_t)C * V * dcap));
+      MVC_HIP(hipMalloc(&q.dT, sizeof(int32_t) * C));
+      MVC_HIP(hipMalloc(&q.dhyp, sizeof(double) * (size_t)C * H));
+      MVC_HIP(hipHostMalloc((void **)&q.hz, sizeof(int32_t) * (size_t)C * std::max(n, 1), hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hdish, sizeof(int32_t) * (size_t)C * V * dcap, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hT, sizeof(int32_t) * C, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hhyp, sizeof(double) * (size_t)C * H, hipHostMallocDefault));
+      q.dcap = dcap;
+    }
+    if (!q.snap) {
+      MVC_HIP(hipEventCreateWithFlags(&q.snap, hipEventDisableTiming));
+      MVC_HIP(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+    }
+    hipLaunchKernelGGL(mvc_exact_snapshot_all_kernel, dim3(std::min(64, (n + 255) / 256 + 1), C), dim3(256), 0, stream,
+                       n, V, (const ExactChain *)chains_dev, q.dcap, q.dz, q.ddish, q.dT, q.dhyp);
+    MVC_HIP(hipGetLastError());
+    MVC_HIP(hipEventRecord(q.snap, stream));
+    MVC_HIP(hipStreamWaitEvent(cstream, q.snap, 0));
+    MVC_HIP(hipMemcpyAsync(q.hz, q.dz, sizeof(int32_t) * (size_t)C * n, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipMemcpyAsync(q.hdish, q.ddish, sizeof(int32_t) * (size_t)C * V * q.dcap, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipMemcpyAsync(q.hT, q.dT, sizeof(int32_t) * C, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipMemcpyAsync(q.hhyp, q.dhyp, sizeof(double) * (size_t)C * H, hipMemcpyDeviceToHost, cstream));
+    MVC_HIP(hipEventRecord(q.done, cstream));
+    q.busy = true;
+    q.fn = fn;
+    save_next = (save_next + 1) % kSaveSlots;
+    return true;
+  }
+  void flush_saves() override {
+    for (int k = 0; k < kSaveSlots; ++k) {
+      SaveSlot &q = saves[(save_next + k) % kSaveSlots];   // oldest first
+      if (q.busy) finish_slot(q);
+    }
+  }
+
   ~ExactSampler() override {
     if (stream) hipStreamSynchronize(stream);
+    if (cstream) hipStreamSynchronize(cstream);
+    for (auto &q : saves) {
+      free_slot(q);
+      if (q.snap) hipEventDestroy(q.snap);
+      if (q.done) hipEventDestroy(q.done);
+    }
+    if (cstream) hipStreamDestroy(cstream);
     for (auto &A : chains) if (A.block) hipFree(A.block);
     if (chains_dev) hipFree(chains_dev);
     if (y_dev) hipFree(y_dev);
@@ -878,6 +1022,18 @@ class ExactSampler : public Sampler {
     return I;
   }
 
+  // dynamic LDS of the sweep kernel: the largest chain's array range that fits
+  // kExactLds (with z when every chain's does), 0 when none fits
+  static constexpr size_t kExactLds = 48 * 1024;
+  int lds_bytes() const {
+    size_t full = 0, part = 0;
+    for (auto &A : chains) {
+      full = std::max(full, (size_t)((char *)A.h.mhbuf - (char *)A.h.z));
+      part = std::max(part, (size_t)((char *)A.h.mhbuf - (char *)A.h.n_t));
+    }
+    return (int)(full <= kExactLds ? full : (part <= kExactLds ? part : 0));
+  }
+
   void push_structs() {
     std::vector<ExactChain> hs(chains.size());
     for (size_t k = 0; k < chains.size(); ++k) hs[k] = chains[k].h;
@@ -922,8 +1078,8 @@ class ExactSampler : public Sampler {
       for (int round = 0;; ++round) {
         hipEvent_t ev = nullptr;
         timers.begin("exact_sweep", &ev);
-        hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), 0, stream,
-                           (const double *)y_dev, n, V, chains_dev, cfg.seed);
+        hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), lds_bytes(), stream,
+                           (const double *)y_dev, n, V, chains_dev, cfg.seed, lds_bytes());
         MVC_HIP(hipGetLastError());
         timers.end("exact_sweep", ev);
         pull_structs();

@@ -95,6 +95,9 @@ class Sampler {
                                       const double *hyper)>;
   virtual bool save_async(int chain, const SampleFn &fn) { (void)chain; (void)fn; return false; }
   virtual void flush_saves() {}
+  // Every chain's sample at once (one snapshot, read back asynchronously;
+  // fn(chain, ...) runs for chains 0..C-1 in order); false where unsupported.
+  virtual bool save_all_async(const SampleFn &fn) { (void)fn; return false; }
   // Device pointer to the chain's table labels [n] (valid until the next
   // sweep; the stream is synchronised), or nullptr when they live on the host.
   virtual const int32_t *device_labels(int chain) { (void)chain; return nullptr; }
@@ -107,6 +110,10 @@ class Sampler {
   // out[0] customers that moved, out[1] births, out[2] repair rounds,
   // out[3] dishes opened.  False for the exact schedule.
   virtual bool repair_stats(int chain, int32_t *out) { (void)chain; (void)out; return false; }
+  // Phase A alone (mvc_sampler_phase_a): the data-parallel pass of the next
+  // sweep against the current state, choices into out[n]; no state changes.
+  // False where unsupported (the exact schedule, several chains per handle).
+  virtual bool phase_a(int chain, int32_t *out) { (void)chain; (void)out; return false; }
   // Within-chain N-sharding (mvc_sampler_set_shard): false where unsupported
   // (the exact schedule, several chains per handle).
   virtual bool set_shard(int rank, int world, int32_t *exch, int (*cb)(void *), void *user) {

@@ -882,6 +882,136 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
 }
 
 #define MVC_ZSTAGE 24          // dishes per wave whose lp rows the register draw keeps in LDS (3 blocks/CU)
+
+// The register draw's block-shared tables (LDS).
+struct ZregLds {
+  const double *base;    // [TM] log mass of each table (or -inf: excluded)
+  const double *w;       // [sumK] dish weights max(l - sigma, 0), -1 for l = 0
+  const int *tix;        // [TM][V] Koff[v] + dish_v(p)
+  const int *koff;       // [V+1]
+  const int *lmin;       // [VMAX] 1: every dish of view v has l >= 1
+  const int *soff;       // [VMAX] staging offset of view v (dishes), -1: not staged
+  const int *dl;         // [sumK] l of each dish
+};
+
+// One customer of the register draw (one lane): the view terms (each lp row
+// read once; rows of K_v <= 16 in registers, staged rows kept in LDS for the
+// gathers), the table scores in view order, weights, block totals and the
+// pw16 descent.  Returns the choice (table position, -1 = birth).
+template <int TM>
+__device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, int i, const LpRow &row, double *s_stage,
+                                             int lane) {
+  const ParState &P = A.P;
+  const int V = P.V, n = P.n;
+  const int T = __builtin_amdgcn_readfirstlane(A.T);
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const int T_ne = A.status[V + 3];
+  const int p0 = P.z[i];
+  const bool alive = (P.n_t[p0] - 1) > 0;
+  double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+  for (int v = 0; v < V; ++v) {
+    const int koff = __builtin_amdgcn_readfirstlane(Z.koff[v]);
+    const int K = __builtin_amdgcn_readfirstlane(Z.koff[v + 1]) - koff;
+    const int j0 = Z.tix[p0 * V + v] - koff;
+    const double sigma = P.hyper[2 * V + v];
+    const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+    const int l0p = Z.dl[koff + j0] - (alive ? 0 : 1);
+    double w0 = (double)l0p - sigma;
+    if (w0 < 0.0) w0 = 0.0;
+    if (!(l0p > 0)) w0 = -1.0;
+    const double *sw = Z.w + koff;
+    const double m = A.vmax[(size_t)v * n + i];
+    double S;
+    const bool allv = __builtin_amdgcn_readfirstlane(Z.lmin[v]) != 0;
+    const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
+    double *stg = so >= 0 ? s_stage + (size_t)so * 64 + lane : nullptr;
+    if (!allv) S = zview_sum<0>(row, koff, K, j0, w0, sw, m);           // general: streamed
+    else if (K <= 8) S = zview_sum<8>(row, koff, K, j0, w0, sw, m, stg);     // row in registers
+    else if (K <= 16) S = zview_sum<16>(row, koff, K, j0, w0, sw, m, stg);
+    else S = zview_sum<0>(row, koff, K, j0, w0, sw, m);
+    const int Kact = K - ((l0p == 0) ? 1 : 0);
+    double wn = P.hyper[V + v] + (double)Kact * sigma;
+    if (wn < 0.0) wn = 0.0;
+    S = S + wn * mvc_exp_le0(lfn - m);
+    const double denom = P.hyper[V + v] + (double)(P.Ltot[v] - (alive ? 0 : 1));
+    const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
+    s_new = s_new + lm;
+  }
+  const int np0 = P.n_t[p0] - 1;
+  const double m0 = (double)np0 - sg;
+  const double base_self = (np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
+  // table scores in view order, 16 tables' gathers in flight per step
+  double sp[TM];
+#pragma unroll
+  for (int p = 0; p < TM; ++p) {   // p >= T: -inf, so its weight below is exp(-inf) = 0 like a dead table's
+    const int pc = min(p, T - 1);
+    sp[p] = p < T ? ((pc == p0) ? base_self : Z.base[pc]) : -MVC_PM_INF;
+  }
+#pragma unroll
+  for (int c = 0; c < TM; c += 16) {
+    for (int v = 0; v < V; ++v) {
+      double x[16];
+      const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
+      if (so >= 0) {                             // staged row: LDS [dish][lane], conflict-free
+        const double *st = s_stage + (size_t)(so - Z.koff[v]) * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = st[(size_t)__builtin_amdgcn_readfirstlane(Z.tix[min(c + u, T - 1) * V + v]) * 64];
+      } else {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) x[u] = row(__builtin_amdgcn_readfirstlane(Z.tix[min(c + u, T - 1) * V + v]));
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
+    }
+  }
+  double M = -MVC_PM_INF;
+#pragma unroll
+  for (int p = 0; p < TM; ++p)
+    if (p < T && sp[p] > M) M = sp[p];
+  if (s_new > M) M = s_new;
+  // weights e_p in place; block sums pw16, running block totals C_b
+  double C[TM / 16];
+  double tot = 0.0;
+#pragma unroll
+  for (int b = 0; b < TM / 16; ++b) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int p = 16 * b + c;
+      // a dead table or p >= T has sp = -inf: exp_le0(-inf) = +0, the spec's 0 weight
+      double xe = sp[p] - M;
+      asm volatile("" : "+v"(xe) : "v"(sp[(p + TM - MVC_ZEXP_LAG) % TM]));   // MVC_ZEXP_LAG exps in flight, not TM live
+      sp[p] = mvc_exp_le0(xe);
+    }
+    double blk[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) blk[c] = sp[16 * b + c];
+    tot = tot + pw16(blk);
+    C[b] = tot;
+  }
+  const double W = mvc_exp_le0(s_new - M) + tot;
+  double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+  int pick = -1;
+  if (r < tot) {
+    int bsel = TM / 16 - 1;
+    double prev = 0.0;
+#pragma unroll
+    for (int b = TM / 16 - 1; b >= 0; --b)
+      if (r < C[b]) { bsel = b; prev = b > 0 ? C[b - 1] : 0.0; }
+    r = r - prev;
+    double blk[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      double x = sp[c];
+#pragma unroll
+      for (int b = 1; b < TM / 16; ++b)
+        if (bsel == b) x = sp[16 * b + c];
+      blk[c] = x;
+    }
+    pick = 16 * bsel + pw16_select(blk, r);
+  }
+  return pick;
+}
+
 template <int TM>
 #ifndef MVC_ZDRAW_MINB
 #define MVC_ZDRAW_MINB 3      // blocks of 4 waves per CU the register budget must allow
@@ -889,7 +1019,7 @@ template <int TM>
 __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
-  const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
+  const int V = P.V, KC = P.KC, TC = P.TC;
   const int T = __builtin_amdgcn_readfirstlane(A.T);
   const int tid = threadIdx.x;
   const int sumK0 = __builtin_amdgcn_readfirstlane(A.Koff[V]);
@@ -902,7 +1032,7 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
   int *s_soff = s_lmin + MVC_Z_VMAX;               // [VMAX] staging offset of view v (dishes), -1: not staged
   int *s_dl = s_soff + MVC_Z_VMAX;                 // [sumK] l of each dish
   s_stage += (size_t)(threadIdx.x >> 6) * MVC_ZSTAGE * 64;
-  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  const double sg = P.hyper[3 * V + 1];
   if (tid <= V) s_koff[tid] = A.Koff[tid];
   __syncthreads();
   const int sumK = s_koff[V];
@@ -934,117 +1064,11 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
     }
   }
   __syncthreads();
-  const int T_ne = A.status[V + 3];
-  {
-    const int li = blockIdx.x * blockDim.x + tid;   // one customer per thread (no loop-invariant hoisting)
-    if (li >= nb) return;
-    const int i = b0 + li;
-    const int p0 = P.z[i];
-    const bool alive = (P.n_t[p0] - 1) > 0;
-    const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
-    double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
-    for (int v = 0; v < V; ++v) {
-      const int koff = __builtin_amdgcn_readfirstlane(s_koff[v]);
-      const int K = __builtin_amdgcn_readfirstlane(s_koff[v + 1]) - koff;
-      const int j0 = s_tix[p0 * V + v] - koff;
-      const double sigma = P.hyper[2 * V + v];
-      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
-      const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
-      double w0 = (double)l0p - sigma;
-      if (w0 < 0.0) w0 = 0.0;
-      if (!(l0p > 0)) w0 = -1.0;
-      const double *sw = s_w + koff;
-      const double m = A.vmax[(size_t)v * n + i];
-      double S;
-      const bool allv = __builtin_amdgcn_readfirstlane(s_lmin[v]) != 0;
-      const int so = __builtin_amdgcn_readfirstlane(s_soff[v]);
-      double *stg = so >= 0 ? s_stage + (size_t)so * 64 + (tid & 63) : nullptr;
-      if (!allv) S = zview_sum<0>(row, koff, K, j0, w0, sw, m);           // general: streamed
-      else if (K <= 8) S = zview_sum<8>(row, koff, K, j0, w0, sw, m, stg);     // row in registers
-      else if (K <= 16) S = zview_sum<16>(row, koff, K, j0, w0, sw, m, stg);
-      else S = zview_sum<0>(row, koff, K, j0, w0, sw, m);
-      const int Kact = K - ((l0p == 0) ? 1 : 0);
-      double wn = P.hyper[V + v] + (double)Kact * sigma;
-      if (wn < 0.0) wn = 0.0;
-      S = S + wn * mvc_exp_le0(lfn - m);
-      const double denom = P.hyper[V + v] + (double)(P.Ltot[v] - (alive ? 0 : 1));
-      const double lm = (denom <= 0.0) ? lfn : (m + mvc_log(S)) - mvc_log(denom);
-      s_new = s_new + lm;
-    }
-    const int np0 = P.n_t[p0] - 1;
-    const double m0 = (double)np0 - sg;
-    const double base_self = (np0 >= 1 && m0 > 0.0) ? mvc_log(m0) : -MVC_PM_INF;
-    // table scores in view order, 16 tables' gathers in flight per step
-    double sp[TM];
-#pragma unroll
-    for (int p = 0; p < TM; ++p) {   // p >= T: -inf, so its weight below is exp(-inf) = 0 like a dead table's
-      const int pc = min(p, T - 1);
-      sp[p] = p < T ? ((pc == p0) ? base_self : s_base[pc]) : -MVC_PM_INF;
-    }
-#pragma unroll
-    for (int c = 0; c < TM; c += 16) {
-      for (int v = 0; v < V; ++v) {
-        double x[16];
-        const int so = __builtin_amdgcn_readfirstlane(s_soff[v]);
-        if (so >= 0) {                             // staged row: LDS [dish][lane], conflict-free
-          const double *st = s_stage + (size_t)(so - s_koff[v]) * 64 + (tid & 63);
-#pragma unroll
-          for (int u = 0; u < 16; ++u) x[u] = st[(size_t)__builtin_amdgcn_readfirstlane(s_tix[min(c + u, T - 1) * V + v]) * 64];
-        } else {
-#pragma unroll
-          for (int u = 0; u < 16; ++u) x[u] = row(__builtin_amdgcn_readfirstlane(s_tix[min(c + u, T - 1) * V + v]));
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
-      }
-    }
-    double M = -MVC_PM_INF;
-#pragma unroll
-    for (int p = 0; p < TM; ++p)
-      if (p < T && sp[p] > M) M = sp[p];
-    if (s_new > M) M = s_new;
-    // weights e_p in place; block sums pw16, running block totals C_b
-    double C[TM / 16];
-    double tot = 0.0;
-#pragma unroll
-    for (int b = 0; b < TM / 16; ++b) {
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int p = 16 * b + c;
-        // a dead table or p >= T has sp = -inf: exp_le0(-inf) = +0, the spec's 0 weight
-        double xe = sp[p] - M;
-        asm volatile("" : "+v"(xe) : "v"(sp[(p + TM - MVC_ZEXP_LAG) % TM]));   // MVC_ZEXP_LAG exps in flight, not TM live
-        sp[p] = mvc_exp_le0(xe);
-      }
-      double blk[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) blk[c] = sp[16 * b + c];
-      tot = tot + pw16(blk);
-      C[b] = tot;
-    }
-    const double W = mvc_exp_le0(s_new - M) + tot;
-    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-    int pick = -1;
-    if (r < tot) {
-      int bsel = TM / 16 - 1;
-      double prev = 0.0;
-#pragma unroll
-      for (int b = TM / 16 - 1; b >= 0; --b)
-        if (r < C[b]) { bsel = b; prev = b > 0 ? C[b - 1] : 0.0; }
-      r = r - prev;
-      double blk[16];
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        double x = sp[c];
-#pragma unroll
-        for (int b = 1; b < TM / 16; ++b)
-          if (bsel == b) x = sp[16 * b + c];
-        blk[c] = x;
-      }
-      pick = 16 * bsel + pw16_select(blk, r);
-    }
-    A.choice[i] = pick;
-  }
+  const ZregLds Z{s_base, s_w, s_tix, s_koff, s_lmin, s_soff, s_dl};
+  const int li = blockIdx.x * blockDim.x + tid;   // one customer per thread (no loop-invariant hoisting)
+  if (li >= nb) return;
+  const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
+  A.choice[b0 + li] = zdraw_reg_one<TM>(A, Z, b0 + li, row, s_stage, tid & 63);
 }
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
   return 8 * ((size_t)TM + (size_t)sumK + (size_t)4 * MVC_ZSTAGE * 64) +
@@ -1092,7 +1116,7 @@ __host__ __device__ inline size_t lpall_shared_bytes(size_t s1t_doubles, int V, 
 }
 
 template <int NT, int SPPT, int RP>
-__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int b0, int li0, int nb, int pz, double y2,
+__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int b0, int li0, int lr0, int nb, int pz, double y2,
                                          const mvc_d2 *cur, const mvc_d2 *nxt, mvc_d2 (&ring)[RP], double *lpb,
                                          double *dslot, double *y2s, double *selfG, double *mrest, int *zs) {
   const ParState &P = A.P;
@@ -1137,7 +1161,7 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
     for (int r = 0; r < 4; ++r) {
       const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
       const int li = li0 + grp + 4 * r;
-      double *dst = (j < K && li < nb) ? lpb + lpb_index(li, koff + j, sumK) : dslot;
+      double *dst = (j < K && li < nb) ? lpb + lpb_index(lr0 + grp + 4 * r, koff + j, sumK) : dslot;
       *dst = val;
       if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
     }
@@ -1157,7 +1181,7 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
   const double hself = (-0.5 * y2) / tau;
   const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
   const bool ok = lane < 16 && li0 + col < nb;
-  double *dst = ok ? lpb + lpb_index(li0 + col, kk, sumK) : dslot;
+  double *dst = ok ? lpb + lpb_index(lr0 + col, kk, sumK) : dslot;
   *dst = sv;
   const bool alive = (L.nt[pz] - 1) > 0;
   const int l0p = L.dl[kk] - (alive ? 0 : 1);
@@ -1171,16 +1195,16 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
 }
 
 template <int SPPT, int RP, uint32_t PAT, int VI>
-__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int b0, int li0, int nb, int pz,
+__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int b0, int li0, int lr0, int nb, int pz,
                                           const double (&y2v)[MVC_Z_VMAX], const mvc_d2 *ybase, size_t vstride,
                                           size_t tcur, size_t tnext, mvc_d2 (&ring)[RP], double *lpb, double *dslot,
                                           double *y2s, double *selfG, double *mrest, int *zs) {
   if constexpr (VI < fz_pat_v(PAT)) {
     const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
     const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
-    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, b0, li0, nb, pz, y2v[VI], cur, nxt, ring, lpb, dslot, y2s, selfG,
-                                           mrest, zs);
-    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, b0, li0, nb, pz, y2v, ybase, vstride, tcur, tnext, ring, lpb, dslot, y2s,
+    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, b0, li0, lr0, nb, pz, y2v[VI], cur, nxt, ring, lpb, dslot, y2s,
+                                           selfG, mrest, zs);
+    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, b0, li0, lr0, nb, pz, y2v, ybase, vstride, tcur, tnext, ring, lpb, dslot, y2s,
                                      selfG, mrest, zs);
   }
 }
@@ -1259,10 +1283,11 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int
     double y2v[MVC_Z_VMAX];
 #pragma unroll
     for (int v = 0; v < MVC_Z_VMAX; ++v) y2v[v] = v < V ? A.Y2[(size_t)v * n + li_row] : 0.0;
-    lpa_views<SPPT, RP, PAT, 0>(A, L, b0, li0, nb, pz, y2v, ybase, vstride, toff(m), toff(m + 1), ring, lpb, dslot, y2s,
-                                selfG, mrest, zs);
+    lpa_views<SPPT, RP, PAT, 0>(A, L, b0, li0, li0, nb, pz, y2v, ybase, vstride, toff(m), toff(m + 1), ring, lpb, dslot,
+                                y2s, selfG, mrest, zs);
   }
 }
+
 
 #include "mvc_repair.h"
 
@@ -1788,6 +1813,8 @@ class ParallelSampler : public Sampler {
   int (*shard_cb)(void *) = nullptr;
   void *shard_user = nullptr;
   bool no_lpall = false;          // MVC_LPALL=0: per-view producer launches even where the all-views producer applies
+  bool phase_a_only = false;      // sweep_chain stops after phase A (mvc_sampler_phase_a)
+  bool phase_a_ran = false;
   int n_cu = 256;
   bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
   bool early_mh_off = false;      // MVC_EARLY_MH=0: the MH launched only after the host has read the repair
@@ -2491,6 +2518,11 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
+    if (phase_a_only) {                            // mvc_sampler_phase_a: the pass alone
+      phase_a_ran = phaseA;
+      zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) | (use_big ? 64 : 0)) : 32;
+      return;
+    }
     if (phaseA && shard_world > 1) {
       // the other ranks' phase-A choices: this shard into the exchange buffer,
       // the caller's all-gather (synchronous), every shard back.  Each rank
@@ -2746,6 +2778,24 @@ class ParallelSampler : public Sampler {
   }
 
   void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }
+
+  bool phase_a(int chain, int32_t *out) override {
+    if (chains.size() != 1 || chain != 0) return false;
+    synchronize();
+    Chain &c = chains[0];
+    phase_a_only = true;
+    try {
+      sweep_chain(c, (uint32_t)sweeps_done);
+    } catch (...) {
+      phase_a_only = false;
+      throw;
+    }
+    phase_a_only = false;
+    if (!phase_a_ran) return false;
+    MVC_HIP(hipMemcpyAsync(out, c.choice, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+    synchronize();
+    return true;
+  }
 
   bool set_shard(int rank, int world, int32_t *exch, int (*cb)(void *), void *user) override {
     if (chains.size() > 1) return false;   // one chain per sharded handle (mvc.h)

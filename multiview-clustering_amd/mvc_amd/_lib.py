@@ -118,6 +118,7 @@ def lib():
         "mvc_sampler_reset_timers": (None, [vp]),
         "mvc_sampler_zpath": (i32, [vp]),
         "mvc_sampler_repair_stats": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int32)]),
+        "mvc_sampler_phase_a": (i32, [vp, i32, ctypes.POINTER(ctypes.c_int32)]),
         "mvc_sampler_set_timing": (i32, [vp, i32]),
         "mvc_sampler_ari": (i32, [vp, i32, ip, dp, cp, sz]),
         "mvc_ari": (i32, [i32, ip, ip, i64, dp, cp, sz]),

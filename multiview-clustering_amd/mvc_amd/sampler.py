@@ -291,6 +291,16 @@ class Sampler:
         -1 exact schedule / no sweep yet."""
         return int(self._lib.mvc_sampler_zpath(self._h))
 
+    def phase_a(self, chain=0):
+        """Phase A alone (mvc_sampler_phase_a): the next parallel sweep's
+        data-parallel choices of every customer against the current state
+        (table position, -1 = new table); the state is unchanged."""
+        out = np.empty(self.n, dtype=np.int32)
+        st = self._lib.mvc_sampler_phase_a(self._h, chain, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+        if st != L.MVC_OK:
+            raise L.MvcError(st, "phase_a failed")
+        return out
+
     def repair_stats(self, chain=0):
         """Counters of the chain's last parallel sweep: dict
         moves (customers that changed table), births, rounds (in-order repair

@@ -399,6 +399,55 @@ def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
         assert h["sigma_global"] == ref["sigma_global"][it]
 
 
+# Phase A alone (mvc_sampler_phase_a) against the oracle's phase-A
+# conditional: ragged tile groups (n % 64 != 0), fewer tiles than waves,
+# T <= 16 / 64, the bench's dish pattern (64, 32, 16, 8) at D = 128 and
+# configs[1]'s (16, 8) at D = 64, up to the bench's full N.
+PHASE_A_SHAPES = [(4100, 4, 128, 64, 64), (3001, 2, 64, 16, 16), (70001, 4, 128, 64, 64), (777, 2, 64, 16, 16),
+                  (300001, 2, 64, 16, 16), (1_000_000, 4, 128, 64, 64)]
+
+
+@pytest.mark.parametrize("n,V,D,K,T", PHASE_A_SHAPES)
+def test_phase_a_vs_oracle(n, V, D, K, T):
+    """Every customer up to 300k, a sample of 40k (incl. the first and last
+    tiles) beyond; from the state after one sweep (statistics kept
+    incrementally)."""
+    m = _mvc()
+    from mvc_amd import data
+    y, z = data.synthetic(n, V, D, T, seed=n + D + 2)
+    uniq, table_of = np.unique(z, return_inverse=True)
+    table_of = table_of.astype(np.int32)
+    T = uniq.size
+    dish = np.stack([np.arange(T) % max(1, K // (2 ** v)) for v in range(V)]).astype(np.int32)
+    hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
+    if n <= 300_001:
+        idx = np.arange(n, dtype=np.int32)
+    else:
+        rng = np.random.default_rng(n)
+        idx = np.unique(np.concatenate([np.arange(256), np.arange(n - 256, n),
+                                        rng.choice(n, 40_000, replace=False)])).astype(np.int32)
+    s = m.Sampler(y, seed=41, mode="parallel")
+    s.set_state(table_of, dish, hyper)
+    s.sweep(1)                            # phase A of sweep 1
+    t1, d1, h1 = s.state()
+    ch = s.phase_a()
+    assert s.zpath() & 4                  # the register draw
+    stats = [s.stats(v) for v in range(V)]
+    rows = np.ascontiguousarray(np.transpose(y[:, idx, :], (1, 0, 2)))
+    ref = O.phase_a(t1, d1, np.concatenate([h1["tau_v"], h1["alpha_v"], h1["sigma_v"],
+                                            [h1["alpha_global"], h1["sigma_global"]]]), stats, 41, 0, 1, idx, rows)
+    assert np.array_equal(ch[idx], ref), int(np.sum(ch[idx] != ref))
+    # the pass changed nothing: a sweep now equals a sweep without the call
+    s2 = m.Sampler(y, seed=41, mode="parallel")
+    s2.set_state(table_of, dish, hyper)
+    s2.sweep(1)
+    s.sweep(1)
+    s2.sweep(1)
+    assert np.array_equal(s.state()[0], s2.state()[0])
+    s.close()
+    s2.close()
+
+
 def test_exact_warm_start():
     m = _mvc()
     from mvc_amd import data
