@@ -292,17 +292,31 @@ def newsim_call_line(seed, device, M=10000, M_short=2000):
 
 def newsim_chains_line(seed, device):
     """The same call with several chains per call (MVC_CHAINS in the drop-in):
-    aggregate chain-sweeps/s, parallel schedule 16 chains, exact 256."""
+    aggregate chain-sweeps/s, parallel schedule 16 chains, exact 2048 (one
+    wavefront each, 8 per CU); for the exact schedule also the sweeps alone,
+    without mvc_run's per-sample bookkeeping (2048 chains x 250 samples)."""
     import mvc_amd
     from mvc_amd import data
+    from mvc_amd.sampler import Sampler
     y, _ = data.new_simulation(seed)
     out = {}
-    for mode, C, Mc in (("parallel", 16, 1000), ("exact", 256, 500)):
+    for mode, C, Mc in (("parallel", 16, 1000), ("exact", 2048, 500)):
         t0 = time.perf_counter()
         mvc_amd.run_gibbs_cpp(y, Mc, Mc // 2, 1, seed=seed, mode=mode, n_chains=C, device=device, quiet=True)
         dt = time.perf_counter() - t0
         out[f"{mode}_gpu_{C}chains"] = {"chains": C, "sweeps": Mc, "s": round(dt, 2),
                                         "chain_sweeps_per_s": round(C * Mc / dt, 1)}
+    C, Mc = 2048, 500
+    s = Sampler(y, seed=seed, mode="exact", n_chains=C, device=device)
+    s.sweep(Mc // 2)                      # past the cold-start transient
+    s.synchronize()
+    t0 = time.perf_counter()
+    s.sweep(Mc)
+    s.synchronize()
+    dt = time.perf_counter() - t0
+    s.close()
+    out[f"exact_gpu_{C}chains_sweeps_only"] = {"chains": C, "sweeps": Mc, "s": round(dt, 2),
+                                               "chain_sweeps_per_s": round(C * Mc / dt, 1)}
     return out
 
 
@@ -545,7 +559,7 @@ def main():
             ch["vs_reference_cpu_same_cores"] = round(ch["value"] / (cores * ref1), 3)
             ns = out["extra"]["newsim_call"]
             r1 = ns["reference_cpu_1core"]["sweeps_per_s"]
-            for key in ("parallel_gpu_16chains", "exact_gpu_256chains"):
+            for key in ("parallel_gpu_16chains", "exact_gpu_2048chains", "exact_gpu_2048chains_sweeps_only"):
                 if key in ns:
                     cores = min(ns[key]["chains"], os.cpu_count() or 1)
                     ns[key]["cpu_cores_compared"] = cores

@@ -310,7 +310,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
   ExactChain &Cg = chains[blockIdx.x];
   ExactChain C = Cg;               // pointers + scalars in registers
   const int lane = threadIdx.x;
-  if (C.status == MVC_ST_DONE || C.status == MVC_ST_ERROR) return;
+  if (C.status == MVC_ST_ERROR || C.todo <= 0) return;
   const int TC = C.TC, KC = C.KC;
   char *gbeg = nullptr;
   size_t nbytes = 0;
@@ -339,278 +339,283 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
   int T = C.T;
   int n_free = C.n_free;
   const double *tau = sh.hyp, *alpha = sh.hyp + V, *sigma = sh.hyp + 2 * V;
-  const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];
   int status = MVC_ST_RUNNING;
   int i = C.resume_i;
+  int todo = C.todo;
 
-  for (; i < n; ++i) {
-    // -------- capacity guard (every step may add 1 table and 1 dish/view)
-    int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
-    for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
-    if (need) { status = MVC_ST_OVERFLOW; break; }
+  for (; todo > 0; --todo, i = 0) {   // the launch's sweeps, each from customer resume_i / 0
+    const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];   // the MH of the previous sweep may have moved them
+    for (; i < n; ++i) {
+      // -------- capacity guard (every step may add 1 table and 1 dish/view)
+      int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
+      for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
+      if (need) { status = MVC_ST_OVERFLOW; break; }
 
-    if (lane < V) sh.ys[lane] = y[(size_t)lane * n + i];
-    // ---------------- remove_customer(i)   utils.cpp:138-192
-    const int s = C.z[i];
-    __syncthreads();
-    if (lane < V) {
-      const int k = C.dish[lane * TC + s];
-      const double yv = sh.ys[lane];
-      C.d_n[lane * KC + k] -= 1;
-      C.d_S1[lane * KC + k] -= yv;
-      C.d_S2[lane * KC + k] -= yv * yv;
-    }
-    int nt_s = C.n_t[s] - 1;
-    __syncthreads();
-    if (lane == 0) C.n_t[s] = nt_s;
-    if (nt_s == 0) {
-      // table dies: l_vk-- (:170-173), swap-and-pop (:175-190)
+      if (lane < V) sh.ys[lane] = y[(size_t)lane * n + i];
+      // ---------------- remove_customer(i)   utils.cpp:138-192
+      const int s = C.z[i];
+      __syncthreads();
       if (lane < V) {
         const int k = C.dish[lane * TC + s];
-        int dead = -1;
-        if (k >= 0) {
-          const int l = C.d_l[lane * KC + k];
-          if (l > 0) {
-            C.d_l[lane * KC + k] = l - 1;
-            if (l - 1 == 0) dead = k;
-          }
-        }
-        sh.died[lane] = dead;
-      }
-      const int pos = C.pos_of_slot[s];
-      const int last = T - 1;
-      __syncthreads();
-      if (lane == 0) {
-        if (pos != last) {
-          const int sl = C.slot_at_pos[last];
-          C.slot_at_pos[pos] = sl;
-          C.pos_of_slot[sl] = pos;
-        }
-        C.free_slots[n_free] = s;
-      }
-      T -= 1;
-      n_free += 1;
-      __syncthreads();
-      // compact the live dish list of every view whose dish died
-      for (int v = 0; v < V; ++v) {
-        const int k = sh.died[v];
-        if (k < 0) continue;
-        const int K = sh.Kact[v];
-        // shift entries k+1..K-1 down by one (read all, barrier, write)
-        for (int base = k + 1; base < K; base += MVC_WAVE) {
-          const int j = base + lane;
-          int id = 0, nn = 0, ll = 0;
-          double s1 = 0.0, s2 = 0.0;
-          if (j < K) {
-            id = C.d_id[v * KC + j]; nn = C.d_n[v * KC + j]; ll = C.d_l[v * KC + j];
-            s1 = C.d_S1[v * KC + j]; s2 = C.d_S2[v * KC + j];
-          }
-          __syncthreads();
-          if (j < K) {
-            C.d_id[v * KC + j - 1] = id; C.d_n[v * KC + j - 1] = nn; C.d_l[v * KC + j - 1] = ll;
-            C.d_S1[v * KC + j - 1] = s1; C.d_S2[v * KC + j - 1] = s2;
-          }
-          __syncthreads();
-        }
-        for (int p = lane; p < T; p += MVC_WAVE) {
-          const int sl = C.slot_at_pos[p];
-          const int dk = C.dish[v * TC + sl];
-          if (dk > k) C.dish[v * TC + sl] = dk - 1;
-        }
-        __syncthreads();
-        if (lane == 0) sh.Kact[v] = K - 1;
-        __syncthreads();
-      }
-    }
-
-    // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
-    if (lane == 0) {
-      int acc = 0;
-      for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
-      sh.Koff[V] = acc;
-    }
-    __syncthreads();
-    const int Ktot = sh.Koff[V];
-    for (int e = lane; e < Ktot; e += MVC_WAVE) {
-      int v = 0;
-      while (sh.Koff[v + 1] <= e) ++v;
-      const int j = e - sh.Koff[v];
-      const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v]);
-      C.f[v * KC + j] = f;
-      C.logf[v * KC + j] = mvc_log(f);
-    }
-    if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane]);
-    __syncthreads();
-
-    // ---------------- marginal of a new table per view (utils.cpp:40-69)
-    if (lane < V) {
-      const int v = lane;
-      const int K = sh.Kact[v];
-      double total = 0.0;
-      for (int j = 0; j < K; ++j) total += C.d_l[v * KC + j];
-      const double denom = alpha[v] + total;
-      double m;
-      if (denom <= 0.0) {
-        m = sh.fnew[v];
-      } else {
-        double acc = 0.0;
-        for (int j = 0; j < K; ++j) {
-          double w = (C.d_l[v * KC + j] - sigma[v]);
-          if (w < 0.0) w = 0.0;
-          acc += w * C.f[v * KC + j];
-        }
-        double wn = (alpha[v] + K * sigma[v]);
-        if (wn < 0.0) wn = 0.0;
-        acc += wn * sh.fnew[v];
-        m = acc / denom;
-      }
-      sh.marg[v] = m;
-    }
-
-    // ---------------- table probabilities (utils.cpp:83-116)
-    int tne = 0;
-    for (int p = lane; p < T; p += MVC_WAVE) {
-      const int sl = C.slot_at_pos[p];
-      const int nt = C.n_t[sl];
-      double pr = 0.0;
-      if (nt != 0) {
-        ++tne;
-        double lpt = 0.0;
-        for (int v = 0; v < V; ++v) lpt += C.logf[v * KC + C.dish[v * TC + sl]];
-        const double mass = nt - sg;
-        pr = (mass <= 0.0) ? 0.0 : mass * mvc_exp(lpt);
-      }
-      C.P[p] = pr;
-    }
-    for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
-    __syncthreads();
-
-    // ---------------- normaliser, draw (gibbs.cpp:169-191)
-    if (lane == 0) {
-      double lnew = 0.0;
-      for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
-      const double mass_new = ag + sg * tne;                          // :124-135
-      const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
-      double sum_p = p_new;
-      for (int p = 0; p < T; ++p) sum_p += C.P[p];
-      sh.dv[1] = sum_p;
-    }
-    __syncthreads();
-    const double sum_p = sh.dv[1];
-    int t_star;
-    if (sum_p <= 0.0) {
-      t_star = -2;                       // gibbs.cpp:172-176 -> table at position 0
-    } else {
-      for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
-      __syncthreads();
-      if (lane == 0) {
-        const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
-        double cum = 0.0;
-        int ts = -1;
-        for (int p = 0; p < T; ++p) {
-          cum += C.P[p];
-          if (u < cum) { ts = p; break; }
-        }
-        sh.iv[0] = ts;
-      }
-      C.draws += 1;
-      __syncthreads();
-      t_star = sh.iv[0];
-    }
-
-    if (t_star != -1) {
-      // add_customer_to_existing_table (utils.cpp:194-207)
-      const int sl = C.slot_at_pos[t_star < 0 ? 0 : t_star];
-      __syncthreads();
-      if (lane == 0) { C.z[i] = sl; C.n_t[sl] = C.n_t[sl] + 1; }
-      if (lane < V) {
-        const int k = C.dish[lane * TC + sl];
         const double yv = sh.ys[lane];
-        C.d_n[lane * KC + k] += 1;
-        C.d_S1[lane * KC + k] += yv;
-        C.d_S2[lane * KC + k] += yv * yv;
+        C.d_n[lane * KC + k] -= 1;
+        C.d_S1[lane * KC + k] -= yv;
+        C.d_S2[lane * KC + k] -= yv * yv;
       }
+      int nt_s = C.n_t[s] - 1;
       __syncthreads();
-    } else {
-      // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
-      n_free -= 1;
-      const int sl = C.free_slots[n_free];
-      const int pos = T;
-      __syncthreads();
+      if (lane == 0) C.n_t[s] = nt_s;
+      if (nt_s == 0) {
+        // table dies: l_vk-- (:170-173), swap-and-pop (:175-190)
+        if (lane < V) {
+          const int k = C.dish[lane * TC + s];
+          int dead = -1;
+          if (k >= 0) {
+            const int l = C.d_l[lane * KC + k];
+            if (l > 0) {
+              C.d_l[lane * KC + k] = l - 1;
+              if (l - 1 == 0) dead = k;
+            }
+          }
+          sh.died[lane] = dead;
+        }
+        const int pos = C.pos_of_slot[s];
+        const int last = T - 1;
+        __syncthreads();
+        if (lane == 0) {
+          if (pos != last) {
+            const int sl = C.slot_at_pos[last];
+            C.slot_at_pos[pos] = sl;
+            C.pos_of_slot[sl] = pos;
+          }
+          C.free_slots[n_free] = s;
+        }
+        T -= 1;
+        n_free += 1;
+        __syncthreads();
+        // compact the live dish list of every view whose dish died
+        for (int v = 0; v < V; ++v) {
+          const int k = sh.died[v];
+          if (k < 0) continue;
+          const int K = sh.Kact[v];
+          // shift entries k+1..K-1 down by one (read all, barrier, write)
+          for (int base = k + 1; base < K; base += MVC_WAVE) {
+            const int j = base + lane;
+            int id = 0, nn = 0, ll = 0;
+            double s1 = 0.0, s2 = 0.0;
+            if (j < K) {
+              id = C.d_id[v * KC + j]; nn = C.d_n[v * KC + j]; ll = C.d_l[v * KC + j];
+              s1 = C.d_S1[v * KC + j]; s2 = C.d_S2[v * KC + j];
+            }
+            __syncthreads();
+            if (j < K) {
+              C.d_id[v * KC + j - 1] = id; C.d_n[v * KC + j - 1] = nn; C.d_l[v * KC + j - 1] = ll;
+              C.d_S1[v * KC + j - 1] = s1; C.d_S2[v * KC + j - 1] = s2;
+            }
+            __syncthreads();
+          }
+          for (int p = lane; p < T; p += MVC_WAVE) {
+            const int sl = C.slot_at_pos[p];
+            const int dk = C.dish[v * TC + sl];
+            if (dk > k) C.dish[v * TC + sl] = dk - 1;
+          }
+          __syncthreads();
+          if (lane == 0) sh.Kact[v] = K - 1;
+          __syncthreads();
+        }
+      }
+
+      // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
       if (lane == 0) {
-        C.slot_at_pos[pos] = sl;
-        C.pos_of_slot[sl] = pos;
-        C.n_t[sl] = 1;
-        C.z[i] = sl;
+        int acc = 0;
+        for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
+        sh.Koff[V] = acc;
       }
-      T += 1;
-      // assign_dishes_new_table (utils.cpp:278-289): per view weights
+      __syncthreads();
+      const int Ktot = sh.Koff[V];
+      for (int e = lane; e < Ktot; e += MVC_WAVE) {
+        int v = 0;
+        while (sh.Koff[v + 1] <= e) ++v;
+        const int j = e - sh.Koff[v];
+        const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v]);
+        C.f[v * KC + j] = f;
+        C.logf[v * KC + j] = mvc_log(f);
+      }
+      if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane]);
+      __syncthreads();
+
+      // ---------------- marginal of a new table per view (utils.cpp:40-69)
       if (lane < V) {
         const int v = lane;
         const int K = sh.Kact[v];
         double total = 0.0;
-        for (int j = 0; j < K; ++j) {
-          double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
-          if (w < 0) w = 0;
-          total += w;
+        for (int j = 0; j < K; ++j) total += C.d_l[v * KC + j];
+        const double denom = alpha[v] + total;
+        double m;
+        if (denom <= 0.0) {
+          m = sh.fnew[v];
+        } else {
+          double acc = 0.0;
+          for (int j = 0; j < K; ++j) {
+            double w = (C.d_l[v * KC + j] - sigma[v]);
+            if (w < 0.0) w = 0.0;
+            acc += w * C.f[v * KC + j];
+          }
+          double wn = (alpha[v] + K * sigma[v]);
+          if (wn < 0.0) wn = 0.0;
+          acc += wn * sh.fnew[v];
+          m = acc / denom;
         }
-        double wn = (alpha[v] + sigma[v] * K) * sh.fnew[v];
-        if (wn < 0) wn = 0;
-        total += wn;
-        sh.tw[v] = total;
+        sh.marg[v] = m;
+      }
+
+      // ---------------- table probabilities (utils.cpp:83-116)
+      int tne = 0;
+      for (int p = lane; p < T; p += MVC_WAVE) {
+        const int sl = C.slot_at_pos[p];
+        const int nt = C.n_t[sl];
+        double pr = 0.0;
+        if (nt != 0) {
+          ++tne;
+          double lpt = 0.0;
+          for (int v = 0; v < V; ++v) lpt += C.logf[v * KC + C.dish[v * TC + sl]];
+          const double mass = nt - sg;
+          pr = (mass <= 0.0) ? 0.0 : mass * mvc_exp(lpt);
+        }
+        C.P[p] = pr;
+      }
+      for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
+      __syncthreads();
+
+      // ---------------- normaliser, draw (gibbs.cpp:169-191)
+      if (lane == 0) {
+        double lnew = 0.0;
+        for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
+        const double mass_new = ag + sg * tne;                          // :124-135
+        const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
+        double sum_p = p_new;
+        for (int p = 0; p < T; ++p) sum_p += C.P[p];
+        sh.dv[1] = sum_p;
       }
       __syncthreads();
-      if (lane == 0) {                       // draws are consumed in view order
-        uint64_t d = C.draws;
-        for (int v = 0; v < V; ++v) sh.draw_ix[v] = (sh.tw[v] <= 0) ? -1 : (int)(d++ - C.draws);
-        sh.iv[1] = (int)(d - C.draws);
+      const double sum_p = sh.dv[1];
+      int t_star;
+      if (sum_p <= 0.0) {
+        t_star = -2;                       // gibbs.cpp:172-176 -> table at position 0
+      } else {
+        for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
+        __syncthreads();
+        if (lane == 0) {
+          const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
+          double cum = 0.0;
+          int ts = -1;
+          for (int p = 0; p < T; ++p) {
+            cum += C.P[p];
+            if (u < cum) { ts = p; break; }
+          }
+          sh.iv[0] = ts;
+        }
+        C.draws += 1;
+        __syncthreads();
+        t_star = sh.iv[0];
       }
-      __syncthreads();
-      if (lane < V) {
-        const int v = lane;
-        const int K = sh.Kact[v];
-        int kk = -1;
-        const double total = sh.tw[v];
-        if (total > 0) {
-          const double u = 0.0 + (total - 0.0) * mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws + (uint64_t)sh.draw_ix[v]);
-          double cum = 0;
+
+      if (t_star != -1) {
+        // add_customer_to_existing_table (utils.cpp:194-207)
+        const int sl = C.slot_at_pos[t_star < 0 ? 0 : t_star];
+        __syncthreads();
+        if (lane == 0) { C.z[i] = sl; C.n_t[sl] = C.n_t[sl] + 1; }
+        if (lane < V) {
+          const int k = C.dish[lane * TC + sl];
+          const double yv = sh.ys[lane];
+          C.d_n[lane * KC + k] += 1;
+          C.d_S1[lane * KC + k] += yv;
+          C.d_S2[lane * KC + k] += yv * yv;
+        }
+        __syncthreads();
+      } else {
+        // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
+        n_free -= 1;
+        const int sl = C.free_slots[n_free];
+        const int pos = T;
+        __syncthreads();
+        if (lane == 0) {
+          C.slot_at_pos[pos] = sl;
+          C.pos_of_slot[sl] = pos;
+          C.n_t[sl] = 1;
+          C.z[i] = sl;
+        }
+        T += 1;
+        // assign_dishes_new_table (utils.cpp:278-289): per view weights
+        if (lane < V) {
+          const int v = lane;
+          const int K = sh.Kact[v];
+          double total = 0.0;
           for (int j = 0; j < K; ++j) {
             double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
             if (w < 0) w = 0;
-            cum += w;
-            if (u < cum) { kk = j; break; }
+            total += w;
           }
+          double wn = (alpha[v] + sigma[v] * K) * sh.fnew[v];
+          if (wn < 0) wn = 0;
+          total += wn;
+          sh.tw[v] = total;
         }
-        if (kk < 0) {                        // fresh dish slot (utils.cpp:250-258,268-275)
-          kk = K;
-          C.d_id[v * KC + kk] = sh.next_id[v];
-          C.d_n[v * KC + kk] = 0;
-          C.d_l[v * KC + kk] = 0;
-          C.d_S1[v * KC + kk] = 0.0;
-          C.d_S2[v * KC + kk] = 0.0;
-          sh.next_id[v] += 1;
-          sh.Kact[v] = K + 1;
+        __syncthreads();
+        if (lane == 0) {                       // draws are consumed in view order
+          uint64_t d = C.draws;
+          for (int v = 0; v < V; ++v) sh.draw_ix[v] = (sh.tw[v] <= 0) ? -1 : (int)(d++ - C.draws);
+          sh.iv[1] = (int)(d - C.draws);
         }
-        const double yv = sh.ys[v];
-        C.dish[v * TC + sl] = kk;
-        C.d_l[v * KC + kk] += 1;
-        C.d_n[v * KC + kk] += 1;
-        C.d_S1[v * KC + kk] += yv;
-        C.d_S2[v * KC + kk] += yv * yv;
+        __syncthreads();
+        if (lane < V) {
+          const int v = lane;
+          const int K = sh.Kact[v];
+          int kk = -1;
+          const double total = sh.tw[v];
+          if (total > 0) {
+            const double u = 0.0 + (total - 0.0) * mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws + (uint64_t)sh.draw_ix[v]);
+            double cum = 0;
+            for (int j = 0; j < K; ++j) {
+              double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
+              if (w < 0) w = 0;
+              cum += w;
+              if (u < cum) { kk = j; break; }
+            }
+          }
+          if (kk < 0) {                        // fresh dish slot (utils.cpp:250-258,268-275)
+            kk = K;
+            C.d_id[v * KC + kk] = sh.next_id[v];
+            C.d_n[v * KC + kk] = 0;
+            C.d_l[v * KC + kk] = 0;
+            C.d_S1[v * KC + kk] = 0.0;
+            C.d_S2[v * KC + kk] = 0.0;
+            sh.next_id[v] += 1;
+            sh.Kact[v] = K + 1;
+          }
+          const double yv = sh.ys[v];
+          C.dish[v * TC + sl] = kk;
+          C.d_l[v * KC + kk] += 1;
+          C.d_n[v * KC + kk] += 1;
+          C.d_S1[v * KC + kk] += yv;
+          C.d_S2[v * KC + kk] += yv * yv;
+        }
+        C.draws += (uint64_t)sh.iv[1];
+        __syncthreads();
       }
-      C.draws += (uint64_t)sh.iv[1];
-      __syncthreads();
     }
-  }
 
-  if (status == MVC_ST_RUNNING) {
+    if (status != MVC_ST_RUNNING) break;
     // end of sweep: hyperparameters (gibbs.cpp:202)
     C.T = T;
     MH mh{C, sh, V, n, lane, seed};
     mh.run();
-    status = MVC_ST_DONE;
-    i = n;
+    // the MH draws on lane 0 only: every lane continues from lane 0's counter
+    // (the next sweep's dish draws run on lanes 0 .. V-1)
+    C.draws = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(C.draws >> 32)) << 32) |
+              (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)C.draws);
   }
+  if (status == MVC_ST_RUNNING) status = MVC_ST_DONE;
   __syncthreads();
   for (int v = lane; v < V; v += MVC_WAVE) {
     C.Kact[v] = sh.Kact[v];
@@ -623,6 +628,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     Cg.draws = C.draws;
     Cg.resume_i = i;
     Cg.status = status;
+    Cg.todo = todo;
   }
   if (gbeg) {                      // the LDS copy back to the chain's allocation
     __syncthreads();
@@ -1047,7 +1053,7 @@ class ExactSampler : public Sampler {
     for (size_t k = 0; k < chains.size(); ++k) {
       ExactChain &C = chains[k].h;
       C.T = hs[k].T; C.n_free = hs[k].n_free; C.draws = hs[k].draws;
-      C.resume_i = hs[k].resume_i; C.status = hs[k].status;
+      C.resume_i = hs[k].resume_i; C.status = hs[k].status; C.todo = hs[k].todo;
     }
   }
 
@@ -1069,9 +1075,14 @@ class ExactSampler : public Sampler {
     A = B;
   }
 
+  // sweeps per kernel launch: each chain runs its sweeps on its own, so a
+  // launch lasts about the longest chain's sum of sweeps rather than the sum
+  // of the longest sweeps, and the per-sweep launch + read-back is amortised
+  static constexpr int kSweepsPerLaunch = 64;
   void sweep(int n_sweeps) override {
-    for (int it = 0; it < n_sweeps; ++it) {
-      for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; }
+    for (int left = n_sweeps; left > 0;) {
+      const int k = std::min(left, kSweepsPerLaunch);
+      for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; A.h.todo = k; }
       push_structs();
       hipEvent_t ev0 = nullptr;
       timers.begin("sweep", &ev0);
@@ -1090,10 +1101,11 @@ class ExactSampler : public Sampler {
         }
         if (!again) break;
         push_structs();
-        if (round > 64) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
+        if (round > 64 + 64 * k) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
       }
       timers.end("sweep", ev0);
-      ++sweeps_done;
+      sweeps_done += k;
+      left -= k;
     }
   }
 

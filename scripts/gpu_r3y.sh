@@ -2,7 +2,7 @@
 # exact schedule with LDS-resident chain arrays: exact parity tests, then the New_Simulation shape probe
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_abi.py -x -v --timeout 300 --timeout-method thread \
-    -k "exact or c_abi or smoke or async" > gpurun_out/pytest_r3y.log 2>&1 \
+    -k "exact or c_abi or smoke or async or golden or live_oracle or capacity or sweeps_per_launch" > gpurun_out/pytest_r3y.log 2>&1 \
     || { echo "tests failed"; grep -E "PASSED|FAILED|Error|error" gpurun_out/pytest_r3y.log | tail -30; exit 1; }
 tail -2 gpurun_out/pytest_r3y.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" || { echo "smoke failed"; exit 1; }

@@ -145,6 +145,29 @@ def test_exact_many_chains_vs_live_oracle():
         _compare(g, ref)
 
 
+@pytest.mark.parametrize("cap", [(256, 128), (8, 4)])
+def test_exact_sweeps_per_launch(cap):
+    """Several sweeps in one kernel launch (Sampler.sweep(k)) equal k calls
+    of one sweep, with and without capacity growth inside the launch."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.config1(1, n=600)
+    a = m.Sampler(y, seed=7, mode="exact", n_chains=3, table_cap=cap[0], dish_cap=cap[1])
+    b = m.Sampler(y, seed=7, mode="exact", n_chains=3, table_cap=cap[0], dish_cap=cap[1])
+    for k in (1, 2, 5, 11):
+        a.sweep(k)
+        for _ in range(k):
+            b.sweep(1)
+        for c in range(3):
+            ta, da, ha = a.state(c)
+            tb, db, hb = b.state(c)
+            assert np.array_equal(ta, tb), (k, c)
+            assert np.array_equal(da, db), (k, c)
+            assert ha["alpha_global"] == hb["alpha_global"], (k, c)
+    a.close()
+    b.close()
+
+
 def test_exact_capacity_growth():
     """Tiny initial capacities force the overflow -> regrow -> resume path."""
     m = _mvc()
