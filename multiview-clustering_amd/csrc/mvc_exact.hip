@@ -57,6 +57,46 @@ struct Shared {
 };
 
 // ---------------------------------------------------------------------------
+// Sequential left-to-right sums and inverse-CDF searches in the reference's
+// order (so the same bits), with the terms loaded 8 at a time: a batch's
+// loads are in flight together instead of one dependent round trip per term.
+// ---------------------------------------------------------------------------
+template <class F>
+__device__ __forceinline__ double seq_sum8(double s, int n, F term) {
+  int j = 0;
+  for (; j + 8 <= n; j += 8) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = term(j + q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += x[q];
+  }
+  for (; j < n; ++j) s += term(j);
+  return s;
+}
+// the first j whose running sum exceeds u, -1 if none
+template <class F>
+__device__ __forceinline__ int seq_find8(double u, int n, F term) {
+  double cum = 0.0;
+  int j = 0;
+  for (; j + 8 <= n; j += 8) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = term(j + q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      cum += x[q];
+      if (u < cum) return j + q;
+    }
+  }
+  for (; j < n; ++j) {
+    cum += term(j);
+    if (u < cum) return j;
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
 // hyperparameter MH (multiview_hyper.cpp:211-292), executed by the wave.
 // Sums are accumulated in the reference's order by lane 0; lanes only
 // produce the addends.
@@ -448,19 +488,17 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
       if (lane < V) {
         const int v = lane;
         const int K = sh.Kact[v];
-        double total = 0.0;
-        for (int j = 0; j < K; ++j) total += C.d_l[v * KC + j];
+        const double total = seq_sum8(0.0, K, [&](int j) { return (double)C.d_l[v * KC + j]; });
         const double denom = alpha[v] + total;
         double m;
         if (denom <= 0.0) {
           m = sh.fnew[v];
         } else {
-          double acc = 0.0;
-          for (int j = 0; j < K; ++j) {
+          double acc = seq_sum8(0.0, K, [&](int j) {
             double w = (C.d_l[v * KC + j] - sigma[v]);
             if (w < 0.0) w = 0.0;
-            acc += w * C.f[v * KC + j];
-          }
+            return w * C.f[v * KC + j];
+          });
           double wn = (alpha[v] + K * sigma[v]);
           if (wn < 0.0) wn = 0.0;
           acc += wn * sh.fnew[v];
@@ -478,7 +516,17 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         if (nt != 0) {
           ++tne;
           double lpt = 0.0;
-          for (int v = 0; v < V; ++v) lpt += C.logf[v * KC + C.dish[v * TC + sl]];
+          for (int v0 = 0; v0 < V; v0 += 8) {   // 8 views' dish indices, then their log f, in flight together
+            int kq[8];
+            double g[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) kq[q] = (v0 + q < V) ? C.dish[(v0 + q) * TC + sl] : 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) g[q] = (v0 + q < V) ? C.logf[(v0 + q) * KC + kq[q]] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (v0 + q < V) lpt += g[q];
+          }
           const double mass = nt - sg;
           pr = (mass <= 0.0) ? 0.0 : mass * mvc_exp(lpt);
         }
@@ -493,9 +541,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
         const double mass_new = ag + sg * tne;                          // :124-135
         const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
-        double sum_p = p_new;
-        for (int p = 0; p < T; ++p) sum_p += C.P[p];
-        sh.dv[1] = sum_p;
+        sh.dv[1] = seq_sum8(p_new, T, [&](int p) { return C.P[p]; });
       }
       __syncthreads();
       const double sum_p = sh.dv[1];
@@ -507,13 +553,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         __syncthreads();
         if (lane == 0) {
           const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
-          double cum = 0.0;
-          int ts = -1;
-          for (int p = 0; p < T; ++p) {
-            cum += C.P[p];
-            if (u < cum) { ts = p; break; }
-          }
-          sh.iv[0] = ts;
+          sh.iv[0] = seq_find8(u, T, [&](int p) { return C.P[p]; });
         }
         C.draws += 1;
         __syncthreads();
@@ -550,12 +590,11 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         if (lane < V) {
           const int v = lane;
           const int K = sh.Kact[v];
-          double total = 0.0;
-          for (int j = 0; j < K; ++j) {
+          double total = seq_sum8(0.0, K, [&](int j) {
             double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
             if (w < 0) w = 0;
-            total += w;
-          }
+            return w;
+          });
           double wn = (alpha[v] + sigma[v] * K) * sh.fnew[v];
           if (wn < 0) wn = 0;
           total += wn;
@@ -575,13 +614,11 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           const double total = sh.tw[v];
           if (total > 0) {
             const double u = 0.0 + (total - 0.0) * mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws + (uint64_t)sh.draw_ix[v]);
-            double cum = 0;
-            for (int j = 0; j < K; ++j) {
+            kk = seq_find8(u, K, [&](int j) {
               double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
               if (w < 0) w = 0;
-              cum += w;
-              if (u < cum) { kk = j; break; }
-            }
+              return w;
+            });
           }
           if (kk < 0) {                        // fresh dish slot (utils.cpp:250-258,268-275)
             kk = K;
