@@ -9,4 +9,7 @@ timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" || { echo "
 timeout -k 10 400 python -u scripts/newsim_probe.py > gpurun_out/newsim_r3y.json 2> gpurun_out/newsim_r3y.err \
     || { echo "probe failed"; tail gpurun_out/newsim_r3y.err; exit 1; }
 cat gpurun_out/newsim_r3y.json
+
+timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-extras --steps 30 > gpurun_out/bench_r3y.json 2>/dev/null || { echo "bench failed"; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/bench_r3y.json'));print('headline',d['value'],d['ms_per_step'],d['hbm']['pass_ms'])"
 echo done

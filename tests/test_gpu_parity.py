@@ -471,6 +471,47 @@ def test_phase_a_vs_oracle(n, V, D, K, T):
     s2.close()
 
 
+@pytest.mark.parametrize("spec", ["1", "0"])
+@pytest.mark.parametrize("warm", [False, True])
+def test_parallel_sweeps_per_call(warm, spec, monkeypatch):
+    """Sampler.sweep(k) (the next sweep's phase A speculated behind each
+    repair) equals k calls of sweep(1): a cold start (moves,
+    births, capacity growth: the speculations are discarded) and a warm start
+    (no moves: they are used), and the warm chain equals the oracle."""
+    m = _mvc()
+    from mvc_amd import data
+    monkeypatch.setenv("MVC_SPEC", spec)
+    y, z = data.synthetic(5000, 4, 128, 64, seed=77)
+    st = None
+    if warm:
+        uniq, table_of = np.unique(z, return_inverse=True)
+        T = uniq.size
+        dish = np.stack([np.arange(T) % max(1, 64 // (2 ** v)) for v in range(4)]).astype(np.int32)
+        st = (table_of.astype(np.int32), dish, np.array([1.69] * 4 + [1.0] * 4 + [0.5] * 4 + [1.0, 0.6]))
+    caps = {} if warm else dict(table_cap=16, dish_cap=8)   # cold: growth inside sweep(k)
+    a = m.Sampler(y, seed=21, mode="parallel", **caps)
+    b = m.Sampler(y, seed=21, mode="parallel", **caps)
+    if st is not None:
+        a.set_state(*st)
+        b.set_state(*st)
+    for k in (1, 3, 4):
+        a.sweep(k)
+        for _ in range(k):
+            b.sweep(1)
+        ta, da, ha = a.state()
+        tb, db, hb = b.state()
+        assert np.array_equal(ta, tb), k
+        assert np.array_equal(da, db), k
+        assert ha["sigma_global"] == hb["sigma_global"], k
+    if warm:
+        ref = O.run(y, 8, 0, 1, seed=21, mode=O.PARALLEL, state=st)
+        t, d, h = a.state()
+        assert np.array_equal(t, ref["table_of"][7])
+        assert np.array_equal(d, ref["dish_of"][7])
+    a.close()
+    b.close()
+
+
 def test_exact_warm_start():
     m = _mvc()
     from mvc_amd import data
