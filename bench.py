@@ -211,7 +211,7 @@ def gpu_chains_line(config, seed, device, chains=16, sweeps=1):
             "s_per_sweep_all_chains": round(dt / sweeps, 2)}
 
 
-def gpu_exact_line(seed, device, chains=256, sweeps=200):
+def gpu_exact_line(seed, device, chains=2048, sweeps=200):
     """BASELINE configs[0] (the New_Simulation.R problem, N = 500, V = 2, K = 3,
     200 sweeps) on the exact schedule (mode E: the reference's arithmetic,
     one wavefront per chain): `chains` independent chains in one handle."""
