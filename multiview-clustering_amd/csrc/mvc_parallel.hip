@@ -2710,15 +2710,14 @@ class ParallelSampler : public Sampler {
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
       }
       MVC_HIP(hipGetLastError());
+      MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
       if (early_mh) {
-        // the MH goes into the stream right behind the repair, gated on the
-        // device by its outcome (it runs iff the repair is done with no move;
-        // a no-op in the other cases, which launch it below), then the copy
-        // of the outcome: the GPU runs the MH without waiting for the host,
-        // and the copy's host-visible completion is off the MH's path
-        launch_hyper(c, 1, s, c.R);
-        MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
+        // the MH goes into the stream behind the copy, gated on the device by
+        // the repair's outcome (it runs iff the repair is done with no move),
+        // so the GPU runs it while the host waits for the copy and decides the
+        // next launches; it is a no-op in the other cases, which launch it below
         MVC_HIP(hipEventRecord(rs_ev, stream));
+        launch_hyper(c, 1, s, c.R);
         spec_last = false;
         if (spec) {
           spec_pa = enqueue_phase_a(c, s + 1, spec_gate);
@@ -2726,7 +2725,6 @@ class ParallelSampler : public Sampler {
         }
         MVC_HIP(hipEventSynchronize(rs_ev));
       } else {
-        MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
         MVC_HIP(hipStreamSynchronize(stream));
       }
       if (rs_host->overflow) {
