@@ -55,7 +55,6 @@ struct Sweep {
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
-  const int32_t *gate;    // non-null: a speculative launch, runs iff *gate (mvc_seq_spec_init_kernel)
 };
 
 }  // namespace
@@ -1019,7 +1018,6 @@ template <int TM>
 #endif
 __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (A.gate && *A.gate == 0) return;              // a speculative launch whose sweep did not happen
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC;
   const int T = __builtin_amdgcn_readfirstlane(A.T);
@@ -1214,7 +1212,6 @@ __device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int b
 template <int SPPT, int RP, uint32_t PAT>
 __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int nb, double *lpb, double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (A.gate && *A.gate == 0) return;              // a speculative launch whose sweep did not happen
   const ParState &P = A.P;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
@@ -1932,7 +1929,6 @@ class ParallelSampler : public Sampler {
     const char *zl = getenv("MVC_ZDRAW_LDS");
     force_zdraw_lds = zl && zl[0] == '1';
     if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
-    if (const char *e = getenv("MVC_SPEC")) spec_on = e[0] == '1';
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
@@ -2307,7 +2303,6 @@ class ParallelSampler : public Sampler {
 
   Sweep make_sweep(Chain &c, uint32_t s) {
     Sweep A;
-    A.gate = nullptr;
     A.P = c.P;
     A.y = y;
     A.Y2 = Y2;
@@ -2380,23 +2375,11 @@ class ParallelSampler : public Sampler {
     MVC_FZ_PATS(X)
 #undef X
   }
-  // What enqueue_phase_a decided (the next steps and zpath need it).
-  struct PhaseA {
-    bool phaseA = false, use_mfma = false, use_zreg = false, lpall = false, use_big = false;
-    size_t lo = 0, hi = 0;
-    bool spec = false;     // a gated (speculative) launch was enqueued
-  };
-  // The sweep's start: the repair cursor reset and phase A (producer + draw)
-  // over this rank's customers.  gate != nullptr: a speculative launch of the
-  // NEXT sweep, enqueued while the host has not yet read this sweep's repair
-  // outcome; only the common path (all-views producer + register draw, one
-  // batch, no buffer growth) is speculated, its kernels gated on the device
-  // (mvc_seq_spec_init_kernel); otherwise nothing is enqueued (spec = false).
-  PhaseA enqueue_phase_a(Chain &c, uint32_t s, int32_t *gate) {
-    PhaseA R;
+  void sweep_chain(Chain &c, uint32_t s) {
     Sweep A = make_sweep(c, s);
-    A.gate = gate;
     const SeqArgs Q0 = make_seq(c, s);
+    hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
+    MVC_HIP(hipGetLastError());
     hipEvent_t e0 = nullptr;
     // phase 1 in customer batches: lp producer (MFMA or generic), then draw
     int Kmax = 0, Kmin = 1 << 30;
@@ -2441,21 +2424,6 @@ class ParallelSampler : public Sampler {
 #undef X
       break;
       default: pat_ok = false;
-    }
-    {
-      const size_t lpa_lds0 = lpall_shared_bytes(s1t_d, V, sk, 8);
-      const bool lpall_ok = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
-                            (spp == 4 || spp == 8 || spp == 16) && lpa_lds0 <= 160 * 1024;
-      const size_t S0 = (size_t)shard_len(n, shard_world);
-      const size_t lo0 = std::min((size_t)n, (size_t)shard_rank * S0), hi0 = std::min((size_t)n, lo0 + S0);
-      if (gate) {
-        if (!(phaseA && use_zreg && lpall_ok && need <= lpb_cap && hi0 - lo0 <= nbatch_sz)) return R;
-        hipLaunchKernelGGL(mvc_seq_spec_init_kernel, dim3(1), dim3(64), 0, stream, Q0, gate);
-      } else {
-        hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
-      }
-      MVC_HIP(hipGetLastError());
-      R.spec = gate != nullptr;
     }
     if (phaseA && need > lpb_cap) {
       retire(lpb, sizeof(double) * (lpb_cap + 64));
@@ -2550,37 +2518,9 @@ class ParallelSampler : public Sampler {
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
-    R.phaseA = phaseA;
-    R.use_mfma = use_mfma;
-    R.use_zreg = use_zreg;
-    R.lpall = zpath_lpall;
-    R.use_big = use_big;
-    R.lo = lo;
-    R.hi = hi;
-    return R;
-  }
-
-  // Speculation state: the next sweep's phase A already in the stream, and
-  // the device flag that gates it.
-  bool spec_on = false;           // MVC_SPEC=1: speculative launches (off until measured on the MI355X)
-  bool spec_pending = false;
-  PhaseA spec_pa;
-  int32_t *spec_gate = nullptr;
-
-  // more: another sweep follows in this sweep() call (it may be speculated)
-  void sweep_chain(Chain &c, uint32_t s, bool more = false) {
-    PhaseA pa;
-    if (spec_pending) {                            // enqueued (and valid) during the previous sweep's repair
-      pa = spec_pa;
-      spec_pending = false;
-    } else {
-      pa = enqueue_phase_a(c, s, nullptr);
-    }
-    const bool phaseA = pa.phaseA;
-    const size_t lo = pa.lo, hi = pa.hi;
     if (phase_a_only) {                            // mvc_sampler_phase_a: the pass alone
       phase_a_ran = phaseA;
-      zpath = phaseA ? ((pa.use_mfma ? 2 : 0) | (pa.use_zreg ? 4 : 0) | (pa.lpall ? 16 : 0) | (pa.use_big ? 64 : 0)) : 32;
+      zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) | (use_big ? 64 : 0)) : 32;
       return;
     }
     if (phaseA && shard_world > 1) {
@@ -2597,9 +2537,9 @@ class ParallelSampler : public Sampler {
         throw Error(MVC_ERR_CALLBACK, "set_shard: the all_gather callback reported failure; the sweep was not run");
       MVC_HIP(hipMemcpyAsync(c.choice, shard_exch, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, stream));
     }
-    zpath = phaseA ? ((pa.use_mfma ? 2 : 0) | (pa.use_zreg ? 4 : 0) | (pa.lpall ? 16 : 0) |
-                      (pa.use_big ? 64 : 0)) : 32;
-    repair(c, s, phaseA, more && spec_on && shard_world == 1 && chains.size() == 1 && !phase_a_only);
+    zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) |
+                      (use_big ? 64 : 0)) : 32;
+    repair(c, s, phaseA);
   }
 
   // LDS layout of the run kernel's per-wave scratch for T tables and dish
@@ -2669,7 +2609,7 @@ class ParallelSampler : public Sampler {
   // and a grid window (sparse movers).  One host synchronisation per batch of
   // rounds; at steady state a single batch of one round.  A birth beyond the
   // capacity grows every chain and resumes.
-  void repair(Chain &c, uint32_t s, bool phaseA, bool spec = false) {
+  void repair(Chain &c, uint32_t s, bool phaseA) {
     hipEvent_t e1 = nullptr;
     timers.begin("repair", &e1);
     SeqArgs Q = make_seq(c, s);
@@ -2686,12 +2626,6 @@ class ParallelSampler : public Sampler {
     // repair and the MH separately (they would time the MH as repair)
     const bool early_mh = !early_mh_off && (!timers.on || timers.coarse);
     if (early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
-    // speculation: the next sweep's phase A right behind the outcome copy,
-    // gated on the device (it does work iff this repair ends with no move),
-    // so the GPU is busy while the host reads the outcome
-    spec = spec && early_mh;
-    if (spec && !spec_gate) spec_gate = dmalloc<int32_t>(1);
-    bool spec_last = false;
     int rounds = 1;
     for (;;) {
       for (int r = 0; r < rounds; ++r) {
@@ -2718,11 +2652,6 @@ class ParallelSampler : public Sampler {
         // next launches; it is a no-op in the other cases, which launch it below
         MVC_HIP(hipEventRecord(rs_ev, stream));
         launch_hyper(c, 1, s, c.R);
-        spec_last = false;
-        if (spec) {
-          spec_pa = enqueue_phase_a(c, s + 1, spec_gate);
-          spec_last = spec_pa.spec;
-        }
         MVC_HIP(hipEventSynchronize(rs_ev));
       } else {
         MVC_HIP(hipStreamSynchronize(stream));
@@ -2745,8 +2674,6 @@ class ParallelSampler : public Sampler {
       rounds = std::min(rounds * 4, 1024);
     }
     const bool moved = rs_host->moves > 0;
-    // the last round's speculative phase A is the next sweep's iff nothing moved
-    spec_pending = spec_last && !moved;
     if (moved) {
       hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, Q, c.pos_new, c.jmap);
       hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
@@ -2844,7 +2771,7 @@ class ParallelSampler : public Sampler {
     for (int it = 0; it < n_sweeps; ++it) {
       hipEvent_t ev = nullptr;
       timers.begin("sweep", &ev);
-      for (auto &c : chains) sweep_chain(c, (uint32_t)sweeps_done, it + 1 < n_sweeps);
+      for (auto &c : chains) sweep_chain(c, (uint32_t)sweeps_done);
       timers.end("sweep", ev);
       ++sweeps_done;
     }

@@ -1529,7 +1529,8 @@ __device__ int seq_dish_draw(const SeqArgs &A, const SView &W, const Cust &C, in
 }  // namespace
 
 // Before phase A: the whole sweep is one pending window [0, n).
-__device__ __forceinline__ void seq_init_state(const SeqArgs &A) {
+extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
+  if (threadIdx.x != 0) return;
   Repair *R = A.R;
   const int V = A.P.V, n = A.P.n;
   R->cur = 0;
@@ -1554,22 +1555,6 @@ __device__ __forceinline__ void seq_init_state(const SeqArgs &A) {
   R->moves = R->births = R->newdish = R->rounds = 0;
   for (int k = 0; k < 12; ++k) R->prof[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
-}
-extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
-  if (threadIdx.x != 0) return;
-  seq_init_state(A);
-}
-// The next sweep's start, enqueued before the host has read this sweep's
-// repair outcome (speculation): gate = 1 iff the repair is
-// done with no move (the state the next sweep was enqueued for), and then the
-// repair cursor is reset as mvc_seq_init_kernel does; the next sweep's phase-A
-// kernels return at once when gate = 0.
-extern "C" __global__ void mvc_seq_spec_init_kernel(SeqArgs A, int32_t *gate) {
-  if (threadIdx.x != 0) return;
-  const Repair *R = A.R;
-  const int ok = (R->done && R->moves == 0 && R->overflow == 0 && R->restride == 0) ? 1 : 0;
-  *gate = ok;
-  if (ok) seq_init_state(A);
 }
 
 // After phase A: the first customer whose choice is not its own table.

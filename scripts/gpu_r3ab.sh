@@ -12,15 +12,6 @@ import json;d=json.load(open('gpurun_out/bench_r3ab.json'));print('headline',d['
 e=d['extra']
 for k in ('north_star_literal_gpu','north_star_literal_gpu_16chains','cold_start_gpu','configs1_gpu','exact_schedule_gpu'): print(k, json.dumps(e.get(k))[:300])
 print('newsim', json.dumps(e.get('newsim_call'))[:1200])"
-for z in 1 0 1 0; do
-  MVC_SPEC=$z timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-extras --steps 30 > gpurun_out/bench_r3ab_spec$z.json 2>/dev/null \
-    || { echo "bench spec=$z failed"; exit 1; }
-  python -c "import json;d=json.load(open('gpurun_out/bench_r3ab_spec$z.json'));print('spec=$z',d['value'],d['ms_per_step'],d['hbm']['pass_ms'])"
-done
-MVC_SPEC=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread \
-    -k "golden or live_oracle or config4_full or chains or repair or capacity or sweeps_per_call or posterior" > gpurun_out/pytest_r3ab_spec.log 2>&1 \
-    || { echo "spec tests failed"; grep -E "FAILED|Error" gpurun_out/pytest_r3ab_spec.log | tail; exit 1; }
-tail -1 gpurun_out/pytest_r3ab_spec.log
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r3ab -o run --output-format csv -- \
     python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-extras > gpurun_out/prof_r3ab.log 2>&1 \

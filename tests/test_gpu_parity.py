@@ -471,16 +471,13 @@ def test_phase_a_vs_oracle(n, V, D, K, T):
     s2.close()
 
 
-@pytest.mark.parametrize("spec", ["1", "0"])
 @pytest.mark.parametrize("warm", [False, True])
-def test_parallel_sweeps_per_call(warm, spec, monkeypatch):
-    """Sampler.sweep(k) (the next sweep's phase A speculated behind each
-    repair) equals k calls of sweep(1): a cold start (moves,
-    births, capacity growth: the speculations are discarded) and a warm start
-    (no moves: they are used), and the warm chain equals the oracle."""
+def test_parallel_sweeps_per_call(warm):
+    """Sampler.sweep(k) equals k calls of sweep(1): a cold start (moves,
+    births, capacity growth) and a warm start, and the warm chain equals the
+    oracle."""
     m = _mvc()
     from mvc_amd import data
-    monkeypatch.setenv("MVC_SPEC", spec)
     y, z = data.synthetic(5000, 4, 128, 64, seed=77)
     st = None
     if warm:
