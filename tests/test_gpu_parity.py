@@ -145,29 +145,6 @@ def test_exact_many_chains_vs_live_oracle():
         _compare(g, ref)
 
 
-@pytest.mark.parametrize("cap", [(256, 128), (8, 4)])
-def test_exact_sweeps_per_launch(cap):
-    """Several sweeps in one kernel launch (Sampler.sweep(k)) equal k calls
-    of one sweep, with and without capacity growth inside the launch."""
-    m = _mvc()
-    from mvc_amd import data
-    y, _ = data.config1(1, n=600)
-    a = m.Sampler(y, seed=7, mode="exact", n_chains=3, table_cap=cap[0], dish_cap=cap[1])
-    b = m.Sampler(y, seed=7, mode="exact", n_chains=3, table_cap=cap[0], dish_cap=cap[1])
-    for k in (1, 2, 5, 11):
-        a.sweep(k)
-        for _ in range(k):
-            b.sweep(1)
-        for c in range(3):
-            ta, da, ha = a.state(c)
-            tb, db, hb = b.state(c)
-            assert np.array_equal(ta, tb), (k, c)
-            assert np.array_equal(da, db), (k, c)
-            assert ha["alpha_global"] == hb["alpha_global"], (k, c)
-    a.close()
-    b.close()
-
-
 def test_exact_capacity_growth():
     """Tiny initial capacities force the overflow -> regrow -> resume path."""
     m = _mvc()
@@ -469,44 +446,6 @@ def test_phase_a_vs_oracle(n, V, D, K, T):
     assert np.array_equal(s.state()[0], s2.state()[0])
     s.close()
     s2.close()
-
-
-@pytest.mark.parametrize("warm", [False, True])
-def test_parallel_sweeps_per_call(warm):
-    """Sampler.sweep(k) equals k calls of sweep(1): a cold start (moves,
-    births, capacity growth) and a warm start, and the warm chain equals the
-    oracle."""
-    m = _mvc()
-    from mvc_amd import data
-    y, z = data.synthetic(5000, 4, 128, 64, seed=77)
-    st = None
-    if warm:
-        uniq, table_of = np.unique(z, return_inverse=True)
-        T = uniq.size
-        dish = np.stack([np.arange(T) % max(1, 64 // (2 ** v)) for v in range(4)]).astype(np.int32)
-        st = (table_of.astype(np.int32), dish, np.array([1.69] * 4 + [1.0] * 4 + [0.5] * 4 + [1.0, 0.6]))
-    caps = {} if warm else dict(table_cap=16, dish_cap=8)   # cold: growth inside sweep(k)
-    a = m.Sampler(y, seed=21, mode="parallel", **caps)
-    b = m.Sampler(y, seed=21, mode="parallel", **caps)
-    if st is not None:
-        a.set_state(*st)
-        b.set_state(*st)
-    for k in (1, 3, 4):
-        a.sweep(k)
-        for _ in range(k):
-            b.sweep(1)
-        ta, da, ha = a.state()
-        tb, db, hb = b.state()
-        assert np.array_equal(ta, tb), k
-        assert np.array_equal(da, db), k
-        assert ha["sigma_global"] == hb["sigma_global"], k
-    if warm:
-        ref = O.run(y, 8, 0, 1, seed=21, mode=O.PARALLEL, state=st)
-        t, d, h = a.state()
-        assert np.array_equal(t, ref["table_of"][7])
-        assert np.array_equal(d, ref["dish_of"][7])
-    a.close()
-    b.close()
 
 
 def test_exact_warm_start():
@@ -916,3 +855,65 @@ def test_value_prediction_same_chain(V, D, K, vp, monkeypatch, capfd):
         assert steps > 0, "value prediction did not run"
     else:
         assert steps == 0
+
+
+# ------------------------------------------------ several sweeps per call
+@pytest.mark.parametrize("cap", [(256, 128), (8, 4)])
+def test_exact_sweeps_per_launch(cap):
+    """Several sweeps in one kernel launch (Sampler.sweep(k)) equal k calls
+    of one sweep, with and without capacity growth inside the launch."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.config1(1, n=600)
+    a = m.Sampler(y, seed=7, mode="exact", n_chains=3, table_cap=cap[0], dish_cap=cap[1])
+    b = m.Sampler(y, seed=7, mode="exact", n_chains=3, table_cap=cap[0], dish_cap=cap[1])
+    for k in (1, 2, 5, 11):
+        a.sweep(k)
+        for _ in range(k):
+            b.sweep(1)
+        for c in range(3):
+            ta, da, ha = a.state(c)
+            tb, db, hb = b.state(c)
+            assert np.array_equal(ta, tb), (k, c)
+            assert np.array_equal(da, db), (k, c)
+            assert ha["alpha_global"] == hb["alpha_global"], (k, c)
+    a.close()
+    b.close()
+
+
+@pytest.mark.parametrize("warm", [False, True])
+def test_parallel_sweeps_per_call(warm):
+    """Sampler.sweep(k) equals k calls of sweep(1): a cold start (moves,
+    births, capacity growth) and a warm start, and the warm chain equals the
+    oracle."""
+    m = _mvc()
+    from mvc_amd import data
+    y, z = data.synthetic(5000, 4, 128, 64, seed=77)
+    st = None
+    if warm:
+        uniq, table_of = np.unique(z, return_inverse=True)
+        T = uniq.size
+        dish = np.stack([np.arange(T) % max(1, 64 // (2 ** v)) for v in range(4)]).astype(np.int32)
+        st = (table_of.astype(np.int32), dish, np.array([1.69] * 4 + [1.0] * 4 + [0.5] * 4 + [1.0, 0.6]))
+    caps = {} if warm else dict(table_cap=16, dish_cap=8)   # cold: growth inside sweep(k)
+    a = m.Sampler(y, seed=21, mode="parallel", **caps)
+    b = m.Sampler(y, seed=21, mode="parallel", **caps)
+    if st is not None:
+        a.set_state(*st)
+        b.set_state(*st)
+    for k in (1, 3, 4):
+        a.sweep(k)
+        for _ in range(k):
+            b.sweep(1)
+        ta, da, ha = a.state()
+        tb, db, hb = b.state()
+        assert np.array_equal(ta, tb), k
+        assert np.array_equal(da, db), k
+        assert ha["sigma_global"] == hb["sigma_global"], k
+    if warm:
+        ref = O.run(y, 8, 0, 1, seed=21, mode=O.PARALLEL, state=st)
+        t, d, h = a.state()
+        assert np.array_equal(t, ref["table_of"][7])
+        assert np.array_equal(d, ref["dish_of"][7])
+    a.close()
+    b.close()
