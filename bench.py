@@ -320,18 +320,42 @@ def newsim_chains_line(seed, device):
     return out
 
 
-CHILD_LEGS = {"ns16": lambda seed, dev: gpu_chains_line("ns", seed, dev), "newsim_chains": newsim_chains_line}
+CHILD_LEGS = {
+    # name: (function(seed, device) -> dict, needs many hardware queues)
+    "north_star_literal_gpu": (lambda seed, dev: gpu_line("ns", seed, dev, 1, 0), False),
+    "north_star_literal_gpu_16chains": (lambda seed, dev: gpu_chains_line("ns", seed, dev), True),
+    "configs1_gpu": (lambda seed, dev: gpu_line("c2", seed, dev), False),
+    "configs4_full_gpu": (lambda seed, dev: config5_line(seed, dev), False),
+    "exact_schedule_gpu": (lambda seed, dev: gpu_exact_line(seed, dev), False),
+    "newsim_call": (lambda seed, dev: newsim_call_line(seed, dev), False),
+    "newsim_chains": (lambda seed, dev: newsim_chains_line(seed, dev), True),
+    "cold_start_gpu": (lambda seed, dev: cold_start(seed, dev), False),
+}
 
 
-def child_leg(name, seed, device, timeout=600):
-    """Run CHILD_LEGS[name] in a child process (its own HIP runtime, 32 hardware queues)."""
+def child_leg(name, seed, device, timeout=300):
+    """Run CHILD_LEGS[name] in a child process (its own HIP runtime; 32
+    hardware queues for the multi-chain legs).  Never raises: a leg that
+    fails, faults or times out is recorded as {"error": ...}, so no extra
+    leg can take the headline line with it."""
     import subprocess
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=HW_QUEUES_MULTI)
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--leg", name, "--seed", str(seed),
-                        "--leg-device", str(device)], env=env, capture_output=True, text=True, timeout=timeout)
+    env = dict(os.environ)
+    if CHILD_LEGS[name][1]:
+        env["GPU_MAX_HW_QUEUES"] = HW_QUEUES_MULTI
+    t = time.perf_counter()
+    try:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--leg", name, "--seed", str(seed),
+                            "--leg-device", str(device)], env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout} s"}
+    finally:
+        print(f"bench: {name} {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
     if r.returncode != 0:
-        raise RuntimeError(f"bench leg {name} failed ({r.returncode}): {r.stderr[-2000:]}")
-    return json.loads(r.stdout.strip().splitlines()[-1])
+        return {"error": f"exit {r.returncode}: {r.stderr.strip()[-600:]}"}
+    try:
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return {"error": "no JSON line from the leg: " + r.stdout[-300:]}
 
 
 def newsim_call_cpu(seed, M_short=2000):
@@ -374,7 +398,7 @@ def cold_start(seed, device, sweeps=4):
 def main():
     args = parse()
     if args.leg:   # a child_leg process: one multi-chain leg, one JSON line
-        print(json.dumps(CHILD_LEGS[args.leg](args.seed, args.leg_device)), flush=True)
+        print(json.dumps(CHILD_LEGS[args.leg][0](args.seed, args.leg_device)), flush=True)
         return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -526,46 +550,49 @@ def main():
         "data_gen_s": round(t_gen, 2),
     }
     def leg(name, fn, *a):
+        """A host-side leg (CPU only); an exception is recorded, not raised."""
         t = time.perf_counter()
-        r = fn(*a)
+        try:
+            r = fn(*a)
+        except Exception as e:   # noqa: BLE001 -- the headline must survive any extra
+            r = {"error": f"{type(e).__name__}: {e}"[:600]}
         print(f"bench: {name} {time.perf_counter() - t:.1f} s", file=sys.stderr, flush=True)
         return r
 
-    if world == 1 and not args.no_extras:
-        # other BASELINE configs and schedules, after the timed region (rank 0, N = 1)
-        out["extra"] = {
-            # D = 1: ~65% of customers move every sweep (1-D clusters overlap), so
-            # the in-order repair dominates; one sweep (~15 s) is timed
-            "north_star_literal_gpu": leg("north_star_literal_gpu", gpu_line, "ns", args.seed, local, 1, 0),
-            # the same with 16 chains at once (compare reference_schedule_cpu: one chain per core)
-            "north_star_literal_gpu_16chains": leg("north_star_literal_gpu_16chains", child_leg, "ns16",
-                                                   args.seed, local),
-            "configs1_gpu": leg("configs1_gpu", gpu_line, "c2", args.seed, local),
-            "configs4_full_gpu": leg("configs4_full_gpu", config5_line, args.seed, local),
-            "exact_schedule_gpu": leg("exact_schedule_gpu", gpu_exact_line, args.seed, local),
-            "newsim_call": {**leg("newsim_call", newsim_call_line, args.seed, local),
-                            **leg("newsim_chains", child_leg, "newsim_chains", args.seed, local)},
-            "cold_start_gpu": leg("cold_start_gpu", cold_start, args.seed, local),
-        }
-        if not args.no_cpu_baseline:
-            out["extra"]["reference_schedule_cpu"] = leg("reference_schedule_cpu", reference_schedule_cpu, args.seed)
-            out["extra"]["newsim_call"]["reference_cpu_1core"] = leg("newsim_call_cpu", newsim_call_cpu, args.seed)
-            # the chains' comparator: min(chains, nproc) host cores, one chain each
-            ch = out["extra"]["north_star_literal_gpu_16chains"]
-            cores = min(ch["chains"], os.cpu_count() or 1)
-            ref1 = out["extra"]["reference_schedule_cpu"]["value"]
-            ch["cpu_cores_compared"] = cores
-            ch["reference_cpu_same_cores"] = round(cores * ref1, 3)
-            ch["vs_reference_cpu_same_cores"] = round(ch["value"] / (cores * ref1), 3)
-            ns = out["extra"]["newsim_call"]
-            r1 = ns["reference_cpu_1core"]["sweeps_per_s"]
-            for key in ("parallel_gpu_16chains", "exact_gpu_2048chains", "exact_gpu_2048chains_sweeps_only"):
-                if key in ns:
-                    cores = min(ns[key]["chains"], os.cpu_count() or 1)
-                    ns[key]["cpu_cores_compared"] = cores
-                    ns[key]["vs_reference_cpu_same_cores"] = round(ns[key]["chain_sweeps_per_s"] / (cores * r1), 3)
+    # the headline's CPU baseline first (host only), then the extras
     if world == 1 and not args.no_cpu_baseline and y is not None:
         out["cpu_baseline"] = leg("cpu_baseline", cpu_baseline, y, z, V, K, D, args.seed)
+    if world == 1 and not args.no_extras:
+        # other BASELINE configs and schedules, after the timed region (rank 0,
+        # N = 1), each GPU leg in its own process so that no failure there can
+        # reach this process's line
+        ex = out["extra"] = {}
+        for name in CHILD_LEGS:
+            if name == "newsim_chains":
+                continue
+            ex[name] = child_leg(name, args.seed, local)
+        ex["newsim_call"] = {**ex.get("newsim_call", {}), "chains": child_leg("newsim_chains", args.seed, local)}
+        if not args.no_cpu_baseline:
+            ex["reference_schedule_cpu"] = leg("reference_schedule_cpu", reference_schedule_cpu, args.seed)
+            ex["newsim_call"]["reference_cpu_1core"] = leg("newsim_call_cpu", newsim_call_cpu, args.seed)
+            try:   # the chains' comparator: min(chains, nproc) host cores, one chain each (SURVEY §8d)
+                ch = ex["north_star_literal_gpu_16chains"]
+                ref1 = ex["reference_schedule_cpu"]["value"]
+                cores = min(ch["chains"], os.cpu_count() or 1)
+                ch["cpu_cores_compared"] = cores
+                ch["reference_cpu_same_cores"] = round(cores * ref1, 3)
+                ch["vs_reference_cpu_same_cores"] = round(ch["value"] / (cores * ref1), 3)
+            except (KeyError, TypeError):
+                pass
+            try:
+                r1 = ex["newsim_call"]["reference_cpu_1core"]["sweeps_per_s"]
+                for key, row in ex["newsim_call"]["chains"].items():
+                    if isinstance(row, dict) and "chains" in row:
+                        cores = min(row["chains"], os.cpu_count() or 1)
+                        row["cpu_cores_compared"] = cores
+                        row["vs_reference_cpu_same_cores"] = round(row["chain_sweeps_per_s"] / (cores * r1), 3)
+            except (KeyError, TypeError):
+                pass
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

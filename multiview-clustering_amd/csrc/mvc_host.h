@@ -20,12 +20,30 @@ struct Error : std::runtime_error {
   Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
 };
 
-#define MVC_HIP(expr)                                                                  \
-  do {                                                                                 \
-    hipError_t _e = (expr);                                                            \
-    if (_e != hipSuccess)                                                              \
-      throw ::mvc::Error(MVC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+#define MVC_STR2(x) #x
+#define MVC_STR(x) MVC_STR2(x)
+#define MVC_HIP(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t _e = (expr);                                                                            \
+    if (_e != hipSuccess)                                                                              \
+      throw ::mvc::Error(MVC_ERR_HIP, std::string(#expr) + " [" + ::mvc::base_name(__FILE__) +          \
+                                          ":" MVC_STR(__LINE__) "]: " + hipGetErrorString(_e));        \
   } while (0)
+inline const char *base_name(const char *p) {
+  const char *b = p;
+  for (; *p; ++p)
+    if (*p == '/') b = p + 1;
+  return b;
+}
+
+// Diagnostics switches, read once from the environment:
+//   MVC_POISON=<byte>  every device allocation of the samplers is filled with
+//                      that byte (uninitialised reads become deterministic);
+//   MVC_DEBUG_SYNC=1   the parallel sampler synchronises its stream after each
+//                      launch and names the kernel in the error (a fault is
+//                      attributed to the launch that caused it).
+int poison_byte();      // -1: off
+bool debug_sync();
 
 // Initial state draws of multiview_gibbs.cpp:12-62 on the sequential Philox
 // stream (shared by both schedules), plus tau_v of :78-94.

@@ -1,25 +1,22 @@
-// mvc_parallel.hip — the parallel ("mode P") sweep on gfx950.
+// mvc_parallel.hip — the parallel ("mode P") execution of the reference's
+// sequential sweep on gfx950.
 //
-// Per sweep (one stream, one host synchronisation after the commit):
-//   phase 1   : every customer draws its table against the state frozen at
-//               sweep start (virtual self-removal), in two kernels per batch:
-//               an lp producer (per-view MFMA kernel mvc_par_lpview_kernel,
-//               or the generic mvc_par_lpgen_kernel) writes lp of every
-//               (customer, dish) to the lp buffer; the draw kernel
-//               mvc_par_zdraw_kernel (one lane per customer) reduces it in
-//               dish / table order and draws with the Philox counter
-//               (chain, sweep, customer).
-//   births    : customers that chose a new table, resolved in customer order
-//               on one wavefront (tree64 reductions).
-//   commit    : survivors + births -> dense positions, live-dish lists,
-//               counts (integer atomics: order independent).
-//   stats     : S1/S2 rebuilt in a fixed chunked order (bit-reproducible).
+// Per sweep (one stream; the host reads the repair's outcome once per batch):
+//   phase A   : every customer draws its table against the sweep-start state
+//               (virtual self-removal), two kernels per batch: an lp producer
+//               (MFMA: mvc_par_lpall_kernel / lpview / lpbig; generic:
+//               lpgen) writes lp of every (customer, dish) to the lp buffer,
+//               the draw kernel (one lane per customer) reduces it in dish /
+//               table order and draws with the Philox counter (customer,
+//               sweep, chain);
+//   repair    : the in-order repair of mvc_repair.h (the decisions after the
+//               first mover, re-evaluated against the moved state);
+//   compaction: dead tables / dishes dropped (only after a sweep with moves);
 //   hyper     : one workgroup: ||S1||^2, the MH updates of
-//               multiview_hyper.cpp:233-292 (EPPF sums via lgamma + size
-//               histograms, tree64 order), then next sweep's coefficients.
-// Every fp64 expression matches ParallelSampler in oracle/mvc_oracle.cpp.
+//               multiview_hyper.cpp:233-292 (closed-form EPPF, tree64
+//               order), then the next sweep's coefficients.
+// Every fp64 expression matches SeqSampler in oracle/mvc_oracle.cpp.
 // Compile with -ffp-contract=off.
-#include <hipcub/hipcub.hpp>
 
 #include "mvc_internal.h"
 
@@ -185,27 +182,21 @@ __device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2
 #pragma unroll
       for (int t = 0; t < 2 * NT; ++t) bc[t] = bn[t];
     }
-    if (false)
-#endif
+#else   // MVC_BPIPE_OFF (tuning builds): B-fragments read at their k-step
 #pragma unroll
     for (int q = 0; q < SPPT; ++q) {
       const int u = q % RP;
       const mvc_d2 a = ring[u];
       ring[u] = (q + RP < SPPT) ? cur[(q + RP) * 64] : nxt[(q + RP - SPPT) * 64];
       const double *bk = Bl + (size_t)(2 * q) * NT * 64;
-#ifdef FZ_ABL_MFMA
-      asm volatile("" :: "v"(a));
-      if (false)
-#endif
-      {
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bk[t * 64], acc[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bk[(NT + t) * 64], acc[t], 0, 0, 0);
-      }
       __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
     }
+#endif
   } else {
     for (int s0 = 0; s0 < SPP; s0 += RP) {
 #pragma unroll
@@ -1758,10 +1749,27 @@ constexpr size_t kSeqLdsBudget = 150 * 1024;   // run kernel: per-wave LDS scrat
 template <class Tp>
 Tp *dmalloc(size_t count) {
   void *p = nullptr;
-  MVC_HIP(hipMalloc(&p, sizeof(Tp) * std::max<size_t>(count, 1)));
+  const size_t bytes = sizeof(Tp) * std::max<size_t>(count, 1);
+  MVC_HIP(hipMalloc(&p, bytes));
+  if (poison_byte() >= 0) MVC_HIP(hipMemset(p, poison_byte(), bytes));
   return (Tp *)p;
 }
 }  // namespace
+
+int poison_byte() {
+  static const int b = [] {
+    const char *e = getenv("MVC_POISON");
+    return (e && e[0]) ? (int)(strtol(e, nullptr, 0) & 0xFF) : -1;
+  }();
+  return b;
+}
+bool debug_sync() {
+  static const bool on = [] {
+    const char *e = getenv("MVC_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 class ParallelSampler : public Sampler {
  public:
@@ -1832,6 +1840,17 @@ class ParallelSampler : public Sampler {
   bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
   bool vp_stats = false;          // MVC_VP_STATS=1
 
+  // MVC_DEBUG_SYNC=1: wait for the launch just made and name it in the error
+  void dbg(const char *what, const Chain &c, uint32_t s) {
+    if (!debug_sync()) return;
+    hipError_t e = hipStreamSynchronize(stream);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess)
+      throw Error(MVC_ERR_HIP, std::string("debug sync after ") + what + " (chain " + std::to_string(c.gid) +
+                                   ", sweep " + std::to_string(s) + ", T " + std::to_string(c.T) +
+                                   "): " + hipGetErrorString(e));
+  }
+
   template <class Tp>
   Tp *own(Chain &c, size_t count) {
     Tp *p = dmalloc<Tp>(count);
@@ -1869,14 +1888,15 @@ class ParallelSampler : public Sampler {
     KC = std::min(kParKC, std::max(15, cf.dish_cap > 0 ? cf.dish_cap : 1023));
     nchunk = (n + 4095) / 4096;
     if (V > MVC_MAXV) throw Error(MVC_ERR_UNSUPPORTED, "at most 64 views");
+    MVC_HIP(hipSetDevice(cf.device));
     {   // the sweep loop waits on the device once per sweep (new T, K): spin
-        // instead of yielding so the GPU idles as briefly as possible.  Only
-        // possible before the device's context exists; otherwise left as is.
+        // instead of yielding so the GPU idles as briefly as possible.  The
+        // flag applies to the current device (set just above), and only
+        // before that device's context exists; otherwise it is left as is.
       const char *e = getenv("MVC_SPIN");
       if (!(e && e[0] == '0')) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
       (void)hipGetLastError();
     }
-    MVC_HIP(hipSetDevice(cf.device));
     MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     timers.stream = stream;
     timers.on = (cf.flags & MVC_FLAG_TIMING) != 0;
@@ -2265,6 +2285,7 @@ class ParallelSampler : public Sampler {
     timers.begin("hyper", &ev);
     hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(kHypThreads), 0, stream, A);
     MVC_HIP(hipGetLastError());
+    if (!gate) dbg("hyper", c, sweep_ix);   // (the gated launch runs behind the outcome copy: synced by its caller)
     timers.end("hyper", ev);
   }
 
@@ -2380,6 +2401,7 @@ class ParallelSampler : public Sampler {
     const SeqArgs Q0 = make_seq(c, s);
     hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
     MVC_HIP(hipGetLastError());
+    dbg("seq_init", c, s);
     hipEvent_t e0 = nullptr;
     // phase 1 in customer batches: lp producer (MFMA or generic), then draw
     int Kmax = 0, Kmin = 1 << 30;
@@ -2486,6 +2508,7 @@ class ParallelSampler : public Sampler {
                            (int)b0, nb, lpb);
       }
       MVC_HIP(hipGetLastError());
+      dbg("lp producer", c, s);
       timers.end("lp", el);
       timers.begin("draw", &ed);
       const dim3 zg((nb + 255) / 256);   // the register kernel takes one customer per thread
@@ -2515,6 +2538,7 @@ class ParallelSampler : public Sampler {
                              zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb, zsc);
       }
       MVC_HIP(hipGetLastError());
+      dbg("z draw", c, s);
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
@@ -2620,6 +2644,7 @@ class ParallelSampler : public Sampler {
     else
       hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
     MVC_HIP(hipGetLastError());
+    dbg("seq_first / eval", c, s);
     bool vp_ok = true;   // value prediction until it stops itself in this sweep (R->vpoff)
     SeqLds L = run_layout(c.T, c.K.data(), vp_ok);
     // the gated early MH (below) only where no per-phase timers bracket the
@@ -2639,9 +2664,16 @@ class ParallelSampler : public Sampler {
                                                    (L.lc == 2 ? (int64_t)kVpE * D : 0)))
                                    : 0,
                              stream, Q, L);
-        if (L.lc && !repair_grid_only)   // its loop leaves births pending
+        MVC_HIP(hipGetLastError());
+        dbg(repair_grid_only ? "seq_apply" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
+        if (L.lc && !repair_grid_only) {   // its loop leaves births pending
           hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, Q);
+          MVC_HIP(hipGetLastError());
+          dbg("seq_birth", c, s);
+        }
         hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
+        MVC_HIP(hipGetLastError());
+        dbg("seq_eval", c, s);
       }
       MVC_HIP(hipGetLastError());
       MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
@@ -2653,6 +2685,7 @@ class ParallelSampler : public Sampler {
         MVC_HIP(hipEventRecord(rs_ev, stream));
         launch_hyper(c, 1, s, c.R);
         MVC_HIP(hipEventSynchronize(rs_ev));
+        dbg("gated hyper", c, s);
       } else {
         MVC_HIP(hipStreamSynchronize(stream));
       }
@@ -2679,6 +2712,7 @@ class ParallelSampler : public Sampler {
       hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
                          stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
       MVC_HIP(hipGetLastError());
+      dbg("seq_compact + relabel", c, s);
     }
     timers.end("repair", e1);
 #ifdef MVC_RUN_PROF

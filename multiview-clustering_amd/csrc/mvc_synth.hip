@@ -53,17 +53,20 @@ extern "C" __global__ void mvc_synth_mu_kernel(int V, int K, int D, double mu_sd
 }
 
 // One thread per (view, customer) row, d ascending: the row's values, its Y2
-// fma chain, and per-d wave sums of y and y^2 added into the block's LDS
-// accumulators (order-free: they only seed tau_v, see the file header).
-constexpr int kSynThreads = 256;
+// fma chain, and per-d wave sums of y and y^2.  Each wave accumulates into
+// its own LDS slot in row order, and the block combines the slots in wave
+// order at the end, so the column sums (and the tau_v they seed) are the
+// same bits on every run.
+constexpr int kSynThreads = 256, kSynWaves = kSynThreads / 64;
 extern "C" __global__ __launch_bounds__(kSynThreads) void mvc_synth_y_kernel(int n, int D, int K, double sd,
                                                                              uint64_t seed, const double *mu,
                                                                              double *y, double *Y2, int32_t *z,
                                                                              double *colpart) {
-  extern __shared__ double s_col[];   // [2 D]: sum y, sum y^2 of this block's rows, per d
-  const int v = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  extern __shared__ double s_col[];   // [kSynWaves][2 D]: each wave's sum y, sum y^2 per d
+  const int v = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int Kv = max(1, K >> v);
-  for (int d = tid; d < 2 * D; d += blockDim.x) s_col[d] = 0.0;
+  double *my = s_col + (size_t)w * 2 * D;
+  for (int d = tid; d < kSynWaves * 2 * D; d += blockDim.x) s_col[d] = 0.0;
   __syncthreads();
   const int64_t nblk = gridDim.x;
   for (int64_t r0 = (int64_t)blockIdx.x * kSynThreads; r0 < n; r0 += nblk * kSynThreads) {
@@ -79,16 +82,20 @@ extern "C" __global__ __launch_bounds__(kSynThreads) void mvc_synth_y_kernel(int
       if (ok) row[d] = x;
       acc = __builtin_fma(x, x, acc);
       const double s1 = wave_tree_sum(x), s2 = wave_tree_sum(x * x);
-      if (lane == 0) {
-        atomicAdd(&s_col[d], s1);
-        atomicAdd(&s_col[D + d], s2);
+      if (lane == 0) {   // this wave's slot only: a fixed order of additions
+        my[d] += s1;
+        my[D + d] += s2;
       }
     }
     if (ok) Y2[(size_t)v * n + i] = acc;
   }
   __syncthreads();
   double *out = colpart + ((size_t)v * gridDim.x + blockIdx.x) * 2 * D;
-  for (int d = tid; d < 2 * D; d += blockDim.x) out[d] = s_col[d];
+  for (int d = tid; d < 2 * D; d += blockDim.x) {
+    double acc = s_col[d];
+    for (int q = 1; q < kSynWaves; ++q) acc += s_col[(size_t)q * 2 * D + d];
+    out[d] = acc;
+  }
 }
 
 extern "C" __global__ void mvc_gather_rows_kernel(int n, int D, const double *y, int view, const int32_t *idx,
@@ -108,6 +115,7 @@ DeviceData synth_device_data(int device, int n, int V, int D, int K, uint64_t se
   if (K < 1) throw Error(MVC_ERR_ARG, "synthetic data: K must be >= 1");
   if (!(sd >= 0.0) || !(mu_sd >= 0.0)) throw Error(MVC_ERR_ARG, "synthetic data: sd and mu_sd must be >= 0");
   if (V > 31) throw Error(MVC_ERR_UNSUPPORTED, "synthetic data: at most 31 views (K_v = K >> v)");
+  if (D > 1024) throw Error(MVC_ERR_UNSUPPORTED, "synthetic data: at most 1024 dims (per-wave column sums in 64 KB of LDS)");
   MVC_HIP(hipSetDevice(device));
   DeviceData DD;
   hipStream_t st = nullptr;
@@ -123,7 +131,7 @@ DeviceData synth_device_data(int device, int n, int V, int D, int K, uint64_t se
     if (z_host) MVC_HIP(hipMalloc(&zd, sizeof(int32_t) * (size_t)n));
     hipLaunchKernelGGL(mvc_synth_mu_kernel, dim3(256), dim3(256), 0, st, V, K, D, mu_sd, seed, mu);
     MVC_HIP(hipGetLastError());
-    hipLaunchKernelGGL(mvc_synth_y_kernel, dim3(grid, V), dim3(kSynThreads), sizeof(double) * 2 * D, st, n, D, K, sd,
+    hipLaunchKernelGGL(mvc_synth_y_kernel, dim3(grid, V), dim3(kSynThreads), sizeof(double) * kSynWaves * 2 * D, st, n, D, K, sd,
                        seed, (const double *)mu, DD.y, DD.Y2, zd, colpart);
     MVC_HIP(hipGetLastError());
     std::vector<double> cp((size_t)V * grid * 2 * D);

@@ -785,6 +785,28 @@ def test_run_chain_ids_and_pooled_summary(mode):
     assert np.allclose(summ["rhat"], rh, rtol=1e-10, equal_nan=True)
 
 
+@pytest.mark.parametrize("mode", ["exact", "parallel"])
+def test_run_n_devices_split(mode):
+    """mvc_run with n_devices = 2 (one host thread per device, chain c on
+    device c % 2 with global id first_chain + c): every chain equals a
+    one-chain call with that id, bit for bit, and the pooled summary covers
+    all chains.  Needs two visible GPUs (skipped on the one-GPU boxes)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(5)
+    M, burn = 20, 10
+    summ = {}
+    multi = m.run_gibbs_cpp(y, M, burn, 1, seed=7, mode=mode, n_chains=4, n_devices=2, summary=summ)
+    assert len(multi) == 4
+    for c, res in enumerate(multi):
+        one = m.run_gibbs_cpp(y, M, burn, 1, seed=7, mode=mode, first_chain=c)
+        _compare(res, one)
+    assert summ["mean"].shape == (3 * y.shape[0] + 2,)
+
+
 def test_shard_exchange_failure_leaves_the_chain_unchanged():
     """A failing all_gather (the callback returns nonzero) stops the sweep
     with MVC_ERR_CALLBACK before the exchange buffer is read: the state is

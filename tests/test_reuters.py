@@ -66,7 +66,9 @@ def test_config3_full_corpus_eight_chains_one_gpu():
     lab, _, _ = reuters.topic_truth()
     sel = lab >= 0
     sweeps = 1
-    pool = get_context("fork").Pool(2)        # the host oracle runs while the GPU sweeps
+    # the host oracle runs while the GPU sweeps, in fresh processes (a fork of
+    # this process would inherit its initialised HIP runtime)
+    pool = get_context("spawn").Pool(2)
     refs = pool.map_async(_oracle_chain, [(y, c, sweeps) for c in (0, 5)])
     s = mvc_amd.Sampler(y, seed=3, mode="parallel", n_chains=8)
     s.sweep(sweeps)
