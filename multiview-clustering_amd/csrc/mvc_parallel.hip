@@ -1763,6 +1763,16 @@ int poison_byte() {
   }();
   return b;
 }
+// MVC_LDS_FILL=<byte>: the repair run kernel fills its LDS with that byte at
+// launch (diagnostics: a read of LDS the launch never wrote becomes
+// deterministic); -1 when unset
+int lds_fill_byte() {
+  static const int b = [] {
+    const char *e = getenv("MVC_LDS_FILL");
+    return (e && e[0]) ? (int)(strtol(e, nullptr, 0) & 0xFF) : -1;
+  }();
+  return b;
+}
 bool debug_sync() {
   static const bool on = [] {
     const char *e = getenv("MVC_DEBUG_SYNC");
@@ -1840,15 +1850,79 @@ class ParallelSampler : public Sampler {
   bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
   bool vp_stats = false;          // MVC_VP_STATS=1
 
-  // MVC_DEBUG_SYNC=1: wait for the launch just made and name it in the error
-  void dbg(const char *what, const Chain &c, uint32_t s) {
+  // MVC_DEBUG_SYNC=1: wait for the launch just made and name it in the error;
+  // =2: also read the chain state back and check its invariants (z against
+  // the table counts, dish indices against the dish lists, the dish table /
+  // customer counts), naming the first launch after which one fails
+  void dbg(const char *what, const Chain &c, uint32_t s, bool rep = true) {
     if (!debug_sync()) return;
     hipError_t e = hipStreamSynchronize(stream);
     if (e == hipSuccess) e = hipGetLastError();
-    if (e != hipSuccess)
-      throw Error(MVC_ERR_HIP, std::string("debug sync after ") + what + " (chain " + std::to_string(c.gid) +
-                                   ", sweep " + std::to_string(s) + ", T " + std::to_string(c.T) +
-                                   "): " + hipGetErrorString(e));
+    const std::string where = std::string(what) + " (chain " + std::to_string(c.gid) + ", sweep " +
+                              std::to_string(s) + ", T " + std::to_string(c.T) + ")";
+    if (e != hipSuccess) throw Error(MVC_ERR_HIP, "debug sync after " + where + ": " + hipGetErrorString(e));
+    if (debug_level() >= 2) {
+      const std::string bad = check_state(c, rep);
+      if (!bad.empty()) throw Error(MVC_ERR_STATE, "state check after " + where + ": " + bad);
+    }
+  }
+  static int debug_level() {
+    static const int l = [] {
+      const char *e = getenv("MVC_DEBUG_SYNC");
+      return e ? atoi(e) : 0;
+    }();
+    return l;
+  }
+  // Invariants of a chain's state between launches:
+  // positions p < T (R->T; table slots are stable within a sweep), dishes
+  // j < Klist[v]; every customer in a table, n_t = members, d_l = live tables
+  // per dish, d_n = customers per dish.  Empty string when they hold.
+  // rep: within a sweep's repair (bounds R->T, R->Klist), else between
+  // sweeps (the status row's T and Kact).
+  std::string check_state(const Chain &c, bool rep) {
+    Repair R;
+    MVC_HIP(hipMemcpy(&R, c.R, sizeof(Repair), hipMemcpyDeviceToHost));
+    std::vector<int32_t> z(n), nt(TC), dish((size_t)V * TC), dl((size_t)V * KC), dn((size_t)V * KC), st(2 * V + 4),
+        kact(V);
+    MVC_HIP(hipMemcpy(z.data(), c.P.z, 4 * z.size(), hipMemcpyDeviceToHost));
+    MVC_HIP(hipMemcpy(nt.data(), c.P.n_t, 4 * nt.size(), hipMemcpyDeviceToHost));
+    MVC_HIP(hipMemcpy(dish.data(), c.P.dish, 4 * dish.size(), hipMemcpyDeviceToHost));
+    MVC_HIP(hipMemcpy(dl.data(), c.P.d_l, 4 * dl.size(), hipMemcpyDeviceToHost));
+    MVC_HIP(hipMemcpy(dn.data(), c.P.d_n, 4 * dn.size(), hipMemcpyDeviceToHost));
+    MVC_HIP(hipMemcpy(st.data(), c.status, 4 * st.size(), hipMemcpyDeviceToHost));
+    MVC_HIP(hipMemcpy(kact.data(), c.P.Kact, 4 * kact.size(), hipMemcpyDeviceToHost));
+    const int T = rep ? R.T : st[0];
+    std::vector<int> K(V);
+    for (int v = 0; v < V; ++v) K[v] = rep ? R.Klist[v] : kact[v];
+    auto msg = [](const std::string &a, long long x, long long y, long long w) {
+      return a + " " + std::to_string(x) + " " + std::to_string(y) + " " + std::to_string(w);
+    };
+    if (T < 1 || T > TC) return msg("T out of range (T, TC, -)", T, TC, 0);
+    for (int v = 0; v < V; ++v)
+      if (K[v] < 1 || K[v] > KC) return msg("K out of range (v, K, KC)", v, K[v], KC);
+    std::vector<int64_t> cnt(T, 0);
+    for (int i = 0; i < n; ++i) {
+      if (z[i] < 0 || z[i] >= T) return msg("z out of range (i, z, T)", i, z[i], T);
+      cnt[z[i]]++;
+    }
+    for (int p = 0; p < T; ++p)
+      if (cnt[p] != nt[p]) return msg("n_t != members (p, n_t, members)", p, nt[p], cnt[p]);
+    for (int v = 0; v < V; ++v) {
+      std::vector<int64_t> l(K[v], 0), m(K[v], 0);
+      for (int p = 0; p < T; ++p) {
+        if (nt[p] <= 0) continue;
+        const int j = dish[(size_t)v * TC + p];
+        if (j < 0 || j >= K[v]) return msg("dish out of range (v, p, j)", v, p, j);
+        l[j]++;
+        m[j] += nt[p];
+      }
+      for (int j = 0; j < K[v]; ++j) {
+        if (l[j] != dl[(size_t)v * KC + j]) return msg("d_l != live tables (v, j, d_l)", v, j, dl[(size_t)v * KC + j]);
+        if (m[j] != dn[(size_t)v * KC + j]) return msg("d_n != customers (v, j, d_n)", v, j, dn[(size_t)v * KC + j]);
+      }
+    }
+    if (rep && (R.cur < 0 || R.cur > n)) return msg("repair cursor out of range (cur, n, -)", R.cur, n, 0);
+    return "";
   }
 
   template <class Tp>
@@ -2285,7 +2359,7 @@ class ParallelSampler : public Sampler {
     timers.begin("hyper", &ev);
     hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(kHypThreads), 0, stream, A);
     MVC_HIP(hipGetLastError());
-    if (!gate) dbg("hyper", c, sweep_ix);   // (the gated launch runs behind the outcome copy: synced by its caller)
+    if (!gate) dbg("hyper", c, sweep_ix, false);   // (the gated launch runs behind the outcome copy: synced by its caller)
     timers.end("hyper", ev);
   }
 
@@ -2508,7 +2582,7 @@ class ParallelSampler : public Sampler {
                            (int)b0, nb, lpb);
       }
       MVC_HIP(hipGetLastError());
-      dbg("lp producer", c, s);
+      dbg("lp producer", c, s, false);
       timers.end("lp", el);
       timers.begin("draw", &ed);
       const dim3 zg((nb + 255) / 256);   // the register kernel takes one customer per thread
@@ -2538,7 +2612,7 @@ class ParallelSampler : public Sampler {
                              zdraw_shared_bytes(V, c.T, sk), stream, A, (int)b0, nb, (const double *)lpb, zsc);
       }
       MVC_HIP(hipGetLastError());
-      dbg("z draw", c, s);
+      dbg("z draw", c, s, false);
       timers.end("draw", ed);
     }
     timers.end("zresample", e0);
@@ -2637,7 +2711,8 @@ class ParallelSampler : public Sampler {
     hipEvent_t e1 = nullptr;
     timers.begin("repair", &e1);
     SeqArgs Q = make_seq(c, s);
-    const dim3 eg(seq_waves / 4), eb(256);
+    dim3 eg(seq_waves / 4);   // the eval grid: one wave per scratch slot (re-read after a capacity growth)
+    const dim3 eb(256);
     if (phaseA)
       hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
                          stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
@@ -2656,14 +2731,15 @@ class ParallelSampler : public Sampler {
       for (int r = 0; r < rounds; ++r) {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
-        else
+        else {
+          L.dyn = L.lds ? 8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D) +
+                               (L.lc == 2 ? (int64_t)kVpE * D : 0))
+                        : 0;
+          L.fill = lds_fill_byte();
           hipLaunchKernelGGL(L.lc ? (L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
                                   : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
-                             dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads),
-                             L.lds ? (size_t)(8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D) +
-                                                   (L.lc == 2 ? (int64_t)kVpE * D : 0)))
-                                   : 0,
-                             stream, Q, L);
+                             dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, Q, L);
+        }
         MVC_HIP(hipGetLastError());
         dbg(repair_grid_only ? "seq_apply" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
         if (L.lc && !repair_grid_only) {   // its loop leaves births pending
@@ -2692,6 +2768,7 @@ class ParallelSampler : public Sampler {
       if (rs_host->overflow) {
         grow_capacity(rs_host->overflow);
         Q = make_seq(c, s);
+        eg = dim3(seq_waves / 4);   // the scratch may have fewer slots now
         continue;
       }
       if (rs_host->vpoff && vp_ok) {   // predictions missed (or a dish list outgrew them): plain lane columns
@@ -2712,7 +2789,7 @@ class ParallelSampler : public Sampler {
       hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
                          stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
       MVC_HIP(hipGetLastError());
-      dbg("seq_compact + relabel", c, s);
+      dbg("seq_compact + relabel", c, s, false);
     }
     timers.end("repair", e1);
 #ifdef MVC_RUN_PROF

@@ -85,6 +85,8 @@ struct SeqLds {
   int32_t tw;           // waves per customer (1: seq_resample; kSeqRunWaves: seq_resample_wide); nws customers per step
   int32_t lc;           // 1: the lane-column evaluation (seq_resample_lc; LDS layout with S1 cached, ts <= 512); 2: + value prediction
   int64_t vpo;          // lc == 2: offset (doubles) of the overlay's S1 columns [kVpE][D] in the dynamic LDS
+  int64_t dyn;          // bytes of dynamic LDS of the launch
+  int32_t fill;         // MVC_LDS_FILL diagnostics: >= 0 fills the block's LDS with this byte at launch
 };
 // ring slot: y rows [V][D], Y2 [V], z (as a double)
 __host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
@@ -2112,8 +2114,6 @@ struct RunCursor {
 
 namespace {
 
-// The run kernel's loop, for state read through the LDS cache (kLds) or the
-// global arrays.  Returns through ovf / restride why it stopped early.
 // The staged-row ring of the run kernel: slot k holds customer c with
 // c % ring == k (y rows [V][D], Y2 [V], z).
 struct Ring {
@@ -2176,10 +2176,12 @@ __device__ __forceinline__ int ring_pred(const Ring &G, int c, int V, int D) {
 }
 
 // The run kernel's loop, for state read through the LDS cache (kLds) or the
-// global arrays.  Returns through ovf / restride why it stopped early.
+// global arrays.  Returns why it stopped early: kRunOvf | kRunRestride (flags
+// by value, so nothing of the kernel lives in scratch memory).
+constexpr int kRunOvf = 1, kRunRestride = 2, kRunVpOff = 4;
 template <bool kLds, bool kWide>
-__device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
-                             const Ring &G, double *tree, RunCursor &U, int &ovf, int &restride) {
+__device__ int seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const SCache *ccp, const SeqScratch &S,
+                            const Ring &G, double *tree, RunCursor &U) {
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
@@ -2198,8 +2200,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
       if (!seq_commit(A, Wv, ccp, Ci, U.cur, U.pp0, U.pc, S.lp, tree, U.cnt,
                              kLds ? L.nws : (int)(blockDim.x >> 6), reuse ? &S0 : nullptr, lsync)) {
         // overflow: the host grows and relaunches
-        ovf = 1;
-        return;
+        return kRunOvf;
       }
       RUN_MARK(3);
       if (tid == 0) {
@@ -2222,10 +2223,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
     }
     seq_bar(lsync);
     RUN_MARK(4);
-    if (U.stop) {
-      restride = U.stop == 2;
-      return;
-    }
+    if (U.stop) return U.stop == 2 ? kRunRestride : 0;
     const int i0 = U.i;
     const int need = min(n, i0 + L.nws);
     int fill_next = 0, landed_next = 0;
@@ -2321,7 +2319,7 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 #ifdef MVC_RUN_PROF
     if (tid == 0) mvc_prof_lds[7] += 1;
 #endif
-    if (!U.go) return;
+    if (!U.go) return 0;
   }
 }
 
@@ -2339,7 +2337,8 @@ __device__ void seq_run_loop(SeqArgs &A, const SeqLds &L, const SView &Wv, const
 //     step without a commit has only one barrier, so a fast wave may write
 //     the next step's choices while a slow one still reads this step's);
 //   * every barrier waits for LDS operations only.
-__device__ __forceinline__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U, int &restride) {
+__device__ __forceinline__ int seq_run_loop_lc(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U) {
+  int flags = 0;
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
@@ -2384,7 +2383,7 @@ __device__ __forceinline__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, con
       bool bad = *cc.T >= L.ts;
       for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks;
       if (bad) {
-        restride = 1;
+        flags |= kRunRestride;
         break;
       }
     }
@@ -2482,6 +2481,7 @@ __device__ __forceinline__ void seq_run_loop_lc(SeqArgs &A, const SeqLds &L, con
     U.lastm = lastm;
     U.gapq = gapq;
   }
+  return flags;
 }
 
 // ---- value prediction: the overlay, its commit, the loop ----
@@ -2783,8 +2783,8 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
 // predictions from the overlay and a differing move the ordinary way.  Births
 // end the loop (mvc_seq_birth_kernel); so does a low hit rate (R->vpoff: the
 // lane-column loop takes the rest of the sweep).
-__device__ __forceinline__ void seq_run_loop_vp(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U, int &restride,
-                                int &vpoff) {
+__device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U) {
+  int flags = 0;
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int V = P.V, D = P.D, n = P.n;
@@ -2801,7 +2801,7 @@ __device__ __forceinline__ void seq_run_loop_vp(SeqArgs &A, const SeqLds &L, con
   int rci = -1, rp0 = 0, rc = 0;
   bool skip = false;
   if (A.R->vpoff) {   // stopped earlier in this sweep (later rounds of the batch): nothing to do
-    vpoff = 1;
+    flags |= kRunVpOff;
     skip = true;
   } else if (pend && pc < 0) {   // a birth: mvc_seq_birth_kernel
     skip = true;
@@ -2835,11 +2835,11 @@ __device__ __forceinline__ void seq_run_loop_vp(SeqArgs &A, const SeqLds &L, con
         big = big || cc.Klist[v] > 128;
       }
       if (bad) {
-        restride = 1;
+        flags |= kRunRestride;
         break;
       }
       if (big || (steps >= 128 && 2 * hits < steps)) {
-        vpoff = 1;
+        flags |= kRunVpOff;
         break;
       }
     }
@@ -2966,6 +2966,7 @@ __device__ __forceinline__ void seq_run_loop_vp(SeqArgs &A, const SeqLds &L, con
     A.R->vpsteps += steps;
     A.R->vphits += hits;
   }
+  return flags;
 }
 
 }  // namespace
@@ -2989,6 +2990,16 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
   const int tid = threadIdx.x, w = tid >> 6, nt = blockDim.x;
   const int V = P.V, D = P.D, n = P.n, KC = P.KC, TC = P.TC;
   __shared__ RunCursor U;
+  if (L.fill >= 0) {   // diagnostics: every LDS byte the launch may read, set to a known pattern first
+    const uint32_t pat = 0x01010101u * (uint32_t)L.fill;
+    uint32_t *dl = (uint32_t *)mvc_seq_lds;
+    for (int64_t k = tid; k < L.dyn / 4; k += nt) dl[k] = pat;
+    for (int k = tid; k < (int)(sizeof(mvc_seq_const) / 4); k += nt) ((uint32_t *)mvc_seq_const)[k] = pat;
+    for (int k = tid; k < (int)(sizeof(RunCursor) / 4); k += nt) ((uint32_t *)&U)[k] = pat;
+    if constexpr (kMode == 4)
+      for (int k = tid; k < (int)(sizeof(VpOv) / 4); k += nt) ((uint32_t *)&mvc_vp_ov)[k] = pat;
+    __syncthreads();
+  }
 #ifdef MVC_RUN_PROF
   if (tid < 12) mvc_prof_lds[tid] = 0;
 #endif
@@ -3032,7 +3043,7 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
     }
     return;
   }
-  int ovf = 0, restride = 0, vpoff = 0;
+  int flags = 0;   // kRunOvf | kRunRestride | kRunVpOff
   double *tree = SeqScratch(A, w).tree;   // global per-wave scratch: the dish draws' tree64 levels
   if (L.lds) {   // the state cache, from the global state at launch
     const int ts = L.ts, ks = L.ks;
@@ -3085,17 +3096,17 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
     G.slot = (int)seq_ring_slot(V, D);
     G.base = mvc_seq_lds + L.cache_dbl + (int64_t)L.nws * L.stride;
     if constexpr (kMode == 3)
-      seq_run_loop_lc(A, L, G, U, restride);
+      flags = seq_run_loop_lc(A, L, G, U);
     else if constexpr (kMode == 4)
-      seq_run_loop_vp(A, L, G, U, restride, vpoff);
+      flags = seq_run_loop_vp(A, L, G, U);
     else
-      seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
-                                SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts), G,
-                                tree, U, ovf, restride);
+      flags = seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
+                                        SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
+                                        G, tree, U);
     __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
   } else if constexpr (kMode < 3) {   // (the lane-column kernels always have the LDS layout)
     Ring G{nullptr, 0, 0};
-    seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U, ovf, restride);
+    flags = seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U);
   }
   if (tid == 0) {   // write the cursor back; open a grid window when handing over
 #ifdef MVC_RUN_PROF
@@ -3111,11 +3122,11 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
     R->newdish = U.cnt[2];
     R->lastm = U.lastm;
     R->gapq = U.gapq;
-    if (restride) R->restride = 1;
-    if (vpoff) R->vpoff = 1;
+    if (flags & kRunRestride) R->restride = 1;
+    if (flags & kRunVpOff) R->vpoff = 1;
     if (U.done && !U.pend) {
       R->done = 1;
-    } else if (!ovf && !restride && U.mode == kSeqScan && !U.pend) {
+    } else if (!(flags & (kRunOvf | kRunRestride)) && U.mode == kSeqScan && !U.pend) {
       R->win0 = U.cur;
       R->win1 = min(n, U.cur + R->W);
       R->fmin = n;
