@@ -253,11 +253,17 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
     R.T[c].push_back(T);
     hv[c].emplace_back(h, h + 3 * V + 2);
   };
-  for (int iter = 0; iter < cf.n_iter; ++iter) {
-    if (!quiet && (iter + 1) % 100 == 0)                          // gibbs.cpp:152-155
-      std::fprintf(stderr, "Iteration %d / %d\n", iter + 1, cf.n_iter);
-    S->sweep(1);
-    if (iter >= cf.burn_in && ((iter - cf.burn_in) % cf.thin == 0)) {   // gibbs.cpp:205
+  auto saved = [&](int it) { return it >= cf.burn_in && ((it - cf.burn_in) % cf.thin == 0); };   // gibbs.cpp:205
+  for (int iter0 = 0, iter = 0; iter0 < cf.n_iter; iter0 = iter + 1) {
+    // the sweeps up to the next saved one in one call (the exact schedule
+    // then runs them without a launch and read-back per sweep)
+    iter = iter0;
+    while (iter + 1 < cf.n_iter && !saved(iter)) ++iter;
+    for (int it = iter0; it <= iter; ++it)
+      if (!quiet && (it + 1) % 100 == 0)                           // gibbs.cpp:152-155
+        std::fprintf(stderr, "Iteration %d / %d\n", it + 1, cf.n_iter);
+    S->sweep(iter - iter0 + 1);
+    if (saved(iter)) {
       if (S->save_all_async(save_fn)) {                   // all chains in one snapshot (exact schedule)
         R.S++;
         continue;

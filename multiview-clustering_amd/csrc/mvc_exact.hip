@@ -57,6 +57,46 @@ struct Shared {
 };
 
 // ---------------------------------------------------------------------------
+// Sequential left-to-right sums and inverse-CDF searches in the reference's
+// order (so the same bits), with the terms loaded 8 at a time: a batch's
+// loads are in flight together instead of one dependent round trip per term.
+// ---------------------------------------------------------------------------
+template <class F>
+__device__ __forceinline__ double seq_sum8(double s, int n, F term) {
+  int j = 0;
+  for (; j + 8 <= n; j += 8) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = term(j + q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s += x[q];
+  }
+  for (; j < n; ++j) s += term(j);
+  return s;
+}
+// the first j whose running sum exceeds u, -1 if none
+template <class F>
+__device__ __forceinline__ int seq_find8(double u, int n, F term) {
+  double cum = 0.0;
+  int j = 0;
+  for (; j + 8 <= n; j += 8) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = term(j + q);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      cum += x[q];
+      if (u < cum) return j + q;
+    }
+  }
+  for (; j < n; ++j) {
+    cum += term(j);
+    if (u < cum) return j;
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------
 // hyperparameter MH (multiview_hyper.cpp:211-292), executed by the wave.
 // Sums are accumulated in the reference's order by lane 0; lanes only
 // produce the addends.
@@ -296,15 +336,38 @@ struct MH {
 
 // ---------------------------------------------------------------------------
 // One sweep (or the rest of one) for every chain: grid = chains, block = 64.
+// The chain's capacity-sized arrays (n_t .. P, and z when it fits) are one
+// contiguous range of its allocation (carve); when the range fits in the
+// lds_bytes of dynamic LDS it is copied in at the start, the kernel works on
+// the copy (every dependent access an LDS round trip instead of an L2 one)
+// and it is written back at the end.  Same operations, same order: the bits
+// do not depend on where the arrays live.
 // ---------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
-    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed) {
+    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, int lds_bytes) {
   __shared__ Shared sh;
+  extern __shared__ __attribute__((aligned(16))) char ex_lds[];
   ExactChain &Cg = chains[blockIdx.x];
   ExactChain C = Cg;               // pointers + scalars in registers
   const int lane = threadIdx.x;
-  if (C.status == MVC_ST_DONE || C.status == MVC_ST_ERROR) return;
+  if (C.status == MVC_ST_ERROR || C.todo <= 0) return;
   const int TC = C.TC, KC = C.KC;
+  char *gbeg = nullptr;
+  size_t nbytes = 0;
+  {
+    const size_t full = (size_t)((char *)C.mhbuf - (char *)C.z), part = (size_t)((char *)C.mhbuf - (char *)C.n_t);
+    if (full <= (size_t)lds_bytes) { gbeg = (char *)C.z; nbytes = full; }
+    else if (part <= (size_t)lds_bytes) { gbeg = (char *)C.n_t; nbytes = part; }
+  }
+  if (gbeg) {
+    const uint4 *src = (const uint4 *)gbeg;   // 256-byte granules (carve)
+    uint4 *dst = (uint4 *)ex_lds;
+    for (size_t e = lane; e < nbytes / 16; e += MVC_WAVE) dst[e] = src[e];
+    auto re = [&](auto *&ptr) { ptr = (std::remove_reference_t<decltype(ptr)>)(ex_lds + ((char *)ptr - gbeg)); };
+    if (gbeg == (char *)C.z) re(C.z);
+    re(C.n_t); re(C.pos_of_slot); re(C.slot_at_pos); re(C.free_slots); re(C.dish);
+    re(C.d_id); re(C.d_n); re(C.d_l); re(C.d_S1); re(C.d_S2); re(C.f); re(C.logf); re(C.P);
+  }
 
   for (int v = lane; v < V; v += MVC_WAVE) {
     sh.Kact[v] = C.Kact[v];
@@ -316,278 +379,280 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
   int T = C.T;
   int n_free = C.n_free;
   const double *tau = sh.hyp, *alpha = sh.hyp + V, *sigma = sh.hyp + 2 * V;
-  const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];
   int status = MVC_ST_RUNNING;
   int i = C.resume_i;
+  int todo = C.todo;
 
-  for (; i < n; ++i) {
-    // -------- capacity guard (every step may add 1 table and 1 dish/view)
-    int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
-    for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
-    if (need) { status = MVC_ST_OVERFLOW; break; }
+  for (; todo > 0; --todo, i = 0) {   // the launch's sweeps, each from customer resume_i / 0
+    const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];   // the MH of the previous sweep may have moved them
+    for (; i < n; ++i) {
+      // -------- capacity guard (every step may add 1 table and 1 dish/view)
+      int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
+      for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
+      if (need) { status = MVC_ST_OVERFLOW; break; }
 
-    if (lane < V) sh.ys[lane] = y[(size_t)lane * n + i];
-    // ---------------- remove_customer(i)   utils.cpp:138-192
-    const int s = C.z[i];
-    __syncthreads();
-    if (lane < V) {
-      const int k = C.dish[lane * TC + s];
-      const double yv = sh.ys[lane];
-      C.d_n[lane * KC + k] -= 1;
-      C.d_S1[lane * KC + k] -= yv;
-      C.d_S2[lane * KC + k] -= yv * yv;
-    }
-    int nt_s = C.n_t[s] - 1;
-    __syncthreads();
-    if (lane == 0) C.n_t[s] = nt_s;
-    if (nt_s == 0) {
-      // table dies: l_vk-- (:170-173), swap-and-pop (:175-190)
+      if (lane < V) sh.ys[lane] = y[(size_t)lane * n + i];
+      // ---------------- remove_customer(i)   utils.cpp:138-192
+      const int s = C.z[i];
+      __syncthreads();
       if (lane < V) {
         const int k = C.dish[lane * TC + s];
-        int dead = -1;
-        if (k >= 0) {
-          const int l = C.d_l[lane * KC + k];
-          if (l > 0) {
-            C.d_l[lane * KC + k] = l - 1;
-            if (l - 1 == 0) dead = k;
-          }
-        }
-        sh.died[lane] = dead;
+        const double yv = sh.ys[lane];
+        C.d_n[lane * KC + k] -= 1;
+        C.d_S1[lane * KC + k] -= yv;
+        C.d_S2[lane * KC + k] -= yv * yv;
       }
-      const int pos = C.pos_of_slot[s];
-      const int last = T - 1;
+      int nt_s = C.n_t[s] - 1;
       __syncthreads();
+      if (lane == 0) C.n_t[s] = nt_s;
+      if (nt_s == 0) {
+        // table dies: l_vk-- (:170-173), swap-and-pop (:175-190)
+        if (lane < V) {
+          const int k = C.dish[lane * TC + s];
+          int dead = -1;
+          if (k >= 0) {
+            const int l = C.d_l[lane * KC + k];
+            if (l > 0) {
+              C.d_l[lane * KC + k] = l - 1;
+              if (l - 1 == 0) dead = k;
+            }
+          }
+          sh.died[lane] = dead;
+        }
+        const int pos = C.pos_of_slot[s];
+        const int last = T - 1;
+        __syncthreads();
+        if (lane == 0) {
+          if (pos != last) {
+            const int sl = C.slot_at_pos[last];
+            C.slot_at_pos[pos] = sl;
+            C.pos_of_slot[sl] = pos;
+          }
+          C.free_slots[n_free] = s;
+        }
+        T -= 1;
+        n_free += 1;
+        __syncthreads();
+        // compact the live dish list of every view whose dish died
+        for (int v = 0; v < V; ++v) {
+          const int k = sh.died[v];
+          if (k < 0) continue;
+          const int K = sh.Kact[v];
+          // shift entries k+1..K-1 down by one (read all, barrier, write)
+          for (int base = k + 1; base < K; base += MVC_WAVE) {
+            const int j = base + lane;
+            int id = 0, nn = 0, ll = 0;
+            double s1 = 0.0, s2 = 0.0;
+            if (j < K) {
+              id = C.d_id[v * KC + j]; nn = C.d_n[v * KC + j]; ll = C.d_l[v * KC + j];
+              s1 = C.d_S1[v * KC + j]; s2 = C.d_S2[v * KC + j];
+            }
+            __syncthreads();
+            if (j < K) {
+              C.d_id[v * KC + j - 1] = id; C.d_n[v * KC + j - 1] = nn; C.d_l[v * KC + j - 1] = ll;
+              C.d_S1[v * KC + j - 1] = s1; C.d_S2[v * KC + j - 1] = s2;
+            }
+            __syncthreads();
+          }
+          for (int p = lane; p < T; p += MVC_WAVE) {
+            const int sl = C.slot_at_pos[p];
+            const int dk = C.dish[v * TC + sl];
+            if (dk > k) C.dish[v * TC + sl] = dk - 1;
+          }
+          __syncthreads();
+          if (lane == 0) sh.Kact[v] = K - 1;
+          __syncthreads();
+        }
+      }
+
+      // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
       if (lane == 0) {
-        if (pos != last) {
-          const int sl = C.slot_at_pos[last];
+        int acc = 0;
+        for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
+        sh.Koff[V] = acc;
+      }
+      __syncthreads();
+      const int Ktot = sh.Koff[V];
+      for (int e = lane; e < Ktot; e += MVC_WAVE) {
+        int v = 0;
+        while (sh.Koff[v + 1] <= e) ++v;
+        const int j = e - sh.Koff[v];
+        const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v]);
+        C.f[v * KC + j] = f;
+        C.logf[v * KC + j] = mvc_log(f);
+      }
+      if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane]);
+      __syncthreads();
+
+      // ---------------- marginal of a new table per view (utils.cpp:40-69)
+      if (lane < V) {
+        const int v = lane;
+        const int K = sh.Kact[v];
+        const double total = seq_sum8(0.0, K, [&](int j) { return (double)C.d_l[v * KC + j]; });
+        const double denom = alpha[v] + total;
+        double m;
+        if (denom <= 0.0) {
+          m = sh.fnew[v];
+        } else {
+          double acc = seq_sum8(0.0, K, [&](int j) {
+            double w = (C.d_l[v * KC + j] - sigma[v]);
+            if (w < 0.0) w = 0.0;
+            return w * C.f[v * KC + j];
+          });
+          double wn = (alpha[v] + K * sigma[v]);
+          if (wn < 0.0) wn = 0.0;
+          acc += wn * sh.fnew[v];
+          m = acc / denom;
+        }
+        sh.marg[v] = m;
+      }
+
+      // ---------------- table probabilities (utils.cpp:83-116)
+      int tne = 0;
+      for (int p = lane; p < T; p += MVC_WAVE) {
+        const int sl = C.slot_at_pos[p];
+        const int nt = C.n_t[sl];
+        double pr = 0.0;
+        if (nt != 0) {
+          ++tne;
+          double lpt = 0.0;
+          for (int v0 = 0; v0 < V; v0 += 8) {   // 8 views' dish indices, then their log f, in flight together
+            int kq[8];
+            double g[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) kq[q] = (v0 + q < V) ? C.dish[(v0 + q) * TC + sl] : 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) g[q] = (v0 + q < V) ? C.logf[(v0 + q) * KC + kq[q]] : 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              if (v0 + q < V) lpt += g[q];
+          }
+          const double mass = nt - sg;
+          pr = (mass <= 0.0) ? 0.0 : mass * mvc_exp(lpt);
+        }
+        C.P[p] = pr;
+      }
+      for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
+      __syncthreads();
+
+      // ---------------- normaliser, draw (gibbs.cpp:169-191)
+      if (lane == 0) {
+        double lnew = 0.0;
+        for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
+        const double mass_new = ag + sg * tne;                          // :124-135
+        const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
+        sh.dv[1] = seq_sum8(p_new, T, [&](int p) { return C.P[p]; });
+      }
+      __syncthreads();
+      const double sum_p = sh.dv[1];
+      int t_star;
+      if (sum_p <= 0.0) {
+        t_star = -2;                       // gibbs.cpp:172-176 -> table at position 0
+      } else {
+        for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
+        __syncthreads();
+        if (lane == 0) {
+          const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
+          sh.iv[0] = seq_find8(u, T, [&](int p) { return C.P[p]; });
+        }
+        C.draws += 1;
+        __syncthreads();
+        t_star = sh.iv[0];
+      }
+
+      if (t_star != -1) {
+        // add_customer_to_existing_table (utils.cpp:194-207)
+        const int sl = C.slot_at_pos[t_star < 0 ? 0 : t_star];
+        __syncthreads();
+        if (lane == 0) { C.z[i] = sl; C.n_t[sl] = C.n_t[sl] + 1; }
+        if (lane < V) {
+          const int k = C.dish[lane * TC + sl];
+          const double yv = sh.ys[lane];
+          C.d_n[lane * KC + k] += 1;
+          C.d_S1[lane * KC + k] += yv;
+          C.d_S2[lane * KC + k] += yv * yv;
+        }
+        __syncthreads();
+      } else {
+        // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
+        n_free -= 1;
+        const int sl = C.free_slots[n_free];
+        const int pos = T;
+        __syncthreads();
+        if (lane == 0) {
           C.slot_at_pos[pos] = sl;
           C.pos_of_slot[sl] = pos;
+          C.n_t[sl] = 1;
+          C.z[i] = sl;
         }
-        C.free_slots[n_free] = s;
-      }
-      T -= 1;
-      n_free += 1;
-      __syncthreads();
-      // compact the live dish list of every view whose dish died
-      for (int v = 0; v < V; ++v) {
-        const int k = sh.died[v];
-        if (k < 0) continue;
-        const int K = sh.Kact[v];
-        // shift entries k+1..K-1 down by one (read all, barrier, write)
-        for (int base = k + 1; base < K; base += MVC_WAVE) {
-          const int j = base + lane;
-          int id = 0, nn = 0, ll = 0;
-          double s1 = 0.0, s2 = 0.0;
-          if (j < K) {
-            id = C.d_id[v * KC + j]; nn = C.d_n[v * KC + j]; ll = C.d_l[v * KC + j];
-            s1 = C.d_S1[v * KC + j]; s2 = C.d_S2[v * KC + j];
-          }
-          __syncthreads();
-          if (j < K) {
-            C.d_id[v * KC + j - 1] = id; C.d_n[v * KC + j - 1] = nn; C.d_l[v * KC + j - 1] = ll;
-            C.d_S1[v * KC + j - 1] = s1; C.d_S2[v * KC + j - 1] = s2;
-          }
-          __syncthreads();
-        }
-        for (int p = lane; p < T; p += MVC_WAVE) {
-          const int sl = C.slot_at_pos[p];
-          const int dk = C.dish[v * TC + sl];
-          if (dk > k) C.dish[v * TC + sl] = dk - 1;
-        }
-        __syncthreads();
-        if (lane == 0) sh.Kact[v] = K - 1;
-        __syncthreads();
-      }
-    }
-
-    // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
-    if (lane == 0) {
-      int acc = 0;
-      for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
-      sh.Koff[V] = acc;
-    }
-    __syncthreads();
-    const int Ktot = sh.Koff[V];
-    for (int e = lane; e < Ktot; e += MVC_WAVE) {
-      int v = 0;
-      while (sh.Koff[v + 1] <= e) ++v;
-      const int j = e - sh.Koff[v];
-      const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v]);
-      C.f[v * KC + j] = f;
-      C.logf[v * KC + j] = mvc_log(f);
-    }
-    if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane]);
-    __syncthreads();
-
-    // ---------------- marginal of a new table per view (utils.cpp:40-69)
-    if (lane < V) {
-      const int v = lane;
-      const int K = sh.Kact[v];
-      double total = 0.0;
-      for (int j = 0; j < K; ++j) total += C.d_l[v * KC + j];
-      const double denom = alpha[v] + total;
-      double m;
-      if (denom <= 0.0) {
-        m = sh.fnew[v];
-      } else {
-        double acc = 0.0;
-        for (int j = 0; j < K; ++j) {
-          double w = (C.d_l[v * KC + j] - sigma[v]);
-          if (w < 0.0) w = 0.0;
-          acc += w * C.f[v * KC + j];
-        }
-        double wn = (alpha[v] + K * sigma[v]);
-        if (wn < 0.0) wn = 0.0;
-        acc += wn * sh.fnew[v];
-        m = acc / denom;
-      }
-      sh.marg[v] = m;
-    }
-
-    // ---------------- table probabilities (utils.cpp:83-116)
-    int tne = 0;
-    for (int p = lane; p < T; p += MVC_WAVE) {
-      const int sl = C.slot_at_pos[p];
-      const int nt = C.n_t[sl];
-      double pr = 0.0;
-      if (nt != 0) {
-        ++tne;
-        double lpt = 0.0;
-        for (int v = 0; v < V; ++v) lpt += C.logf[v * KC + C.dish[v * TC + sl]];
-        const double mass = nt - sg;
-        pr = (mass <= 0.0) ? 0.0 : mass * mvc_exp(lpt);
-      }
-      C.P[p] = pr;
-    }
-    for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
-    __syncthreads();
-
-    // ---------------- normaliser, draw (gibbs.cpp:169-191)
-    if (lane == 0) {
-      double lnew = 0.0;
-      for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
-      const double mass_new = ag + sg * tne;                          // :124-135
-      const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
-      double sum_p = p_new;
-      for (int p = 0; p < T; ++p) sum_p += C.P[p];
-      sh.dv[1] = sum_p;
-    }
-    __syncthreads();
-    const double sum_p = sh.dv[1];
-    int t_star;
-    if (sum_p <= 0.0) {
-      t_star = -2;                       // gibbs.cpp:172-176 -> table at position 0
-    } else {
-      for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
-      __syncthreads();
-      if (lane == 0) {
-        const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
-        double cum = 0.0;
-        int ts = -1;
-        for (int p = 0; p < T; ++p) {
-          cum += C.P[p];
-          if (u < cum) { ts = p; break; }
-        }
-        sh.iv[0] = ts;
-      }
-      C.draws += 1;
-      __syncthreads();
-      t_star = sh.iv[0];
-    }
-
-    if (t_star != -1) {
-      // add_customer_to_existing_table (utils.cpp:194-207)
-      const int sl = C.slot_at_pos[t_star < 0 ? 0 : t_star];
-      __syncthreads();
-      if (lane == 0) { C.z[i] = sl; C.n_t[sl] = C.n_t[sl] + 1; }
-      if (lane < V) {
-        const int k = C.dish[lane * TC + sl];
-        const double yv = sh.ys[lane];
-        C.d_n[lane * KC + k] += 1;
-        C.d_S1[lane * KC + k] += yv;
-        C.d_S2[lane * KC + k] += yv * yv;
-      }
-      __syncthreads();
-    } else {
-      // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
-      n_free -= 1;
-      const int sl = C.free_slots[n_free];
-      const int pos = T;
-      __syncthreads();
-      if (lane == 0) {
-        C.slot_at_pos[pos] = sl;
-        C.pos_of_slot[sl] = pos;
-        C.n_t[sl] = 1;
-        C.z[i] = sl;
-      }
-      T += 1;
-      // assign_dishes_new_table (utils.cpp:278-289): per view weights
-      if (lane < V) {
-        const int v = lane;
-        const int K = sh.Kact[v];
-        double total = 0.0;
-        for (int j = 0; j < K; ++j) {
-          double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
-          if (w < 0) w = 0;
-          total += w;
-        }
-        double wn = (alpha[v] + sigma[v] * K) * sh.fnew[v];
-        if (wn < 0) wn = 0;
-        total += wn;
-        sh.tw[v] = total;
-      }
-      __syncthreads();
-      if (lane == 0) {                       // draws are consumed in view order
-        uint64_t d = C.draws;
-        for (int v = 0; v < V; ++v) sh.draw_ix[v] = (sh.tw[v] <= 0) ? -1 : (int)(d++ - C.draws);
-        sh.iv[1] = (int)(d - C.draws);
-      }
-      __syncthreads();
-      if (lane < V) {
-        const int v = lane;
-        const int K = sh.Kact[v];
-        int kk = -1;
-        const double total = sh.tw[v];
-        if (total > 0) {
-          const double u = 0.0 + (total - 0.0) * mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws + (uint64_t)sh.draw_ix[v]);
-          double cum = 0;
-          for (int j = 0; j < K; ++j) {
+        T += 1;
+        // assign_dishes_new_table (utils.cpp:278-289): per view weights
+        if (lane < V) {
+          const int v = lane;
+          const int K = sh.Kact[v];
+          double total = seq_sum8(0.0, K, [&](int j) {
             double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
             if (w < 0) w = 0;
-            cum += w;
-            if (u < cum) { kk = j; break; }
+            return w;
+          });
+          double wn = (alpha[v] + sigma[v] * K) * sh.fnew[v];
+          if (wn < 0) wn = 0;
+          total += wn;
+          sh.tw[v] = total;
+        }
+        __syncthreads();
+        if (lane == 0) {                       // draws are consumed in view order
+          uint64_t d = C.draws;
+          for (int v = 0; v < V; ++v) sh.draw_ix[v] = (sh.tw[v] <= 0) ? -1 : (int)(d++ - C.draws);
+          sh.iv[1] = (int)(d - C.draws);
+        }
+        __syncthreads();
+        if (lane < V) {
+          const int v = lane;
+          const int K = sh.Kact[v];
+          int kk = -1;
+          const double total = sh.tw[v];
+          if (total > 0) {
+            const double u = 0.0 + (total - 0.0) * mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws + (uint64_t)sh.draw_ix[v]);
+            kk = seq_find8(u, K, [&](int j) {
+              double w = (C.d_l[v * KC + j] - sigma[v]) * C.f[v * KC + j];
+              if (w < 0) w = 0;
+              return w;
+            });
           }
+          if (kk < 0) {                        // fresh dish slot (utils.cpp:250-258,268-275)
+            kk = K;
+            C.d_id[v * KC + kk] = sh.next_id[v];
+            C.d_n[v * KC + kk] = 0;
+            C.d_l[v * KC + kk] = 0;
+            C.d_S1[v * KC + kk] = 0.0;
+            C.d_S2[v * KC + kk] = 0.0;
+            sh.next_id[v] += 1;
+            sh.Kact[v] = K + 1;
+          }
+          const double yv = sh.ys[v];
+          C.dish[v * TC + sl] = kk;
+          C.d_l[v * KC + kk] += 1;
+          C.d_n[v * KC + kk] += 1;
+          C.d_S1[v * KC + kk] += yv;
+          C.d_S2[v * KC + kk] += yv * yv;
         }
-        if (kk < 0) {                        // fresh dish slot (utils.cpp:250-258,268-275)
-          kk = K;
-          C.d_id[v * KC + kk] = sh.next_id[v];
-          C.d_n[v * KC + kk] = 0;
-          C.d_l[v * KC + kk] = 0;
-          C.d_S1[v * KC + kk] = 0.0;
-          C.d_S2[v * KC + kk] = 0.0;
-          sh.next_id[v] += 1;
-          sh.Kact[v] = K + 1;
-        }
-        const double yv = sh.ys[v];
-        C.dish[v * TC + sl] = kk;
-        C.d_l[v * KC + kk] += 1;
-        C.d_n[v * KC + kk] += 1;
-        C.d_S1[v * KC + kk] += yv;
-        C.d_S2[v * KC + kk] += yv * yv;
+        C.draws += (uint64_t)sh.iv[1];
+        __syncthreads();
       }
-      C.draws += (uint64_t)sh.iv[1];
-      __syncthreads();
     }
-  }
 
-  if (status == MVC_ST_RUNNING) {
+    if (status != MVC_ST_RUNNING) break;
     // end of sweep: hyperparameters (gibbs.cpp:202)
     C.T = T;
     MH mh{C, sh, V, n, lane, seed};
     mh.run();
-    status = MVC_ST_DONE;
-    i = n;
+    // the MH draws on lane 0 only: every lane continues from lane 0's counter
+    // (the next sweep's dish draws run on lanes 0 .. V-1)
+    C.draws = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(C.draws >> 32)) << 32) |
+              (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)C.draws);
   }
+  if (status == MVC_ST_RUNNING) status = MVC_ST_DONE;
   __syncthreads();
   for (int v = lane; v < V; v += MVC_WAVE) {
     C.Kact[v] = sh.Kact[v];
@@ -600,6 +665,13 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     Cg.draws = C.draws;
     Cg.resume_i = i;
     Cg.status = status;
+    Cg.todo = todo;
+  }
+  if (gbeg) {                      // the LDS copy back to the chain's allocation
+    __syncthreads();
+    const uint4 *src = (const uint4 *)ex_lds;
+    uint4 *dst = (uint4 *)gbeg;
+    for (size_t e = lane; e < nbytes / 16; e += MVC_WAVE) dst[e] = src[e];
   }
 }
 
@@ -993,6 +1065,18 @@ class ExactSampler : public Sampler {
     return I;
   }
 
+  // dynamic LDS of the sweep kernel: the largest chain's array range that fits
+  // kExactLds (with z when every chain's does), 0 when none fits
+  static constexpr size_t kExactLds = 48 * 1024;
+  int lds_bytes() const {
+    size_t full = 0, part = 0;
+    for (auto &A : chains) {
+      full = std::max(full, (size_t)((char *)A.h.mhbuf - (char *)A.h.z));
+      part = std::max(part, (size_t)((char *)A.h.mhbuf - (char *)A.h.n_t));
+    }
+    return (int)(full <= kExactLds ? full : (part <= kExactLds ? part : 0));
+  }
+
   void push_structs() {
     std::vector<ExactChain> hs(chains.size());
     for (size_t k = 0; k < chains.size(); ++k) hs[k] = chains[k].h;
@@ -1006,7 +1090,7 @@ class ExactSampler : public Sampler {
     for (size_t k = 0; k < chains.size(); ++k) {
       ExactChain &C = chains[k].h;
       C.T = hs[k].T; C.n_free = hs[k].n_free; C.draws = hs[k].draws;
-      C.resume_i = hs[k].resume_i; C.status = hs[k].status;
+      C.resume_i = hs[k].resume_i; C.status = hs[k].status; C.todo = hs[k].todo;
     }
   }
 
@@ -1028,17 +1112,22 @@ class ExactSampler : public Sampler {
     A = B;
   }
 
+  // sweeps per kernel launch: each chain runs its sweeps on its own, so a
+  // launch lasts about the longest chain's sum of sweeps rather than the sum
+  // of the longest sweeps, and the per-sweep launch + read-back is amortised
+  static constexpr int kSweepsPerLaunch = 64;
   void sweep(int n_sweeps) override {
-    for (int it = 0; it < n_sweeps; ++it) {
-      for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; }
+    for (int left = n_sweeps; left > 0;) {
+      const int k = std::min(left, kSweepsPerLaunch);
+      for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; A.h.todo = k; }
       push_structs();
       hipEvent_t ev0 = nullptr;
       timers.begin("sweep", &ev0);
       for (int round = 0;; ++round) {
         hipEvent_t ev = nullptr;
         timers.begin("exact_sweep", &ev);
-        hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), 0, stream,
-                           (const double *)y_dev, n, V, chains_dev, cfg.seed);
+        hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), lds_bytes(), stream,
+                           (const double *)y_dev, n, V, chains_dev, cfg.seed, lds_bytes());
         MVC_HIP(hipGetLastError());
         timers.end("exact_sweep", ev);
         pull_structs();
@@ -1049,10 +1138,11 @@ class ExactSampler : public Sampler {
         }
         if (!again) break;
         push_structs();
-        if (round > 64) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
+        if (round > 64 + 64 * k) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
       }
       timers.end("sweep", ev0);
-      ++sweeps_done;
+      sweeps_done += k;
+      left -= k;
     }
   }
 

@@ -44,6 +44,7 @@ inline const char *base_name(const char *p) {
 //                      attributed to the launch that caused it).
 int poison_byte();      // -1: off
 int lds_fill_byte();    // MVC_LDS_FILL, -1: off
+bool run_check();       // MVC_RUN_CHECK
 bool debug_sync();
 
 // Initial state draws of multiview_gibbs.cpp:12-62 on the sequential Philox

@@ -43,7 +43,7 @@ struct ExactChain {
   int32_t resume_i;            // next customer of the current sweep
   int32_t status;              // MVC_ST_*
   int32_t chain_id;            // global chain id (Philox stream)
-  int32_t pad;
+  int32_t todo;                // sweeps left in the current launch (mvc_exact_sweep_kernel)
 };
 
 #define MVC_ST_RUNNING 0

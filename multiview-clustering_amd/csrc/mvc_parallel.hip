@@ -1773,6 +1773,15 @@ int lds_fill_byte() {
   }();
   return b;
 }
+// MVC_RUN_CHECK=1: the repair run kernels check every index their commits
+// write through and report the first bad one (Repair::dbg) instead of storing
+bool run_check() {
+  static const bool on = [] {
+    const char *e = getenv("MVC_RUN_CHECK");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 bool debug_sync() {
   static const bool on = [] {
     const char *e = getenv("MVC_DEBUG_SYNC");
@@ -2736,6 +2745,7 @@ class ParallelSampler : public Sampler {
                                (L.lc == 2 ? (int64_t)kVpE * D : 0))
                         : 0;
           L.fill = lds_fill_byte();
+          L.chk = run_check() ? 1 : 0;
           hipLaunchKernelGGL(L.lc ? (L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
                                   : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
                              dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, Q, L);
@@ -2764,6 +2774,13 @@ class ParallelSampler : public Sampler {
         dbg("gated hyper", c, s);
       } else {
         MVC_HIP(hipStreamSynchronize(stream));
+      }
+      if (rs_host->dbg[0]) {   // MVC_RUN_CHECK: a run kernel's index check failed
+        std::string v;
+        for (int k = 1; k < 8; ++k) v += " " + std::to_string(rs_host->dbg[k]);
+        throw Error(MVC_ERR_STATE, "run kernel index check " + std::to_string(rs_host->dbg[0]) + " failed (chain " +
+                                       std::to_string(c.gid) + ", sweep " + std::to_string(s) + ", lc " +
+                                       std::to_string(L.lc) + "):" + v);
       }
       if (rs_host->overflow) {
         grow_capacity(rs_host->overflow);

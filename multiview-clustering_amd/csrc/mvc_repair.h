@@ -42,6 +42,7 @@ struct Repair {
   int32_t lastm, gapq;  // the last mover, and the moving average (x16) of the gaps between movers
   int32_t vpoff;        // 1: value prediction stopped for this sweep (predictions miss, or a dish list > 128)
   int32_t vpsteps, vphits;   // vp steps, and those whose predictions all held
+  int32_t dbg[8];       // MVC_RUN_CHECK: the first index check that failed in a run kernel (code, values), 0: none
   int32_t Klist[MVC_MAXV];
   unsigned long long prof[12];  // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz), steps, decided customers, phase-A hits
 };
@@ -87,7 +88,23 @@ struct SeqLds {
   int64_t vpo;          // lc == 2: offset (doubles) of the overlay's S1 columns [kVpE][D] in the dynamic LDS
   int64_t dyn;          // bytes of dynamic LDS of the launch
   int32_t fill;         // MVC_LDS_FILL diagnostics: >= 0 fills the block's LDS with this byte at launch
+  int32_t chk;          // MVC_RUN_CHECK diagnostics: check every index a commit writes through (R->dbg)
 };
+
+// MVC_RUN_CHECK: the first failed index check of the run kernel's block
+// (code, then up to 7 values); a failed check skips the write it guards and
+// the loop stops at its next barrier, so a bad index is reported instead of
+// becoming a wild store.
+__shared__ int mvc_run_bad[8];
+__device__ __forceinline__ bool run_chk(bool ok, int code, int a = 0, int b = 0, int c = 0, int d = 0, int e = 0,
+                                        int f = 0) {
+  if (ok) return true;
+  if (atomicCAS(&mvc_run_bad[0], 0, code) == 0) {
+    mvc_run_bad[1] = a; mvc_run_bad[2] = b; mvc_run_bad[3] = c;
+    mvc_run_bad[4] = d; mvc_run_bad[5] = e; mvc_run_bad[6] = f;
+  }
+  return false;
+}
 // ring slot: y rows [V][D], Y2 [V], z (as a double)
 __host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
 
@@ -1556,6 +1573,7 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->T_ne = A.status[V + 3];
   R->moves = R->births = R->newdish = R->rounds = 0;
   for (int k = 0; k < 12; ++k) R->prof[k] = 0;
+  for (int k = 0; k < 8; ++k) R->dbg[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
 }
 
@@ -1876,11 +1894,19 @@ __device__ __forceinline__ void gst(T *p, T v) {
 // barrier inside: the caller's next barrier publishes the LDS writes; global
 // arrays are written through (store only) for the kernels after this one.
 __device__ __forceinline__ void seq_commit_move_split(SeqArgs &A, const SCache &cc, const Cust &Ci, int i, int p0, int c, int nt0,
-                                      int ntc, int32_t *cnt) {
+                                      int ntc, int32_t *cnt, bool chk = false) {
   ParState &P = A.P;
   Repair *R = A.R;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int V = P.V, D = P.D, KC = P.KC, ks = cc.ks, ts = cc.ts;
+  if (chk) {   // MVC_RUN_CHECK: the move's tables and every view's two dishes
+    bool ok = run_chk(p0 >= 0 && p0 < *cc.T && c >= 0 && c < *cc.T && i >= 0 && i < P.n, 6, i, p0, c, *cc.T);
+    for (int v = 0; v < V && ok; ++v) {
+      const int j0 = cc.dish[v * ts + p0], j1 = cc.dish[v * ts + c];
+      ok = run_chk(j0 >= 0 && j0 < cc.Klist[v] && j1 >= 0 && j1 < cc.Klist[v], 7, i, v, j0, j1, cc.Klist[v]);
+    }
+    if (!ok) return;
+  }
   const double *hyp = cc.hyp, *l2pt = cc.L2pt;
   const bool dies = nt0 == 1, born = ntc == 0;
   if (w == 0) {
@@ -2095,6 +2121,9 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_birth_kerne
     R->cur = s_i + 1;
     R->pend = 0;
     R->streak = 0;
+    // the birth was the sweep's last customer: every customer is final (a
+    // run kernel must not start its loop at cur == n)
+    if (R->cur >= A.P.n) R->done = 1;
   }
 }
 
@@ -2368,7 +2397,7 @@ __device__ __forceinline__ int seq_run_loop_lc(SeqArgs &A, const SeqLds &L, cons
                            // general commit costs the loop 184 B of scratch and flat accesses)
       // the mover was evaluated in the previous step (or staged above), so its
       // row is in the ring (landed, not yet reused: requests stop a ring ahead of it)
-      seq_commit_move_split(A, cc, G.cust(cur, V, D), cur, pp0, pc, pnt0, pntc, U.cnt);
+      seq_commit_move_split(A, cc, G.cust(cur, V, D), cur, pp0, pc, pnt0, pntc, U.cnt, L.chk);
       cur = cur + 1;
       pend = 0;
       streak = 0;
@@ -2378,6 +2407,7 @@ __device__ __forceinline__ int seq_run_loop_lc(SeqArgs &A, const SeqLds &L, cons
         break;
       }
       seq_bar(true);   // the commit, visible to every wave
+      if (L.chk && mvc_run_bad[0]) break;
     }
     {   // the LDS layout must hold the current lists plus one birth
       bool bad = *cc.T >= L.ts;
@@ -2669,7 +2699,7 @@ __device__ __forceinline__ void vp_build(const SeqArgs &A, const SCache &cc, con
 // overlay's values after the last of them into the LDS state and HBM, S1 and
 // S2 updated in move order (one thread per element).  Block-wide.
 __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const VpMoves &M, int i0, int nc,
-                                          const double *const (&yr)[kVpMoves], int32_t *cnt) {
+                                          const double *const (&yr)[kVpMoves], int32_t *cnt, bool chk) {
   ParState &P = A.P;
   Repair *R = A.R;
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -2691,6 +2721,9 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
     for (int m = 0; m < kVpMoves; ++m)
       if (m < nc && M.mv[m]) {
         const int j0 = cc.dish[v * ts + M.p0[m]], j1 = cc.dish[v * ts + M.c[m]];
+        if (chk && !run_chk(j0 >= 0 && j0 < cc.Klist[v] && j1 >= 0 && j1 < cc.Klist[v], 1, i0, m, v, j0, j1,
+                            cc.Klist[v]))
+          continue;
         if (j0 != j1) {
           const double yd = yr[m][v * D + d];
           const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
@@ -2707,6 +2740,9 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
     for (int m = 0; m < kVpMoves; ++m)
       if (m < nc && M.mv[m]) {
         const int j0 = cc.dish[v * ts + M.p0[m]], j1 = cc.dish[v * ts + M.c[m]];
+        if (chk && !run_chk(j0 >= 0 && j0 < cc.Klist[v] && j1 >= 0 && j1 < cc.Klist[v], 2, i0, m, v, j0, j1,
+                            cc.Klist[v]))
+          continue;
         if (j0 != j1) {
           const double y2 = yr[m][V * D + v];
           const double a0 = cc.S2[v * ks + j0] - y2, a1 = cc.S2[v * ks + j1] + y2;
@@ -2731,6 +2767,7 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
           const int e2 = (m2 * kVpV + v) * 2;
           if (mvc_vp_ov.j[e2] == j || mvc_vp_ov.j[e2 + 1] == j) fin = false;
         }
+      if (chk && !run_chk(j < cc.Klist[v], 3, i0, e, v, j, cc.Klist[v])) fin = false;
       if (fin) {
         cc.d_n[v * ks + j] = mvc_vp_ov.dn[e];
         cc.d_l[v * ks + j] = mvc_vp_ov.dl[e];
@@ -2757,6 +2794,7 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
 #pragma unroll
       for (int m2 = 0; m2 < kVpMoves; ++m2)
         if (m2 > m && m2 < nc && M.mv[m2] && (M.p0[m2] == p || M.c[m2] == p)) fin = false;
+      if (chk && !run_chk(p >= 0 && p < *cc.T && i0 + m < A.P.n, 4, i0, m, which, p, *cc.T)) fin = false;
       if (fin) {
         const int n_ = which ? mvc_vp_ov.ntc[m] : mvc_vp_ov.ntp0[m];
         const double lm = which ? mvc_vp_ov.lmc[m] : mvc_vp_ov.lmp0[m];
@@ -2823,10 +2861,12 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
     if (rci >= 0) {   // (its row is in the ring: landed, and requests stop a ring ahead)
       const int nt0 = cc.n_t[rp0], ntc = cc.n_t[rc];
       seq_bar(true);
-      seq_commit_move_split(A, cc, G.cust(rci, V, D), rci, rp0, rc, nt0, ntc, U.cnt);
+      seq_commit_move_split(A, cc, G.cust(rci, V, D), rci, rp0, rc, nt0, ntc, U.cnt, L.chk);
       rci = -1;
       seq_bar(true);
+      if (L.chk && mvc_run_bad[0]) break;
     }
+    if (cur >= n) done = 1;   // (a run launched at cur == n: nothing left to decide)
     if (done || mode != kSeqRun) break;
     {   // the LDS layout must hold the lists plus one birth; the vp evaluation needs K_v <= 128
       bool bad = *cc.T >= L.ts, big = false;
@@ -2845,6 +2885,9 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
     }
     const int i0 = cur;
     const int need = min(n, i0 + kSeqLcThreads / 64);
+    if (L.chk)
+      run_chk(i0 >= 0 && i0 < n && fill >= 0 && fill <= n && landed <= fill && (fill < need || need - max(fill, i0) <= G.n),
+              10, i0, fill, landed, need, G.n);
     if (need > landed) {
       if (fill < need) {
         ring_fill_async<kSeqLcThreads / 64>(A, G, max(fill, i0), need);
@@ -2871,6 +2914,8 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
       pcs[k] = ring_pred(G, ik, V, D);
       yr[k] = G.at(ik);
       if (k < depth && pcs[k] < 0) depth = k + 1;
+      if (L.chk && k < nav)
+        run_chk(pz[k] >= 0 && pz[k] < *cc.T && pcs[k] >= -1 && pcs[k] < *cc.T, 8, i0, k, pz[k], pcs[k], *cc.T);
     }
     const VpMoves M = vp_moves(cc, depth, pz, pcs);
     vp_publish(M, pz, pcs);
@@ -2890,6 +2935,7 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
       const int c = seq_resample_lc<true>(A, Wv, G.cust(i0 + w, V, D), i0 + w,
                                           mvc_vp_ov.pz[w], S, cc.hyp, cc.cnew, X);
       if (lane == 0) U.chb[par][w] = c;
+      if (L.chk && lane == 0) run_chk(c >= -1 && c < *cc.T, 9, i0, w, c, *cc.T);
     }
     seq_bar(true);
     RUN_MARK(5);
@@ -2900,10 +2946,11 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
       if (k < depth && U.chb[par][k] != pcs[k]) a = k;
     ++steps;
     if (a == depth) ++hits;
-    // a held predicted birth is the step's last customer (depth was cut there)
-    const bool pbirth = a == depth && mvc_vp_ov.pcs[depth - 1] < 0;
+    // a held predicted birth is the step's last customer (depth was cut there;
+    // depth >= 1 here: cur < n)
+    const bool pbirth = a == depth && depth > 0 && mvc_vp_ov.pcs[depth - 1] < 0;
     const int nc = pbirth ? depth - 1 : a;   // customers whose held predictions commit from the overlay
-    vp_commit(A, cc, M, i0, nc, yr, U.cnt);
+    vp_commit(A, cc, M, i0, nc, yr, U.cnt, L.chk);
     int mlast = -1;   // the last mover decided in this step
 #pragma unroll
     for (int k = 0; k < kVpMoves; ++k)
@@ -2944,6 +2991,7 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
     if (cur >= n) done = 1;
     par ^= 1;
     seq_bar(true);
+    if (L.chk && mvc_run_bad[0]) break;
     RUN_MARK(6);
 #ifdef MVC_RUN_PROF
     if (tid == 0) mvc_prof_lds[7] += 1;
@@ -3003,6 +3051,7 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
 #ifdef MVC_RUN_PROF
   if (tid < 12) mvc_prof_lds[tid] = 0;
 #endif
+  if (tid < 8) mvc_run_bad[tid] = 0;   // (MVC_RUN_CHECK; published by the barrier below)
   if (tid == 0) {
     const int go = !(R->done || R->overflow || R->restride);
     if (go && R->win1 > R->win0) {
@@ -3122,6 +3171,8 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
     R->newdish = U.cnt[2];
     R->lastm = U.lastm;
     R->gapq = U.gapq;
+    if (L.chk && mvc_run_bad[0])
+      for (int k = 0; k < 8; ++k) R->dbg[k] = mvc_run_bad[k];
     if (flags & kRunRestride) R->restride = 1;
     if (flags & kRunVpOff) R->vpoff = 1;
     if (U.done && !U.pend) {

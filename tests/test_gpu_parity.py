@@ -643,8 +643,6 @@ print("chains OK")
 """
 
 
-@pytest.mark.xfail(strict=False, reason="illegal memory access on the MI355X in round 3's last four runs "
-                   "(DESIGN.md §9, root cause not found); run in a child process so a fault cannot poison the suite")
 def test_chains_concurrent_equal_serial():
     """Several chains in one handle run concurrently (ChainSet: a stream and a
     host thread per chain, shared device data); every chain equals the same
@@ -743,8 +741,6 @@ def test_run_chain_ids_and_pooled_summary(mode):
     give every chain the chain a one-chain call with that id gives, bit for
     bit; mvc_result_summary's pooled means and R-hat equal a host
     computation over the saved draws."""
-    if mode == "parallel":   # DESIGN.md §9: open defect (illegal memory access, multi-chain handles, r3ag)
-        pytest.skip("open defect at the end of round 3: multi-chain parallel handles fault on the MI355X (DESIGN.md §9)")
     m = _mvc()
     from mvc_amd import data
     from mvc_amd import _lib as L
