@@ -2664,7 +2664,11 @@ class ParallelSampler : public Sampler {
       const bool s1 = attempt == 0;
       const int kgrow = attempt < 2 ? std::max(8, kmax / 2) : 4;
       const int tgrow = attempt < 2 ? std::max(64, T / 2) : 16;
-      L.ks = (kmax + kgrow + 7) / 8 * 8;
+      // ks = 16 (mod 32): the lane-column evaluation's rows (views) read dish
+      // j of [v][ks] arrays at v ks + j, so rows 0 / 1 (and 2 / 3) of a
+      // ds_read_b64 lane group then fall on disjoint banks (2 ks dwords = 32
+      // mod 64), and of a ds_read_b32 too (ks = 16 mod 32)
+      L.ks = (kmax + kgrow + 15) / 32 * 32 + 16;
       L.ts = (T + tgrow + 63) / 64 * 64;   // whole 64-table chunks (the lane-column evaluation's e[] scratch)
       L.s1 = s1 ? 1 : 0;
       L.cache_dbl = seq_lds_cache(V, D, L.ks, L.ts, s1);

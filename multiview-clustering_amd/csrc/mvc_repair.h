@@ -108,9 +108,13 @@ __device__ __forceinline__ bool run_chk(bool ok, int code, int a = 0, int b = 0,
 // ring slot: y rows [V][D], Y2 [V], z (as a double)
 __host__ __device__ inline int64_t seq_ring_slot(int V, int D) { return (int64_t)V * D + V + 1; }
 
+// lp row stride of the LDS scratch: the lane-column evaluation stores dish j
+// of a row at j + j / 32 (lc_lpx), so the table gathers of dishes j and j + 32
+// (the same bank of ds_read_b64 otherwise) fall on different banks
+__host__ __device__ inline int seq_lps(int ks) { return ks + (ks >> 5) + 1; }
 __host__ __device__ inline int64_t seq_lds_stride(int V, int D, int ks, int ts) {
-  // ... + ys [V][D] + Y2 [V] + lm_v [V] + member maxima [4] (unused by seq_resample)
-  return 2 * (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + V + 4;
+  // lp [V][seq_lps] | aux [V][ks] | e | B, C | mv | koff | ys [V][D] + Y2 [V] + lm_v [V] + member maxima [4]
+  return (int64_t)V * seq_lps(ks) + (int64_t)V * ks + ts + 16 + ts / 16 + 2 + V + V + 2 + (int64_t)V * D + V + V + 4;
 }
 __host__ __device__ inline int64_t seq_lds_cache(int V, int D, int ks, int ts, bool s1) {
   const int64_t ints = (int64_t)ts + (int64_t)V * ts + 2 * (int64_t)V * ks + 2 * V + 2;
@@ -146,10 +150,10 @@ struct SeqScratch {
   int32_t *koff;
   double *ys;   // run kernel: the customer's y rows [V][D] and Y2 [V]
   int lps;      // lp / aux stride per view
-  __device__ void carve(double *base, int V, int ks, int ts) {
-    lps = ks;
+  __device__ void carve(double *base, int V, int ks, int ts, int lp_stride) {
+    lps = lp_stride;
     lp = base;
-    aux = lp + (size_t)V * ks;
+    aux = lp + (size_t)V * lp_stride;
     e = aux + (size_t)V * ks;
     B = e + ts + 16;
     mv = B + ts / 16 + 2;
@@ -158,14 +162,14 @@ struct SeqScratch {
   }
   double *wide;   // global scratch: the wide evaluation's shared values (seq_wide_len)
   __device__ SeqScratch(const SeqArgs &A, int wave) {
-    carve(A.scr + (int64_t)wave * A.scr_stride, A.P.V, A.P.KC, A.P.TC);
+    carve(A.scr + (int64_t)wave * A.scr_stride, A.P.V, A.P.KC, A.P.TC, A.P.KC);
     tree = ys;   // the global scratch has no staged rows
     ys = nullptr;
     wide = A.scr + (int64_t)(wave + 1) * A.scr_stride - (17 * A.P.V + 16);
   }
   // run kernel, LDS (no dish-draw tree)
   __device__ SeqScratch(double *base, int V, int ks, int ts) {
-    carve(base, V, ks, ts);
+    carve(base, V, ks, ts, seq_lps(ks));
     tree = nullptr;
     wide = nullptr;
   }
@@ -1135,6 +1139,10 @@ __device__ __forceinline__ int vp_ltot(const VpCtx &X, int v, int base) {
   return L;
 }
 
+// Where the lane-column evaluation keeps dish j of a view's lp row in the
+// LDS scratch (seq_lps): one pad double per 32 dishes.
+__device__ __forceinline__ int lc_lpx(int j) { return j + (j >> 5); }
+
 // The own dish's value with the customer removed from its
 // dot product G = y . S1[:, j0].
 template <bool kVp = false>
@@ -1233,7 +1241,7 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
     const double fr = __builtin_fma(G[u] + hy, cbj, c0j) + h;
     lp[u] = own ? self : fr;
     lj[u] = valid ? (own ? l0p : dlj) : 0;
-    if (valid) lpv[j] = lp[u];
+    if (valid) lpv[lc_lpx(j)] = lp[u];
     if (lj[u] > 0) {
       ++cnt;
       if (lp[u] > mx) mx = lp[u];
@@ -1267,7 +1275,7 @@ __device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double 
     const bool own = j == j0;
     const double val = own ? self : fr;
     const int l = own ? l0p : dl[j];
-    lpv[j] = val;
+    lpv[lc_lpx(j)] = val;
     if (l > 0) {
       ++cnt;
       if (val > mx) mx = val;
@@ -1281,7 +1289,7 @@ __device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double 
     const int l = (j == j0) ? l0p : dl[j];
     double w = (double)l - sigma;
     if (w < 0.0) w = 0.0;
-    cs = cs + w * mvc_exp_le0(l > 0 ? lpv[j] - m : -MVC_PM_INF);
+    cs = cs + w * mvc_exp_le0(l > 0 ? lpv[lc_lpx(j)] - m : -MVC_PM_INF);
   }
 }
 
@@ -1327,7 +1335,7 @@ __device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScrat
 #pragma unroll
       for (int h2 = 0; h2 < QB; ++h2)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + dj[h2][u]];
+        for (int u = 0; u < 4; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + lc_lpx(dj[h2][u])];
 #pragma unroll
       for (int h2 = 0; h2 < QB; ++h2)
 #pragma unroll
