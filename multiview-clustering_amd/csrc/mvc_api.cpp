@@ -254,6 +254,9 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
     hv[c].emplace_back(h, h + 3 * V + 2);
   };
   auto saved = [&](int it) { return it >= cf.burn_in && ((it - cf.burn_in) % cf.thin == 0); };   // gibbs.cpp:205
+  if (S->run_saving(cf.n_iter, cf.burn_in, cf.thin, quiet, save_fn)) {   // samples written on the device (exact)
+    for (int it = 0; it < cf.n_iter; ++it) R.S += saved(it) ? 1 : 0;
+  } else {
   for (int iter0 = 0, iter = 0; iter0 < cf.n_iter; iter0 = iter + 1) {
     // the sweeps up to the next saved one in one call (the exact schedule
     // then runs them without a launch and read-back per sweep)
@@ -284,6 +287,7 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
       }
       R.S++;
     }
+  }
   }
   S->flush_saves();
   S->synchronize();

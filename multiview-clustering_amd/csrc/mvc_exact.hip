@@ -334,6 +334,30 @@ struct MH {
 
 }  // namespace
 
+// In-kernel sample output (mvc_run with the exact schedule): the kernel
+// writes each saved sweep's state (save_state, utils.cpp:291-303) into the
+// chain's slot of a device buffer as it finishes the sweep, so a launch can run
+// many sweeps even when every sweep is saved.  Chain c's sample s lives at
+// slot c * nslot + s; s = (g - first) / thin for global sweep g.
+struct ExactSave {
+  int32_t *z;          // [C][nslot][n] table_of (nullptr: no saving)
+  int32_t *dish;       // [C][nslot][V][dcap] raw dish ids, positions < T
+  int32_t *T;          // [C][nslot]
+  double *hyp;         // [C][nslot][3V+2]
+  int32_t dcap, nslot, ktot, thin;
+  int64_t sweep_base, burn, first;   // global index of the launch's first sweep, burn-in, first saved sweep
+};
+// table_of[i] = position of i's table; dish_of[v][p] = raw dish id (the
+// snapshot kernels' layout), by one wavefront
+__device__ __forceinline__ void exact_snapshot_wave(const ExactChain &C, int n, int V, int T, const double *hyp, int lane,
+                                                    int32_t *tz, int32_t *dd, int dcap) {
+  (void)hyp;
+  for (int i = lane; i < n; i += MVC_WAVE) tz[i] = C.pos_of_slot[C.z[i]];
+  for (int v = 0; v < V; ++v)
+    for (int p = lane; p < T && p < dcap; p += MVC_WAVE)
+      dd[v * dcap + p] = C.d_id[v * C.KC + C.dish[v * C.TC + C.slot_at_pos[p]]];
+}
+
 // ---------------------------------------------------------------------------
 // One sweep (or the rest of one) for every chain: grid = chains, block = 64.
 // The chain's capacity-sized arrays (n_t .. P, and z when it fits) are one
@@ -344,7 +368,7 @@ struct MH {
 // do not depend on where the arrays live.
 // ---------------------------------------------------------------------------
 extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
-    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, int lds_bytes) {
+    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, int lds_bytes, ExactSave SV) {
   __shared__ Shared sh;
   extern __shared__ __attribute__((aligned(16))) char ex_lds[];
   ExactChain &Cg = chains[blockIdx.x];
@@ -651,6 +675,16 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     // (the next sweep's dish draws run on lanes 0 .. V-1)
     C.draws = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(C.draws >> 32)) << 32) |
               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)C.draws);
+    if (SV.z) {   // a saved sweep (gibbs.cpp:205-206): save_state into this chain's sample slot
+      const int64_t g = SV.sweep_base + (SV.ktot - todo);
+      if (g >= SV.burn && (g - SV.burn) % SV.thin == 0) {
+        const size_t slot = (size_t)blockIdx.x * SV.nslot + (size_t)((g - SV.first) / SV.thin);
+        __syncthreads();
+        exact_snapshot_wave(C, n, V, T, sh.hyp, lane, SV.z + slot * n, SV.dish + slot * V * SV.dcap, SV.dcap);
+        if (lane == 0) SV.T[slot] = T;
+        for (int q = lane; q < 3 * V + 2; q += MVC_WAVE) SV.hyp[slot * (3 * V + 2) + q] = sh.hyp[q];
+      }
+    }
   }
   if (status == MVC_ST_RUNNING) status = MVC_ST_DONE;
   __syncthreads();
@@ -1116,34 +1150,116 @@ class ExactSampler : public Sampler {
   // launch lasts about the longest chain's sum of sweeps rather than the sum
   // of the longest sweeps, and the per-sweep launch + read-back is amortised
   static constexpr int kSweepsPerLaunch = 64;
+  // k sweeps from every chain's current state in launches (capacity growth
+  // relaunches from where a chain stopped); SV: the in-kernel sample output
+  void run_launch(int k, const ExactSave &SV) {
+    for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; A.h.todo = k; }
+    push_structs();
+    hipEvent_t ev0 = nullptr;
+    timers.begin("sweep", &ev0);
+    for (int round = 0;; ++round) {
+      hipEvent_t ev = nullptr;
+      timers.begin("exact_sweep", &ev);
+      hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), lds_bytes(), stream,
+                         (const double *)y_dev, n, V, chains_dev, cfg.seed, lds_bytes(), SV);
+      MVC_HIP(hipGetLastError());
+      timers.end("exact_sweep", ev);
+      pull_structs();
+      bool again = false;
+      for (auto &A : chains) {
+        if (A.h.status == MVC_ST_OVERFLOW) { grow_chain(A); again = true; }
+        else if (A.h.status != MVC_ST_DONE) throw Error(MVC_ERR_STATE, "exact sweep kernel left a chain unfinished");
+      }
+      if (!again) break;
+      push_structs();
+      if (round > 64 + 64 * k) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
+    }
+    timers.end("sweep", ev0);
+    sweeps_done += k;
+  }
   void sweep(int n_sweeps) override {
     for (int left = n_sweeps; left > 0;) {
       const int k = std::min(left, kSweepsPerLaunch);
-      for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; A.h.todo = k; }
-      push_structs();
-      hipEvent_t ev0 = nullptr;
-      timers.begin("sweep", &ev0);
-      for (int round = 0;; ++round) {
-        hipEvent_t ev = nullptr;
-        timers.begin("exact_sweep", &ev);
-        hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), lds_bytes(), stream,
-                           (const double *)y_dev, n, V, chains_dev, cfg.seed, lds_bytes());
-        MVC_HIP(hipGetLastError());
-        timers.end("exact_sweep", ev);
-        pull_structs();
-        bool again = false;
-        for (auto &A : chains) {
-          if (A.h.status == MVC_ST_OVERFLOW) { grow_chain(A); again = true; }
-          else if (A.h.status != MVC_ST_DONE) throw Error(MVC_ERR_STATE, "exact sweep kernel left a chain unfinished");
-        }
-        if (!again) break;
-        push_structs();
-        if (round > 64 + 64 * k) throw Error(MVC_ERR_STATE, "capacity growth did not converge");
-      }
-      timers.end("sweep", ev0);
-      sweeps_done += k;
+      run_launch(k, ExactSave{});
       left -= k;
     }
+  }
+
+  // mvc_run's loop (gibbs.cpp:150-206) with every saved sweep written by the
+  // kernel itself (ExactSave): launches of up to kSweepsPerLaunch sweeps
+  // whatever the thinning, the samples of a launch read back in one copy.
+  // The device buffer holds one launch's samples of every chain (at most
+  // kSaveBudget bytes; fewer sweeps per launch when that is short).
+  static constexpr size_t kSaveBudget = (size_t)4 << 30;
+  bool run_saving(int n_iter, int burn_in, int thin, bool quiet, const SampleFn &fn) override {
+    const int C = (int)chains.size(), H = 3 * V + 2, dcap = std::max(n, 1);
+    const size_t per_sample = sizeof(int32_t) * ((size_t)n + (size_t)V * dcap + 1) + sizeof(double) * H;
+    const int64_t fit = (int64_t)(kSaveBudget / std::max<size_t>(1, per_sample * C));
+    if (fit < 1 || thin < 1) return false;
+    const int klim = (int)std::min<int64_t>(kSweepsPerLaunch, fit * thin);
+    int32_t *dz = nullptr, *dd = nullptr, *dT = nullptr;
+    double *dh = nullptr;
+    std::vector<int32_t> hz, hd, hT, dtmp;
+    std::vector<double> hh;
+    int nslot = 0;
+    try {
+      for (int it0 = 0; it0 < n_iter;) {
+        const int k = std::min(klim, n_iter - it0);
+        // the saved sweeps of [it0, it0 + k): global index = sweeps_done + offset
+        const int64_t g0 = sweeps_done;
+        auto saved = [&](int it) { return it >= burn_in && (it - burn_in) % thin == 0; };
+        int first = -1, m = 0;
+        for (int it = it0; it < it0 + k; ++it)
+          if (saved(it)) { if (first < 0) first = it; ++m; }
+        ExactSave SV{};
+        if (m > 0) {
+          if (m > nslot) {
+            for (void *p : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (p) hipFree(p);
+            dz = dd = dT = nullptr; dh = nullptr;
+            nslot = m;
+            MVC_HIP(hipMalloc(&dz, sizeof(int32_t) * (size_t)C * nslot * std::max(n, 1)));
+            MVC_HIP(hipMalloc(&dd, sizeof(int32_t) * (size_t)C * nslot * V * dcap));
+            MVC_HIP(hipMalloc(&dT, sizeof(int32_t) * (size_t)C * nslot));
+            MVC_HIP(hipMalloc(&dh, sizeof(double) * (size_t)C * nslot * H));
+          }
+          SV.z = dz; SV.dish = dd; SV.T = dT; SV.hyp = dh;
+          SV.dcap = dcap; SV.nslot = nslot; SV.ktot = k; SV.thin = thin;
+          // sweep it of the call is global sweep g0 + (it - it0)
+          SV.sweep_base = g0;
+          SV.burn = g0 + (burn_in - it0);
+          SV.first = g0 + (first - it0);
+        }
+        run_launch(k, SV);
+        if (!quiet)
+          for (int it = it0; it < it0 + k; ++it)
+            if ((it + 1) % 100 == 0) std::fprintf(stderr, "Iteration %d / %d\n", it + 1, n_iter);   // gibbs.cpp:152-155
+        if (m > 0) {   // samples in order, chain by chain (the callback's per-chain order)
+          hz.resize((size_t)C * nslot * n); hd.resize((size_t)C * nslot * V * dcap);
+          hT.resize((size_t)C * nslot); hh.resize((size_t)C * nslot * H);
+          MVC_HIP(hipMemcpyAsync(hz.data(), dz, sizeof(int32_t) * hz.size(), hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipMemcpyAsync(hd.data(), dd, sizeof(int32_t) * hd.size(), hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipMemcpyAsync(hT.data(), dT, sizeof(int32_t) * hT.size(), hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipMemcpyAsync(hh.data(), dh, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipStreamSynchronize(stream));
+          for (int sm = 0; sm < m; ++sm)
+            for (int c = 0; c < C; ++c) {
+              const size_t slot = (size_t)c * nslot + sm;
+              const int T = hT[slot];
+              dtmp.assign((size_t)V * T, 0);
+              for (int v = 0; v < V; ++v)
+                std::copy(hd.begin() + (slot * V + v) * dcap, hd.begin() + (slot * V + v) * dcap + T,
+                          dtmp.begin() + (size_t)v * T);
+              fn(c, T, hz.data() + slot * n, dtmp.data(), hh.data() + slot * H);
+            }
+        }
+        it0 += k;
+      }
+    } catch (...) {
+      for (void *p : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (p) hipFree(p);
+      throw;
+    }
+    for (void *p : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (p) hipFree(p);
+    return true;
   }
 
   void synchronize() override { MVC_HIP(hipStreamSynchronize(stream)); timers.collect(); }

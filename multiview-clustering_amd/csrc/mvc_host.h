@@ -118,6 +118,13 @@ class Sampler {
   // Every chain's sample at once (one snapshot, read back asynchronously;
   // fn(chain, ...) runs for chains 0..C-1 in order); false where unsupported.
   virtual bool save_all_async(const SampleFn &fn) { (void)fn; return false; }
+  // mvc_run's whole loop (gibbs.cpp:150-206) with the saved sweeps written on
+  // the device as the sweeps run (fn per chain and sample, in sample order);
+  // false where unsupported (the caller then sweeps and saves itself).
+  virtual bool run_saving(int n_iter, int burn_in, int thin, bool quiet, const SampleFn &fn) {
+    (void)n_iter; (void)burn_in; (void)thin; (void)quiet; (void)fn;
+    return false;
+  }
   // Device pointer to the chain's table labels [n] (valid until the next
   // sweep; the stream is synchronised), or nullptr when they live on the host.
   virtual const int32_t *device_labels(int chain) { (void)chain; return nullptr; }
