@@ -16,24 +16,26 @@
 
 namespace {
 
-// multiview_utils.cpp:307-338 compute_f_vk, literal expression order.
-__device__ __forceinline__ double ref_f_vk(int nk, double S1, double S2, double tau, double yvi) {
+// multiview_utils.cpp:307-338 compute_f_vk, literal expression order.  l2pt
+// is mvc_log(2.0 * MVC_PI * tau), the same value for every dish of a view
+// until the MH moves tau, so the caller computes it once per view and sweep.
+__device__ __forceinline__ double ref_f_vk(int nk, double S1, double S2, double tau, double yvi, double l2pt) {
   const double term1_old = -0.5 * S2 / tau;
   const double term2_old = 0.5 * (S1 * S1) / (tau * (tau + nk));
-  const double log_det_old = -0.5 * nk * mvc_log(2.0 * MVC_PI * tau) - 0.5 * mvc_log(tau * (tau + nk));
+  const double log_det_old = -0.5 * nk * l2pt - 0.5 * mvc_log(tau * (tau + nk));
   const int n_new = nk + 1;
   const double S1_new = S1 + yvi;
   const double S2_new = S2 + yvi * yvi;
   const double term1_new = -0.5 * S2_new / tau;
   const double term2_new = 0.5 * (S1_new * S1_new) / (tau * (tau + n_new));
-  const double log_det_new = -0.5 * n_new * mvc_log(2.0 * MVC_PI * tau) - 0.5 * mvc_log(tau * (tau + n_new));
+  const double log_det_new = -0.5 * n_new * l2pt - 0.5 * mvc_log(tau * (tau + n_new));
   const double lp = (log_det_new + term1_new + term2_new) - (log_det_old + term1_old + term2_old);
   return mvc_exp(lp);
 }
 
-// multiview_utils.cpp:340-350 compute_f_vk_new
-__device__ __forceinline__ double ref_f_new(double tau, double yvi) {
-  const double log_norm = -0.5 * mvc_log(2.0 * MVC_PI * tau);
+// multiview_utils.cpp:340-350 compute_f_vk_new (l2pt as in ref_f_vk)
+__device__ __forceinline__ double ref_f_new(double tau, double yvi, double l2pt) {
+  const double log_norm = -0.5 * l2pt;
   const double log_exp = -0.5 * (yvi * yvi) / tau;
   return mvc_exp(log_norm + log_exp);
 }
@@ -49,6 +51,7 @@ struct Shared {
   double hyp[3 * MVC_MAXV + 2];
   double ys[MVC_MAXV];
   double fnew[MVC_MAXV];
+  double l2pt[MVC_MAXV];   // mvc_log(2 pi tau_v) of the current sweep
   double marg[MVC_MAXV];
   double tw[MVC_MAXV];
   double buf[MVC_WAVE];
@@ -409,6 +412,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
 
   for (; todo > 0; --todo, i = 0) {   // the launch's sweeps, each from customer resume_i / 0
     const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];   // the MH of the previous sweep may have moved them
+    if (lane < V) sh.l2pt[lane] = mvc_log(2.0 * MVC_PI * tau[lane]);   // (read after the barrier of customer i's first step)
     for (; i < n; ++i) {
       // -------- capacity guard (every step may add 1 table and 1 dish/view)
       int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
@@ -501,11 +505,12 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         int v = 0;
         while (sh.Koff[v + 1] <= e) ++v;
         const int j = e - sh.Koff[v];
-        const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v]);
+        const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v],
+                                  sh.l2pt[v]);
         C.f[v * KC + j] = f;
         C.logf[v * KC + j] = mvc_log(f);
       }
-      if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane]);
+      if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane], sh.l2pt[lane]);
       __syncthreads();
 
       // ---------------- marginal of a new table per view (utils.cpp:40-69)
