@@ -1745,6 +1745,8 @@ constexpr int kSeqWmin = 1024;     // repair window after a mover
 constexpr int kSeqWmax = 1 << 16;  // cap of the window doubling over mover-free stretches
 constexpr int kSeqRunLimit = 64;   // stays in a row after which the run kernel hands over to grid windows
 constexpr size_t kSeqLdsBudget = 150 * 1024;   // run kernel: per-wave LDS scratch of all its waves
+constexpr int kWideGridMax = 256;  // grid-wide evaluation: at most this many blocks per customer
+constexpr int kWideBatch = 32;     // grid-wide evaluation: customers (lp + fin pairs) per repair round
 
 template <class Tp>
 Tp *dmalloc(size_t count) {
@@ -1853,6 +1855,8 @@ class ParallelSampler : public Sampler {
   // customer's issue rate, and with dense movers the first customer decides)
   int run_waves = 4;
   bool use_wide = true;           // MVC_WIDE=0: global-scratch run kernel speculates one customer per wave
+  bool wide_grid = true;          // MVC_WIDE=block: the wide evaluation on the run kernel's one block instead of the grid
+  double *wide_part = nullptr;    // grid-wide evaluation: per-block partials [kWideGridMax][2V]
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
   bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
@@ -2066,7 +2070,10 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
     if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
     if (const char *e = getenv("MVC_VP_STATS")) vp_stats = e[0] == '1';
-    if (const char *e = getenv("MVC_WIDE")) use_wide = e[0] != '0';
+    if (const char *e = getenv("MVC_WIDE")) {
+      use_wide = e[0] != '0';
+      wide_grid = e[0] != 'b';
+    }
     if (const char *e = getenv("MVC_EARLY_MH")) early_mh_off = e[0] == '0';
     if (const char *e = getenv("MVC_RUN_LDS")) force_global = e[0] == '0';
     chains.resize(cf.n_chains);
@@ -2191,7 +2198,7 @@ class ParallelSampler : public Sampler {
       for (void *p : {(void *)y, (void *)Y2, (void *)yt})
         if (p) hipFree(p);
     for (void *p : {(void *)seq_scr, (void *)lpb, (void *)part1, (void *)part2, (void *)vmax,
-                    (void *)zsc})
+                    (void *)zsc, (void *)wide_part})
       if (p) hipFree(p);
     if (st_host) hipHostFree(st_host);
     if (rs_host) hipHostFree(rs_host);
@@ -2741,10 +2748,31 @@ class ParallelSampler : public Sampler {
     if (early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
     int rounds = 1;
     for (;;) {
+      // the grid-wide evaluation where the state is on the global layout (L.lds = 0) and
+      // the block-wide evaluation applies (L.tw > 1): one customer over many CUs
+      const bool wgrid = !repair_grid_only && wide_grid && L.lds == 0 && L.tw > 1;
+      int wblk = 1;
+      if (wgrid) {
+        if (!wide_part) wide_part = dmalloc<double>((size_t)kWideGridMax * 2 * V);
+        // blocks for the dish list (plus the births a round may add): two 64-dish chunks per wave
+        int nk = 0;
+        for (int k : c.K) nk += k;
+        nk += nk / 4 + 64;
+        wblk = std::max(1, std::min(kWideGridMax, (nk + 2 * kWideGridThreads - 1) / (2 * kWideGridThreads)));
+      }
       for (int r = 0; r < rounds; ++r) {
         if (repair_grid_only)
           hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
-        else {
+        else if (wgrid) {
+          hipLaunchKernelGGL(mvc_seq_wide_begin_kernel, dim3(1), dim3(64), 0, stream, Q);
+          for (int b = 0; b < kWideBatch; ++b) {
+            hipLaunchKernelGGL(mvc_seq_wide_lp_kernel, dim3(wblk), dim3(kWideGridThreads), 0, stream, Q, wide_part);
+            hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, Q,
+                               (const double *)wide_part, wblk, L.limit);
+          }
+          MVC_HIP(hipGetLastError());
+          dbg("seq_wide (begin + lp/fin pairs)", c, s);
+        } else {
           L.dyn = L.lds ? 8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D) +
                                (L.lc == 2 ? (int64_t)kVpE * D : 0))
                         : 0;

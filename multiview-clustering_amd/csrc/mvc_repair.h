@@ -651,8 +651,11 @@ __device__ int seq_resample(const SeqArgs &A, const SView &W, const Cust &C, int
 // the draw.  Same operations in the same order per quantity as seq_resample,
 // so the same bits.  Block-wide (seven __syncthreads); S is the team's
 // scratch (wave 0's), S.wide its shared values.  Returns the pick on member 0.
+// rest_only: pass 1 (the lp rows) and the per-member max / count already ran
+// elsewhere (the grid-wide evaluation, mvc_seq_wide_lp_kernel): S.lp holds the
+// rows and member row 0 of pmx / pcnt the combined max / count per view.
 __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
-                                 int r, int tw, bool act) {
+                                 int r, int tw, bool act, bool rest_only = false) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
   const int V = P.V, D = P.D, ts = W.ts, ks = W.ks, lps = S.lps;
@@ -695,7 +698,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
   constexpr int kWideY = 2048;
   __shared__ double s_yw[kWideY];
   const bool ylds = V * D <= kWideY;
-  if (ylds) {
+  if (ylds && !rest_only) {
     if (act)
       for (int e = threadIdx.x; e < V * D; e += blockDim.x) {
         const int v = e / D, d = e - v * D;
@@ -704,7 +707,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
     __syncthreads();
   }
   // pass 1: lp, two dishes per lane (chunks c and c + tw), two fma chains in ascending d
-  if (act && ylds) {
+  if (act && ylds && !rest_only) {
     for (int c = r; 64 * c < NK; c += 2 * tw) {
       const int ga = 64 * c + lane, gb = 64 * (c + tw) + lane;
       const bool va = ga < NK, vb = gb < NK;
@@ -737,7 +740,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
       if (vb) S.lp[v_b * lps + j_b] = lp_val(v_b, j_b, acc_b);
     }
   }
-  if (act && !ylds) {
+  if (act && !ylds && !rest_only) {
     for (int c = r; 64 * c < NK; c += 2 * tw) {
       const int ga = 64 * c + lane, gb = 64 * (c + tw) + lane;
       const bool va = ga < NK, vb = gb < NK;
@@ -774,7 +777,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
   }
   __syncthreads();
   // per-member max / count of the included dishes, four views at once (rows)
-  if (act) {
+  if (act && !rest_only) {
     for (int vg = 0; vg < V; vg += 4) {
       const int v = vg + row;
       double mx = -MVC_PM_INF;
@@ -804,7 +807,7 @@ __device__ int seq_resample_wide(const SeqArgs &A, const SView &W, const Cust &C
     for (int v = lane; v < V; v += 64) {
       double mx = -MVC_PM_INF;
       int cnt = 0;
-      for (int q = 0; q < tw; ++q) {
+      for (int q = 0; q < (rest_only ? 1 : tw); ++q) {
         const double x = pmx[q * V + v];
         if (x > mx) mx = x;
         cnt += (int)pcnt[q * V + v];
@@ -2132,6 +2135,269 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_birth_kerne
     // the birth was the sweep's last customer: every customer is final (a
     // run kernel must not start its loop at cur == n)
     if (R->cur >= A.P.n) R->done = 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Grid-wide evaluation: where the state outgrows the run
+// kernel's LDS (the Reuters transient: T ~ 18k tables, thousands of dishes per
+// view) nearly every customer moves and one customer's evaluation is long
+// (sum K_v D dot products against S1 columns in HBM, T V table gathers), so a
+// customer is spread over the whole grid: a round is
+//   mvc_seq_wide_begin_kernel   resolve the last grid window (as the run kernel);
+//   B x { mvc_seq_wide_lp_kernel   the lp rows of customer cur over every block
+//                                  (pass 1 of seq_resample_wide), per-block max /
+//                                  count of the included dishes per view;
+//         mvc_seq_wide_fin_kernel  one block: the rest of seq_resample_wide from
+//                                  the combined partials (the order-sensitive sums
+//                                  on wave 0), then the decision and its commit
+//                                  (births draw their dishes from the same rows) };
+//   mvc_seq_eval_kernel         the grid window when the stays run long.
+// Every quantity has the operations and order of seq_resample_wide, so the
+// decisions are the oracle's bit for bit; only the partition of the
+// order-free max / count over the dishes differs.
+// ---------------------------------------------------------------------------
+constexpr int kWideGridThreads = 256;
+extern "C" __global__ void mvc_seq_wide_begin_kernel(SeqArgs A) {
+  if (threadIdx.x != 0) return;
+  Repair *R = A.R;
+  const int n = A.P.n;
+  const int go = !(R->done || R->overflow || R->restride);
+  if (go && R->win1 > R->win0) {
+    seq_resolve_window(A, R);
+    if (R->pend) {
+      R->mode = kSeqRun;
+      R->streak = 0;
+    }
+  }
+  if (!go) return;
+  R->rounds += 1;
+  if (!(R->mode == kSeqRun || R->pend)) {   // scan mode: the next grid window
+    if (R->cur >= n) {
+      R->done = 1;
+    } else {
+      R->win0 = R->cur;
+      R->win1 = min(n, R->cur + R->W);
+      R->fmin = n;
+    }
+  } else if (R->cur >= n && !R->pend) {
+    R->done = 1;
+  }
+}
+
+// part: [gridDim.x][2 V] per-block max (or -inf) and count (as a double)
+extern "C" __global__ __launch_bounds__(kWideGridThreads) void mvc_seq_wide_lp_kernel(SeqArgs A, double *part) {
+  const Repair *R = A.R;
+  const ParState &P = A.P;
+  if (R->done || R->overflow || R->restride || R->mode != kSeqRun || R->pend || R->cur >= P.n) return;   // block-uniform
+  const int i = R->cur;
+  const int V = P.V, D = P.D;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  constexpr int NW = kWideGridThreads / 64;
+  const int gr = blockIdx.x * NW + w, gtw = gridDim.x * NW;
+  const SView W = global_view(A);
+  const SeqScratch S(A, 0);
+  const Cust C = global_cust(A, i);
+  const int p0 = P.z[i];
+  const bool alive = (W.n_t[p0] - 1) > 0;
+  const int ts = W.ts, ks = W.ks, lps = S.lps;
+  __shared__ double s_mx[NW][MVC_MAXV];
+  __shared__ int s_cnt[NW][MVC_MAXV];
+  constexpr int kWideY = 2048;
+  __shared__ double s_yw[kWideY];
+  const bool ylds = V * D <= kWideY;
+  for (int v = lane; v < V; v += 64) {
+    s_mx[w][v] = -MVC_PM_INF;
+    s_cnt[w][v] = 0;
+  }
+  if (ylds)
+    for (int e = tid; e < V * D; e += blockDim.x) {
+      const int v = e / D, d = e - v * D;
+      s_yw[e] = C.y[(size_t)v * C.ystride + d];
+    }
+  __syncthreads();
+  int NK = 0;
+  for (int v = 0; v < V; ++v) NK += W.Klist[v];
+  auto locate = [&](int g, int &v, int &j) {
+    v = 0;
+    int off = 0;
+    while (v + 1 < V && g >= off + W.Klist[v]) { off += W.Klist[v]; ++v; }
+    j = g - off;
+  };
+  // lp of dish j of view v from its dot product G (seq_resample_wide's lp_val)
+  auto lp_val = [&](int v, int j, double G) -> double {
+    const double tau = P.hyper[v];
+    const double Y2i = C.Y2[(size_t)v * C.y2stride];
+    const double hy = 0.5 * Y2i;
+    const double h = (-0.5 * Y2i) / tau;
+    if (j == W.dish[v * ts + p0]) {
+      const double Gp = G - Y2i;
+      const double Qp = (W.Q[v * ks + j] - 2.0 * G) + Y2i;
+      const Coef c = coef(W.d_n[v * ks + j] - 1, Qp, tau, A.L2pt[v], D);
+      return __builtin_fma(Gp + hy, c.cb, c.c0) + h;
+    }
+    return __builtin_fma(G + hy, W.cb[v * ks + j], W.c0[v * ks + j]) + h;
+  };
+  // the chunk's views (its dishes are consecutive in the concatenated list): a
+  // segmented max / count of the included dishes into this wave's row
+  auto fold = [&](int g, bool valid, int v, int j, double x) {
+    const int gl = min(64 * (g / 64) + 63, NK - 1);
+    int vf, jf, vl, jl;
+    locate(64 * (g / 64), vf, jf);
+    locate(gl, vl, jl);
+    bool inc = false;
+    if (valid) {
+      const int l = W.d_l[v * ks + j] - ((j == W.dish[v * ts + p0] && !alive) ? 1 : 0);
+      inc = l > 0;
+    }
+    for (int vv = vf; vv <= vl; ++vv) {
+      const bool in = inc && v == vv;
+      const double m = wave_max(in ? x : -MVC_PM_INF);
+      const int c = wave_count(in);
+      if (lane == 0) {
+        if (m > s_mx[w][vv]) s_mx[w][vv] = m;
+        s_cnt[w][vv] += c;
+      }
+    }
+  };
+  // pass 1 of seq_resample_wide: two dishes per lane (chunks c and c + gtw),
+  // two fma chains in ascending d
+  for (int c = gr; 64 * c < NK; c += 2 * gtw) {
+    const int ga = 64 * c + lane, gb = 64 * (c + gtw) + lane;
+    const bool va = ga < NK, vb = gb < NK;
+    int v_a = 0, j_a = 0, v_b = 0, j_b = 0;
+    if (va) locate(ga, v_a, j_a);
+    if (vb) locate(gb, v_b, j_b);
+    const double *sa = W.S1T + (size_t)v_a * D * W.s1s + j_a, *sb = W.S1T + (size_t)v_b * D * W.s1s + j_b;
+    const size_t bs = (size_t)W.s1s;
+    double acc_a = 0.0, acc_b = 0.0;
+    if (ylds) {
+      const int oa = v_a * D, ob = v_b * D;
+      int d = 0;
+      for (; d + 16 <= D; d += 16) {
+        double za[16], zb[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          za[u] = sa[(size_t)(d + u) * bs];
+          zb[u] = sb[(size_t)(d + u) * bs];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          acc_a = __builtin_fma(s_yw[oa + d + u], za[u], acc_a);
+          acc_b = __builtin_fma(s_yw[ob + d + u], zb[u], acc_b);
+        }
+      }
+      for (; d < D; ++d) {
+        acc_a = __builtin_fma(s_yw[oa + d], sa[(size_t)d * bs], acc_a);
+        acc_b = __builtin_fma(s_yw[ob + d], sb[(size_t)d * bs], acc_b);
+      }
+    } else {
+      const double *ya = C.y + (size_t)v_a * C.ystride, *yb = C.y + (size_t)v_b * C.ystride;
+      for (int d = 0; d < D; ++d) {
+        acc_a = __builtin_fma(ya[d], sa[(size_t)d * bs], acc_a);
+        acc_b = __builtin_fma(yb[d], sb[(size_t)d * bs], acc_b);
+      }
+    }
+    const double xa = va ? lp_val(v_a, j_a, acc_a) : 0.0, xb = vb ? lp_val(v_b, j_b, acc_b) : 0.0;
+    if (va) S.lp[v_a * lps + j_a] = xa;
+    if (vb) S.lp[v_b * lps + j_b] = xb;
+    fold(64 * c, va, v_a, j_a, xa);
+    if (64 * (c + gtw) < NK) fold(64 * (c + gtw), vb, v_b, j_b, xb);
+  }
+  __syncthreads();
+  for (int v = tid; v < V; v += blockDim.x) {   // the block's partials (max and count: order-free)
+    double m = -MVC_PM_INF;
+    int cnt = 0;
+    for (int q = 0; q < NW; ++q) {
+      if (s_mx[q][v] > m) m = s_mx[q][v];
+      cnt += s_cnt[q][v];
+    }
+    part[(size_t)blockIdx.x * 2 * V + v] = m;
+    part[(size_t)blockIdx.x * 2 * V + V + v] = (double)cnt;
+  }
+}
+
+// One block of kSeqRunThreads: a pending mover from a resolved window is
+// committed; otherwise customer cur is decided from the lp rows and partials
+// of mvc_seq_wide_lp_kernel (nblk blocks) and committed when it moves.  After
+// `limit` stays in a row (stay_limit) it hands over to the grid windows.
+extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_kernel(SeqArgs A, const double *part,
+                                                                                     int nblk, int limit) {
+  Repair *R = A.R;
+  ParState &P = A.P;
+  const int tid = threadIdx.x, w = tid >> 6, nw = blockDim.x >> 6;
+  const int n = P.n, V = P.V;
+  __shared__ int s_go, s_i, s_pend, s_pc, s_c;
+  if (tid == 0) {
+    s_go = !(R->done || R->overflow || R->restride) && R->mode == kSeqRun && R->cur < n;
+    s_i = R->cur;
+    s_pend = R->pend;
+    s_pc = R->pchoice;
+  }
+  __syncthreads();
+  if (!s_go) return;
+  const int i = s_i;
+  const int p0 = P.z[i];
+  const SeqScratch Sw(A, w);
+  if (s_pend) {   // a window's first mover (its lp rows are not in the scratch: computed by the commit)
+    if (!seq_commit(A, global_view(A), nullptr, global_cust(A, i), i, p0, s_pc, Sw.lp, Sw.tree, &R->moves, nw))
+      return;   // overflow: the host grows and the next round redoes this commit
+    if (tid == 0) {
+      R->cur = i + 1;
+      R->pend = 0;
+      R->streak = 0;
+      if (R->cur >= n) R->done = 1;
+    }
+    return;
+  }
+  const SeqScratch S0(A, 0);
+  {   // the per-block partials combined into member row 0 of the wide scratch
+    double *pmx = S0.wide + V + 8, *pcnt = pmx + 8 * V;
+    for (int v = tid; v < V; v += blockDim.x) {
+      double m = -MVC_PM_INF, c = 0.0;
+      for (int b = 0; b < nblk; ++b) {
+        const double x = part[(size_t)b * 2 * V + v];
+        if (x > m) m = x;
+        c += part[(size_t)b * 2 * V + V + v];   // integers below 2^53: exact in any order
+      }
+      pmx[v] = m;
+      pcnt[v] = c;
+    }
+  }
+  __syncthreads();
+  const int c = seq_resample_wide(A, global_view(A), global_cust(A, i), i, p0, S0, w, nw, true, true);
+  if (tid == 0) s_c = c;   // member 0's pick
+  __syncthreads();
+  const int ch = s_c;
+  if (ch == p0) {   // stays
+    if (tid == 0) {
+      R->cur = i + 1;
+      R->streak += 1;
+      if (R->streak >= stay_limit(limit, R->gapq)) {
+        R->mode = kSeqScan;
+        if (R->cur < n) {
+          R->win0 = R->cur;
+          R->win1 = min(n, R->cur + R->W);
+          R->fmin = n;
+        }
+      }
+      if (R->cur >= n) R->done = 1;
+    }
+    return;
+  }
+  // a move or a birth: committed on the global state, dish draws from the rows above
+  if (!seq_commit(A, global_view(A), nullptr, global_cust(A, i), i, p0, ch, Sw.lp, Sw.tree, &R->moves, nw, &S0)) {
+    if (tid == 0) {   // overflow: left pending (the next round commits it after the growth)
+      R->pend = 1;
+      R->pchoice = ch;
+    }
+    return;
+  }
+  if (tid == 0) {
+    note_mover(R->lastm, R->gapq, i);
+    R->cur = i + 1;
+    R->streak = 0;
+    if (R->cur >= n) R->done = 1;
   }
 }
 

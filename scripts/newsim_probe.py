@@ -15,14 +15,14 @@ from mvc_amd import data  # noqa: E402
 y, _ = data.new_simulation(1999)
 out = {}
 for mode, C, M in (("exact", 1, 2000), ("parallel", 1, 2000), ("exact", 256, 500), ("exact", 1024, 500),
-                   ("exact", 2048, 500)):
+                   ("exact", 1536, 500), ("exact", 2048, 500)):
     t0 = time.perf_counter()
     mvc_amd.run_gibbs_cpp(y, M, M // 2, 1, seed=1999, mode=mode, n_chains=C, quiet=True)
     dt = time.perf_counter() - t0
     out[f"{mode}_{C}"] = {"chains": C, "sweeps": M, "s": round(dt, 3), "chain_sweeps_per_s": round(C * M / dt, 1)}
     print(f"{mode} {C} chains: {C * M / dt:.1f} chain-sweeps/s", file=sys.stderr, flush=True)
 # the same without mvc_run's sample bookkeeping: sweeps only
-for mode, C, M in (("exact", 1, 2000), ("exact", 256, 500), ("exact", 2048, 500)):
+for mode, C, M in (("exact", 1, 2000), ("exact", 256, 500), ("exact", 1536, 500), ("exact", 2048, 500)):
     smp = mvc_amd.Sampler(y, seed=1999, mode=mode, n_chains=C)
     smp.sweep(2)
     smp.synchronize()

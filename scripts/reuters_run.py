@@ -31,11 +31,21 @@ def main():
     ap.add_argument("--budget-s", type=float, default=150.0)
     ap.add_argument("--drop-topics", action="store_true",
                     help="zero the TOPICS columns of the third view (the ARI truth; mvc_amd.reuters)")
+    ap.add_argument("--save", default=None, help="write every chain's state here (npz) at the end")
+    ap.add_argument("--resume", default=None,
+                    help="start every chain from a state --save wrote (the chains continue with fresh sweep "
+                         "counters: a valid continuation of each chain, not the bitwise one)")
     a = ap.parse_args()
     y = reuters.views(drop_topics=a.drop_topics)
     lab, names, _ = reuters.topic_truth()
     sel = lab >= 0
     s = mvc_amd.Sampler(y, seed=a.seed, mode="parallel", n_chains=a.chains)
+    start = 0
+    if a.resume:
+        st = np.load(a.resume)
+        start = int(st["sweeps"])
+        for c in range(a.chains):
+            s.set_state(st[f"t{c}"], st[f"d{c}"], st[f"h{c}"], chain=c)
     s.synchronize()
     t_all = time.perf_counter()
     for it in range(a.sweeps):
@@ -43,21 +53,30 @@ def main():
         s.sweep(1)
         s.synchronize()
         dt = time.perf_counter() - t0
-        rec = {"sweep": it, "s": round(dt, 4), "drop_topics": a.drop_topics}
-        Ts, aris, moves = [], [], []
+        rec = {"sweep": start + it, "s": round(dt, 4), "drop_topics": a.drop_topics}
+        Ts, aris, moves, taus = [], [], [], []
         for c in range(a.chains):
             t, d, h = s.state(chain=c)
             Ts.append(int(d.shape[1]))
+            taus.append([round(float(x), 5) for x in h["tau_v"]])
             moves.append(s.repair_stats(chain=c)["moves"])
             if (it + 1) % a.ari_every == 0 or it == a.sweeps - 1:
                 aris.append(round(float(mvc_amd.ari(t[sel], lab[sel])), 4))
         rec["T"] = Ts
         rec["moves"] = moves
+        rec["tau_v_chain0"] = taus[0]
         if aris:
             rec["ari_top6"] = aris
         print(json.dumps(rec), flush=True)
         if time.perf_counter() - t_all > a.budget_s:
             break
+    if a.save:
+        out = {"sweeps": np.int64(start + it + 1)}
+        for c in range(a.chains):
+            t, d, h = s.state(chain=c)
+            hv = np.concatenate([h["tau_v"], h["alpha_v"], h["sigma_v"], [h["alpha_global"], h["sigma_global"]]])
+            out[f"t{c}"], out[f"d{c}"], out[f"h{c}"] = t, d, hv
+        np.savez(a.save, **out)
     s.close()
 
 

@@ -715,7 +715,7 @@ def test_shard_ranks_equal_unsharded(world, tmp_path):
     s.close()
 
 
-@pytest.mark.parametrize("wide,V", [("1", 3), ("0", 3), ("1", 5)])
+@pytest.mark.parametrize("wide,V", [("1", 3), ("0", 3), ("1", 5), ("block", 3), ("block", 5)])
 def test_repair_global_wide(wide, V, monkeypatch):
     """The run kernel on its global-scratch layout (MVC_RUN_LDS=0, as when
     the state outgrows the LDS): the whole block evaluating one customer
