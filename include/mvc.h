@@ -108,6 +108,11 @@ const int32_t *mvc_result_dish_of(const mvc_result *r, int chain, int s);       
 #define MVC_TRACE_ALPHA_GLOBAL 3
 #define MVC_TRACE_SIGMA_GLOBAL 4
 const double *mvc_result_trace(const mvc_result *r, int chain, int which);
+/* Every saved sample of one chain in one call (bulk form of the three
+ * accessors above): table_of[S][n], n_tables[S], dish_of = the samples'
+ * view-major [V][T_s] blocks one after the other (V * sum_s T_s entries).
+ * Any pointer may be NULL (e.g. n_tables alone first, to size dish_of). */
+int mvc_result_copy_chain(const mvc_result *r, int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of);
 /* Posterior summary over every chain's saved samples (no reference
  * counterpart: the reference runs one chain).  mean[3V+2] and rhat[3V+2] in
  * the hyper order tau[V], alpha[V], sigma[V], alpha_g, sigma_g: pooled means

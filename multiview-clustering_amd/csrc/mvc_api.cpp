@@ -671,6 +671,17 @@ const int32_t *mvc_result_dish_of(const mvc_result *r, int chain, int s) {
   if (!r || chain < 0 || chain >= r->C || s < 0 || s >= r->S) return nullptr;
   return r->dish_of[chain][s].data();
 }
+int mvc_result_copy_chain(const mvc_result *r, int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of) {
+  if (!r || chain < 0 || chain >= r->C) return MVC_ERR_ARG;
+  size_t off = 0;
+  for (int s = 0; s < r->S; ++s) {
+    if (table_of) std::copy(r->table_of[chain][s].begin(), r->table_of[chain][s].end(), table_of + (size_t)s * r->n);
+    if (n_tables) n_tables[s] = r->T[chain][s];
+    if (dish_of) std::copy(r->dish_of[chain][s].begin(), r->dish_of[chain][s].end(), dish_of + off);
+    off += r->dish_of[chain][s].size();
+  }
+  return MVC_OK;
+}
 const double *mvc_result_trace(const mvc_result *r, int chain, int which) {
   if (!r || chain < 0 || chain >= r->C || which < 0 || which > 4) return nullptr;
   return r->traces[chain][which].data();

@@ -104,6 +104,7 @@ def lib():
         "mvc_result_table_of": (ip, [vp, i32, i32]),
         "mvc_result_dish_of": (ip, [vp, i32, i32]),
         "mvc_result_trace": (dp, [vp, i32, i32]),
+        "mvc_result_copy_chain": (i32, [vp, i32, ip, ip, ip]),
         "mvc_result_summary": (i32, [vp, dp, dp]),
         "mvc_result_free": (None, [vp]),
         "mvc_sampler_create": (i32, [cfgp, ctypes.POINTER(dp), vpp, cp, sz]),

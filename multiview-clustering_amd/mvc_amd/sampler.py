@@ -16,6 +16,7 @@ libmvc_hip.so.  Errors from the library raise ``MvcError`` (the reference
 raises R conditions via Rcpp::stop, multiview_utils.cpp:141,145).
 """
 import ctypes
+import time
 
 import numpy as np
 
@@ -75,7 +76,7 @@ def _view_ptrs(y):
 
 
 def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chains=1, device=0,
-                  first_chain=0, quiet=False, n_devices=1, summary=None):
+                  first_chain=0, quiet=False, n_devices=1, summary=None, timing=None):
     """Drop-in for the reference's ``run_gibbs_cpp`` (see module docstring).
 
     With ``n_chains > 1`` a list of per-chain result dicts is returned; the
@@ -83,7 +84,9 @@ def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chain
     n_devices``, one host thread per device).  ``summary`` (a dict) receives
     the pooled posterior means and Gelman-Rubin R-hat of the hyperparameters
     (mvc_result_summary: keys ``mean`` and ``rhat``, float64[3V+2] in the
-    order tau_v, alpha_v, sigma_v, alpha_global, sigma_global).
+    order tau_v, alpha_v, sigma_v, alpha_global, sigma_global).  ``timing``
+    (a dict) receives ``mvc_run_s``, the seconds of the library call alone
+    (the rest is building these Python lists).
     """
     y = _views_to_array(data_views)
     V, n, D = y.shape
@@ -92,7 +95,10 @@ def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chain
     lib = L.lib()
     res = ctypes.c_void_p()
     buf = L.errbuf()
+    t0 = time.perf_counter()
     L.check(lib.mvc_run(ctypes.byref(cfg), _view_ptrs(y), ctypes.byref(res), buf, len(buf)), buf)
+    if timing is not None:
+        timing["mvc_run_s"] = time.perf_counter() - t0
     try:
         S = lib.mvc_result_num_saved(res)
         if summary is not None:
@@ -101,14 +107,19 @@ def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chain
             lib.mvc_result_summary(res, mean.ctypes.data_as(dp), rhat.ctypes.data_as(dp))
             summary["mean"], summary["rhat"] = mean, rhat
         outs = []
+        ip = ctypes.POINTER(ctypes.c_int32)
         for c in range(n_chains):
-            table_of, dish_of = [], []
-            for s in range(S):
-                T = lib.mvc_result_num_tables(res, c, s)
-                t = np.ctypeslib.as_array(lib.mvc_result_table_of(res, c, s), shape=(n,)).copy()
-                d = np.ctypeslib.as_array(lib.mvc_result_dish_of(res, c, s), shape=(V * max(T, 1),))[: V * T]
-                d = d.copy().reshape(V, T)
-                table_of.append(t)
+            # every sample of the chain in two bulk copies (mvc_result_copy_chain)
+            Ts = np.zeros(S, dtype=np.int32)
+            lib.mvc_result_copy_chain(res, c, None, Ts.ctypes.data_as(ip), None)
+            tab = np.empty((S, n), dtype=np.int32)
+            dsh = np.empty(max(1, V * int(Ts.sum())), dtype=np.int32)
+            lib.mvc_result_copy_chain(res, c, tab.ctypes.data_as(ip), None, dsh.ctypes.data_as(ip))
+            table_of = list(tab)
+            ends = np.cumsum(V * Ts.astype(np.int64))
+            dish_of = []
+            for s, blk in enumerate(np.split(dsh[: int(ends[-1]) if S else 0], ends[:-1]) if S else []):
+                d = blk.reshape(V, int(Ts[s]))
                 dish_of.append([d[v] for v in range(V)])
 
             def tr(which, per_view):
