@@ -57,6 +57,7 @@ struct Shared {
   double buf[MVC_WAVE];
   double dv[4];
   int iv[8];
+  long long prof[8];   // MVC_EXACT_PROF: shader clocks per phase (ExactSave.prof)
 };
 
 // ---------------------------------------------------------------------------
@@ -349,6 +350,7 @@ struct ExactSave {
   double *hyp;         // [C][nslot][3V+2]
   int32_t dcap, nslot, ktot, thin;
   int64_t sweep_base, burn, first;   // global index of the launch's first sweep, burn-in, first saved sweep
+  long long *prof;     // MVC_EXACT_PROF=1: [C][8] shader clocks per phase of the customer step (else nullptr)
 };
 // table_of[i] = position of i's table; dish_of[v][p] = raw dish id (the
 // snapshot kernels' layout), by one wavefront
@@ -401,7 +403,20 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     sh.next_id[v] = C.next_id[v];
   }
   for (int q = lane; q < 3 * V + 2; q += MVC_WAVE) sh.hyp[q] = C.hyper[q];
+  if (lane < 8) sh.prof[lane] = 0;
   __syncthreads();
+  // phase clocks (diagnostic, off unless SV.prof): 0 remove, 1 f_vk, 2 marginals +
+  // table probabilities, 3 normaliser, 4 normalise + find, 5 join a table,
+  // 6 open a table, 7 MH + sample output
+  const bool prof = SV.prof != nullptr;
+  long long tp = prof ? clock64() : 0;
+  auto tick = [&](int k) {
+    if (prof) {
+      const long long t = clock64();
+      if (lane == 0) sh.prof[k] += t - tp;
+      tp = t;
+    }
+  };
 
   int T = C.T;
   int n_free = C.n_free;
@@ -493,6 +508,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         }
       }
 
+      tick(0);
       // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
       if (lane == 0) {
         int acc = 0;
@@ -512,6 +528,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
       }
       if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane], sh.l2pt[lane]);
       __syncthreads();
+      tick(1);
 
       // ---------------- marginal of a new table per view (utils.cpp:40-69)
       if (lane < V) {
@@ -563,6 +580,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
       }
       for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
       __syncthreads();
+      tick(2);
 
       // ---------------- normaliser, draw (gibbs.cpp:169-191)
       if (lane == 0) {
@@ -573,6 +591,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         sh.dv[1] = seq_sum8(p_new, T, [&](int p) { return C.P[p]; });
       }
       __syncthreads();
+      tick(3);
       const double sum_p = sh.dv[1];
       int t_star;
       if (sum_p <= 0.0) {
@@ -588,6 +607,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         __syncthreads();
         t_star = sh.iv[0];
       }
+      tick(4);
 
       if (t_star != -1) {
         // add_customer_to_existing_table (utils.cpp:194-207)
@@ -602,6 +622,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           C.d_S2[lane * KC + k] += yv * yv;
         }
         __syncthreads();
+        tick(5);
       } else {
         // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
         n_free -= 1;
@@ -668,6 +689,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         }
         C.draws += (uint64_t)sh.iv[1];
         __syncthreads();
+        tick(6);
       }
     }
 
@@ -690,9 +712,11 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         for (int q = lane; q < 3 * V + 2; q += MVC_WAVE) SV.hyp[slot * (3 * V + 2) + q] = sh.hyp[q];
       }
     }
+    tick(7);
   }
   if (status == MVC_ST_RUNNING) status = MVC_ST_DONE;
   __syncthreads();
+  if (prof && lane < 8) SV.prof[(size_t)blockIdx.x * 8 + lane] += sh.prof[lane];
   for (int v = lane; v < V; v += MVC_WAVE) {
     C.Kact[v] = sh.Kact[v];
     C.next_id[v] = sh.next_id[v];
@@ -952,7 +976,35 @@ class ExactSampler : public Sampler {
     }
     MVC_HIP(hipMalloc(&chains_dev, sizeof(ExactChain) * chains.size()));
     push_structs();
+    if (const char *e = getenv("MVC_EXACT_PROF"); e && e[0] == '1') {
+      MVC_HIP(hipMalloc(&prof_dev, sizeof(long long) * 8 * chains.size()));
+      MVC_HIP(hipMemsetAsync(prof_dev, 0, sizeof(long long) * 8 * chains.size(), stream));
+    }
     MVC_HIP(hipStreamSynchronize(stream));
+  }
+
+  // MVC_EXACT_PROF=1: the kernel's shader clocks per phase, summed over the
+  // handle's launches; printed per customer step (mean over chains) at close
+  long long *prof_dev = nullptr;
+  void report_prof() {
+    if (!prof_dev) return;
+    const size_t C = chains.size();
+    std::vector<long long> h(8 * C);
+    if (hipMemcpy(h.data(), prof_dev, sizeof(long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess) return;
+    double tot[8] = {0};
+    for (size_t c = 0; c < C; ++c)
+      for (int k = 0; k < 8; ++k) tot[k] += (double)h[c * 8 + k];
+    const double steps = (double)C * (double)sweeps_done * n;
+    static const char *names[8] = {"remove", "f_vk", "marg+tables", "normaliser", "normalise+find", "join", "open",
+                                   "mh+save"};
+    std::fprintf(stderr, "{\"exact_prof_clocks_per_customer\": {");
+    double all = 0;
+    for (int k = 0; k < 8; ++k) {
+      std::fprintf(stderr, "%s\"%s\": %.1f", k ? ", " : "", names[k], tot[k] / steps);
+      all += tot[k];
+    }
+    std::fprintf(stderr, ", \"total\": %.1f, \"chains\": %zu, \"sweeps\": %lld}}\n", all / steps, C,
+                 (long long)sweeps_done);
   }
 
   // save slots of save_all_async (every chain's sample in one snapshot)
@@ -1043,6 +1095,8 @@ class ExactSampler : public Sampler {
 
   ~ExactSampler() override {
     if (stream) hipStreamSynchronize(stream);
+    report_prof();
+    if (prof_dev) hipFree(prof_dev);
     if (cstream) hipStreamSynchronize(cstream);
     for (auto &q : saves) {
       free_slot(q);
@@ -1157,7 +1211,8 @@ class ExactSampler : public Sampler {
   static constexpr int kSweepsPerLaunch = 64;
   // k sweeps from every chain's current state in launches (capacity growth
   // relaunches from where a chain stopped); SV: the in-kernel sample output
-  void run_launch(int k, const ExactSave &SV) {
+  void run_launch(int k, ExactSave SV) {
+    SV.prof = prof_dev;
     for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; A.h.todo = k; }
     push_structs();
     hipEvent_t ev0 = nullptr;
