@@ -16,19 +16,23 @@
 
 namespace {
 
-// multiview_utils.cpp:307-338 compute_f_vk, literal expression order.  l2pt
-// is mvc_log(2.0 * MVC_PI * tau), the same value for every dish of a view
-// until the MH moves tau, so the caller computes it once per view and sweep.
-__device__ __forceinline__ double ref_f_vk(int nk, double S1, double S2, double tau, double yvi, double l2pt) {
+// multiview_utils.cpp:307-338 compute_f_vk, literal expression order.  The
+// two log-determinant terms, -0.5 m log(2 pi tau) - 0.5 log(tau (tau + m)),
+// depend on the view and the count m only and are the same until the MH moves
+// tau, so they come from the sweep's table ref_log_det (ld[m], m = 0 .. n + 1).
+__device__ __forceinline__ double ref_log_det(int m, double tau, double l2pt) {
+  return -0.5 * m * l2pt - 0.5 * mvc_log(tau * (tau + m));
+}
+__device__ __forceinline__ double ref_f_vk(int nk, double S1, double S2, double tau, double yvi, const double *ld) {
   const double term1_old = -0.5 * S2 / tau;
   const double term2_old = 0.5 * (S1 * S1) / (tau * (tau + nk));
-  const double log_det_old = -0.5 * nk * l2pt - 0.5 * mvc_log(tau * (tau + nk));
+  const double log_det_old = ld[nk];
   const int n_new = nk + 1;
   const double S1_new = S1 + yvi;
   const double S2_new = S2 + yvi * yvi;
   const double term1_new = -0.5 * S2_new / tau;
   const double term2_new = 0.5 * (S1_new * S1_new) / (tau * (tau + n_new));
-  const double log_det_new = -0.5 * n_new * l2pt - 0.5 * mvc_log(tau * (tau + n_new));
+  const double log_det_new = ld[n_new];
   const double lp = (log_det_new + term1_new + term2_new) - (log_det_old + term1_old + term2_old);
   return mvc_exp(lp);
 }
@@ -42,18 +46,22 @@ __device__ __forceinline__ double ref_f_new(double tau, double yvi, double l2pt)
 
 constexpr double kEps = 1e-6;   // multiview_hyper.cpp:13
 
+// the wave's per-view values, sized for at most MV views (kernel instance
+// MV = 8 for the reference's few views: 1.5 KB instead of 6 KB of LDS per
+// chain, i.e. more chains resident per CU)
+template <int MV>
 struct Shared {
-  int Kact[MVC_MAXV];
-  int next_id[MVC_MAXV];
-  int Koff[MVC_MAXV + 1];
-  int died[MVC_MAXV];
-  int draw_ix[MVC_MAXV];
-  double hyp[3 * MVC_MAXV + 2];
-  double ys[MVC_MAXV];
-  double fnew[MVC_MAXV];
-  double l2pt[MVC_MAXV];   // mvc_log(2 pi tau_v) of the current sweep
-  double marg[MVC_MAXV];
-  double tw[MVC_MAXV];
+  int Kact[MV];
+  int next_id[MV];
+  int Koff[MV + 1];
+  int died[MV];
+  int draw_ix[MV];
+  double hyp[3 * MV + 2];
+  double ys[MV];
+  double fnew[MV];
+  double l2pt[MV];   // mvc_log(2 pi tau_v) of the current sweep
+  double marg[MV];   // log of the view's new-table marginal
+  double tw[MV];
   double buf[MVC_WAVE];
   double dv[4];
   int iv[8];
@@ -87,11 +95,13 @@ __device__ __forceinline__ int seq_find8(double u, int n, F term) {
     double x[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) x[q] = term(j + q);
+    int hit = 8;   // the batch's first crossing by selects: one branch per batch
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       cum += x[q];
-      if (u < cum) return j + q;
+      hit = (hit == 8 && u < cum) ? q : hit;
     }
+    if (hit < 8) return j + hit;
   }
   for (; j < n; ++j) {
     cum += term(j);
@@ -105,9 +115,10 @@ __device__ __forceinline__ int seq_find8(double u, int n, F term) {
 // Sums are accumulated in the reference's order by lane 0; lanes only
 // produce the addends.
 // ---------------------------------------------------------------------------
+template <class Sh>
 struct MH {
   ExactChain &C;
-  Shared &sh;
+  Sh &sh;
   int V, n, lane;
   uint64_t seed;
 
@@ -372,9 +383,20 @@ __device__ __forceinline__ void exact_snapshot_wave(const ExactChain &C, int n, 
 // and it is written back at the end.  Same operations, same order: the bits
 // do not depend on where the arrays live.
 // ---------------------------------------------------------------------------
-extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
-    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, int lds_bytes, ExactSave SV) {
-  __shared__ Shared sh;
+// kMode (per launch, from the largest chain): 2 = every array n_t .. P and z
+// in LDS, 1 = z in global memory, 0 = all in global memory.  The pointers are
+// rebuilt from the LDS symbol (or from y, for global ones) inside the
+// instance, so the compiler emits ds_* (or global_*) instructions instead of
+// flat ones that wait on both counters.
+template <class T>
+__device__ __forceinline__ T *ex_global(const double *base, T *p) {
+  return (T *)((const char *)base + ((const char *)p - (const char *)base));
+}
+
+template <int kMode, int MV>
+__global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
+    const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, ExactSave SV) {
+  __shared__ Shared<MV> sh;
   extern __shared__ __attribute__((aligned(16))) char ex_lds[];
   ExactChain &Cg = chains[blockIdx.x];
   ExactChain C = Cg;               // pointers + scalars in registers
@@ -383,17 +405,23 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
   const int TC = C.TC, KC = C.KC;
   char *gbeg = nullptr;
   size_t nbytes = 0;
-  {
-    const size_t full = (size_t)((char *)C.mhbuf - (char *)C.z), part = (size_t)((char *)C.mhbuf - (char *)C.n_t);
-    if (full <= (size_t)lds_bytes) { gbeg = (char *)C.z; nbytes = full; }
-    else if (part <= (size_t)lds_bytes) { gbeg = (char *)C.n_t; nbytes = part; }
-  }
-  if (gbeg) {
-    const uint4 *src = (const uint4 *)gbeg;   // 256-byte granules (carve)
+  C.mhbuf = ex_global(y, C.mhbuf);
+  C.ldt = ex_global(y, C.ldt);
+  if constexpr (kMode == 0) {
+    C.z = ex_global(y, C.z); C.n_t = ex_global(y, C.n_t); C.pos_of_slot = ex_global(y, C.pos_of_slot);
+    C.slot_at_pos = ex_global(y, C.slot_at_pos); C.free_slots = ex_global(y, C.free_slots);
+    C.dish = ex_global(y, C.dish); C.d_id = ex_global(y, C.d_id); C.d_n = ex_global(y, C.d_n);
+    C.d_l = ex_global(y, C.d_l); C.d_S1 = ex_global(y, C.d_S1); C.d_S2 = ex_global(y, C.d_S2);
+    C.f = ex_global(y, C.f); C.logf = ex_global(y, C.logf); C.P = ex_global(y, C.P);
+  } else {
+    gbeg = kMode == 2 ? (char *)C.z : (char *)C.n_t;
+    nbytes = (size_t)((char *)C.mhbuf - gbeg);
+    const uint4 *src = (const uint4 *)gbeg;   // 16-byte granules (carve)
     uint4 *dst = (uint4 *)ex_lds;
     for (size_t e = lane; e < nbytes / 16; e += MVC_WAVE) dst[e] = src[e];
     auto re = [&](auto *&ptr) { ptr = (std::remove_reference_t<decltype(ptr)>)(ex_lds + ((char *)ptr - gbeg)); };
-    if (gbeg == (char *)C.z) re(C.z);
+    if constexpr (kMode == 2) re(C.z);
+    else C.z = ex_global(y, C.z);
     re(C.n_t); re(C.pos_of_slot); re(C.slot_at_pos); re(C.free_slots); re(C.dish);
     re(C.d_id); re(C.d_n); re(C.d_l); re(C.d_S1); re(C.d_S2); re(C.f); re(C.logf); re(C.P);
   }
@@ -427,7 +455,11 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
 
   for (; todo > 0; --todo, i = 0) {   // the launch's sweeps, each from customer resume_i / 0
     const double ag = sh.hyp[3 * V], sg = sh.hyp[3 * V + 1];   // the MH of the previous sweep may have moved them
-    if (lane < V) sh.l2pt[lane] = mvc_log(2.0 * MVC_PI * tau[lane]);   // (read after the barrier of customer i's first step)
+    if (lane < V) sh.l2pt[lane] = mvc_log(2.0 * MVC_PI * tau[lane]);
+    __syncthreads();
+    for (int v = 0; v < V; ++v)   // the sweep's log-determinant table (ref_f_vk)
+      for (int m = lane; m < n + 2; m += MVC_WAVE) C.ldt[(size_t)v * (n + 2) + m] = ref_log_det(m, tau[v], sh.l2pt[v]);
+    __syncthreads();
     for (; i < n; ++i) {
       // -------- capacity guard (every step may add 1 table and 1 dish/view)
       int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
@@ -522,7 +554,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         while (sh.Koff[v + 1] <= e) ++v;
         const int j = e - sh.Koff[v];
         const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v],
-                                  sh.l2pt[v]);
+                                  C.ldt + (size_t)v * (n + 2));
         C.f[v * KC + j] = f;
         C.logf[v * KC + j] = mvc_log(f);
       }
@@ -550,7 +582,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           acc += wn * sh.fnew[v];
           m = acc / denom;
         }
-        sh.marg[v] = m;
+        sh.marg[v] = mvc_log(m);   // the normaliser's log term, one view per lane
       }
 
       // ---------------- table probabilities (utils.cpp:83-116)
@@ -585,7 +617,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
       // ---------------- normaliser, draw (gibbs.cpp:169-191)
       if (lane == 0) {
         double lnew = 0.0;
-        for (int v = 0; v < V; ++v) lnew += mvc_log(sh.marg[v]);      // utils.cpp:118-122
+        for (int v = 0; v < V; ++v) lnew += sh.marg[v];      // utils.cpp:118-122 (logs taken per view above)
         const double mass_new = ag + sg * tne;                          // :124-135
         const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
         sh.dv[1] = seq_sum8(p_new, T, [&](int p) { return C.P[p]; });
@@ -696,7 +728,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     if (status != MVC_ST_RUNNING) break;
     // end of sweep: hyperparameters (gibbs.cpp:202)
     C.T = T;
-    MH mh{C, sh, V, n, lane, seed};
+    MH<Shared<MV>> mh{C, sh, V, n, lane, seed};
     mh.run();
     // the MH draws on lane 0 only: every lane continues from lane 0's counter
     // (the next sweep's dish draws run on lanes 0 .. V-1)
@@ -730,7 +762,7 @@ extern "C" __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     Cg.status = status;
     Cg.todo = todo;
   }
-  if (gbeg) {                      // the LDS copy back to the chain's allocation
+  if constexpr (kMode != 0) {      // the LDS copy back to the chain's allocation
     __syncthreads();
     const uint4 *src = (const uint4 *)ex_lds;
     uint4 *dst = (uint4 *)gbeg;
@@ -797,7 +829,7 @@ struct ExactAlloc {
 
 size_t exact_bytes(int n, int V, int TC, int KC) {
   size_t b = 0;
-  auto add = [&](size_t x) { b += (x + 255) & ~(size_t)255; };
+  auto add = [&](size_t x) { b += (x + 15) & ~(size_t)15; };   // 16-byte granules: the LDS copy moves uint4
   add(sizeof(int32_t) * n);                 // z
   for (int k = 0; k < 4; ++k) add(sizeof(int32_t) * TC);  // n_t pos slot free
   add(sizeof(int32_t) * (size_t)V * TC);    // dish
@@ -805,6 +837,7 @@ size_t exact_bytes(int n, int V, int TC, int KC) {
   for (int k = 0; k < 4; ++k) add(sizeof(double) * (size_t)V * KC);  // S1 S2 f logf
   add(sizeof(double) * TC);                 // P
   add(sizeof(double) * (size_t)(n + 1));    // mhbuf
+  add(sizeof(double) * (size_t)V * (n + 2));   // ldt
   add(sizeof(int32_t) * V);                 // Kact
   add(sizeof(int32_t) * V);                 // next_id
   add(sizeof(double) * (3 * V + 2));        // hyper
@@ -813,7 +846,7 @@ size_t exact_bytes(int n, int V, int TC, int KC) {
 
 void carve(ExactAlloc &A, int n, int V, int TC, int KC) {
   char *p = (char *)A.block;
-  auto take = [&](size_t x) { char *r = p; p += (x + 255) & ~(size_t)255; return (void *)r; };
+  auto take = [&](size_t x) { char *r = p; p += (x + 15) & ~(size_t)15; return (void *)r; };
   ExactChain &C = A.h;
   C.TC = TC;
   C.KC = KC;
@@ -832,6 +865,7 @@ void carve(ExactAlloc &A, int n, int V, int TC, int KC) {
   C.logf = (double *)take(sizeof(double) * (size_t)V * KC);
   C.P = (double *)take(sizeof(double) * TC);
   C.mhbuf = (double *)take(sizeof(double) * (size_t)(n + 1));
+  C.ldt = (double *)take(sizeof(double) * (size_t)V * (n + 2));
   C.Kact = (int32_t *)take(sizeof(int32_t) * V);
   C.next_id = (int32_t *)take(sizeof(int32_t) * V);
   C.hyper = (double *)take(sizeof(double) * (3 * V + 2));
@@ -1161,13 +1195,16 @@ class ExactSampler : public Sampler {
   // dynamic LDS of the sweep kernel: the largest chain's array range that fits
   // kExactLds (with z when every chain's does), 0 when none fits
   static constexpr size_t kExactLds = 48 * 1024;
-  int lds_bytes() const {
+  int lds_bytes(int *mode = nullptr) const {
     size_t full = 0, part = 0;
     for (auto &A : chains) {
       full = std::max(full, (size_t)((char *)A.h.mhbuf - (char *)A.h.z));
       part = std::max(part, (size_t)((char *)A.h.mhbuf - (char *)A.h.n_t));
     }
-    return (int)(full <= kExactLds ? full : (part <= kExactLds ? part : 0));
+    int m = full <= kExactLds ? 2 : (part <= kExactLds ? 1 : 0);
+    if (const char *e = getenv("MVC_EXACT_MODE"); e && e[0] >= '0' && e[0] <= '2') m = std::min(m, e[0] - '0');   // tests
+    if (mode) *mode = m;
+    return (int)(m == 2 ? full : (m == 1 ? part : 0));
   }
 
   void push_structs() {
@@ -1191,8 +1228,10 @@ class ExactSampler : public Sampler {
     ExactImage I;
     download(A, I, n, V, stream);
     int TC2 = I.TC, KC2 = I.KC;
-    if (I.n_free < 1) TC2 = I.TC * 2;
-    for (int v = 0; v < V; ++v) if (I.Kact[v] + 1 > I.KC) KC2 = I.KC * 2;
+    // doubling, capped at n + 1: T <= n and K_v <= T, so a step's T + 1 and
+    // K_v + 1 never exceed it (a smaller footprint keeps more chains per CU)
+    if (I.n_free < 1) TC2 = std::max(I.TC + 1, std::min(I.TC * 2, n + 1));
+    for (int v = 0; v < V; ++v) if (I.Kact[v] + 1 > I.KC) KC2 = std::max(I.KC + 1, std::min(I.KC * 2, n + 1));
     grow(I, V, TC2, KC2);
     ExactAlloc B;
     B.h = A.h;
@@ -1211,6 +1250,22 @@ class ExactSampler : public Sampler {
   static constexpr int kSweepsPerLaunch = 64;
   // k sweeps from every chain's current state in launches (capacity growth
   // relaunches from where a chain stopped); SV: the in-kernel sample output
+  // the kernel instance of the storage mode (mvc_exact_sweep_kernel) and view bound
+  template <int M>
+  void launch_mode(int lb, const ExactSave &SV) {
+    const dim3 g((unsigned)chains.size()), b(64);
+    if (V <= 8)
+      hipLaunchKernelGGL((mvc_exact_sweep_kernel<M, 8>), g, b, lb, stream, (const double *)y_dev, n, V, chains_dev,
+                         cfg.seed, SV);
+    else
+      hipLaunchKernelGGL((mvc_exact_sweep_kernel<M, MVC_MAXV>), g, b, lb, stream, (const double *)y_dev, n, V,
+                         chains_dev, cfg.seed, SV);
+  }
+  void launch_sweep(int mode, int lb, const ExactSave &SV) {
+    if (mode == 2) launch_mode<2>(lb, SV);
+    else if (mode == 1) launch_mode<1>(lb, SV);
+    else launch_mode<0>(lb, SV);
+  }
   void run_launch(int k, ExactSave SV) {
     SV.prof = prof_dev;
     for (auto &A : chains) { A.h.status = MVC_ST_RUNNING; A.h.resume_i = 0; A.h.todo = k; }
@@ -1220,8 +1275,9 @@ class ExactSampler : public Sampler {
     for (int round = 0;; ++round) {
       hipEvent_t ev = nullptr;
       timers.begin("exact_sweep", &ev);
-      hipLaunchKernelGGL(mvc_exact_sweep_kernel, dim3((unsigned)chains.size()), dim3(64), lds_bytes(), stream,
-                         (const double *)y_dev, n, V, chains_dev, cfg.seed, lds_bytes(), SV);
+      int mode = 0;
+      const int lb = lds_bytes(&mode);
+      launch_sweep(mode, lb, SV);
       MVC_HIP(hipGetLastError());
       timers.end("exact_sweep", ev);
       pull_structs();

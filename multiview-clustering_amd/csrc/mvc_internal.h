@@ -35,6 +35,7 @@ struct ExactChain {
   double *f, *logf;            // [V*KC] per-customer scratch
   double *P;                   // [TC] per-customer table probabilities
   double *mhbuf;               // [n+1] log(m - sigma) table for the EPPF
+  double *ldt;                 // [V][n+2] the sweep's log-determinant terms (ref_f_vk)
   int32_t *Kact;               // [V] live dishes
   int32_t *next_id;            // [V] next raw dish id (reference: V.K)
   double *hyper;               // [3V+2] tau, alpha, sigma, alpha_g, sigma_g

@@ -145,6 +145,22 @@ def test_exact_many_chains_vs_live_oracle():
         _compare(g, ref)
 
 
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_exact_storage_modes(mode, monkeypatch):
+    """The sweep kernel's three storage instances (every chain array in global
+    memory / all but z in LDS / all in LDS; MVC_EXACT_MODE caps the one the
+    sizes allow) give the oracle's chain, through the table-capacity growth of
+    New_Simulation's first sweeps (64 -> 128 -> n + 1)."""
+    monkeypatch.setenv("MVC_EXACT_MODE", mode)
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(11)
+    gpus = m.run_gibbs_cpp(y, 40, 10, 3, seed=9, mode="exact", n_chains=3, quiet=True)
+    for c, g in enumerate(gpus):
+        ref = O.run(y, 40, 10, 3, seed=9, chain=c, mode=O.EXACT, math=O.PORTABLE)
+        _compare(g, ref)
+
+
 def test_exact_capacity_growth():
     """Tiny initial capacities force the overflow -> regrow -> resume path."""
     m = _mvc()
