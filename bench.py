@@ -294,7 +294,7 @@ def newsim_chains_line(seed, device):
     """The same call with several chains per call (MVC_CHAINS in the drop-in):
     aggregate chain-sweeps/s, parallel schedule 16 chains, exact 2048 (one
     wavefront each, 8 per CU); for the exact schedule also the sweeps alone,
-    without mvc_run's per-sample bookkeeping (2048 chains x 250 samples)."""
+    without mvc_run's per-sample bookkeeping, at 2048 and 4096 chains."""
     import mvc_amd
     from mvc_amd import data
     from mvc_amd.sampler import Sampler
@@ -311,17 +311,18 @@ def newsim_chains_line(seed, device):
         out[f"{mode}_gpu_{C}chains"] = {"chains": C, "sweeps": Mc, "s": round(tm["mvc_run_s"], 2),
                                         "chain_sweeps_per_s": round(C * Mc / tm["mvc_run_s"], 1),
                                         "python_result_lists_s": round(dt - tm["mvc_run_s"], 2)}
-    C, Mc = 2048, 500
-    s = Sampler(y, seed=seed, mode="exact", n_chains=C, device=device)
-    s.sweep(Mc // 2)                      # past the cold-start transient
-    s.synchronize()
-    t0 = time.perf_counter()
-    s.sweep(Mc)
-    s.synchronize()
-    dt = time.perf_counter() - t0
-    s.close()
-    out[f"exact_gpu_{C}chains_sweeps_only"] = {"chains": C, "sweeps": Mc, "s": round(dt, 2),
-                                               "chain_sweeps_per_s": round(C * Mc / dt, 1)}
+    Mc = 500
+    for C in (2048, 4096):   # 8 chains per CU resident (2 per SIMD): 4096 is two full rounds
+        s = Sampler(y, seed=seed, mode="exact", n_chains=C, device=device)
+        s.sweep(Mc // 2)                      # past the cold-start transient
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.sweep(Mc)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        s.close()
+        out[f"exact_gpu_{C}chains_sweeps_only"] = {"chains": C, "sweeps": Mc, "s": round(dt, 2),
+                                                   "chain_sweeps_per_s": round(C * Mc / dt, 1)}
     return out
 
 

@@ -216,11 +216,8 @@ struct MH {
       C.mhbuf[m] = mvc_log(term);
     }
     __syncthreads();
-    if (lane == 0)
-      for (int j = 0; j < K; ++j) {
-        const int lk = C.d_l[v * KC + j];
-        for (int m = 1; m < lk; ++m) lp += C.mhbuf[m];
-      }
+    if (lane == 0)   // the same additions in the same order, 8 loads in flight
+      for (int j = 0; j < K; ++j) lp = seq_sum8(lp, C.d_l[v * KC + j] - 1, [&](int m) { return C.mhbuf[1 + m]; });
     __syncthreads();
     bad = __any(bad);
     lp = bcast(lp);
@@ -262,10 +259,8 @@ struct MH {
     }
     __syncthreads();
     if (lane == 0)
-      for (int p = 0; p < T; ++p) {   // n_t in position order (hyper.cpp:74)
-        const int c = C.n_t[C.slot_at_pos[p]];
-        for (int m = 1; m < c; ++m) lp += C.mhbuf[m];
-      }
+      for (int p = 0; p < T; ++p)   // n_t in position order (hyper.cpp:74)
+        lp = seq_sum8(lp, C.n_t[C.slot_at_pos[p]] - 1, [&](int m) { return C.mhbuf[1 + m]; });
     __syncthreads();
     bad = __any(bad);
     lp = bcast(lp);
@@ -393,6 +388,22 @@ __device__ __forceinline__ T *ex_global(const double *base, T *p) {
   return (T *)((const char *)base + ((const char *)p - (const char *)base));
 }
 
+// The customer step's barriers.  The workgroup is one wavefront, so a barrier
+// only has to order memory: with the chain's arrays in LDS (kMode >= 1; z, if
+// global, is read at step i and written at its commit only) an LDS-only fence
+// suffices, which leaves global loads (the next customer's y, the log-det
+// table) in flight across it; kMode 0 keeps __syncthreads.
+template <int kMode>
+__device__ __forceinline__ void ex_sync() {
+  if constexpr (kMode >= 1) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  } else {
+    __syncthreads();
+  }
+}
+
 template <int kMode, int MV>
 __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, ExactSave SV) {
@@ -460,16 +471,18 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     for (int v = 0; v < V; ++v)   // the sweep's log-determinant table (ref_f_vk)
       for (int m = lane; m < n + 2; m += MVC_WAVE) C.ldt[(size_t)v * (n + 2) + m] = ref_log_det(m, tau[v], sh.l2pt[v]);
     __syncthreads();
+    double ynx = lane < V ? y[(size_t)lane * n + i] : 0.0;
     for (; i < n; ++i) {
       // -------- capacity guard (every step may add 1 table and 1 dish/view)
       int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
       for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
       if (need) { status = MVC_ST_OVERFLOW; break; }
 
-      if (lane < V) sh.ys[lane] = y[(size_t)lane * n + i];
+      if (lane < V) sh.ys[lane] = ynx;
+      if (lane < V && i + 1 < n) ynx = y[(size_t)lane * n + i + 1];   // the next customer's y, in flight during this step
       // ---------------- remove_customer(i)   utils.cpp:138-192
       const int s = C.z[i];
-      __syncthreads();
+      ex_sync<kMode>();
       if (lane < V) {
         const int k = C.dish[lane * TC + s];
         const double yv = sh.ys[lane];
@@ -478,7 +491,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         C.d_S2[lane * KC + k] -= yv * yv;
       }
       int nt_s = C.n_t[s] - 1;
-      __syncthreads();
+      ex_sync<kMode>();
       if (lane == 0) C.n_t[s] = nt_s;
       if (nt_s == 0) {
         // table dies: l_vk-- (:170-173), swap-and-pop (:175-190)
@@ -496,7 +509,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         }
         const int pos = C.pos_of_slot[s];
         const int last = T - 1;
-        __syncthreads();
+        ex_sync<kMode>();
         if (lane == 0) {
           if (pos != last) {
             const int sl = C.slot_at_pos[last];
@@ -507,7 +520,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         }
         T -= 1;
         n_free += 1;
-        __syncthreads();
+        ex_sync<kMode>();
         // compact the live dish list of every view whose dish died
         for (int v = 0; v < V; ++v) {
           const int k = sh.died[v];
@@ -522,21 +535,21 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
               id = C.d_id[v * KC + j]; nn = C.d_n[v * KC + j]; ll = C.d_l[v * KC + j];
               s1 = C.d_S1[v * KC + j]; s2 = C.d_S2[v * KC + j];
             }
-            __syncthreads();
+            ex_sync<kMode>();
             if (j < K) {
               C.d_id[v * KC + j - 1] = id; C.d_n[v * KC + j - 1] = nn; C.d_l[v * KC + j - 1] = ll;
               C.d_S1[v * KC + j - 1] = s1; C.d_S2[v * KC + j - 1] = s2;
             }
-            __syncthreads();
+            ex_sync<kMode>();
           }
           for (int p = lane; p < T; p += MVC_WAVE) {
             const int sl = C.slot_at_pos[p];
             const int dk = C.dish[v * TC + sl];
             if (dk > k) C.dish[v * TC + sl] = dk - 1;
           }
-          __syncthreads();
+          ex_sync<kMode>();
           if (lane == 0) sh.Kact[v] = K - 1;
-          __syncthreads();
+          ex_sync<kMode>();
         }
       }
 
@@ -547,7 +560,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
         sh.Koff[V] = acc;
       }
-      __syncthreads();
+      ex_sync<kMode>();
       const int Ktot = sh.Koff[V];
       for (int e = lane; e < Ktot; e += MVC_WAVE) {
         int v = 0;
@@ -559,7 +572,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         C.logf[v * KC + j] = mvc_log(f);
       }
       if (lane < V) sh.fnew[lane] = ref_f_new(tau[lane], sh.ys[lane], sh.l2pt[lane]);
-      __syncthreads();
+      ex_sync<kMode>();
       tick(1);
 
       // ---------------- marginal of a new table per view (utils.cpp:40-69)
@@ -611,7 +624,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         C.P[p] = pr;
       }
       for (int m = 32; m >= 1; m >>= 1) tne += __shfl_xor(tne, m, 64);
-      __syncthreads();
+      ex_sync<kMode>();
       tick(2);
 
       // ---------------- normaliser, draw (gibbs.cpp:169-191)
@@ -622,7 +635,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         const double p_new = (mass_new <= 0.0) ? 0.0 : mass_new * mvc_exp(lnew);
         sh.dv[1] = seq_sum8(p_new, T, [&](int p) { return C.P[p]; });
       }
-      __syncthreads();
+      ex_sync<kMode>();
       tick(3);
       const double sum_p = sh.dv[1];
       int t_star;
@@ -630,13 +643,13 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         t_star = -2;                       // gibbs.cpp:172-176 -> table at position 0
       } else {
         for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
-        __syncthreads();
+        ex_sync<kMode>();
         if (lane == 0) {
           const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
           sh.iv[0] = seq_find8(u, T, [&](int p) { return C.P[p]; });
         }
         C.draws += 1;
-        __syncthreads();
+        ex_sync<kMode>();
         t_star = sh.iv[0];
       }
       tick(4);
@@ -644,7 +657,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
       if (t_star != -1) {
         // add_customer_to_existing_table (utils.cpp:194-207)
         const int sl = C.slot_at_pos[t_star < 0 ? 0 : t_star];
-        __syncthreads();
+        ex_sync<kMode>();
         if (lane == 0) { C.z[i] = sl; C.n_t[sl] = C.n_t[sl] + 1; }
         if (lane < V) {
           const int k = C.dish[lane * TC + sl];
@@ -653,14 +666,14 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           C.d_S1[lane * KC + k] += yv;
           C.d_S2[lane * KC + k] += yv * yv;
         }
-        __syncthreads();
+        ex_sync<kMode>();
         tick(5);
       } else {
         // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
         n_free -= 1;
         const int sl = C.free_slots[n_free];
         const int pos = T;
-        __syncthreads();
+        ex_sync<kMode>();
         if (lane == 0) {
           C.slot_at_pos[pos] = sl;
           C.pos_of_slot[sl] = pos;
@@ -682,13 +695,13 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           total += wn;
           sh.tw[v] = total;
         }
-        __syncthreads();
+        ex_sync<kMode>();
         if (lane == 0) {                       // draws are consumed in view order
           uint64_t d = C.draws;
           for (int v = 0; v < V; ++v) sh.draw_ix[v] = (sh.tw[v] <= 0) ? -1 : (int)(d++ - C.draws);
           sh.iv[1] = (int)(d - C.draws);
         }
-        __syncthreads();
+        ex_sync<kMode>();
         if (lane < V) {
           const int v = lane;
           const int K = sh.Kact[v];
@@ -720,7 +733,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           C.d_S2[v * KC + kk] += yv * yv;
         }
         C.draws += (uint64_t)sh.iv[1];
-        __syncthreads();
+        ex_sync<kMode>();
         tick(6);
       }
     }

@@ -2849,6 +2849,13 @@ class ParallelSampler : public Sampler {
             rs_host->prof[5] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[6] * 0.01 / std::max(1ull, rs_host->prof[7]));
     fprintf(stderr, "runprof decided %llu same-as-phase-A %llu | movers %llu same-as-phase-A %llu\n", rs_host->prof[8],
             rs_host->prof[9], rs_host->prof[10], rs_host->prof[11]);
+    if (rs_host->prof[18] + rs_host->prof[19]) {
+      const double nd = (double)std::max(1ull, rs_host->prof[18]), nc = (double)std::max(1ull, rs_host->prof[19]);
+      fprintf(stderr, "wideprof decided %llu commits %llu | combine %.2f lm %.2f tables %.2f weights %.2f draw %.2f (us per decided) "
+              "commit %.2f (us per commit)\n", rs_host->prof[18], rs_host->prof[19], rs_host->prof[12] * 0.01 / nd,
+              rs_host->prof[13] * 0.01 / nd, rs_host->prof[14] * 0.01 / nd, rs_host->prof[15] * 0.01 / nd,
+              rs_host->prof[16] * 0.01 / nd, rs_host->prof[17] * 0.01 / nc);
+    }
 #endif
     if (vp_stats)   // MVC_VP_STATS=1: value prediction's steps and full hits of this sweep, on stderr
       fprintf(stderr, "mvc vp steps %d hits %d off %d\n", rs_host->vpsteps, rs_host->vphits, rs_host->vpoff);

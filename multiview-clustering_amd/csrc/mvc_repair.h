@@ -44,7 +44,8 @@ struct Repair {
   int32_t vpsteps, vphits;   // vp steps, and those whose predictions all held
   int32_t dbg[8];       // MVC_RUN_CHECK: the first index check that failed in a run kernel (code, values), 0: none
   int32_t Klist[MVC_MAXV];
-  unsigned long long prof[12];  // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz), steps, decided customers, phase-A hits
+  unsigned long long prof[20];  // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz), steps, decided customers, phase-A hits;
+                                // [12..19] the grid-wide fin kernel's (combine, lm, table scores, weights, draw, commit, decided, commits)
 };
 
 constexpr int32_t kSeqScan = 0, kSeqRun = 1;
@@ -1583,7 +1584,7 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->T = A.status[0];
   R->T_ne = A.status[V + 3];
   R->moves = R->births = R->newdish = R->rounds = 0;
-  for (int k = 0; k < 12; ++k) R->prof[k] = 0;
+  for (int k = 0; k < 20; ++k) R->prof[k] = 0;
   for (int k = 0; k < 8; ++k) R->dbg[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
 }
@@ -2339,9 +2340,27 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_ke
   const int i = s_i;
   const int p0 = P.z[i];
   const SeqScratch Sw(A, w);
+#ifdef MVC_RUN_PROF
+  if (tid < 12) mvc_prof_lds[tid] = 0;
+  __syncthreads();
+  uint64_t f0 = wall_clock64();
+  auto fin_flush = [&](int decided, int committed) {   // thread 0: this launch's phases into R->prof[12..]
+    if (tid == 0) {
+      R->prof[17] += committed ? wall_clock64() - f0 : 0;
+      for (int k = 0; k < 4; ++k) R->prof[13 + k] += mvc_prof_lds[k];
+      R->prof[18] += decided;
+      R->prof[19] += committed;
+    }
+  };
+#define FIN_MARK(k) do { const uint64_t _n = wall_clock64(); if (tid == 0) R->prof[k] += _n - f0; f0 = _n; } while (0)
+#else
+  auto fin_flush = [](int, int) {};
+#define FIN_MARK(k) do {} while (0)
+#endif
   if (s_pend) {   // a window's first mover (its lp rows are not in the scratch: computed by the commit)
     if (!seq_commit(A, global_view(A), nullptr, global_cust(A, i), i, p0, s_pc, Sw.lp, Sw.tree, &R->moves, nw))
       return;   // overflow: the host grows and the next round redoes this commit
+    fin_flush(0, 1);
     if (tid == 0) {
       R->cur = i + 1;
       R->pend = 0;
@@ -2365,11 +2384,16 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_ke
     }
   }
   __syncthreads();
+  FIN_MARK(12);
   const int c = seq_resample_wide(A, global_view(A), global_cust(A, i), i, p0, S0, w, nw, true, true);
   if (tid == 0) s_c = c;   // member 0's pick
   __syncthreads();
+#ifdef MVC_RUN_PROF
+  f0 = wall_clock64();
+#endif
   const int ch = s_c;
   if (ch == p0) {   // stays
+    fin_flush(1, 0);
     if (tid == 0) {
       R->cur = i + 1;
       R->streak += 1;
@@ -2393,6 +2417,8 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_ke
     }
     return;
   }
+  fin_flush(1, 1);
+#undef FIN_MARK
   if (tid == 0) {
     note_mover(R->lastm, R->gapq, i);
     R->cur = i + 1;
