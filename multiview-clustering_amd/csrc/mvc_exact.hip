@@ -404,8 +404,11 @@ __device__ __forceinline__ void ex_sync() {
   }
 }
 
+#ifndef MVC_EXACT_WAVES
+#define MVC_EXACT_WAVES 2   // waves per SIMD the register allocation must allow (LDS allows ~8 chains per CU at n = 200)
+#endif
 template <int kMode, int MV>
-__global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MVC_EXACT_WAVES, 8))) void mvc_exact_sweep_kernel(
     const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, ExactSave SV) {
   __shared__ Shared<MV> sh;
   extern __shared__ __attribute__((aligned(16))) char ex_lds[];

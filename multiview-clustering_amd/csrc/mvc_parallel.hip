@@ -1747,6 +1747,7 @@ constexpr int kSeqRunLimit = 64;   // stays in a row after which the run kernel 
 constexpr size_t kSeqLdsBudget = 150 * 1024;   // run kernel: per-wave LDS scratch of all its waves
 constexpr int kWideGridMax = 256;  // grid-wide evaluation: at most this many blocks per customer
 constexpr int kWideBatch = 32;     // grid-wide evaluation: customers (lp + fin pairs) per repair round
+constexpr int kWideFinLds = 152 * 1024;   // the fin kernel's dynamic LDS (wide_fin_resample: dish list, block totals)
 
 template <class Tp>
 Tp *dmalloc(size_t count) {
@@ -1857,6 +1858,7 @@ class ParallelSampler : public Sampler {
   bool use_wide = true;           // MVC_WIDE=0: global-scratch run kernel speculates one customer per wave
   bool wide_grid = true;          // MVC_WIDE=block: the wide evaluation on the run kernel's one block instead of the grid
   double *wide_part = nullptr;    // grid-wide evaluation: per-block partials [kWideGridMax][2V]
+  int wide_fin_lds = kWideFinLds; // the fin kernel's LDS evaluation up to this many bytes (MVC_WIDE_FIN=0: off)
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
   bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
@@ -2056,6 +2058,9 @@ class ParallelSampler : public Sampler {
     for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>,
                           (const void *)mvc_seq_run_kernel<4>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
+    MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_wide_fin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kWideFinLds));
+    if (const char *e = getenv("MVC_WIDE_FIN")) wide_fin_lds = e[0] == '0' ? 0 : kWideFinLds;   // 0: the global-scratch evaluation
     if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
     if (const char *e = getenv("MVC_BIG")) {
       no_big = e[0] == '0';
@@ -2767,8 +2772,8 @@ class ParallelSampler : public Sampler {
           hipLaunchKernelGGL(mvc_seq_wide_begin_kernel, dim3(1), dim3(64), 0, stream, Q);
           for (int b = 0; b < kWideBatch; ++b) {
             hipLaunchKernelGGL(mvc_seq_wide_lp_kernel, dim3(wblk), dim3(kWideGridThreads), 0, stream, Q, wide_part);
-            hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, Q,
-                               (const double *)wide_part, wblk, L.limit);
+            hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), kWideFinLds, stream, Q,
+                               (const double *)wide_part, wblk, L.limit, wide_fin_lds);
           }
           MVC_HIP(hipGetLastError());
           dbg("seq_wide (begin + lp/fin pairs)", c, s);
@@ -2855,6 +2860,9 @@ class ParallelSampler : public Sampler {
               "commit %.2f (us per commit)\n", rs_host->prof[18], rs_host->prof[19], rs_host->prof[12] * 0.01 / nd,
               rs_host->prof[13] * 0.01 / nd, rs_host->prof[14] * 0.01 / nd, rs_host->prof[15] * 0.01 / nd,
               rs_host->prof[16] * 0.01 / nd, rs_host->prof[17] * 0.01 / nc);
+      fprintf(stderr, "wideprof effective shader clock %.0f MHz (%llu clocks over %llu ticks of 100 MHz)\n",
+              rs_host->prof[20] ? 100.0 * (double)rs_host->prof[21] / (double)rs_host->prof[20] : 0.0, rs_host->prof[21],
+              rs_host->prof[20]);
     }
 #endif
     if (vp_stats)   // MVC_VP_STATS=1: value prediction's steps and full hits of this sweep, on stderr

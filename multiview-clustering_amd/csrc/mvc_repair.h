@@ -44,8 +44,9 @@ struct Repair {
   int32_t vpsteps, vphits;   // vp steps, and those whose predictions all held
   int32_t dbg[8];       // MVC_RUN_CHECK: the first index check that failed in a run kernel (code, values), 0: none
   int32_t Klist[MVC_MAXV];
-  unsigned long long prof[20];  // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz), steps, decided customers, phase-A hits;
-                                // [12..19] the grid-wide fin kernel's (combine, lm, table scores, weights, draw, commit, decided, commits)
+  unsigned long long prof[22];  // MVC_RUN_PROF builds: run-kernel phase ticks (100 MHz), steps, decided customers, phase-A hits;
+                                // [12..19] the grid-wide fin kernel's (combine, lm, table scores, weights, draw, commit, decided, commits),
+                                // [20] / [21] its wall ticks / shader clocks from decision start to exit (the effective clock)
 };
 
 constexpr int32_t kSeqScan = 0, kSeqRun = 1;
@@ -1557,6 +1558,85 @@ __device__ int seq_dish_draw(const SeqArgs &A, const SView &W, const Cust &C, in
   return seq_tree_select(tree, K + 1, nlev, r);
 }
 
+// seq_tree_build / seq_tree_select with the leaf level read through leaf(e)
+// (e < m) instead of stored: the levels above it go to `up` one after the
+// other.  The same sums in the same association, so the same root and pick.
+template <class F>
+__device__ double seq_tree_build_f(F leaf, int m, double *up, int &nlev) {
+  const int lane = threadIdx.x & 63;
+  int cnt = (m + 63) / 64;
+  double root = 0.0;
+  for (int c = 0; c < cnt; ++c) {
+    const int e = c * 64 + lane;
+    const double s = wave_tree_sum(e < m ? leaf(e) : 0.0);
+    if (lane == 0) up[c] = s;
+    root = s;
+  }
+  __threadfence_block();
+  nlev = 2;
+  int o = 0;
+  while (cnt > 1) {
+    const int nc = (cnt + 63) / 64;
+    const int o2 = o + cnt;
+    for (int c = 0; c < nc; ++c) {
+      const int e = c * 64 + lane;
+      const double s = wave_tree_sum(e < cnt ? up[o + e] : 0.0);
+      if (lane == 0) up[o2 + c] = s;
+      root = s;
+    }
+    __threadfence_block();
+    o = o2;
+    cnt = nc;
+    ++nlev;
+  }
+  return root;
+}
+template <class F>
+__device__ int seq_tree_select_f(F leaf, const double *up, int m, int nlev, double r) {
+  const int lane = threadIdx.x & 63;
+  int idx = 0;
+  for (int k = nlev - 2; k >= 0; --k) {
+    int cnt = m, off = 0;
+    for (int q = 0; q < k; ++q) {
+      off += cnt;
+      cnt = (cnt + 63) / 64;
+    }
+    const int base = idx * 64;
+    const int c = min(64, cnt - base);
+    const double x = lane < c ? (k == 0 ? leaf(base + lane) : up[off - m + base + lane]) : 0.0;
+    Tree64Levels L;
+    wave_tree_sum_levels(x, L);
+    const int l = wave_tree_select(L, x, r);
+    idx = base + l;
+  }
+  return idx;
+}
+
+// The fin kernel's evaluation left in LDS (wide_fin_resample): every view's
+// weighted dish terms w_j exp(lp_j - m_v) -- exactly seq_dish_draw's leaves
+// for the same customer and state -- and the new dish's leaf; `up` holds V
+// tree scratches of upstride doubles.  L == nullptr: none.
+struct FinLeaves {
+  const double *L;
+  const int *koff;
+  const double *newleaf;
+  double *up;
+  int upstride;
+};
+// seq_dish_draw from those leaves (no lp row, no exps): the same tree64, the same draw.
+__device__ int seq_dish_draw_leaves(const SeqArgs &A, const SView &W, int i, int v, const FinLeaves &fl) {
+  const int K = W.Klist[v];
+  const double *lv = fl.L + fl.koff[v];
+  const double nl = fl.newleaf[v];
+  auto leaf = [&](int e) { return e < K ? lv[e] : nl; };
+  double *up = fl.up + (size_t)v * fl.upstride;
+  int nlev;
+  const double tot = seq_tree_build_f(leaf, K + 1, up, nlev);
+  if (!(tot > 0.0)) return K;
+  const double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_DISH + 1u + (uint32_t)v) * tot;
+  return seq_tree_select_f(leaf, up, K + 1, nlev, r);
+}
+
 }  // namespace
 
 // Before phase A: the whole sweep is one pending window [0, n).
@@ -1584,7 +1664,7 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->T = A.status[0];
   R->T_ne = A.status[V + 3];
   R->moves = R->births = R->newdish = R->rounds = 0;
-  for (int k = 0; k < 20; ++k) R->prof[k] = 0;
+  for (int k = 0; k < 22; ++k) R->prof[k] = 0;
   for (int k = 0; k < 8; ++k) R->dbg[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
 }
@@ -1700,7 +1780,7 @@ __device__ __forceinline__ void seq_bar(bool lds_only) {
 // kernel's LDS copies).
 __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const Cust &Ci, int i, int p0, int c,
                            double *lpw, double *treew, int32_t *cnt, int nwd, const SeqScratch *pre = nullptr,
-                           bool lds_only = false) {
+                           bool lds_only = false, FinLeaves fl = FinLeaves{}) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1716,9 +1796,10 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
     // a birth: dishes drawn against the current state, then the table
     const bool alive = (W.n_t[p0] - 1) > 0;
     for (int v = w; v < V && w < nwd; v += nwd) {   // waves w < nwd own a scratch (lpw, treew)
-      const int t = pre ? seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew,
-                                        pre->lp + (size_t)v * pre->lps, pre->mv[v], pre->koff[V + 1 + v])
-                        : seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew);
+      const int t = fl.L  ? seq_dish_draw_leaves(A, W, i, v, fl)
+                    : pre ? seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew,
+                                          pre->lp + (size_t)v * pre->lps, pre->mv[v], pre->koff[V + 1 + v])
+                          : seq_dish_draw(A, W, Ci, i, v, alive, W.dish[v * ts + p0], lpw, treew);
       if (lane == 0) s_tup[v] = t;
     }
     __syncthreads();
@@ -2318,12 +2399,302 @@ extern "C" __global__ __launch_bounds__(kWideGridThreads) void mvc_seq_wide_lp_k
   }
 }
 
+// The fin kernel's part of seq_resample_wide (rest_only: the grid wrote the lp
+// rows to S.lp and the combined per-view max / count to member row 0) with its
+// block-local arrays in the dynamic LDS L (max(NK, TB) doubles, the caller
+// checks the fit): the lp rows copied in once, the table scores gathered from
+// there, the weighted terms written over the rows, the column sums and the
+// running block totals read back from LDS.  In seq_resample_wide those were
+// global round trips inside wave 0's order-sensitive loops (Reuters, 16k
+// tables and 15k dishes: ~165 us per customer, `profiles/r4m_*`).  The table
+// scores are formed before the view terms (they do not depend on them; M and
+// s_new are taken after both), and every quantity keeps seq_resample_wide's
+// operations and order, so the pick is the same bit for bit.  Block-wide.
+// Also writes S.mv and the K_act row of S.koff, which a birth's dish draws
+// read.  Returns the pick on member 0 (r == 0), -1 elsewhere.
+// doubles of one view's tree levels above the leaves (K + 1 leaves)
+__host__ __device__ inline int fin_tree_up(int K) { return (K + 1) / 63 + 8; }
+// wide_fin_resample's LDS: the dish terms, the block totals, V tree scratches
+__host__ __device__ inline int64_t fin_lds_doubles(int NK, int TB, int V, int kmax) {
+  return (int64_t)NK + TB + (int64_t)V * fin_tree_up(kmax);
+}
+__device__ int wide_fin_resample(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0, const SeqScratch &S,
+                                 int r, int tw, double *L, FinLeaves &fl) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, row = lane >> 4, col = lane & 15;
+  const int V = P.V, ts = W.ts, ks = W.ks, lps = S.lps;
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  int32_t *kact = S.koff + V + 1;
+  __shared__ int f_koff[MVC_MAXV + 1], f_j0[MVC_MAXV];
+  __shared__ double f_mv[MVC_MAXV], f_lmv[MVC_MAXV], f_nl[MVC_MAXV], f_mxr[kSeqRunWaves];
+  RUN_T0();
+  const int np0 = W.n_t[p0] - 1;
+  const bool alive = np0 > 0;
+  const int Tne_i = *W.T_ne - (alive ? 0 : 1);
+  const double mass0 = (double)np0 - sg;
+  const double lmass0 = (np0 >= 1 && mass0 > 0.0) ? mvc_log(mass0) : 0.0;
+  const int T = *W.T;
+  const int TB = (T + 15) / 16;
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int v = 0; v < V; ++v) { f_koff[v] = o; o += W.Klist[v]; }
+    f_koff[V] = o;
+  }
+  for (int v = threadIdx.x; v < V; v += blockDim.x) f_j0[v] = W.dish[v * ts + p0];
+  if (r == 0) {   // the combined max and count (member row 0), the new dish
+    for (int v = lane; v < V; v += 64) {
+      double mx = -MVC_PM_INF;
+      int cnt = 0;
+      {
+        const double x = S.wide[V + 8 + v];
+        if (x > mx) mx = x;
+        cnt += (int)S.wide[V + 8 + 8 * V + v];
+      }
+      const double Y2i = C.Y2[(size_t)v * C.y2stride];
+      const double lfn = A.cnew[v] + (-0.5 * Y2i) / P.hyper[v];
+      const double m = lfn > mx ? lfn : mx;
+      S.mv[v] = m;
+      f_mv[v] = m;
+      kact[v] = cnt;
+    }
+  }
+  __syncthreads();
+  const int NK = f_koff[V];
+  auto view_of = [&](int g) {
+    int v = 0;
+    while (v + 1 < V && g >= f_koff[v + 1]) ++v;
+    return v;
+  };
+  {   // the lp rows, concatenated by view: 8 loads per thread in flight
+    constexpr int kC = 8;
+    const int bd = blockDim.x;
+    for (int g0 = threadIdx.x; g0 < NK; g0 += kC * bd) {
+      double x[kC];
+#pragma unroll
+      for (int u = 0; u < kC; ++u) {
+        const int g = min(g0 + u * bd, NK - 1);
+        const int v = view_of(g);
+        x[u] = S.lp[(size_t)v * lps + (g - f_koff[v])];
+      }
+#pragma unroll
+      for (int u = 0; u < kC; ++u)
+        if (g0 + u * bd < NK) L[g0 + u * bd] = x[u];
+    }
+  }
+  __syncthreads();
+  // table scores in view order (every load of a step issued at once), member maxima
+  double M = -MVC_PM_INF;
+  {
+    constexpr int kU = 8;
+    const int nch = TB * 16;
+    constexpr int kVR = 4;   // views whose dish indices are loaded with the step's other loads
+    for (int c0 = r; c0 * 64 < nch; c0 += tw * kU) {
+      int np[kU], dj[kU][kVR];
+      double lm[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        const int pc = min(p, T - 1);
+        np[u] = p < T ? W.n_t[pc] - (p == p0 ? 1 : 0) : 0;
+        lm[u] = p < T ? ((p == p0) ? lmass0 : W.lmass[pc]) : 0.0;
+#pragma unroll
+        for (int v = 0; v < kVR; ++v) dj[u][v] = W.dish[min(v, V - 1) * ts + pc];
+      }
+      double sp[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        const double mass = (double)np[u] - sg;
+        sp[u] = (p < T && np[u] >= 1 && mass > 0.0) ? lm[u] : -MVC_PM_INF;
+      }
+#pragma unroll
+      for (int v = 0; v < kVR; ++v) {
+        if (v < V) {
+#pragma unroll
+          for (int u = 0; u < kU; ++u)
+            if (sp[u] != -MVC_PM_INF) sp[u] = sp[u] + L[f_koff[v] + dj[u][v]];
+        }
+      }
+      for (int v = kVR; v < V; ++v) {   // views past kVR: their dish index loaded here
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int p = (c0 + u * tw) * 64 + lane;
+          const int d = W.dish[v * ts + min(p, T - 1)];
+          if (sp[u] != -MVC_PM_INF) sp[u] = sp[u] + L[f_koff[v] + d];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int p = (c0 + u * tw) * 64 + lane;
+        if (p < nch) S.e[p] = sp[u];
+        if (sp[u] > M) M = sp[u];
+      }
+    }
+    M = wave_max(M);
+    if (lane == 0) f_mxr[r] = M;
+  }
+  __syncthreads();
+  RUN_MARK(1);
+  // pass 2: the weighted terms, over the rows in LDS (the table counts of 4
+  // chunks loaded at once)
+  for (int c0 = r; 64 * c0 < NK; c0 += 4 * tw) {
+    int lq[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int g = min(64 * (c0 + u * tw) + lane, NK - 1);
+      const int v = view_of(g), j = g - f_koff[v];
+      lq[u] = W.d_l[v * ks + j] - ((j == f_j0[v] && !alive) ? 1 : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int g = 64 * (c0 + u * tw) + lane;
+      if (g < NK) {
+        const int v = view_of(g);
+        const int l = lq[u];
+        double t = 0.0;
+        if (l > 0) {
+          double wgt = (double)l - P.hyper[2 * V + v];
+          if (wgt < 0.0) wgt = 0.0;
+          t = wgt * mvc_exp(L[g] - f_mv[v]);
+        }
+        L[g] = t;
+      }
+    }
+  }
+  __syncthreads();
+  // member 0: column partials in ascending j, pw16, the new dish, lm_v
+  if (r == 0) {
+    for (int vg = 0; vg < V; vg += 4) {
+      const int v = vg + row;
+      double cs = 0.0;
+      if (v < V) {
+        const int K = W.Klist[v];
+        const double *ax = L + f_koff[v] + col;
+        const int cnt = K > col ? (K - col + 15) >> 4 : 0;
+        double xa[16];
+        for (int e0 = 0; e0 < cnt; e0 += 16) {
+#pragma unroll
+          for (int u = 0; u < 16; ++u) xa[u] = e0 + u < cnt ? ax[16 * (e0 + u)] : 0.0;
+#pragma unroll
+          for (int u = 0; u < 16; ++u)
+            if (e0 + u < cnt) cs = cs + xa[u];
+        }
+      }
+      double Sv = row_pw16(cs);
+      if (v < V && col == 0) {
+        const double tau = P.hyper[v], alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+        const double Y2i = C.Y2[(size_t)v * C.y2stride];
+        const double lfn = A.cnew[v] + (-0.5 * Y2i) / tau;
+        const double m = f_mv[v];
+        double wn = alpha + (double)kact[v] * sigma;
+        if (wn < 0.0) wn = 0.0;
+        const double nl = wn * mvc_exp(lfn - m);   // also the new dish's leaf of a birth's dish draw
+        f_nl[v] = nl;
+        Sv = Sv + nl;
+        const double denom = alpha + (double)(W.Ltot[v] - (alive ? 0 : 1));
+        f_lmv[v] = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - mvc_log(denom);
+      }
+    }
+  }
+  __syncthreads();
+  RUN_MARK(0);
+  // s_new in view order (every member); weights, block sums B_b into L after the terms
+  double *Lb = L + NK;
+  double s_new = mvc_log(ag + sg * (double)Tne_i);
+  for (int v = 0; v < V; ++v) s_new = s_new + f_lmv[v];
+  for (int k = 0; k < tw; ++k) M = f_mxr[k] > M ? f_mxr[k] : M;
+  if (s_new > M) M = s_new;
+  for (int c0 = r; c0 * 64 < TB * 16; c0 += tw) {
+    const int p = c0 * 64 + lane;
+    double wgt = 0.0;
+    if (p < TB * 16) {
+      const double x = S.e[p];
+      wgt = x != -MVC_PM_INF ? mvc_exp(x - M) : 0.0;
+      S.e[p] = wgt;
+    }
+    const double Bv = row_pw16(wgt);
+    const int b = c0 * 4 + row;
+    if (col == 0 && b < TB) Lb[b] = Bv;
+  }
+  __syncthreads();
+  RUN_MARK(2);
+  int pick = -1;
+  if (r == 0) {   // running block totals in block order on lane 0 from LDS (8 reads in flight), the draw
+    __shared__ double f_tot;
+    __shared__ int f_bsel;
+    __shared__ double f_cprev;
+    const double u0 = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);
+    if (lane == 0) {
+      double tot = 0.0;
+      int b = 0;
+      for (; b + 8 <= TB; b += 8) {
+        double x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = Lb[b + q];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tot = tot + x[q];
+      }
+      for (; b < TB; ++b) tot = tot + Lb[b];
+      const double Wt = mvc_exp(s_new - M) + tot;
+      const double u = u0 * Wt;
+      int bsel = -1;
+      double cprev = 0.0;
+      if (u < tot) {   // the first block whose running total exceeds u (the same sums again)
+        double c = 0.0;
+        bsel = TB - 1;
+        b = 0;
+        bool found = false;
+        for (; b + 8 <= TB && !found; b += 8) {
+          double x[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) x[q] = Lb[b + q];
+          int hit = 8;
+          double cp = c;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const double c2 = c + x[q];
+            if (hit == 8 && u < c2) { hit = q; cp = c; }
+            c = c2;
+          }
+          if (hit < 8) { bsel = b + hit; cprev = cp; found = true; }
+        }
+        for (; b < TB && !found; ++b) {
+          const double c2 = c + Lb[b];
+          if (u < c2) { bsel = b; cprev = c; found = true; }
+          c = c2;
+        }
+      }
+      f_tot = u;
+      f_bsel = bsel;
+      f_cprev = cprev;
+    }
+    wave_lds_sync();
+    const int bsel = f_bsel;
+    if (bsel >= 0) {
+      const double u = f_tot - f_cprev;
+      const double x = lane < 16 ? S.e[bsel * 16 + lane] : 0.0;
+      pick = bsel * 16 + pw16_select_wave(x, u);
+    } else {
+      pick = -1;
+    }
+  }
+  RUN_MARK(3);
+  int kmax = 0;
+  for (int v = 0; v < V; ++v) kmax = max(kmax, W.Klist[v]);
+  fl.L = L;
+  fl.koff = f_koff;
+  fl.newleaf = f_nl;
+  fl.up = Lb + TB;
+  fl.upstride = fin_tree_up(kmax);
+  return pick;
+}
+
 // One block of kSeqRunThreads: a pending mover from a resolved window is
 // committed; otherwise customer cur is decided from the lp rows and partials
 // of mvc_seq_wide_lp_kernel (nblk blocks) and committed when it moves.  After
 // `limit` stays in a row (stay_limit) it hands over to the grid windows.
 extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_kernel(SeqArgs A, const double *part,
-                                                                                     int nblk, int limit) {
+                                                                                     int nblk, int limit, int lds_cap) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, w = tid >> 6, nw = blockDim.x >> 6;
@@ -2344,8 +2715,11 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_ke
   if (tid < 12) mvc_prof_lds[tid] = 0;
   __syncthreads();
   uint64_t f0 = wall_clock64();
+  const uint64_t w_start = f0, c_start = clock64();
   auto fin_flush = [&](int decided, int committed) {   // thread 0: this launch's phases into R->prof[12..]
     if (tid == 0) {
+      R->prof[20] += wall_clock64() - w_start;
+      R->prof[21] += clock64() - c_start;
       R->prof[17] += committed ? wall_clock64() - f0 : 0;
       for (int k = 0; k < 4; ++k) R->prof[13 + k] += mvc_prof_lds[k];
       R->prof[18] += decided;
@@ -2385,7 +2759,24 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_ke
   }
   __syncthreads();
   FIN_MARK(12);
-  const int c = seq_resample_wide(A, global_view(A), global_cust(A, i), i, p0, S0, w, nw, true, true);
+  int c;
+  FinLeaves fl{};
+  bool use_fl = false;
+  {   // the LDS-resident evaluation when the dish terms, block totals and dish-draw trees fit
+    const SView W0 = global_view(A);
+    int nk = 0, kmax = 0;
+    for (int v = 0; v < V; ++v) {
+      nk += W0.Klist[v];
+      kmax = max(kmax, W0.Klist[v]);
+    }
+    const int tb = (*W0.T + 15) / 16;
+    if (fin_lds_doubles(nk, tb, V, kmax) * 8 <= (int64_t)lds_cap) {
+      c = wide_fin_resample(A, W0, global_cust(A, i), i, p0, S0, w, nw, mvc_seq_lds, fl);
+      use_fl = true;
+    } else {
+      c = seq_resample_wide(A, W0, global_cust(A, i), i, p0, S0, w, nw, true, true);
+    }
+  }
   if (tid == 0) s_c = c;   // member 0's pick
   __syncthreads();
 #ifdef MVC_RUN_PROF
@@ -2410,7 +2801,8 @@ extern "C" __global__ __launch_bounds__(kSeqRunThreads) void mvc_seq_wide_fin_ke
     return;
   }
   // a move or a birth: committed on the global state, dish draws from the rows above
-  if (!seq_commit(A, global_view(A), nullptr, global_cust(A, i), i, p0, ch, Sw.lp, Sw.tree, &R->moves, nw, &S0)) {
+  if (!seq_commit(A, global_view(A), nullptr, global_cust(A, i), i, p0, ch, Sw.lp, Sw.tree, &R->moves, nw, &S0, false,
+                  use_fl ? fl : FinLeaves{})) {
     if (tid == 0) {   // overflow: left pending (the next round commits it after the growth)
       R->pend = 1;
       R->pchoice = ch;

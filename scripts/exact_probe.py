@@ -2,7 +2,7 @@
 chains, two launches of 64 sweeps each (the PMC target of
 scripts/gpu_pmc_exact.sh; also prints the sweeps/s of the second launch).
 
-    python scripts/exact_probe.py [C]
+    python scripts/exact_probe.py [C] [n]   (n < 200: the first n customers)
 """
 import json
 import os
@@ -16,6 +16,8 @@ from mvc_amd import data  # noqa: E402
 
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
 y, _ = data.new_simulation(1999)
+if len(sys.argv) > 2:
+    y = [v[: int(sys.argv[2])].copy() for v in y]
 s = mvc_amd.Sampler(y, seed=1999, mode="exact", n_chains=C)
 s.sweep(64)
 s.synchronize()
@@ -24,4 +26,4 @@ s.sweep(64)
 s.synchronize()
 dt = time.perf_counter() - t0
 s.close()
-print(json.dumps({"chains": C, "sweeps": 64, "s": round(dt, 4), "chain_sweeps_per_s": round(C * 64 / dt, 1)}))
+print(json.dumps({"chains": C, "n": len(y[0]), "lib": os.path.basename(os.path.dirname(mvc_amd.lib()._name)), "sweeps": 64, "s": round(dt, 4), "chain_sweeps_per_s": round(C * 64 / dt, 1)}))

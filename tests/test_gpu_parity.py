@@ -731,15 +731,19 @@ def test_shard_ranks_equal_unsharded(world, tmp_path):
     s.close()
 
 
-@pytest.mark.parametrize("wide,V", [("1", 3), ("0", 3), ("1", 5), ("block", 3), ("block", 5)])
-def test_repair_global_wide(wide, V, monkeypatch):
+@pytest.mark.parametrize("wide,V,fin", [("1", 3, "1"), ("1", 3, "0"), ("0", 3, "1"), ("1", 5, "1"), ("1", 5, "0"),
+                                        ("block", 3, "1"), ("block", 5, "1")])
+def test_repair_global_wide(wide, V, fin, monkeypatch):
     """The run kernel on its global-scratch layout (MVC_RUN_LDS=0, as when
-    the state outgrows the LDS): the whole block evaluating one customer
-    (seq_resample_wide: dishes, tables and scans split over the 8 waves) or
-    one customer per wave (MVC_WIDE=0); bitwise vs oracle SeqSampler through
-    the births of a cold start."""
+    the state outgrows the LDS): one customer over the grid (MVC_WIDE=1: lp
+    kernel + fin kernel, the fin kernel's evaluation in LDS or, MVC_WIDE_FIN=0,
+    in the global scratch), over the whole block (seq_resample_wide: dishes,
+    tables and scans split over the 8 waves) or one customer per wave
+    (MVC_WIDE=0); bitwise vs oracle SeqSampler through the births of a cold
+    start."""
     monkeypatch.setenv("MVC_RUN_LDS", "0")
     monkeypatch.setenv("MVC_WIDE", wide)
+    monkeypatch.setenv("MVC_WIDE_FIN", fin)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.synthetic(3000, V, 16, 6, seed=80 + V)
