@@ -16,6 +16,60 @@
 
 namespace {
 
+// Byte offsets of a chain's arrays in its allocation (carve), 16-byte
+// granules; the sweep kernel also uses it to write a compacted chain back.
+struct ExactLayout {
+  size_t z, n_t, pos, slot, fre, dish, d_id, d_n, d_l, S1, S2, f, logf, P, mh, ldt, Kact, next_id, hyper, total;
+};
+__host__ __device__ inline ExactLayout exact_layout(int n, int V, int TC, int KC) {
+  ExactLayout L{};
+  size_t o = 0;
+  auto take = [&](size_t x) { const size_t r = o; o += (x + 15) & ~(size_t)15; return r; };
+  L.z = take(4 * (size_t)n);
+  L.n_t = take(4 * (size_t)TC);
+  L.pos = take(4 * (size_t)TC);
+  L.slot = take(4 * (size_t)TC);
+  L.fre = take(4 * (size_t)TC);
+  L.dish = take(4 * (size_t)V * TC);
+  L.d_id = take(4 * (size_t)V * KC);
+  L.d_n = take(4 * (size_t)V * KC);
+  L.d_l = take(4 * (size_t)V * KC);
+  L.S1 = take(8 * (size_t)V * KC);
+  L.S2 = take(8 * (size_t)V * KC);
+  L.f = take(8 * (size_t)V * KC);
+  L.logf = take(8 * (size_t)V * KC);
+  L.P = take(8 * (size_t)TC);
+  L.mh = take(8 * (size_t)(n + 1));
+  L.ldt = take(8 * (size_t)V * (n + 2));
+  L.Kact = take(4 * (size_t)V);
+  L.next_id = take(4 * (size_t)V);
+  L.hyper = take(8 * (size_t)(3 * V + 2));
+  L.total = o;
+  return L;
+}
+// the chain's pointers over its allocation `base` in layout L
+__host__ __device__ inline void exact_point(ExactChain &C, char *base, const ExactLayout &L) {
+  C.z = (int32_t *)(base + L.z);
+  C.n_t = (int32_t *)(base + L.n_t);
+  C.pos_of_slot = (int32_t *)(base + L.pos);
+  C.slot_at_pos = (int32_t *)(base + L.slot);
+  C.free_slots = (int32_t *)(base + L.fre);
+  C.dish = (int32_t *)(base + L.dish);
+  C.d_id = (int32_t *)(base + L.d_id);
+  C.d_n = (int32_t *)(base + L.d_n);
+  C.d_l = (int32_t *)(base + L.d_l);
+  C.d_S1 = (double *)(base + L.S1);
+  C.d_S2 = (double *)(base + L.S2);
+  C.f = (double *)(base + L.f);
+  C.logf = (double *)(base + L.logf);
+  C.P = (double *)(base + L.P);
+  C.mhbuf = (double *)(base + L.mh);
+  C.ldt = (double *)(base + L.ldt);
+  C.Kact = (int32_t *)(base + L.Kact);
+  C.next_id = (int32_t *)(base + L.next_id);
+  C.hyper = (double *)(base + L.hyper);
+}
+
 // multiview_utils.cpp:307-338 compute_f_vk, literal expression order.  The
 // two log-determinant terms, -0.5 m log(2 pi tau) - 0.5 log(tau (tau + m)),
 // depend on the view and the count m only and are the same until the MH moves
@@ -765,6 +819,51 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MVC_EXACT_WA
   if (status == MVC_ST_RUNNING) status = MVC_ST_DONE;
   __syncthreads();
   if (prof && lane < 8) SV.prof[(size_t)blockIdx.x * 8 + lane] += sh.prof[lane];
+  // Table capacity back down when T stays far below it (the cold transient
+  // grows it to ~n): tables relabelled slot = position and written back in the
+  // layout of TC / 2, so the next launch copies (and reserves) less LDS and
+  // more chains are resident per CU.  Slots are storage only (every sum and
+  // draw runs over positions), so the chain is unchanged.
+  int TC2 = TC;
+#ifndef MVC_EXACT_SHRINK
+#define MVC_EXACT_SHRINK 0
+#endif
+  if constexpr (kMode == 2 && MVC_EXACT_SHRINK)
+    if (status == MVC_ST_DONE && TC > 64 && T + 1 <= TC / 4) TC2 = max(64, TC / 2);
+  if (TC2 != TC) {
+    char *base = (char *)Cg.z;   // z is first in the allocation
+    const ExactLayout Ln = exact_layout(n, V, TC2, KC);
+    ExactChain Cn = C;
+    exact_point(Cn, base, Ln);
+    Cn.z = ex_global(y, Cn.z); Cn.n_t = ex_global(y, Cn.n_t); Cn.pos_of_slot = ex_global(y, Cn.pos_of_slot);
+    Cn.slot_at_pos = ex_global(y, Cn.slot_at_pos); Cn.free_slots = ex_global(y, Cn.free_slots);
+    Cn.dish = ex_global(y, Cn.dish); Cn.d_id = ex_global(y, Cn.d_id); Cn.d_n = ex_global(y, Cn.d_n);
+    Cn.d_l = ex_global(y, Cn.d_l); Cn.d_S1 = ex_global(y, Cn.d_S1); Cn.d_S2 = ex_global(y, Cn.d_S2);
+    for (int q = lane; q < n; q += MVC_WAVE) Cn.z[q] = C.pos_of_slot[C.z[q]];
+    for (int p = lane; p < TC2; p += MVC_WAVE) {
+      const int sl = p < T ? C.slot_at_pos[p] : 0;
+      Cn.n_t[p] = p < T ? C.n_t[sl] : 0;
+      Cn.pos_of_slot[p] = p < T ? p : -1;
+      Cn.slot_at_pos[p] = p < T ? p : -1;
+      Cn.free_slots[p] = p < TC2 - T ? TC2 - 1 - p : -1;   // pop gives slot T first
+      for (int v = 0; v < V; ++v) Cn.dish[v * TC2 + p] = p < T ? C.dish[v * TC + sl] : 0;
+    }
+    for (int e = lane; e < V * KC; e += MVC_WAVE) {
+      Cn.d_id[e] = C.d_id[e];
+      Cn.d_n[e] = C.d_n[e];
+      Cn.d_l[e] = C.d_l[e];
+      Cn.d_S1[e] = C.d_S1[e];
+      Cn.d_S2[e] = C.d_S2[e];
+    }
+    n_free = TC2 - T;
+    C.Kact = Cn.Kact;
+    C.next_id = Cn.next_id;
+    C.hyper = Cn.hyper;
+    if (lane == 0) {   // the device struct follows (the snapshot kernels read it); the host re-carves from TC
+      Cg.TC = TC2;
+      exact_point(Cg, base, Ln);
+    }
+  }
   for (int v = lane; v < V; v += MVC_WAVE) {
     C.Kact[v] = sh.Kact[v];
     C.next_id[v] = sh.next_id[v];
@@ -779,6 +878,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MVC_EXACT_WA
     Cg.todo = todo;
   }
   if constexpr (kMode != 0) {      // the LDS copy back to the chain's allocation
+    if (TC2 != TC) return;         // written back compacted above
     __syncthreads();
     const uint4 *src = (const uint4 *)ex_lds;
     uint4 *dst = (uint4 *)gbeg;
@@ -843,48 +943,13 @@ struct ExactAlloc {
   void *block = nullptr;   // single device allocation
 };
 
-size_t exact_bytes(int n, int V, int TC, int KC) {
-  size_t b = 0;
-  auto add = [&](size_t x) { b += (x + 15) & ~(size_t)15; };   // 16-byte granules: the LDS copy moves uint4
-  add(sizeof(int32_t) * n);                 // z
-  for (int k = 0; k < 4; ++k) add(sizeof(int32_t) * TC);  // n_t pos slot free
-  add(sizeof(int32_t) * (size_t)V * TC);    // dish
-  for (int k = 0; k < 3; ++k) add(sizeof(int32_t) * (size_t)V * KC);
-  for (int k = 0; k < 4; ++k) add(sizeof(double) * (size_t)V * KC);  // S1 S2 f logf
-  add(sizeof(double) * TC);                 // P
-  add(sizeof(double) * (size_t)(n + 1));    // mhbuf
-  add(sizeof(double) * (size_t)V * (n + 2));   // ldt
-  add(sizeof(int32_t) * V);                 // Kact
-  add(sizeof(int32_t) * V);                 // next_id
-  add(sizeof(double) * (3 * V + 2));        // hyper
-  return b;
-}
+size_t exact_bytes(int n, int V, int TC, int KC) { return exact_layout(n, V, TC, KC).total; }
 
 void carve(ExactAlloc &A, int n, int V, int TC, int KC) {
-  char *p = (char *)A.block;
-  auto take = [&](size_t x) { char *r = p; p += (x + 15) & ~(size_t)15; return (void *)r; };
   ExactChain &C = A.h;
   C.TC = TC;
   C.KC = KC;
-  C.z = (int32_t *)take(sizeof(int32_t) * n);
-  C.n_t = (int32_t *)take(sizeof(int32_t) * TC);
-  C.pos_of_slot = (int32_t *)take(sizeof(int32_t) * TC);
-  C.slot_at_pos = (int32_t *)take(sizeof(int32_t) * TC);
-  C.free_slots = (int32_t *)take(sizeof(int32_t) * TC);
-  C.dish = (int32_t *)take(sizeof(int32_t) * (size_t)V * TC);
-  C.d_id = (int32_t *)take(sizeof(int32_t) * (size_t)V * KC);
-  C.d_n = (int32_t *)take(sizeof(int32_t) * (size_t)V * KC);
-  C.d_l = (int32_t *)take(sizeof(int32_t) * (size_t)V * KC);
-  C.d_S1 = (double *)take(sizeof(double) * (size_t)V * KC);
-  C.d_S2 = (double *)take(sizeof(double) * (size_t)V * KC);
-  C.f = (double *)take(sizeof(double) * (size_t)V * KC);
-  C.logf = (double *)take(sizeof(double) * (size_t)V * KC);
-  C.P = (double *)take(sizeof(double) * TC);
-  C.mhbuf = (double *)take(sizeof(double) * (size_t)(n + 1));
-  C.ldt = (double *)take(sizeof(double) * (size_t)V * (n + 2));
-  C.Kact = (int32_t *)take(sizeof(int32_t) * V);
-  C.next_id = (int32_t *)take(sizeof(int32_t) * V);
-  C.hyper = (double *)take(sizeof(double) * (3 * V + 2));
+  exact_point(C, (char *)A.block, exact_layout(n, V, TC, KC));
 }
 
 // Host-side image of a chain's state (used for init and capacity growth).
@@ -1235,6 +1300,7 @@ class ExactSampler : public Sampler {
     MVC_HIP(hipStreamSynchronize(stream));
     for (size_t k = 0; k < chains.size(); ++k) {
       ExactChain &C = chains[k].h;
+      if (hs[k].TC != C.TC) carve(chains[k], n, V, hs[k].TC, C.KC);   // the kernel compacted the tables (TC / 2)
       C.T = hs[k].T; C.n_free = hs[k].n_free; C.draws = hs[k].draws;
       C.resume_i = hs[k].resume_i; C.status = hs[k].status; C.todo = hs[k].todo;
     }
