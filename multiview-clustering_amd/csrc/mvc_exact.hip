@@ -17,7 +17,7 @@
 namespace {
 
 // Byte offsets of a chain's arrays in its allocation (carve), 16-byte
-// granules; the sweep kernel also uses it to write a compacted chain back.
+// granules.
 struct ExactLayout {
   size_t z, n_t, pos, slot, fre, dish, d_id, d_n, d_l, S1, S2, f, logf, P, mh, ldt, Kact, next_id, hyper, total;
 };
@@ -458,11 +458,8 @@ __device__ __forceinline__ void ex_sync() {
   }
 }
 
-#ifndef MVC_EXACT_WAVES
-#define MVC_EXACT_WAVES 2   // waves per SIMD the register allocation must allow (LDS allows ~8 chains per CU at n = 200)
-#endif
 template <int kMode, int MV>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MVC_EXACT_WAVES, 8))) void mvc_exact_sweep_kernel(
+__global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
     const double *__restrict__ y, int n, int V, ExactChain *chains, uint64_t seed, ExactSave SV) {
   __shared__ Shared<MV> sh;
   extern __shared__ __attribute__((aligned(16))) char ex_lds[];
@@ -819,51 +816,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MVC_EXACT_WA
   if (status == MVC_ST_RUNNING) status = MVC_ST_DONE;
   __syncthreads();
   if (prof && lane < 8) SV.prof[(size_t)blockIdx.x * 8 + lane] += sh.prof[lane];
-  // Table capacity back down when T stays far below it (the cold transient
-  // grows it to ~n): tables relabelled slot = position and written back in the
-  // layout of TC / 2, so the next launch copies (and reserves) less LDS and
-  // more chains are resident per CU.  Slots are storage only (every sum and
-  // draw runs over positions), so the chain is unchanged.
-  int TC2 = TC;
-#ifndef MVC_EXACT_SHRINK
-#define MVC_EXACT_SHRINK 0
-#endif
-  if constexpr (kMode == 2 && MVC_EXACT_SHRINK)
-    if (status == MVC_ST_DONE && TC > 64 && T + 1 <= TC / 4) TC2 = max(64, TC / 2);
-  if (TC2 != TC) {
-    char *base = (char *)Cg.z;   // z is first in the allocation
-    const ExactLayout Ln = exact_layout(n, V, TC2, KC);
-    ExactChain Cn = C;
-    exact_point(Cn, base, Ln);
-    Cn.z = ex_global(y, Cn.z); Cn.n_t = ex_global(y, Cn.n_t); Cn.pos_of_slot = ex_global(y, Cn.pos_of_slot);
-    Cn.slot_at_pos = ex_global(y, Cn.slot_at_pos); Cn.free_slots = ex_global(y, Cn.free_slots);
-    Cn.dish = ex_global(y, Cn.dish); Cn.d_id = ex_global(y, Cn.d_id); Cn.d_n = ex_global(y, Cn.d_n);
-    Cn.d_l = ex_global(y, Cn.d_l); Cn.d_S1 = ex_global(y, Cn.d_S1); Cn.d_S2 = ex_global(y, Cn.d_S2);
-    for (int q = lane; q < n; q += MVC_WAVE) Cn.z[q] = C.pos_of_slot[C.z[q]];
-    for (int p = lane; p < TC2; p += MVC_WAVE) {
-      const int sl = p < T ? C.slot_at_pos[p] : 0;
-      Cn.n_t[p] = p < T ? C.n_t[sl] : 0;
-      Cn.pos_of_slot[p] = p < T ? p : -1;
-      Cn.slot_at_pos[p] = p < T ? p : -1;
-      Cn.free_slots[p] = p < TC2 - T ? TC2 - 1 - p : -1;   // pop gives slot T first
-      for (int v = 0; v < V; ++v) Cn.dish[v * TC2 + p] = p < T ? C.dish[v * TC + sl] : 0;
-    }
-    for (int e = lane; e < V * KC; e += MVC_WAVE) {
-      Cn.d_id[e] = C.d_id[e];
-      Cn.d_n[e] = C.d_n[e];
-      Cn.d_l[e] = C.d_l[e];
-      Cn.d_S1[e] = C.d_S1[e];
-      Cn.d_S2[e] = C.d_S2[e];
-    }
-    n_free = TC2 - T;
-    C.Kact = Cn.Kact;
-    C.next_id = Cn.next_id;
-    C.hyper = Cn.hyper;
-    if (lane == 0) {   // the device struct follows (the snapshot kernels read it); the host re-carves from TC
-      Cg.TC = TC2;
-      exact_point(Cg, base, Ln);
-    }
-  }
   for (int v = lane; v < V; v += MVC_WAVE) {
     C.Kact[v] = sh.Kact[v];
     C.next_id[v] = sh.next_id[v];
@@ -878,7 +830,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MVC_EXACT_WA
     Cg.todo = todo;
   }
   if constexpr (kMode != 0) {      // the LDS copy back to the chain's allocation
-    if (TC2 != TC) return;         // written back compacted above
     __syncthreads();
     const uint4 *src = (const uint4 *)ex_lds;
     uint4 *dst = (uint4 *)gbeg;
@@ -1300,7 +1251,6 @@ class ExactSampler : public Sampler {
     MVC_HIP(hipStreamSynchronize(stream));
     for (size_t k = 0; k < chains.size(); ++k) {
       ExactChain &C = chains[k].h;
-      if (hs[k].TC != C.TC) carve(chains[k], n, V, hs[k].TC, C.KC);   // the kernel compacted the tables (TC / 2)
       C.T = hs[k].T; C.n_free = hs[k].n_free; C.draws = hs[k].draws;
       C.resume_i = hs[k].resume_i; C.status = hs[k].status; C.todo = hs[k].todo;
     }

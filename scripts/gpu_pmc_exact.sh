@@ -31,3 +31,4 @@ for grp in ("a", "b", "c", "d"):
         out["counters"].update(per[last])
 print(json.dumps(out, indent=1))
 PY
+rm -rf gpurun_out/pmcx_${TAG}_*/   # the raw CSVs (tens of MB); the summary above is what is kept

@@ -161,29 +161,6 @@ def test_exact_storage_modes(mode, monkeypatch):
         _compare(g, ref)
 
 
-def test_exact_capacity_grows_and_shrinks():
-    """New_Simulation's cold transient grows the table capacity to n + 1
-    (T ~ 170), then T falls to a handful and the sweep kernel compacts the
-    tables into half the capacity at the end of a launch (slots relabelled by
-    position, written back in the smaller layout); one-sweep launches, every
-    sweep bitwise vs the oracle, samples through the snapshot kernel."""
-    m = _mvc()
-    from mvc_amd import data
-    y, _ = data.new_simulation(1999)
-    M = 110
-    s = m.Sampler(y, seed=1999, mode="exact", n_chains=2)
-    refs = [O.run(y, M, 0, 1, seed=1999, chain=c, mode=O.EXACT, math=O.PORTABLE) for c in range(2)]
-    for it in range(M):
-        s.sweep(1)
-        for c in range(2):
-            t, d, h = s.state(chain=c)
-            assert np.array_equal(t, refs[c]["table_of"][it]), (it, c)
-            assert np.array_equal(d, refs[c]["dish_of"][it]), (it, c)
-            assert h["alpha_global"] == refs[c]["alpha_global"][it]
-    s.close()
-    assert len(np.unique(refs[0]["table_of"][-1])) < 201 // 4   # the shrink condition was reached
-
-
 def test_exact_capacity_growth():
     """Tiny initial capacities force the overflow -> regrow -> resume path."""
     m = _mvc()
