@@ -1023,8 +1023,12 @@ class ExactSampler : public Sampler {
     for (int v = 0; v < V; ++v) std::memcpy(&y[(size_t)v * n], views[v], sizeof(double) * n);
     MVC_HIP(hipMalloc(&y_dev, sizeof(double) * y.size()));
     MVC_HIP(hipMemcpyAsync(y_dev, y.data(), sizeof(double) * y.size(), hipMemcpyHostToDevice, stream));
-    const int TC = std::max(c.table_cap > 0 ? c.table_cap : 64, 8);
-    const int KC = std::max(c.dish_cap > 0 ? c.dish_cap : 32, 4);
+    // Default capacities 71 and 39 (7 mod 32), not 64 and 32: the per-view rows
+    // [V][TC] and [V][KC] are read with one lane per view at the same index
+    // (v * KC + j) and with one lane per dish across views, and a row stride
+    // that is a multiple of 32 dwords puts every view on the same LDS bank.
+    const int TC = std::max(c.table_cap > 0 ? c.table_cap : 71, 8);
+    const int KC = std::max(c.dish_cap > 0 ? c.dish_cap : 39, 4);
     chains.resize(c.n_chains);
     for (int ch = 0; ch < c.n_chains; ++ch) {
       const uint32_t gid = chain_gid(c, ch);

@@ -2772,7 +2772,7 @@ class ParallelSampler : public Sampler {
           hipLaunchKernelGGL(mvc_seq_wide_begin_kernel, dim3(1), dim3(64), 0, stream, Q);
           for (int b = 0; b < kWideBatch; ++b) {
             hipLaunchKernelGGL(mvc_seq_wide_lp_kernel, dim3(wblk), dim3(kWideGridThreads), 0, stream, Q, wide_part);
-            hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), kWideFinLds, stream, Q,
+            hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), wide_fin_lds, stream, Q,
                                (const double *)wide_part, wblk, L.limit, wide_fin_lds);
           }
           MVC_HIP(hipGetLastError());

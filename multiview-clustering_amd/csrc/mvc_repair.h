@@ -2535,18 +2535,18 @@ __device__ int wide_fin_resample(const SeqArgs &A, const SView &W, const Cust &C
   }
   __syncthreads();
   RUN_MARK(1);
-  // pass 2: the weighted terms, over the rows in LDS (the table counts of 4
+  // pass 2: the weighted terms, over the rows in LDS (the table counts of 8
   // chunks loaded at once)
-  for (int c0 = r; 64 * c0 < NK; c0 += 4 * tw) {
-    int lq[4];
+  for (int c0 = r; 64 * c0 < NK; c0 += 8 * tw) {
+    int lq[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int g = min(64 * (c0 + u * tw) + lane, NK - 1);
       const int v = view_of(g), j = g - f_koff[v];
       lq[u] = W.d_l[v * ks + j] - ((j == f_j0[v] && !alive) ? 1 : 0);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < 8; ++u) {
       const int g = 64 * (c0 + u * tw) + lane;
       if (g < NK) {
         const int v = view_of(g);
