@@ -526,11 +526,15 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
       for (int m = lane; m < n + 2; m += MVC_WAVE) C.ldt[(size_t)v * (n + 2) + m] = ref_log_det(m, tau[v], sh.l2pt[v]);
     __syncthreads();
     double ynx = lane < V ? y[(size_t)lane * n + i] : 0.0;
+    bool koff_dirty = true;   // uniform: Koff must be rebuilt (sweep start, a dish died or was opened)
     for (; i < n; ++i) {
       // -------- capacity guard (every step may add 1 table and 1 dish/view)
       int need = (T + 1 > TC || n_free < 1) ? 1 : 0;
       for (int v = 0; v < V; ++v) need |= (sh.Kact[v] + 1 > KC) ? 1 : 0;
       if (need) { status = MVC_ST_OVERFLOW; break; }
+      // the table draw's uniform (gibbs.cpp:185): its counter is the step's
+      // first draw, so it is formed here, beside the step's LDS waits
+      const double u_tab = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
 
       if (lane < V) sh.ys[lane] = ynx;
       if (lane < V && i + 1 < n) ynx = y[(size_t)lane * n + i + 1];   // the next customer's y, in flight during this step
@@ -603,22 +607,26 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
           }
           ex_sync<kMode>();
           if (lane == 0) sh.Kact[v] = K - 1;
+          koff_dirty = true;
           ex_sync<kMode>();
         }
       }
 
       tick(0);
       // ---------------- f_vk and log f_vk for every live dish (utils.cpp:83-108)
-      if (lane == 0) {
-        int acc = 0;
-        for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
-        sh.Koff[V] = acc;
+      if (koff_dirty) {   // the views' offsets in the dish list, after a dish count changed
+        if (lane == 0) {
+          int acc = 0;
+          for (int v = 0; v < V; ++v) { sh.Koff[v] = acc; acc += sh.Kact[v]; }
+          sh.Koff[V] = acc;
+        }
+        ex_sync<kMode>();
+        koff_dirty = false;
       }
-      ex_sync<kMode>();
       const int Ktot = sh.Koff[V];
       for (int e = lane; e < Ktot; e += MVC_WAVE) {
-        int v = 0;
-        while (sh.Koff[v + 1] <= e) ++v;
+        int v = 0;   // the view of entry e: how many view offsets 1 .. V-1 lie at or below it
+        for (int k = 1; k < V; ++k) v += (e >= sh.Koff[k]) ? 1 : 0;
         const int j = e - sh.Koff[v];
         const double f = ref_f_vk(C.d_n[v * KC + j], C.d_S1[v * KC + j], C.d_S2[v * KC + j], tau[v], sh.ys[v],
                                   C.ldt + (size_t)v * (n + 2));
@@ -699,7 +707,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         for (int p = lane; p < T; p += MVC_WAVE) C.P[p] = C.P[p] / sum_p;
         ex_sync<kMode>();
         if (lane == 0) {
-          const double u = mvc_seq_uniform(seed, (uint32_t)C.chain_id, C.draws);
+          const double u = u_tab;
           sh.iv[0] = seq_find8(u, T, [&](int p) { return C.P[p]; });
         }
         C.draws += 1;
@@ -724,6 +732,7 @@ __global__ __launch_bounds__(64) void mvc_exact_sweep_kernel(
         tick(5);
       } else {
         // create_empty_table + add_customer_to_new_table (utils.cpp:209-222)
+        koff_dirty = true;   // a view may open a dish
         n_free -= 1;
         const int sl = C.free_slots[n_free];
         const int pos = T;
