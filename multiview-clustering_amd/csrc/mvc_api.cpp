@@ -229,31 +229,47 @@ namespace {
 
 // One device's share of mvc_run: its chains in one handle, sweeps and the
 // saved samples (multiview_gibbs.cpp:150-210 incl. save_state at :205-206).
+// Samples are stored contiguously per chain (thousands of chains x hundreds of
+// samples would otherwise be millions of small allocations): table_of[c] is
+// S x n, dish_of[c] the samples' [V][T_s] blocks one after the other, doff[c]
+// their S + 1 offsets.
 struct RunPart {
   int S = 0;
-  std::vector<std::vector<std::vector<int32_t>>> table_of, dish_of;   // [chain][s]
+  std::vector<std::vector<int32_t>> table_of, dish_of;   // [chain] flat
+  std::vector<std::vector<size_t>> doff;                 // [chain][s]
   std::vector<std::vector<int>> T;
-  std::vector<std::vector<std::vector<double>>> traces;               // [chain][which]
+  std::vector<std::vector<std::vector<double>>> traces;  // [chain][which]
 };
 
 void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
   std::unique_ptr<mvc::Sampler> S(cf.mode == MVC_MODE_EXACT ? mvc::make_exact_sampler(cf, views)
                                                            : mvc::make_parallel_sampler(cf, views));
   const int C = cf.n_chains, V = cf.n_views, n = cf.n;
+  const int H = 3 * V + 2;
+  auto saved = [&](int it) { return it >= cf.burn_in && ((it - cf.burn_in) % cf.thin == 0); };   // gibbs.cpp:205
+  int64_t S_exp = 0;
+  for (int it = 0; it < cf.n_iter; ++it) S_exp += saved(it) ? 1 : 0;
   R.table_of.resize(C);
   R.dish_of.resize(C);
+  R.doff.assign(C, std::vector<size_t>(1, 0));
   R.T.resize(C);
   R.traces.assign(C, std::vector<std::vector<double>>(5));
-  std::vector<std::vector<std::vector<double>>> hv(C);   // [chain][s] hyper vectors
-  std::vector<double> hyper(3 * V + 2);
+  std::vector<std::vector<double>> hv(C);   // [chain] S x (3V + 2) hyper vectors
+  for (int c = 0; c < C; ++c) {
+    R.table_of[c].reserve((size_t)S_exp * n);
+    R.doff[c].reserve((size_t)S_exp + 1);
+    R.T[c].reserve((size_t)S_exp);
+    hv[c].reserve((size_t)S_exp * H);
+  }
+  std::vector<double> hyper(H);
   const bool quiet = (cf.flags & MVC_FLAG_QUIET) != 0;
   const mvc::Sampler::SampleFn save_fn = [&](int c, int T, const int32_t *t, const int32_t *d, const double *h) {
-    R.table_of[c].emplace_back(t, t + n);
-    R.dish_of[c].emplace_back(d, d + (size_t)V * T);
+    R.table_of[c].insert(R.table_of[c].end(), t, t + n);
+    R.dish_of[c].insert(R.dish_of[c].end(), d, d + (size_t)V * T);
+    R.doff[c].push_back(R.dish_of[c].size());
     R.T[c].push_back(T);
-    hv[c].emplace_back(h, h + 3 * V + 2);
+    hv[c].insert(hv[c].end(), h, h + H);
   };
-  auto saved = [&](int it) { return it >= cf.burn_in && ((it - cf.burn_in) % cf.thin == 0); };   // gibbs.cpp:205
   if (S->run_saving(cf.n_iter, cf.burn_in, cf.thin, quiet, save_fn)) {   // samples written on the device (exact)
     for (int it = 0; it < cf.n_iter; ++it) R.S += saved(it) ? 1 : 0;
   } else {
@@ -279,11 +295,7 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
         S->get_state(c, t.data(), &T, nullptr, 0, hyper.data());
         std::vector<int32_t> d((size_t)V * std::max(T, 1));
         S->get_state(c, nullptr, &T, d.data(), std::max(T, 1), nullptr);
-        d.resize((size_t)V * T);
-        R.table_of[c].push_back(std::move(t));
-        R.dish_of[c].push_back(std::move(d));
-        R.T[c].push_back(T);
-        hv[c].push_back(hyper);
+        save_fn(c, T, t.data(), d.data(), hyper.data());
       }
       R.S++;
     }
@@ -300,7 +312,7 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
     tr[MVC_TRACE_ALPHA_GLOBAL].resize(Sn);
     tr[MVC_TRACE_SIGMA_GLOBAL].resize(Sn);
     for (int s = 0; s < Sn; ++s) {
-      const auto &h = hv[c][s];
+      const double *h = hv[c].data() + (size_t)s * H;
       for (int v = 0; v < V; ++v) {
         tr[MVC_TRACE_TAU_V][(size_t)v * Sn + s] = h[v];
         tr[MVC_TRACE_ALPHA_V][(size_t)v * Sn + s] = h[V + v];
@@ -316,8 +328,9 @@ void run_part(const mvc_config &cf, const double *const *views, RunPart &R) {
 
 struct mvc_result {
   int S = 0, C = 0, n = 0, V = 0;
-  // [chain][s]
-  std::vector<std::vector<std::vector<int32_t>>> table_of, dish_of;
+  // [chain] flat, as RunPart: table_of S x n, dish_of the [V][T_s] blocks at doff[chain][s]
+  std::vector<std::vector<int32_t>> table_of, dish_of;
+  std::vector<std::vector<size_t>> doff;
   std::vector<std::vector<int>> T;
   // [chain][which] traces
   std::vector<std::vector<std::vector<double>>> traces;
@@ -603,6 +616,7 @@ int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out,
       const int k = c / nd;
       R->table_of.push_back(std::move(P.table_of[k]));
       R->dish_of.push_back(std::move(P.dish_of[k]));
+      R->doff.push_back(std::move(P.doff[k]));
       R->T.push_back(std::move(P.T[k]));
       R->traces.push_back(std::move(P.traces[k]));
     }
@@ -665,21 +679,17 @@ int mvc_result_num_tables(const mvc_result *r, int chain, int s) {
 }
 const int32_t *mvc_result_table_of(const mvc_result *r, int chain, int s) {
   if (!r || chain < 0 || chain >= r->C || s < 0 || s >= r->S) return nullptr;
-  return r->table_of[chain][s].data();
+  return r->table_of[chain].data() + (size_t)s * r->n;
 }
 const int32_t *mvc_result_dish_of(const mvc_result *r, int chain, int s) {
   if (!r || chain < 0 || chain >= r->C || s < 0 || s >= r->S) return nullptr;
-  return r->dish_of[chain][s].data();
+  return r->dish_of[chain].data() + r->doff[chain][s];
 }
 int mvc_result_copy_chain(const mvc_result *r, int chain, int32_t *table_of, int32_t *n_tables, int32_t *dish_of) {
   if (!r || chain < 0 || chain >= r->C) return MVC_ERR_ARG;
-  size_t off = 0;
-  for (int s = 0; s < r->S; ++s) {
-    if (table_of) std::copy(r->table_of[chain][s].begin(), r->table_of[chain][s].end(), table_of + (size_t)s * r->n);
-    if (n_tables) n_tables[s] = r->T[chain][s];
-    if (dish_of) std::copy(r->dish_of[chain][s].begin(), r->dish_of[chain][s].end(), dish_of + off);
-    off += r->dish_of[chain][s].size();
-  }
+  if (table_of) std::copy(r->table_of[chain].begin(), r->table_of[chain].end(), table_of);
+  if (n_tables) std::copy(r->T[chain].begin(), r->T[chain].end(), n_tables);
+  if (dish_of) std::copy(r->dish_of[chain].begin(), r->dish_of[chain].end(), dish_of);
   return MVC_OK;
 }
 const double *mvc_result_trace(const mvc_result *r, int chain, int which) {

@@ -1360,8 +1360,23 @@ class ExactSampler : public Sampler {
     const int klim = (int)std::min<int64_t>(kSweepsPerLaunch, fit * thin);
     int32_t *dz = nullptr, *dd = nullptr, *dT = nullptr;
     double *dh = nullptr;
-    std::vector<int32_t> hz, hd, hT, dtmp;
-    std::vector<double> hh;
+    std::vector<int32_t> hT, dtmp;
+    // pinned host buffers for the samples (grown as needed): z, dish (Tmax wide), hyper
+    int32_t *hz = nullptr, *hd = nullptr;
+    double *hh = nullptr;
+    size_t hz_cap = 0, hd_cap = 0, hh_cap = 0;
+    auto pinned = [&](auto *&ptr, size_t &cap, size_t count) {
+      using Tp = std::remove_reference_t<decltype(*ptr)>;
+      if (count <= cap) return;
+      if (ptr) hipHostFree(ptr);
+      ptr = nullptr;
+      MVC_HIP(hipHostMalloc((void **)&ptr, sizeof(Tp) * count, hipHostMallocDefault));
+      cap = count;
+    };
+    auto release = [&]() {
+      for (void *q : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (q) hipFree(q);
+      for (void *q : {(void *)hz, (void *)hd, (void *)hh}) if (q) hipHostFree(q);
+    };
     int nslot = 0;
     try {
       for (int it0 = 0; it0 < n_iter;) {
@@ -1395,31 +1410,38 @@ class ExactSampler : public Sampler {
           for (int it = it0; it < it0 + k; ++it)
             if ((it + 1) % 100 == 0) std::fprintf(stderr, "Iteration %d / %d\n", it + 1, n_iter);   // gibbs.cpp:152-155
         if (m > 0) {   // samples in order, chain by chain (the callback's per-chain order)
-          hz.resize((size_t)C * nslot * n); hd.resize((size_t)C * nslot * V * dcap);
-          hT.resize((size_t)C * nslot); hh.resize((size_t)C * nslot * H);
-          MVC_HIP(hipMemcpyAsync(hz.data(), dz, sizeof(int32_t) * hz.size(), hipMemcpyDeviceToHost, stream));
-          MVC_HIP(hipMemcpyAsync(hd.data(), dd, sizeof(int32_t) * hd.size(), hipMemcpyDeviceToHost, stream));
-          MVC_HIP(hipMemcpyAsync(hT.data(), dT, sizeof(int32_t) * hT.size(), hipMemcpyDeviceToHost, stream));
-          MVC_HIP(hipMemcpyAsync(hh.data(), dh, sizeof(double) * hh.size(), hipMemcpyDeviceToHost, stream));
+          const size_t ns = (size_t)C * nslot;
+          hT.resize(ns);
+          MVC_HIP(hipMemcpyAsync(hT.data(), dT, sizeof(int32_t) * ns, hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipStreamSynchronize(stream));
+          int Tmax = 1;   // only the first Tmax dish entries of each [dcap] row are copied
+          for (int c = 0; c < C; ++c)
+            for (int sm = 0; sm < m; ++sm) Tmax = std::max(Tmax, hT[(size_t)c * nslot + sm]);
+          pinned(hz, hz_cap, ns * n);
+          pinned(hd, hd_cap, ns * V * Tmax);
+          pinned(hh, hh_cap, ns * H);
+          MVC_HIP(hipMemcpyAsync(hz, dz, sizeof(int32_t) * ns * n, hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipMemcpy2DAsync(hd, sizeof(int32_t) * Tmax, dd, sizeof(int32_t) * dcap, sizeof(int32_t) * Tmax,
+                                   ns * V, hipMemcpyDeviceToHost, stream));
+          MVC_HIP(hipMemcpyAsync(hh, dh, sizeof(double) * ns * H, hipMemcpyDeviceToHost, stream));
           MVC_HIP(hipStreamSynchronize(stream));
           for (int sm = 0; sm < m; ++sm)
             for (int c = 0; c < C; ++c) {
               const size_t slot = (size_t)c * nslot + sm;
               const int T = hT[slot];
-              dtmp.assign((size_t)V * T, 0);
+              dtmp.resize((size_t)V * T);
               for (int v = 0; v < V; ++v)
-                std::copy(hd.begin() + (slot * V + v) * dcap, hd.begin() + (slot * V + v) * dcap + T,
-                          dtmp.begin() + (size_t)v * T);
-              fn(c, T, hz.data() + slot * n, dtmp.data(), hh.data() + slot * H);
+                std::copy(hd + (slot * V + v) * Tmax, hd + (slot * V + v) * Tmax + T, dtmp.begin() + (size_t)v * T);
+              fn(c, T, hz + slot * n, dtmp.data(), hh + slot * H);
             }
         }
         it0 += k;
       }
     } catch (...) {
-      for (void *p : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (p) hipFree(p);
+      release();
       throw;
     }
-    for (void *p : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (p) hipFree(p);
+    release();
     return true;
   }
 
