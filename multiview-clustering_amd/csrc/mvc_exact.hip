@@ -1036,7 +1036,10 @@ class ExactSampler : public Sampler {
     // [V][TC] and [V][KC] are read with one lane per view at the same index
     // (v * KC + j) and with one lane per dish across views, and a row stride
     // that is a multiple of 32 dwords puts every view on the same LDS bank.
-    const int TC = std::max(c.table_cap > 0 ? c.table_cap : 71, 8);
+    // For n <= 512 the table capacity starts at its bound n + 1 (T <= n), so
+    // the cold transient (T ~ n at New_Simulation's sweeps 3-10) needs no
+    // overflow relaunch and per-chain regrowth.
+    const int TC = std::max(c.table_cap > 0 ? c.table_cap : (n + 1 <= 512 ? std::max(n + 1, 71) : 71), 8);
     const int KC = std::max(c.dish_cap > 0 ? c.dish_cap : 39, 4);
     chains.resize(c.n_chains);
     for (int ch = 0; ch < c.n_chains; ++ch) {

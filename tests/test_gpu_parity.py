@@ -149,8 +149,8 @@ def test_exact_many_chains_vs_live_oracle():
 def test_exact_storage_modes(mode, monkeypatch):
     """The sweep kernel's three storage instances (every chain array in global
     memory / all but z in LDS / all in LDS; MVC_EXACT_MODE caps the one the
-    sizes allow) give the oracle's chain, through the table-capacity growth of
-    New_Simulation's first sweeps (64 -> 128 -> n + 1)."""
+    sizes allow) give the oracle's chain through New_Simulation's cold
+    transient (T ~ 170 of n = 200)."""
     monkeypatch.setenv("MVC_EXACT_MODE", mode)
     m = _mvc()
     from mvc_amd import data
