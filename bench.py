@@ -334,7 +334,9 @@ CHILD_LEGS = {
     "configs4_full_gpu": (lambda seed, dev: config5_line(seed, dev), False),
     "exact_schedule_gpu": (lambda seed, dev: gpu_exact_line(seed, dev), False),
     "newsim_call": (lambda seed, dev: newsim_call_line(seed, dev), False),
-    "newsim_chains": (lambda seed, dev: newsim_chains_line(seed, dev), True),
+    # HIP's default hardware queues: at N = 200 the launches are short and 32 queues
+    # halved these chains' throughput (r4v bench vs the leg alone, r4x / r4y)
+    "newsim_chains": (lambda seed, dev: newsim_chains_line(seed, dev), False),
     "cold_start_gpu": (lambda seed, dev: cold_start(seed, dev), False),
 }
 
