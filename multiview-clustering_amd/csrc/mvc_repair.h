@@ -1180,6 +1180,19 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
   int jc[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) jc[u] = min(col + 16 * u, ks - 1);
+  // vp: the dishes of this view the overlay's moves m < nw touch, loaded once
+  // (vp_de's lookup against registers instead of LDS reads per dish; -2
+  // matches no dish)
+  int oj[2 * kVpMoves];
+#pragma unroll
+  for (int q = 0; q < 2 * kVpMoves; ++q) oj[q] = (kVp && q / 2 < X.nw) ? mvc_vp_ov.j[((q / 2) * kVpV + vv) * 2 + (q & 1)] : -2;
+  auto de = [&](int j) {
+    int e = -1;
+#pragma unroll
+    for (int q = 0; q < 2 * kVpMoves; ++q)
+      if (oj[q] == j) e = ((q / 2) * kVpV + vv) * 2 + (q & 1);
+    return e;
+  };
   // vp: a dish whose S1 column an earlier predicted move changed is read from
   // the overlay's copy of that column (stride 1) instead of the state's
   const double *colp[NU];
@@ -1189,7 +1202,7 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
     colp[u] = S1v + jc[u];
     cst[u] = s1s;
     if constexpr (kVp) {
-      const int e = vp_de<kVp>(X, vv, col + 16 * u);
+      const int e = de(col + 16 * u);
       if (e >= 0 && mvc_vp_ov.s1x[e]) {
         colp[u] = X.s1 + (size_t)e * D;
         cst[u] = 1;
@@ -1224,7 +1237,7 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
 #pragma unroll
   for (int u = 0; u < NU; ++u)
     if (col + 16 * u == j0) Gown = G[u];
-  const double self = lc_self<kVp>(W, vv, ks, j0, Gown, Y2i, hy, h, vp_de<kVp>(X, vv, j0));
+  const double self = lc_self<kVp>(W, vv, ks, j0, Gown, Y2i, hy, h, kVp ? de(j0) : -1);
   double lp[NU];
   int lj[NU];
   mx = -MVC_PM_INF;
@@ -1236,7 +1249,7 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
     double cbj = W.cb[vv * ks + jc[u]], c0j = W.c0[vv * ks + jc[u]];
     int dlj = dl[jc[u]];
     if constexpr (kVp) {
-      const int e = vp_de<kVp>(X, vv, j);
+      const int e = de(j);
       if (e >= 0) {
         cbj = mvc_vp_ov.cb[e];
         c0j = mvc_vp_ov.c0[e];
