@@ -8,7 +8,7 @@ import sys
 from collections import defaultdict
 
 tag = sys.argv[1]
-out = {"tag": tag, "kernel": "mvc_seq_run_kernel<3>", "counters": {}}
+out = {"tag": tag, "kernel": "mvc_seq_run_kernel (every instance the sweep launched)", "counters": {}}
 for grp in ("a", "b", "c"):
     tot = defaultdict(float)
     launches = set()
