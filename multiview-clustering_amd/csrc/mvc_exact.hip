@@ -888,6 +888,7 @@ extern "C" __global__ void mvc_exact_snapshot_all_kernel(int n, int V, const Exa
 // ===========================================================================
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "mvc_host.h"
@@ -1363,7 +1364,7 @@ class ExactSampler : public Sampler {
     const int klim = (int)std::min<int64_t>(kSweepsPerLaunch, fit * thin);
     int32_t *dz = nullptr, *dd = nullptr, *dT = nullptr;
     double *dh = nullptr;
-    std::vector<int32_t> hT, dtmp;
+    std::vector<int32_t> hT;
     // pinned host buffers for the samples (grown as needed): z, dish (Tmax wide), hyper
     int32_t *hz = nullptr, *hd = nullptr;
     double *hh = nullptr;
@@ -1428,15 +1429,28 @@ class ExactSampler : public Sampler {
                                    ns * V, hipMemcpyDeviceToHost, stream));
           MVC_HIP(hipMemcpyAsync(hh, dh, sizeof(double) * ns * H, hipMemcpyDeviceToHost, stream));
           MVC_HIP(hipStreamSynchronize(stream));
-          for (int sm = 0; sm < m; ++sm)
-            for (int c = 0; c < C; ++c) {
-              const size_t slot = (size_t)c * nslot + sm;
-              const int T = hT[slot];
-              dtmp.resize((size_t)V * T);
-              for (int v = 0; v < V; ++v)
-                std::copy(hd + (slot * V + v) * Tmax, hd + (slot * V + v) * Tmax + T, dtmp.begin() + (size_t)v * T);
-              fn(c, T, hz + slot * n, dtmp.data(), hh + slot * H);
-            }
+          // each chain's samples in order; the chains split over host threads
+          // (fn writes per chain: thousands of chains x the launch's samples)
+          auto emit = [&](int c0, int c1) {
+            std::vector<int32_t> dt;
+            for (int c = c0; c < c1; ++c)
+              for (int sm = 0; sm < m; ++sm) {
+                const size_t slot = (size_t)c * nslot + sm;
+                const int T = hT[slot];
+                dt.resize((size_t)V * T);
+                for (int v = 0; v < V; ++v)
+                  std::copy(hd + (slot * V + v) * Tmax, hd + (slot * V + v) * Tmax + T, dt.begin() + (size_t)v * T);
+                fn(c, T, hz + slot * n, dt.data(), hh + slot * H);
+              }
+          };
+          const int nth = C >= 256 ? std::min(8, std::max(1, (int)std::thread::hardware_concurrency())) : 1;
+          if (nth <= 1) {
+            emit(0, C);
+          } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nth; ++t) th.emplace_back(emit, (int)((int64_t)C * t / nth), (int)((int64_t)C * (t + 1) / nth));
+            for (auto &x : th) x.join();
+          }
         }
         it0 += k;
       }

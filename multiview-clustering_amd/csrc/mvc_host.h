@@ -119,8 +119,9 @@ class Sampler {
   // fn(chain, ...) runs for chains 0..C-1 in order); false where unsupported.
   virtual bool save_all_async(const SampleFn &fn) { (void)fn; return false; }
   // mvc_run's whole loop (gibbs.cpp:150-206) with the saved sweeps written on
-  // the device as the sweeps run (fn per chain and sample, in sample order);
-  // false where unsupported (the caller then sweeps and saves itself).
+  // the device as the sweeps run (fn per chain and sample, each chain's
+  // samples in order; calls for DIFFERENT chains may run concurrently on host
+  // threads); false where unsupported (the caller then sweeps and saves itself).
   virtual bool run_saving(int n_iter, int burn_in, int thin, bool quiet, const SampleFn &fn) {
     (void)n_iter; (void)burn_in; (void)thin; (void)quiet; (void)fn;
     return false;

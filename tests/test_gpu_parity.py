@@ -145,6 +145,20 @@ def test_exact_many_chains_vs_live_oracle():
         _compare(g, ref)
 
 
+def test_exact_run_many_chains_threaded_samples():
+    """mvc_run with 256 chains: the saved samples are emitted on several host
+    threads (one range of chains each); chains spread over the range are
+    bitwise the oracle's, samples in order."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(5)
+    gpus = m.run_gibbs_cpp(y, 8, 2, 2, seed=21, mode="exact", n_chains=256, quiet=True)
+    assert len(gpus) == 256
+    for c in (0, 37, 128, 255):
+        ref = O.run(y, 8, 2, 2, seed=21, chain=c, mode=O.EXACT, math=O.PORTABLE)
+        _compare(gpus[c], ref)
+
+
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
 def test_exact_storage_modes(mode, monkeypatch):
     """The sweep kernel's three storage instances (every chain array in global
