@@ -41,6 +41,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
 # alone, 1.44 s after a 16-stream run, r3r), so the headline and the
 # single-chain legs keep the caller's setting.
 HW_QUEUES_MULTI = "32"
+# the caller's setting, recorded before the library loads (mvc_amd's loader
+# sets 32 when the variable is unset); the other legs run with it, or with
+# HIP's own default of 4 when the caller set none
+CALLER_HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
 
 import numpy as np  # noqa: E402
 
@@ -348,8 +352,8 @@ def child_leg(name, seed, device, timeout=300):
     leg can take the headline line with it."""
     import subprocess
     env = dict(os.environ)
-    if CHILD_LEGS[name][1]:
-        env["GPU_MAX_HW_QUEUES"] = HW_QUEUES_MULTI
+    env["GPU_MAX_HW_QUEUES"] = (HW_QUEUES_MULTI if CHILD_LEGS[name][1] else
+                                CALLER_HW_QUEUES if CALLER_HW_QUEUES is not None else "4")
     t = time.perf_counter()
     try:
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--leg", name, "--seed", str(seed),

@@ -201,6 +201,32 @@ int guarded(char *err, size_t errlen, F &&f) {
   }
 }
 
+// MVC_DEVICE_MAP=a,b,...: logical device d of mvc_run's n_devices split runs
+// on physical device map[d % len] instead of device + d.  A test aid: with
+// "0,0" the per-device threads, chain striding and result interleave of
+// n_devices = 2 run on one GPU (two handles on one device).  Empty or unset:
+// no map.
+std::vector<int> device_map() {
+  std::vector<int> map;
+  const char *e = std::getenv("MVC_DEVICE_MAP");
+  if (!e) return map;
+  const std::string s(e);
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    const std::string tok = s.substr(i, j - i);
+    if (!tok.empty()) {
+      char *end = nullptr;
+      const long d = std::strtol(tok.c_str(), &end, 10);
+      if (!end || *end != '\0') throw mvc::Error(MVC_ERR_ARG, "MVC_DEVICE_MAP: not a list of device ordinals");
+      map.push_back((int)d);
+    }
+    i = j + 1;
+  }
+  return map;
+}
+
 void validate(const mvc_config *c, const double *const *views) {
   using mvc::Error;
   if (!c) throw Error(MVC_ERR_ARG, "config is NULL");
@@ -219,8 +245,13 @@ void validate(const mvc_config *c, const double *const *views) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) throw Error(MVC_ERR_HIP, "no HIP device visible");
   if (c->device < 0 || c->device >= ndev) throw Error(MVC_ERR_ARG, "device ordinal out of range");
-  if (c->n_devices > 1 && c->device + std::min(c->n_devices, c->n_chains) > ndev)
+  const std::vector<int> map = device_map();
+  if (!map.empty()) {
+    for (int d : map)
+      if (d < 0 || d >= ndev) throw Error(MVC_ERR_ARG, "MVC_DEVICE_MAP names a device that is not visible");
+  } else if (c->n_devices > 1 && c->device + std::min(c->n_devices, c->n_chains) > ndev) {
     throw Error(MVC_ERR_ARG, "n_devices: devices device .. device + n_devices - 1 are not all visible");
+  }
 }
 
 }  // namespace
@@ -581,12 +612,13 @@ int mvc_run(const mvc_config *cfg, const double *const *views, mvc_result **out,
     // * stride, k = 0, 1, ... (the id keys every Philox counter, so a chain
     // is the same wherever it runs)
     const int nd = std::max(1, std::min(cfg->n_devices, C));
+    const std::vector<int> dmap = nd > 1 ? device_map() : std::vector<int>();
     std::vector<RunPart> parts(nd);
     std::vector<std::exception_ptr> errs(nd);
     auto one = [&](int d) {
       try {
         mvc_config sc = *cfg;
-        sc.device = cfg->device + d;
+        sc.device = dmap.empty() ? cfg->device + d : dmap[d % dmap.size()];
         sc.n_devices = 1;
         sc.first_chain = (int32_t)mvc::chain_gid(*cfg, d);
         sc.chain_stride = (cfg->chain_stride > 0 ? cfg->chain_stride : 1) * nd;

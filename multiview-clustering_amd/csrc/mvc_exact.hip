@@ -887,7 +887,9 @@ extern "C" __global__ void mvc_exact_snapshot_all_kernel(int n, int V, const Exa
 // Host side of the exact schedule.
 // ===========================================================================
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <thread>
 #include <vector>
 
@@ -1359,29 +1361,62 @@ class ExactSampler : public Sampler {
   bool run_saving(int n_iter, int burn_in, int thin, bool quiet, const SampleFn &fn) override {
     const int C = (int)chains.size(), H = 3 * V + 2, dcap = std::max(n, 1);
     const size_t per_sample = sizeof(int32_t) * ((size_t)n + (size_t)V * dcap + 1) + sizeof(double) * H;
-    const int64_t fit = (int64_t)(kSaveBudget / std::max<size_t>(1, per_sample * C));
+    // the sample buffers of one launch: at most kSaveBudget and a quarter of
+    // the device's free memory (the run_part fallback saves without them)
+    size_t budget = kSaveBudget, free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) budget = std::min(budget, free_b / 4);
+    const int64_t fit = (int64_t)(budget / std::max<size_t>(1, per_sample * C));
     if (fit < 1 || thin < 1) return false;
     const int klim = (int)std::min<int64_t>(kSweepsPerLaunch, fit * thin);
     int32_t *dz = nullptr, *dd = nullptr, *dT = nullptr;
     double *dh = nullptr;
     std::vector<int32_t> hT;
-    // pinned host buffers for the samples (grown as needed): z, dish (Tmax wide), hyper
+    // pinned host buffers for the samples (grown as needed): z, dish (Tmax
+    // wide), hyper; pageable memory where pinned memory is refused
     int32_t *hz = nullptr, *hd = nullptr;
     double *hh = nullptr;
     size_t hz_cap = 0, hd_cap = 0, hh_cap = 0;
+    std::vector<void *> pageable;
+    auto host_free = [&](void *q) {
+      auto it = std::find(pageable.begin(), pageable.end(), q);
+      if (it != pageable.end()) { std::free(q); pageable.erase(it); }
+      else hipHostFree(q);
+    };
     auto pinned = [&](auto *&ptr, size_t &cap, size_t count) {
       using Tp = std::remove_reference_t<decltype(*ptr)>;
       if (count <= cap) return;
-      if (ptr) hipHostFree(ptr);
+      if (ptr) host_free(ptr);
       ptr = nullptr;
-      MVC_HIP(hipHostMalloc((void **)&ptr, sizeof(Tp) * count, hipHostMallocDefault));
+      if (hipHostMalloc((void **)&ptr, sizeof(Tp) * count, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        ptr = (Tp *)std::malloc(sizeof(Tp) * count);
+        if (!ptr) throw Error(MVC_ERR_HIP, "out of host memory for the samples");
+        pageable.push_back(ptr);
+      }
       cap = count;
     };
     auto release = [&]() {
       for (void *q : {(void *)dz, (void *)dd, (void *)dT, (void *)dh}) if (q) hipFree(q);
-      for (void *q : {(void *)hz, (void *)hd, (void *)hh}) if (q) hipHostFree(q);
+      for (void *q : {(void *)hz, (void *)hd, (void *)hh}) if (q) host_free(q);
     };
+    // the device buffers for the most samples one launch can hold, before the
+    // first launch: if they do not fit, nothing has run yet and the caller's
+    // sweep + save_all_async path takes over
     int nslot = 0;
+    {
+      if (n_iter > std::max(burn_in, 0)) {
+        nslot = std::min(klim, (klim + thin - 1) / thin + 1);
+        const bool ok = hipMalloc(&dz, sizeof(int32_t) * (size_t)C * nslot * std::max(n, 1)) == hipSuccess &&
+                        hipMalloc(&dd, sizeof(int32_t) * (size_t)C * nslot * V * dcap) == hipSuccess &&
+                        hipMalloc(&dT, sizeof(int32_t) * (size_t)C * nslot) == hipSuccess &&
+                        hipMalloc(&dh, sizeof(double) * (size_t)C * nslot * H) == hipSuccess;
+        if (!ok) {
+          (void)hipGetLastError();
+          release();
+          return false;
+        }
+      }
+    }
     try {
       for (int it0 = 0; it0 < n_iter;) {
         const int k = std::min(klim, n_iter - it0);
@@ -1447,9 +1482,22 @@ class ExactSampler : public Sampler {
           if (nth <= 1) {
             emit(0, C);
           } else {
+            // an exception on a worker (fn grows vectors) is carried back to
+            // this thread and rethrown after every thread has joined, so the
+            // C ABI returns a status instead of std::terminate
+            std::vector<std::exception_ptr> err(nth);
+            auto part = [&](int t) {
+              try { emit((int)((int64_t)C * t / nth), (int)((int64_t)C * (t + 1) / nth)); }
+              catch (...) { err[t] = std::current_exception(); }
+            };
             std::vector<std::thread> th;
-            for (int t = 0; t < nth; ++t) th.emplace_back(emit, (int)((int64_t)C * t / nth), (int)((int64_t)C * (t + 1) / nth));
+            for (int t = 1; t < nth; ++t) {
+              try { th.emplace_back(part, t); }
+              catch (...) { part(t); }       // no thread: run the range here
+            }
+            part(0);
             for (auto &x : th) x.join();
+            for (auto &e : err) if (e) std::rethrow_exception(e);
           }
         }
         it0 += k;

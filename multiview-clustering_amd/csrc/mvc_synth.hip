@@ -56,45 +56,52 @@ extern "C" __global__ void mvc_synth_mu_kernel(int V, int K, int D, double mu_sd
 // fma chain, and per-d wave sums of y and y^2.  Each wave accumulates into
 // its own LDS slot in row order, and the block combines the slots in wave
 // order at the end, so the column sums (and the tau_v they seed) are the
-// same bits on every run.
-constexpr int kSynThreads = 256, kSynWaves = kSynThreads / 64;
+// same bits on every run.  Dimensions go in tiles of kSynDT (the LDS slots
+// hold one tile); a row's Y2 chain is carried from tile to tile through Y2
+// itself, so it stays the one fma chain in ascending d.
+constexpr int kSynThreads = 256, kSynWaves = kSynThreads / 64, kSynDT = 1024;
 extern "C" __global__ __launch_bounds__(kSynThreads) void mvc_synth_y_kernel(int n, int D, int K, double sd,
                                                                              uint64_t seed, const double *mu,
                                                                              double *y, double *Y2, int32_t *z,
                                                                              double *colpart) {
-  extern __shared__ double s_col[];   // [kSynWaves][2 D]: each wave's sum y, sum y^2 per d
+  extern __shared__ double s_col[];   // [kSynWaves][2 DT]: each wave's sum y, sum y^2 per d of the tile
   const int v = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int Kv = max(1, K >> v);
-  double *my = s_col + (size_t)w * 2 * D;
-  for (int d = tid; d < kSynWaves * 2 * D; d += blockDim.x) s_col[d] = 0.0;
-  __syncthreads();
   const int64_t nblk = gridDim.x;
-  for (int64_t r0 = (int64_t)blockIdx.x * kSynThreads; r0 < n; r0 += nblk * kSynThreads) {
-    const int64_t i = r0 + tid;
-    const bool ok = i < n;
-    const int32_t zi = syn_label(seed, ok ? i : 0, K);
-    if (ok && v == 0 && z) z[i] = zi;
-    const double *m = mu + ((size_t)v * K + (size_t)(zi % Kv)) * D;
-    double *row = y + ((size_t)v * n + (size_t)(ok ? i : 0)) * D;
-    double acc = 0.0;
-    for (int d = 0; d < D; ++d) {
-      const double x = ok ? m[d] + sd * syn_normal(seed, (uint32_t)i, (uint32_t)d, (uint32_t)v, MVC_TAG_SYN_Y) : 0.0;
-      if (ok) row[d] = x;
-      acc = __builtin_fma(x, x, acc);
-      const double s1 = wave_tree_sum(x), s2 = wave_tree_sum(x * x);
-      if (lane == 0) {   // this wave's slot only: a fixed order of additions
-        my[d] += s1;
-        my[D + d] += s2;
+  for (int d0 = 0; d0 < D; d0 += kSynDT) {
+    const int DT = min(kSynDT, D - d0);
+    double *my = s_col + (size_t)w * 2 * DT;
+    for (int d = tid; d < kSynWaves * 2 * DT; d += blockDim.x) s_col[d] = 0.0;
+    __syncthreads();
+    for (int64_t r0 = (int64_t)blockIdx.x * kSynThreads; r0 < n; r0 += nblk * kSynThreads) {
+      const int64_t i = r0 + tid;
+      const bool ok = i < n;
+      const int32_t zi = syn_label(seed, ok ? i : 0, K);
+      if (ok && v == 0 && z && d0 == 0) z[i] = zi;
+      const double *m = mu + ((size_t)v * K + (size_t)(zi % Kv)) * D;
+      double *row = y + ((size_t)v * n + (size_t)(ok ? i : 0)) * D;
+      double acc = (ok && d0 > 0) ? Y2[(size_t)v * n + i] : 0.0;
+      for (int dd = 0; dd < DT; ++dd) {
+        const int d = d0 + dd;
+        const double x = ok ? m[d] + sd * syn_normal(seed, (uint32_t)i, (uint32_t)d, (uint32_t)v, MVC_TAG_SYN_Y) : 0.0;
+        if (ok) row[d] = x;
+        acc = __builtin_fma(x, x, acc);
+        const double s1 = wave_tree_sum(x), s2 = wave_tree_sum(x * x);
+        if (lane == 0) {   // this wave's slot only: a fixed order of additions
+          my[dd] += s1;
+          my[DT + dd] += s2;
+        }
       }
+      if (ok) Y2[(size_t)v * n + i] = acc;
     }
-    if (ok) Y2[(size_t)v * n + i] = acc;
-  }
-  __syncthreads();
-  double *out = colpart + ((size_t)v * gridDim.x + blockIdx.x) * 2 * D;
-  for (int d = tid; d < 2 * D; d += blockDim.x) {
-    double acc = s_col[d];
-    for (int q = 1; q < kSynWaves; ++q) acc += s_col[(size_t)q * 2 * D + d];
-    out[d] = acc;
+    __syncthreads();
+    double *out = colpart + ((size_t)v * gridDim.x + blockIdx.x) * 2 * D;
+    for (int q = tid; q < 2 * DT; q += blockDim.x) {
+      double acc = s_col[q];
+      for (int u = 1; u < kSynWaves; ++u) acc += s_col[(size_t)u * 2 * DT + q];
+      out[(q < DT ? 0 : D) + d0 + (q < DT ? q : q - DT)] = acc;
+    }
+    __syncthreads();
   }
 }
 
@@ -115,7 +122,6 @@ DeviceData synth_device_data(int device, int n, int V, int D, int K, uint64_t se
   if (K < 1) throw Error(MVC_ERR_ARG, "synthetic data: K must be >= 1");
   if (!(sd >= 0.0) || !(mu_sd >= 0.0)) throw Error(MVC_ERR_ARG, "synthetic data: sd and mu_sd must be >= 0");
   if (V > 31) throw Error(MVC_ERR_UNSUPPORTED, "synthetic data: at most 31 views (K_v = K >> v)");
-  if (D > 1024) throw Error(MVC_ERR_UNSUPPORTED, "synthetic data: at most 1024 dims (per-wave column sums in 64 KB of LDS)");
   MVC_HIP(hipSetDevice(device));
   DeviceData DD;
   hipStream_t st = nullptr;
@@ -131,7 +137,7 @@ DeviceData synth_device_data(int device, int n, int V, int D, int K, uint64_t se
     if (z_host) MVC_HIP(hipMalloc(&zd, sizeof(int32_t) * (size_t)n));
     hipLaunchKernelGGL(mvc_synth_mu_kernel, dim3(256), dim3(256), 0, st, V, K, D, mu_sd, seed, mu);
     MVC_HIP(hipGetLastError());
-    hipLaunchKernelGGL(mvc_synth_y_kernel, dim3(grid, V), dim3(kSynThreads), sizeof(double) * kSynWaves * 2 * D, st, n, D, K, sd,
+    hipLaunchKernelGGL(mvc_synth_y_kernel, dim3(grid, V), dim3(kSynThreads), sizeof(double) * kSynWaves * 2 * std::min(D, kSynDT), st, n, D, K, sd,
                        seed, (const double *)mu, DD.y, DD.Y2, zd, colpart);
     MVC_HIP(hipGetLastError());
     std::vector<double> cp((size_t)V * grid * 2 * D);

@@ -111,10 +111,16 @@ def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chain
         for c in range(n_chains):
             # every sample of the chain in two bulk copies (mvc_result_copy_chain)
             Ts = np.zeros(S, dtype=np.int32)
-            lib.mvc_result_copy_chain(res, c, None, Ts.ctypes.data_as(ip), None)
+            st = lib.mvc_result_copy_chain(res, c, None, Ts.ctypes.data_as(ip), None)
+            if st != L.MVC_OK:
+                raise L.MvcError(st, f"mvc_result_copy_chain(chain {c}) failed")
+            if S > 0 and not int(Ts.sum()) > 0:
+                raise L.MvcError(3, f"chain {c}: saved samples with no tables")
             tab = np.empty((S, n), dtype=np.int32)
             dsh = np.empty(max(1, V * int(Ts.sum())), dtype=np.int32)
-            lib.mvc_result_copy_chain(res, c, tab.ctypes.data_as(ip), None, dsh.ctypes.data_as(ip))
+            st = lib.mvc_result_copy_chain(res, c, tab.ctypes.data_as(ip), None, dsh.ctypes.data_as(ip))
+            if st != L.MVC_OK:
+                raise L.MvcError(st, f"mvc_result_copy_chain(chain {c}) failed")
             table_of = list(tab)
             ends = np.cumsum(V * Ts.astype(np.int64))
             dish_of = []

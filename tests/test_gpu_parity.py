@@ -685,6 +685,57 @@ def test_chains_concurrent_equal_serial():
     assert r.returncode == 0 and "chains OK" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
 
 
+_LAST_BIRTH_CHILD = r"""
+import os, sys
+root = sys.argv[1]
+sys.path[:0] = [root, os.path.join(root, "multiview-clustering_amd")]
+import numpy as np
+import mvc_amd as m
+from mvc_amd import data
+from oracle import oracle as O
+y, _ = data.new_simulation(1)
+n, C, M = y.shape[1], 4, 12
+res = m.run_gibbs_cpp(y, M, 0, 1, seed=1, mode="parallel", n_chains=C, quiet=True)
+last = 0
+for c in range(C):
+    ref = O.run(y, M, 0, 1, 1, chain=c, mode=O.PARALLEL)
+    for s in range(M):
+        assert np.array_equal(res[c]["table_of"][s], ref["table_of"][s]), (c, s)
+        assert np.array_equal(np.stack(res[c]["dish_of"][s]), ref["dish_of"][s]), (c, s)
+        t = ref["table_of"][s]
+        last += int(np.bincount(t)[t[n - 1]] == 1)   # the last customer sits alone: a birth
+    assert np.array_equal(res[c]["sigma_global"], ref["sigma_global"]), c
+print("last-birth OK", last)
+"""
+
+
+def test_last_customer_birth_with_poisoned_lds():
+    """Regression test of the round-3 multi-chain fault: a
+    birth decided for the sweep's LAST customer is committed by the birth
+    kernel, and the next repair round's run kernel then starts at cur == n.
+    The New_Simulation shape with seed 1 has such births in every chain
+    (19 over 4 chains x 12 cold sweeps; the oracle counts them below, since
+    only a birth can leave the last customer alone at a table).  Four
+    chains run concurrently in one handle with the run kernel's LDS filled
+    with 0xA5 at every launch (MVC_LDS_FILL: a read of a ring slot the
+    launch never wrote sees the same garbage every time) and every index a
+    run-kernel commit writes through checked (MVC_RUN_CHECK: a bad one fails
+    the sweep with the check's number instead of storing).  Without the fix
+    the value-prediction loop read pcs[depth - 1] and ring slots at cur == n
+    and the check fired (round 4: check 10, i0 = n); with it every chain is
+    bitwise the oracle's."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MVC_LDS_FILL="0xA5", MVC_RUN_CHECK="1")
+    env.pop("MVC_CHAIN_THREADS", None)
+    env.pop("MVC_VP", None)
+    r = subprocess.run([sys.executable, "-c", _LAST_BIRTH_CHILD, root], capture_output=True, text=True, timeout=240,
+                       env=env)
+    assert r.returncode == 0 and "last-birth OK" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+    assert int(r.stdout.split("last-birth OK")[1].split()[0]) >= 4
+
+
 @pytest.mark.parametrize("force", ["", "1"])
 def test_dish_block_producer(force, monkeypatch):
     """The dish-block MFMA producer (mvc_par_lpbig_kernel: A-fragments from y
@@ -835,6 +886,35 @@ def test_run_n_devices_split(mode):
         one = m.run_gibbs_cpp(y, M, burn, 1, seed=7, mode=mode, first_chain=c)
         _compare(res, one)
     assert summ["mean"].shape == (3 * y.shape[0] + 2,)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["exact", "parallel"])
+def test_run_n_devices_split_on_one_gpu(mode, monkeypatch):
+    """The same n_devices = 2 split with both logical devices mapped to
+    device 0 (MVC_DEVICE_MAP=0,0): mvc_run's per-device host threads, the
+    chain striding (device d holds chains d, d + 2, ... with ids first_chain
+    + c) and the result interleave run on one MI355X.  Every chain equals a
+    one-chain call with its id, bit for bit, and the pooled summary equals
+    the one of the same chains run on one logical device."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(5)
+    M, burn = 20, 10
+    s1, s2 = {}, {}
+    single = m.run_gibbs_cpp(y, M, burn, 1, seed=7, mode=mode, n_chains=5, summary=s1)
+    monkeypatch.setenv("MVC_DEVICE_MAP", "0,0")
+    multi = m.run_gibbs_cpp(y, M, burn, 1, seed=7, mode=mode, n_chains=5, n_devices=2, summary=s2)
+    assert len(multi) == 5
+    for c, res in enumerate(multi):
+        _compare(res, single[c])
+        if c in (0, 3):
+            _compare(res, m.run_gibbs_cpp(y, M, burn, 1, seed=7, mode=mode, first_chain=c))
+    assert np.array_equal(s1["mean"], s2["mean"])
+    assert np.array_equal(s1["rhat"], s2["rhat"], equal_nan=True)
+    monkeypatch.setenv("MVC_DEVICE_MAP", "0,9")
+    with pytest.raises(Exception, match="MVC_DEVICE_MAP"):
+        m.run_gibbs_cpp(y, 2, 0, 1, seed=7, mode=mode, n_chains=2, n_devices=2)
 
 
 def test_shard_exchange_failure_leaves_the_chain_unchanged():
