@@ -916,6 +916,9 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     const bool allv = __builtin_amdgcn_readfirstlane(Z.lmin[v]) != 0;
     const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
     double *stg = so >= 0 ? s_stage + (size_t)so * 64 + lane : nullptr;
+#ifdef MVC_ABL_DRAW_NOVIEW   // timing ablation: no view pass
+    if (true) S = 1.0 + m; else
+#endif
     if (!allv) S = zview_sum<0>(row, koff, K, j0, w0, sw, m);           // general: streamed
     else if (K <= 8) S = zview_sum<8>(row, koff, K, j0, w0, sw, m, stg);     // row in registers
     else if (K <= 16) S = zview_sum<16>(row, koff, K, j0, w0, sw, m, stg);
@@ -938,6 +941,7 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     const int pc = min(p, T - 1);
     sp[p] = p < T ? ((pc == p0) ? base_self : Z.base[pc]) : -MVC_PM_INF;
   }
+#ifndef MVC_ABL_DRAW_NOGATHER   // timing ablation: no table gathers
 #pragma unroll
   for (int c = 0; c < TM; c += 16) {
     for (int v = 0; v < V; ++v) {
@@ -955,6 +959,7 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
       for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
     }
   }
+#endif
   double M = -MVC_PM_INF;
 #pragma unroll
   for (int p = 0; p < TM; ++p)
@@ -1119,6 +1124,15 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
   lpview_tile_mfma<NT, SPPT, RP>(cur, nxt, SPPT, L.Bs + L.boff[v] + lane, ring, acc);
+#ifdef MVC_ABL_LP_NOEPI   // timing ablation (scripts/zprobe.py): the MFMA stream alone
+  {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < NT; ++q) t += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
+    if (t == 1.2345) *dslot = t;
+    return;
+  }
+#endif
   if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
   wave_lds_sync();
   double hy[4], hr[4];
@@ -1153,7 +1167,11 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
       const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
       const int li = li0 + grp + 4 * r;
       double *dst = (j < K && li < nb) ? lpb + lpb_index(lr0 + grp + 4 * r, koff + j, sumK) : dslot;
+#ifndef MVC_ABL_LP_NOSTORE   // timing ablation: no lp stores
       *dst = val;
+#else
+      (void)dst;
+#endif
       if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
     }
   }
