@@ -1104,44 +1104,71 @@ __host__ __device__ constexpr int fz_pat_nt(uint32_t pat, int v) { return (int)(
 // ---------------------------------------------------------------------------
 struct LpaLds {
   const double *Bs, *c0, *cb, *Q;
+  const double *xs, *dens, *cbs;   // per dish: the own-dish coefficient parts (see lpall_self_coef)
   const int *dn, *dl, *tix, *nt, *koff, *boff;
 };
+// Per-wave LDS of the all-views producer: the tile's y2 and h = (-y2/2)/tau
+// per (view, row), the own-dish G and the max over the other included dishes
+// per (view, row) [4][16] each, and the rows' tables [16].
+constexpr int kLpaWaveD = 4 * 4 * 16;   // doubles
+constexpr int kLpaWaveI = 16;           // ints
 __host__ __device__ inline size_t lpall_shared_bytes(size_t s1t_doubles, int V, int sumK, int waves) {
-  return 16 * 4 + 8 * (s1t_doubles + 3 * (size_t)sumK + (size_t)waves * 80) +
-         4 * (2 * (size_t)sumK + (size_t)MVC_FZ_TB * 16 * V + MVC_FZ_TB * 16 + (size_t)waves * 16) + 64;
+  return 16 * 4 + 8 * (s1t_doubles + 6 * (size_t)sumK + (size_t)waves * kLpaWaveD) +
+         4 * (2 * (size_t)sumK + (size_t)MVC_FZ_TB * 16 * V + MVC_FZ_TB * 16 + (size_t)waves * kLpaWaveI) + 64;
 }
 
+// The own-dish coefficient of coef(n - 1, Q', tau, L2pt, D) split into its
+// parts that do not depend on the customer: c0 = X - (0.5 Q') / den with
+// X = D ((-0.5 L2pt) - 0.5 log(b / a)), den = (tau a) b, and cb = 1 / (tau b),
+// a = tau + (n - 1), b = tau + n (the same operations as coef, so the same
+// bits), staged once per block instead of one log and three divisions per
+// customer and view.
+__device__ __forceinline__ void lpall_self_coef(int dn, double tau, double L2pt, int D, double &X, double &den,
+                                                double &cb) {
+  const int n_ = dn - 1;
+  const double a = tau + (double)n_;
+  const double b = tau + (double)(n_ + 1);
+  X = (double)D * ((-0.5 * L2pt) - 0.5 * mvc_log(b / a));
+  den = (tau * a) * b;
+  cb = 1.0 / (tau * b);
+}
+
+extern "C" __device__ void mvc_raw_buffer_store_f64(double v, mvc_i4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.f64");
+
+// One view of one 16-customer tile: the MFMA block, then the lp of every
+// (row, frozen dish) stored (buffer stores: a 32-bit lane offset, invalid
+// lanes to their discard slot), the own dish's G and the max over the other
+// included dishes per row to LDS; the own dish itself is done for all views
+// at once at the end of the tile (lpa_tile_end).
 template <int NT, int SPPT, int RP>
-__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int b0, int li0, int lr0, int nb, int pz, double y2,
-                                         const mvc_d2 *cur, const mvc_d2 *nxt, mvc_d2 (&ring)[RP], double *lpb,
-                                         double *dslot, double *y2s, double *selfG, double *mrest, int *zs) {
-  const ParState &P = A.P;
+__device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int li0, int nb, const mvc_d2 *cur,
+                                         const mvc_d2 *nxt, mvc_d2 (&ring)[RP], mvc_i4 rsrc, int tile_boff,
+                                         int disc_boff, double *wsp, const int *zs) {
   const int lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
-  const int V = P.V, D = P.D, n = P.n;
-  const int koff = L.koff[v], K = L.koff[v + 1] - koff, sumK = L.koff[V];
-  const double tau = P.hyper[v], L2pt = A.L2pt[v], cnew = A.cnew[v];
+  const int V = A.P.V;
+  const int koff = L.koff[v], K = L.koff[v + 1] - koff;
   mvc_d4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
   lpview_tile_mfma<NT, SPPT, RP>(cur, nxt, SPPT, L.Bs + L.boff[v] + lane, ring, acc);
+  const double *y2t = wsp + v * 16, *ht = wsp + 64 + v * 16;
+  double *selfG = wsp + 128 + v * 16, *mrest = wsp + 192 + v * 16;
 #ifdef MVC_ABL_LP_NOEPI   // timing ablation (scripts/zprobe.py): the MFMA stream alone
   {
     double t = 0.0;
 #pragma unroll
     for (int q = 0; q < NT; ++q) t += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
-    if (t == 1.2345) *dslot = t;
+    if (t == 1.2345) selfG[col] = t;
     return;
   }
 #endif
-  if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
-  wave_lds_sync();
   double hy[4], hr[4];
   int j0[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const double y2r = y2s[grp + 4 * r];
-    hy[r] = 0.5 * y2r;
-    hr[r] = (-0.5 * y2r) / tau;
+    hy[r] = 0.5 * y2t[grp + 4 * r];
+    hr[r] = ht[grp + 4 * r];
     j0[r] = L.tix[zs[grp + 4 * r] * V + v] - koff;
   }
 #pragma unroll
@@ -1153,9 +1180,14 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
       if (jt == t) g = acc[t][r];
     if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
   }
+  // frozen-dish lp for every (row, dish): a fixed number of unconditional
+  // stores (the own dish is overwritten at the end of the tile by this same
+  // wave, in program order); the max over the other included dishes per row
   double mx[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) mx[r] = -MVC_PM_INF;
+  // byte offset of (row grp + 4 r, dish koff + 16 t + col) within the tile: 128 (koff + 16 t + col) + 8 (grp + 4 r)
+  const int lbase = tile_boff + 128 * (koff + col) + 8 * grp;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int j = 16 * t + col;
@@ -1165,56 +1197,67 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
-      const int li = li0 + grp + 4 * r;
-      double *dst = (j < K && li < nb) ? lpb + lpb_index(lr0 + grp + 4 * r, koff + j, sumK) : dslot;
+      const bool ok = j < K && li0 + grp + 4 * r < nb;
+      const int off = ok ? lbase + 2048 * t + 32 * r : disc_boff;
 #ifndef MVC_ABL_LP_NOSTORE   // timing ablation: no lp stores
-      *dst = val;
+      mvc_raw_buffer_store_f64(val, rsrc, off, 0, 0);
 #else
-      (void)dst;
+      (void)off;
 #endif
       if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
     }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const double mr = row16_max(mx[r]);
-    if (col == 0) mrest[grp + 4 * r] = mr;
+    double x = mx[r];
+    x = dmax(x, down_d<8>(x));
+    x = dmax(x, down_d<4>(x));
+    x = dmax(x, down_d<2>(x));
+    x = dmax(x, down_d<1>(x));
+    if (col == 0) mrest[grp + 4 * r] = x;   // lane 0 of the row holds the row's max
   }
-  wave_lds_sync();
-  // own dish, one row per lane
-  const double G = selfG[col];
-  const int kk = L.tix[pz * V + v];
+}
+
+// The own dish of every (view, row) of the tile, one lane each (lane = row +
+// 16 view, V <= 4): its lp with the customer removed (oracle: the self-removed
+// coefficients) overwrites the frozen value, and the view maximum m_v (the
+// max over the included dishes and the new dish, oracle eval_view_seq) goes
+// to vmax, so the draw reads each lp row once.
+__device__ __forceinline__ void lpa_tile_end(const Sweep &A, const LpaLds &L, int b0, int li0, int nb, double y2,
+                                             double h, int pz, mvc_i4 rsrc, int tile_boff, int disc_boff,
+                                             const double *wsp, double *dslot) {
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, row = lane & 15, v = lane >> 4;
+  const int V = P.V, n = P.n;
+  const int vv = min(v, V - 1);
+  const double G = wsp[128 + vv * 16 + row];
+  const int kk = L.tix[pz * V + vv];
   const double Gp = G - y2;
   const double Qp = (L.Q[kk] - 2.0 * G) + y2;
-  const Coef cf = coef(L.dn[kk] - 1, Qp, tau, L2pt, D);
-  const double hself = (-0.5 * y2) / tau;
-  const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
-  const bool ok = lane < 16 && li0 + col < nb;
-  double *dst = ok ? lpb + lpb_index(lr0 + col, kk, sumK) : dslot;
-  *dst = sv;
+  const double c0 = L.xs[kk] - (0.5 * Qp) / L.dens[kk];
+  const double sv = __builtin_fma(Gp + 0.5 * y2, L.cbs[kk], c0) + h;
+  const bool ok = v < V && li0 + row < nb;
+  mvc_raw_buffer_store_f64(sv, rsrc, ok ? tile_boff + 128 * kk + 8 * row : disc_boff, 0, 0);
   const bool alive = (L.nt[pz] - 1) > 0;
   const int l0p = L.dl[kk] - (alive ? 0 : 1);
-  double m = mrest[col];
+  double m = wsp[192 + vv * 16 + row];
   if (l0p > 0 && sv > m) m = sv;
-  const double lfn = cnew + hself;
+  const double lfn = A.cnew[vv] + h;
   if (lfn > m) m = lfn;
-  double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
+  double *dm = ok ? A.vmax + (size_t)vv * n + b0 + li0 + row : dslot;
   *dm = m;
-  wave_lds_sync();
 }
 
 template <int SPPT, int RP, uint32_t PAT, int VI>
-__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int b0, int li0, int lr0, int nb, int pz,
-                                          const double (&y2v)[MVC_Z_VMAX], const mvc_d2 *ybase, size_t vstride,
-                                          size_t tcur, size_t tnext, mvc_d2 (&ring)[RP], double *lpb, double *dslot,
-                                          double *y2s, double *selfG, double *mrest, int *zs) {
+__device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int li0, int nb, const mvc_d2 *ybase,
+                                          size_t vstride, size_t tcur, size_t tnext, mvc_d2 (&ring)[RP], mvc_i4 rsrc,
+                                          int tile_boff, int disc_boff, double *wsp, const int *zs) {
   if constexpr (VI < fz_pat_v(PAT)) {
     const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
     const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
-    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, b0, li0, lr0, nb, pz, y2v[VI], cur, nxt, ring, lpb, dslot, y2s,
-                                           selfG, mrest, zs);
-    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, b0, li0, lr0, nb, pz, y2v, ybase, vstride, tcur, tnext, ring, lpb, dslot, y2s,
-                                     selfG, mrest, zs);
+    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, li0, nb, cur, nxt, ring, rsrc, tile_boff, disc_boff, wsp, zs);
+    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, li0, nb, ybase, vstride, tcur, tnext, ring, rsrc, tile_boff, disc_boff, wsp,
+                                     zs);
   }
 }
 
@@ -1224,9 +1267,8 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int
   const ParState &P = A.P;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
-  const int col = lane & 15;
   constexpr int V = fz_pat_v(PAT);
-  const int KC = P.KC, TC = P.TC, n = P.n;
+  const int KC = P.KC, TC = P.TC, n = P.n, D = P.D;
   const int T = __builtin_amdgcn_readfirstlane(A.T);
   constexpr int SP = 2 * SPPT;
   int *s_koff = (int *)smem;                                   // [V+1]
@@ -1242,10 +1284,11 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int
   const int nB = s_boff[V];
   double *Bs = (double *)(smem + 16 * 4);
   double *f_c0 = Bs + nB, *f_cb = f_c0 + sumK, *f_Q = f_cb + sumK;
-  double *wsp = f_Q + sumK + (size_t)w * 80;                   // per wave: y2s, selfG, mrest, w0s, Ss
-  int *f_dn = (int *)(f_Q + sumK + (size_t)BW * 80), *f_dl = f_dn + sumK;
+  double *f_xs = f_Q + sumK, *f_dens = f_xs + sumK, *f_cbs = f_dens + sumK;
+  double *wsp = f_cbs + sumK + (size_t)w * kLpaWaveD;          // per wave: y2, h, selfG, mrest [4][16] each
+  int *f_dn = (int *)(f_cbs + sumK + (size_t)BW * kLpaWaveD), *f_dl = f_dn + sumK;
   int *f_tix = f_dl + sumK, *f_nt = f_tix + MVC_FZ_TB * 16 * V;
-  int *zs = f_nt + MVC_FZ_TB * 16 + w * 16;
+  int *zs = f_nt + MVC_FZ_TB * 16 + w * kLpaWaveI;
   {
     const mvc_d2 *src = (const mvc_d2 *)A.S1t;
     mvc_d2 *dst = (mvc_d2 *)Bs;
@@ -1258,16 +1301,17 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int
     f_c0[k] = P.c0[v * KC + j];
     f_cb[k] = P.cb[v * KC + j];
     f_Q[k] = P.Q[v * KC + j];
-    f_dn[k] = P.d_n[v * KC + j];
+    const int dn = P.d_n[v * KC + j];
+    f_dn[k] = dn;
     f_dl[k] = P.d_l[v * KC + j];
+    lpall_self_coef(dn, P.hyper[v], A.L2pt[v], D, f_xs[k], f_dens[k], f_cbs[k]);
   }
   for (int p = tid; p < MVC_FZ_TB * 16; p += blockDim.x) {
     f_nt[p] = p < T ? P.n_t[p] : 0;
     for (int v = 0; v < V; ++v) f_tix[p * V + v] = s_koff[v] + (p < T ? P.dish[v * TC + p] : 0);
   }
   __syncthreads();
-  const LpaLds L{Bs, f_c0, f_cb, f_Q, f_dn, f_dl, f_tix, f_nt, s_koff, s_boff};
-  double *y2s = wsp, *selfG = wsp + 16, *mrest = wsp + 32;
+  const LpaLds L{Bs, f_c0, f_cb, f_Q, f_xs, f_dens, f_cbs, f_dn, f_dl, f_tix, f_nt, s_koff, s_boff};
 
   // customers [b0, b0 + nb) (b0 a multiple of 16): local tiles; yt, z, Y2 and
   // vmax are indexed by customer, the lp buffer by batch position
@@ -1285,15 +1329,32 @@ __global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int
     for (int u = 0; u < RP; ++u) ring[u] = c0p[u * 64];
   }
   double *const dslot = discard + lane;
+  // the lp buffer through a buffer resource: 32-bit byte offsets (the
+  // buffer is < 2^31 bytes, kLpbBudget); the discard slots follow it
+  const uint64_t lpa = (uint64_t)lpb;
+  const mvc_i4 rsrc = (mvc_i4){(int)(uint32_t)lpa, (int)(uint32_t)(lpa >> 32), -1, 0x00020000};
+  const int disc_boff = (int)((uint64_t)(discard - lpb) * 8) + 8 * lane;
+  const int row = lane & 15, vl = lane >> 4;      // this lane's (row, view) in the tile start / end passes
+  const int vq = min(vl, V - 1);
+  const double tau_l = P.hyper[vq];
   for (int m = 0; m < nmy; ++m) {
     const int li0 = (gw + m * NWT) * 16;
-    const int li_row = min(b0 + li0 + col, n - 1);
+    const int li_row = min(b0 + li0 + row, n - 1);
     const int pz = P.z[li_row];
-    double y2v[MVC_Z_VMAX];
-#pragma unroll
-    for (int v = 0; v < MVC_Z_VMAX; ++v) y2v[v] = v < V ? A.Y2[(size_t)v * n + li_row] : 0.0;
-    lpa_views<SPPT, RP, PAT, 0>(A, L, b0, li0, li0, nb, pz, y2v, ybase, vstride, toff(m), toff(m + 1), ring, lpb, dslot,
-                                y2s, selfG, mrest, zs);
+    // tile start: y2 and h of (view vl, row) -- one division per lane per tile
+    const double y2 = A.Y2[(size_t)vq * n + li_row];
+    const double h = (-0.5 * y2) / tau_l;
+    if (vl < V) { wsp[vl * 16 + row] = y2; wsp[64 + vl * 16 + row] = h; }
+    if (vl == 0) zs[row] = pz;
+    wave_lds_sync();
+    const int tile_boff = li0 * sumK * 8;           // (li0 >> 4) * sumK * 16 doubles
+    lpa_views<SPPT, RP, PAT, 0>(A, L, li0, nb, ybase, vstride, toff(m), toff(m + 1), ring, rsrc, tile_boff, disc_boff,
+                                wsp, zs);
+    wave_lds_sync();
+#ifndef MVC_ABL_LP_NOEPI
+    lpa_tile_end(A, L, b0, li0, nb, y2, h, pz, rsrc, tile_boff, disc_boff, wsp, dslot);
+#endif
+    wave_lds_sync();
   }
 }
 
