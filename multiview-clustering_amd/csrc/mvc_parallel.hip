@@ -1262,7 +1262,14 @@ __device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int l
 }
 
 template <int SPPT, int RP, uint32_t PAT>
-__global__ __launch_bounds__(512) void mvc_par_lpall_kernel(Sweep A, int b0, int nb, double *lpb, double *discard) {
+#ifndef MVC_LPA_WAVES
+#define MVC_LPA_WAVES 8       // waves per block (one block per CU) of the all-views producer
+#endif
+#ifndef MVC_LPA_RP16
+#define MVC_LPA_RP16 8        // ring depth (k-step pairs in flight per wave) at D = 128
+#endif
+__global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep A, int b0, int nb, double *lpb,
+                                                                          double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int tid = threadIdx.x;
@@ -2635,16 +2642,16 @@ class ParallelSampler : public Sampler {
       const int nb = (int)std::min(nbatch_sz, hi - b0);
       hipEvent_t el = nullptr, ed = nullptr;
       timers.begin("lp", &el);
-      const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, 8);
+      const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, MVC_LPA_WAVES);
       const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                              (spp == 4 || spp == 8 || spp == 16) && lpa_lds <= 160 * 1024;
       if (use_lpall) {
         const int ntile = (nb + 15) / 16;
-        const int grid = std::max(1, std::min(n_cu, (ntile + 7) / 8));
+        const int grid = std::max(1, std::min(n_cu, (ntile + MVC_LPA_WAVES - 1) / MVC_LPA_WAVES));
         switch (spp) {
-          case 4: launch_lpall<4, 4>(fz_pat, dim3(grid), dim3(512), lpa_lds, A, (int)b0, nb); break;
-          case 8: launch_lpall<8, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A, (int)b0, nb); break;
-          default: launch_lpall<16, 8>(fz_pat, dim3(grid), dim3(512), lpa_lds, A, (int)b0, nb); break;
+          case 4: launch_lpall<4, 4>(fz_pat, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
+          case 8: launch_lpall<8, 8>(fz_pat, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
+          default: launch_lpall<16, MVC_LPA_RP16>(fz_pat, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
         }
         zpath_lpall = true;
       } else if (use_mfma) {
@@ -2662,17 +2669,25 @@ class ParallelSampler : public Sampler {
         // K_v > 64 or no tiled copy: dish blocks of 16 * NTB, A-fragments from y
         const int ntile = (nb + 15) / 16;
         for (int v = 0; v < V; ++v) {
-          for (int jb0 = 0, first = 1; jb0 < c.K[v]; jb0 += 16 * big_ntb, first = 0) {
-            const int kb = std::min(16 * big_ntb, c.K[v] - jb0);
-            const size_t lds = lpbig_shared_bytes(SPb, big_ntb, c.T, big_waves);
-            const int per_cu = big_waves == 8 ? 1 : 2;
-            const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + big_waves - 1) / big_waves));
+          // a view with few dishes takes the narrowest block that holds them
+          // (the MFMAs of the padding columns are not issued); the blocks'
+          // lp values and the max-combined view maximum are the same bits
+          // whatever the blocking
+          int vntb = big_ntb;
+          while (vntb > 1 && 16 * (vntb / 2) >= c.K[v]) vntb /= 2;
+          int vwaves = big_waves;
+          if (vntb != big_ntb) vwaves = lpbig_shared_bytes(SPb, vntb, c.T, 4) <= 80 * 1024 ? 4 : 8;
+          for (int jb0 = 0, first = 1; jb0 < c.K[v]; jb0 += 16 * vntb, first = 0) {
+            const int kb = std::min(16 * vntb, c.K[v] - jb0);
+            const size_t lds = lpbig_shared_bytes(SPb, vntb, c.T, vwaves);
+            const int per_cu = vwaves == 8 ? 1 : 2;
+            const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + vwaves - 1) / vwaves));
             Sweep Ab = A;
             Ab.SP = SPb;
-            switch (big_ntb) {
-              case 4: hipLaunchKernelGGL((mvc_par_lpbig_kernel<4>), dim3(grid), dim3(64 * big_waves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
-              case 2: hipLaunchKernelGGL((mvc_par_lpbig_kernel<2>), dim3(grid), dim3(64 * big_waves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
-              default: hipLaunchKernelGGL((mvc_par_lpbig_kernel<1>), dim3(grid), dim3(64 * big_waves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+            switch (vntb) {
+              case 4: hipLaunchKernelGGL((mvc_par_lpbig_kernel<4>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              case 2: hipLaunchKernelGGL((mvc_par_lpbig_kernel<2>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              default: hipLaunchKernelGGL((mvc_par_lpbig_kernel<1>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
             }
             MVC_HIP(hipGetLastError());
           }
