@@ -171,8 +171,10 @@ int mvc_sampler_ari(mvc_sampler *s, int chain, const int32_t *truth, double *ari
 int mvc_sampler_set_timing(mvc_sampler *s, int32_t flags);
 /* z-resample kernels used by the last parallel sweep: bits 0-1 the lp
  * producer (0 generic, one lane per customer; 2 per-view MFMA tiles), bit 2
- * set when the register-resident draw kernel ran (T <= 64, K_v <= 64);
- * -1 for the exact schedule or before the first sweep.  (No reference
+ * set when the register-resident draw kernel ran (T <= 64, K_v <= 64), bit 4
+ * the all-views MFMA producer, bit 5 phase A left to the repair, bit 6 the
+ * dish-block MFMA producer, bit 7 the row draw (16 lanes per customer,
+ * T <= 512); -1 for the exact schedule or before the first sweep.  (No reference
  * counterpart: diagnostics of this implementation.) */
 int mvc_sampler_zpath(mvc_sampler *s);
 /* Counters of the chain's last parallel sweep: out[0]

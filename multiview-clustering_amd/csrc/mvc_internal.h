@@ -158,6 +158,15 @@ __device__ __forceinline__ double wave_tree_sum(double x) {
   x = x + down_d<1>(x);
   return readlane_d(x, 0);
 }
+// pw16 of the 16 lanes of each row (pairs (c, c + h), h = 1, 2, 4, 8: the
+// oracle's pw16 association), broadcast to the row.
+__device__ __forceinline__ double row_pw16(double x) {
+  x = x + down_d<1>(x);
+  x = x + down_d<2>(x);
+  x = x + down_d<4>(x);
+  x = x + down_d<8>(x);
+  return row_bcast0_d(x);
+}
 // tree16 over each row's 16 lanes (tree64 of a chunk whose upper 48 slots
 // were already folded in by the caller), root broadcast to the row.
 __device__ __forceinline__ double row16_tree_sum(double x) {

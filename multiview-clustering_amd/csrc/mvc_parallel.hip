@@ -811,6 +811,8 @@ struct LpRow {
   }
   // k must be wave-uniform (it becomes the SGPR soffset)
   __device__ __forceinline__ double operator()(int k) const { return mvc_raw_buffer_load_f64(rsrc, boff, k * 128, 0); }
+  // k per lane
+  __device__ __forceinline__ double at(int k) const { return mvc_raw_buffer_load_f64(rsrc, boff + k * 128, 0, 0); }
 };
 
 // View reduction of the draw (oracle eval_view_seq): the sum of
@@ -1069,6 +1071,151 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
   return 8 * ((size_t)TM + (size_t)sumK + (size_t)4 * MVC_ZSTAGE * 64) +
          4 * ((size_t)V * TM + (size_t)V + 1 + 2 * MVC_Z_VMAX + (size_t)sumK) + 16;
+}
+
+// Row draw for T > 64 tables (or K_v > 64 dishes): one 16-lane DPP row per
+// customer, four customers per wavefront, a block (16 rows) on one 16-customer
+// slab of the lp buffer at a time.  The same arithmetic in the same order as
+// mvc_par_zdraw_kernel / the register draw (oracle resample_customer):
+//   * view terms: lane c of the row owns column c (dishes j = 16 t + c), its
+//     partial is the sequential sum over ascending t, and the row's DPP tree
+//     (row_pw16) is the spec's pw16 over the 16 columns;
+//   * table scores: lane c owns positions p = 16 k + c (k < NB), each a
+//     view-order sum; block k of 16 positions is register k of the row, so
+//     B_k = row_pw16(e_k), and the running block totals C_k are formed in
+//     block order in every lane;
+//   * the pick: the first block with r < C_k, then the pw16 descent over that
+//     block's 16 leaves (staged in LDS).
+// One lane-per-customer kernel would gather V*T values per customer through
+// every lane; here each lane gathers V*T/16 and the row's values share cache
+// lines (the slab layout interleaves the 16 customers of a block).
+template <int NB>
+__global__ __launch_bounds__(256) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb, const double *lpb) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const ParState &P = A.P;
+  const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
+  const int T = __builtin_amdgcn_readfirstlane(A.T);
+  const int tid = threadIdx.x, row = tid >> 4, c = tid & 15;
+  const int sumK0 = __builtin_amdgcn_readfirstlane(A.Koff[V]);
+  double *s_base = (double *)smem;                 // [16 NB] log mass (or -inf: excluded / padding)
+  double *s_w = s_base + 16 * NB;                  // [sumK] dish weights max(l - sigma, 0) / -1 for l = 0
+  double *s_sel = s_w + sumK0;                     // [16 rows][16] the picked block's leaves
+  int *s_tix = (int *)(s_sel + 256);               // [16 NB][V] Koff[v] + dish_v(p) (padding: Koff[v])
+  int *s_koff = s_tix + 16 * NB * V;               // [V+1]
+  int *s_dl = s_koff + V + 1;                      // [sumK] l of each dish
+  const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
+  if (tid <= V) s_koff[tid] = A.Koff[tid];
+  __syncthreads();
+  const int sumK = s_koff[V];
+  for (int p = tid; p < 16 * NB; p += blockDim.x) {
+    const int np = p < T ? P.n_t[p] : 0;
+    s_base[p] = (p < T && np >= 1 && (double)np - sg > 0.0) ? P.lmass[p] : -MVC_PM_INF;
+    for (int v = 0; v < V; ++v) s_tix[p * V + v] = s_koff[v] + (p < T ? P.dish[v * TC + p] : 0);
+  }
+  for (int k = tid; k < sumK; k += blockDim.x) {
+    int v = 0;
+    while (v + 1 < V && s_koff[v + 1] <= k) ++v;
+    const int l = P.d_l[v * KC + (k - s_koff[v])];
+    double w = (double)l - P.hyper[2 * V + v];
+    if (w < 0.0) w = 0.0;
+    s_dl[k] = l;
+    s_w[k] = l > 0 ? w : -1.0;
+  }
+  __syncthreads();
+  const int T_ne = A.status[V + 3];
+  double *sel = s_sel + row * 16;
+  for (int g = blockIdx.x; g * 16 < nb; g += gridDim.x) {
+    const int li = g * 16 + row;
+    const bool ok = li < nb;
+    const int lic = min(li, nb - 1);
+    const int i = b0 + lic;
+    const LpRow lp(lpb, (int)(lpb_index(lic, 0, sumK) * 8));   // dish k of this customer: lp(k)
+    const int p0 = P.z[i];
+    const bool alive = (P.n_t[p0] - 1) > 0;
+    double s_new = mvc_log_nb(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+    for (int v = 0; v < V; ++v) {
+      const int koff = s_koff[v], K = s_koff[v + 1] - koff;
+      const int j0 = s_tix[p0 * V + v] - koff;
+      const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+      const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
+      double w0 = (double)l0p - sigma;
+      if (w0 < 0.0) w0 = 0.0;
+      if (!(l0p > 0)) w0 = -1.0;
+      const double m = A.vmax[(size_t)v * n + i];
+      // column c: included dishes j = 16 t + c in ascending t (an excluded
+      // dish adds +0: its weight and argument are zeroed)
+      double col = 0.0;
+      for (int j = c; j - c < K; j += 16) {
+        const int jc = min(j, K - 1);
+        const double x = lp.at(koff + jc);
+        const double w = (j == j0) ? w0 : s_w[koff + jc];
+        const bool in = j < K && w >= 0.0;
+        col = col + (in ? w : 0.0) * mvc_exp_le0(in ? x - m : 0.0);
+      }
+      double S = row_pw16(col);
+      const int Kact = K - ((l0p == 0) ? 1 : 0);
+      double wn = alpha + (double)Kact * sigma;
+      if (wn < 0.0) wn = 0.0;
+      S = S + wn * mvc_exp_le0(lfn - m);
+      const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
+      const double lm = (denom <= 0.0) ? lfn : (m + mvc_log_nb(S)) - mvc_log_nb(denom);
+      s_new = s_new + lm;
+    }
+    // table scores of positions 16 k + c, view order
+    const int np0 = P.n_t[p0] - 1;
+    const double m0 = (double)np0 - sg;
+    const double base_self = (np0 >= 1 && m0 > 0.0) ? mvc_log_nb(m0) : -MVC_PM_INF;
+    double sp[NB];
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int p = 16 * k + c;
+      sp[k] = (p == p0) ? base_self : s_base[p];
+    }
+    for (int v = 0; v < V; ++v) {
+      double x[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) x[k] = lp.at(s_tix[(16 * k + c) * V + v]);
+#pragma unroll
+      for (int k = 0; k < NB; ++k) sp[k] = sp[k] + x[k];
+    }
+    double M = -MVC_PM_INF;
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (16 * k + c < T && sp[k] > M) M = sp[k];
+    M = row16_max(M);
+    if (s_new > M) M = s_new;
+    // weights in place, block sums, running block totals (block order)
+    double C[NB];
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      sp[k] = (16 * k + c < T) ? mvc_exp_le0(sp[k] - M) : 0.0;   // excluded: exp(-inf) = +0
+      tot = tot + row_pw16(sp[k]);
+      C[k] = tot;
+    }
+    const double W = mvc_exp_le0(s_new - M) + tot;
+    double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
+    int pick = -1;
+    int kb = NB - 1;
+    double prev = 0.0, leaf = sp[NB - 1];
+#pragma unroll
+    for (int k = NB - 1; k >= 0; --k)
+      if (r < C[k]) { kb = k; prev = k > 0 ? C[k - 1] : 0.0; leaf = sp[k]; }
+    sel[c] = leaf;                                  // the row's candidate block leaves (LDS)
+    wave_lds_sync();
+    if (r < tot) {
+      double a[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) a[u] = sel[u];
+      pick = 16 * kb + pw16_select(a, r - prev);
+    }
+    if (ok && c == 0) A.choice[i] = pick;
+    wave_lds_sync();
+  }
+}
+__host__ __device__ inline size_t zdraw_row_shared_bytes(int V, int NB, int sumK) {
+  return 8 * ((size_t)16 * NB + (size_t)sumK + 256) + 4 * ((size_t)16 * NB * V + (size_t)V + 1 + (size_t)sumK) + 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -1922,6 +2069,7 @@ class ParallelSampler : public Sampler {
   bool force_generic = false;
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
+  bool force_zdraw_row = false;   // MVC_ZDRAW_ROW=1: the row draw for every T <= 512 (default: 64 < T <= 512)
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
   int shard_rank = 0, shard_world = 1;
@@ -2123,6 +2271,8 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_LPV_BPC")) lpv_bpc = std::max(0, std::min(8, atoi(e)));
     const char *zl = getenv("MVC_ZDRAW_LDS");
     force_zdraw_lds = zl && zl[0] == '1';
+    const char *zr = getenv("MVC_ZDRAW_ROW");
+    force_zdraw_row = zr && zr[0] == '1';
     if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
     {
       hipDeviceProp_t prop;
@@ -2608,11 +2758,15 @@ class ParallelSampler : public Sampler {
     const size_t nb_full = ((size_t)n + 63) / 64 * 64;
     const size_t nbatch_sz = std::min(nb_max, nb_full);
     const size_t need = (nbatch_sz / 64) * per64;
-    const bool use_zreg = !force_zdraw_lds && c.T <= 64 && Kmax <= 64 && sk <= MVC_Z_VMAX * 64 &&
+    const bool use_zreg = !force_zdraw_lds && !force_zdraw_row && c.T <= 64 && Kmax <= 64 && sk <= MVC_Z_VMAX * 64 &&
                           zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
+    // the row draw (16 lanes per customer) where the register draw does not apply
+    const int row_nb = c.T <= 64 ? 4 : c.T <= 128 ? 8 : c.T <= 256 ? 16 : 32;
+    const bool use_zrow = !use_zreg && !force_zdraw_lds && c.T <= 512 &&
+                          zdraw_row_shared_bytes(V, row_nb, sk) <= 64 * 1024;
     // phase A on the two-kernel path needs the draw's LDS tables; beyond them
     // the repair's eval kernel evaluates the sweep from customer 0 instead
-    const bool phaseA = use_zreg || zdraw_shared_bytes(V, c.T, sk) <= 160 * 1024;
+    const bool phaseA = use_zreg || use_zrow || zdraw_shared_bytes(V, c.T, sk) <= 160 * 1024;
     // the all-views producer: T <= 64, K_v <= 64, every view's S1
     // B-fragments in LDS at once, fully unrolled k-step pairs
     size_t s1t_d = 0;
@@ -2710,7 +2864,16 @@ class ParallelSampler : public Sampler {
       else if (use_zreg)
         hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<64>, zg, dim3(256), zdraw_reg_shared_bytes(V, 64, sk), stream, A,
                            (int)b0, nb, (const double *)lpb);
-      else {
+      else if (use_zrow) {
+        const dim3 rg(std::max(1, std::min((nb + 15) / 16, 8 * n_cu)));   // 16 customers per block and round
+        const size_t rl = zdraw_row_shared_bytes(V, row_nb, sk);
+        switch (row_nb) {
+          case 4: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<4>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
+          case 8: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<8>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
+          case 16: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<16>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
+          default: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<32>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
+        }
+      } else {
         // the table-score scratch (T x nb doubles) when it stays under 1 GiB
         const size_t scn = (size_t)c.T * (size_t)nb;
         const bool use_sc = scn * sizeof(double) <= ((size_t)1 << 30);
@@ -2733,7 +2896,8 @@ class ParallelSampler : public Sampler {
     timers.end("zresample", e0);
     if (phase_a_only) {                            // mvc_sampler_phase_a: the pass alone
       phase_a_ran = phaseA;
-      zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) | (use_big ? 64 : 0)) : 32;
+      zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) | (use_big ? 64 : 0) |
+                        (use_zrow ? 128 : 0)) : 32;
       return;
     }
     if (phaseA && shard_world > 1) {
@@ -2751,7 +2915,7 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipMemcpyAsync(c.choice, shard_exch, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToDevice, stream));
     }
     zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) |
-                      (use_big ? 64 : 0)) : 32;
+                      (use_big ? 64 : 0) | (use_zrow ? 128 : 0)) : 32;
     repair(c, s, phaseA);
   }
 

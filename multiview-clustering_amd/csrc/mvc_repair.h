@@ -389,15 +389,6 @@ __device__ int seq_view_lp(const SeqArgs &A, const SView &W, const Cust &C, int 
   return nl;
 }
 
-// pw16 of the 16 lanes of each row (pairs (c, c + h), h = 1, 2, 4, 8: the
-// oracle's pw16 association), broadcast to the row.
-__device__ __forceinline__ double row_pw16(double x) {
-  x = x + down_d<1>(x);
-  x = x + down_d<2>(x);
-  x = x + down_d<4>(x);
-  x = x + down_d<8>(x);
-  return row_bcast0_d(x);
-}
 __device__ __forceinline__ int row16_isum(int x) {
   x += __shfl_xor(x, 1, 64);
   x += __shfl_xor(x, 2, 64);

@@ -304,8 +304,10 @@ class Sampler:
 
     def zpath(self):
         """z-resample kernels of the last parallel sweep: bits 0-1 the lp
-        producer (0 generic, 2 MFMA), bit 2 the register-resident draw kernel;
-        -1 exact schedule / no sweep yet."""
+        producer (0 generic, 2 MFMA), bit 2 the register-resident draw kernel,
+        bit 4 the all-views producer, bit 5 phase A left to the repair, bit 6
+        the dish-block producer, bit 7 the row draw; -1 exact schedule / no
+        sweep yet."""
         return int(self._lib.mvc_sampler_zpath(self._h))
 
     def phase_a(self, chain=0):
