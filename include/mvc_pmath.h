@@ -197,6 +197,29 @@ static __device__ __forceinline__ double mvc_exp_le0(double x) {
   return mvc_exp(x);
 #endif
 }
+/* mvc_exp_le0 with the Horner coefficients as SGPR operands (bitwise equal):
+ * for kernels whose VGPR budget sets their occupancy. */
+static __device__ __forceinline__ double mvc_exp_le0_sk(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double shifter = 6755399441055744.0;
+  double kd = x * MVC_INVLN2;
+  kd = kd + shifter;
+  kd = kd - shifter;
+  kd = __builtin_fmin(__builtin_fmax(kd, -1100.0), 1100.0);
+  const int k = (int)kd;
+  double r = __builtin_fma(-kd, MVC_LN2_HI, x);
+  r = __builtin_fma(-kd, MVC_LN2_LO, r);
+  double p;
+  MVC_HORNER12(p, r, "v", "s");
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  const double e = __builtin_fma(p, r, 1.0);
+  const double res = __builtin_amdgcn_ldexp(e, k);
+  return (x < -745.1332191019412) ? 0.0 : res;
+#else
+  return mvc_exp(x);
+#endif
+}
 #endif
 
 MVC_PM double mvc_log(double x) {

@@ -1089,8 +1089,12 @@ __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK
 // One lane-per-customer kernel would gather V*T values per customer through
 // every lane; here each lane gathers V*T/16 and the row's values share cache
 // lines (the slab layout interleaves the 16 customers of a block).
+#ifndef MVC_ZROW_MINB
+#define MVC_ZROW_MINB 4       // blocks of 4 waves per CU the row draw's register budget must allow
+#endif
+__device__ __forceinline__ int lane_row_base(int row) { return 16 * (row & 3); }   // first lane of a row in its wave
 template <int NB>
-__global__ __launch_bounds__(256) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb, const double *lpb) {
+__global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb, const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
@@ -1144,20 +1148,28 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_row_kernel(Sweep A, int b0,
       if (!(l0p > 0)) w0 = -1.0;
       const double m = A.vmax[(size_t)v * n + i];
       // column c: included dishes j = 16 t + c in ascending t (an excluded
-      // dish adds +0: its weight and argument are zeroed)
+      // dish adds +0: its weight and argument are zeroed); the loads of 8
+      // t at a time are issued before their exps
       double col = 0.0;
-      for (int j = c; j - c < K; j += 16) {
-        const int jc = min(j, K - 1);
-        const double x = lp.at(koff + jc);
-        const double w = (j == j0) ? w0 : s_w[koff + jc];
-        const bool in = j < K && w >= 0.0;
-        col = col + (in ? w : 0.0) * mvc_exp_le0(in ? x - m : 0.0);
+      for (int t0 = 0; 16 * t0 < K; t0 += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = lp.at(koff + min(16 * (t0 + u) + c, K - 1));
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = 16 * (t0 + u) + c;
+          const double w = (j == j0) ? w0 : s_w[koff + min(j, K - 1)];
+          const bool in = j < K && w >= 0.0;
+          double xe = in ? x[u] - m : 0.0;
+          asm volatile("" : "+v"(xe) : "v"(col));   // one exp in flight (registers)
+          col = col + (in ? w : 0.0) * mvc_exp_le0_sk(xe);
+        }
       }
       double S = row_pw16(col);
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = alpha + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
-      S = S + wn * mvc_exp_le0(lfn - m);
+      S = S + wn * mvc_exp_le0_sk(lfn - m);
       const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
       const double lm = (denom <= 0.0) ? lfn : (m + mvc_log_nb(S)) - mvc_log_nb(denom);
       s_new = s_new + lm;
@@ -1185,25 +1197,28 @@ __global__ __launch_bounds__(256) void mvc_par_zdraw_row_kernel(Sweep A, int b0,
       if (16 * k + c < T && sp[k] > M) M = sp[k];
     M = row16_max(M);
     if (s_new > M) M = s_new;
-    // weights in place, block sums, running block totals (block order)
-    double C[NB];
-    double tot = 0.0;
+    // weights in place, block sums, running block totals C_k (block order,
+    // formed in every lane of the row; lane k keeps C_k)
+    double tot = 0.0, Cmine = 0.0;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      sp[k] = (16 * k + c < T) ? mvc_exp_le0(sp[k] - M) : 0.0;   // excluded: exp(-inf) = +0
+      sp[k] = (16 * k + c < T) ? mvc_exp_le0_sk(sp[k] - M) : 0.0;   // excluded: exp(-inf) = +0
       tot = tot + row_pw16(sp[k]);
-      C[k] = tot;
+      if (c == k) Cmine = tot;
     }
-    const double W = mvc_exp_le0(s_new - M) + tot;
+    const double W = mvc_exp_le0_sk(s_new - M) + tot;
     double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-    int pick = -1;
-    int kb = NB - 1;
-    double prev = 0.0, leaf = sp[NB - 1];
+    // the first block k with r < C_k: the lowest such lane of the row
+    const uint64_t hit = __ballot(c < NB && r < Cmine);
+    const int kb = min(NB - 1, __builtin_ctzll(((hit >> (16 * (row & 3))) & 0xFFFFull) | 0x10000ull));
+    const double prev = kb > 0 ? __shfl(Cmine, (lane_row_base(row) + kb - 1), 64) : 0.0;
+    double leaf = sp[0];
 #pragma unroll
-    for (int k = NB - 1; k >= 0; --k)
-      if (r < C[k]) { kb = k; prev = k > 0 ? C[k - 1] : 0.0; leaf = sp[k]; }
-    sel[c] = leaf;                                  // the row's candidate block leaves (LDS)
+    for (int k = 1; k < NB; ++k)
+      if (kb == k) leaf = sp[k];
+    sel[c] = leaf;                                  // the block's leaves (LDS)
     wave_lds_sync();
+    int pick = -1;
     if (r < tot) {
       double a[16];
 #pragma unroll
