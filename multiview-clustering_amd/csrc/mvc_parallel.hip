@@ -1093,17 +1093,25 @@ __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK
 #define MVC_ZROW_MINB 4       // blocks of 4 waves per CU the row draw's register budget must allow
 #endif
 __device__ __forceinline__ int lane_row_base(int row) { return 16 * (row & 3); }   // first lane of a row in its wave
-template <int NB>
-__global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb, const double *lpb) {
+// One customer's lp row for the row draw: in the lp buffer (buffer loads,
+// per-lane dish index) or in the block's LDS copy of its 16-customer slab.
+struct LdsRow {
+  const double *p;     // the slab in LDS, this customer's column: dish k at p[16 k]
+  __device__ __forceinline__ double at(int k) const { return p[16 * k]; }
+};
+
+template <int NB, bool kLds>
+__global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb,
+                                                                                            const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC, n = P.n;
   const int T = __builtin_amdgcn_readfirstlane(A.T);
   const int tid = threadIdx.x, row = tid >> 4, c = tid & 15;
   const int sumK0 = __builtin_amdgcn_readfirstlane(A.Koff[V]);
-  double *s_base = (double *)smem;                 // [16 NB] log mass (or -inf: excluded / padding)
-  double *s_w = s_base + 16 * NB;                  // [sumK] dish weights max(l - sigma, 0) / -1 for l = 0
-  double *s_sel = s_w + sumK0;                     // [16 rows][16] the picked block's leaves
+  double *s_slab = (double *)smem;                 // kLds: [sumK][16] the block's slab of the lp buffer
+  double *s_base = s_slab + (kLds ? (size_t)16 * sumK0 : 0);   // [16 NB] log mass (or -inf: excluded / padding)
+  double *s_sel = s_base + 16 * NB;                // [16 rows][16] the picked block's leaves
   int *s_tix = (int *)(s_sel + 256);               // [16 NB][V] Koff[v] + dish_v(p) (padding: Koff[v])
   int *s_koff = s_tix + 16 * NB * V;               // [V+1]
   int *s_dl = s_koff + V + 1;                      // [sumK] l of each dish
@@ -1119,11 +1127,7 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
   for (int k = tid; k < sumK; k += blockDim.x) {
     int v = 0;
     while (v + 1 < V && s_koff[v + 1] <= k) ++v;
-    const int l = P.d_l[v * KC + (k - s_koff[v])];
-    double w = (double)l - P.hyper[2 * V + v];
-    if (w < 0.0) w = 0.0;
-    s_dl[k] = l;
-    s_w[k] = l > 0 ? w : -1.0;
+    s_dl[k] = P.d_l[v * KC + (k - s_koff[v])];
   }
   __syncthreads();
   const int T_ne = A.status[V + 3];
@@ -1133,7 +1137,24 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
     const bool ok = li < nb;
     const int lic = min(li, nb - 1);
     const int i = b0 + lic;
-    const LpRow lp(lpb, (int)(lpb_index(lic, 0, sumK) * 8));   // dish k of this customer: lp(k)
+    if constexpr (kLds) {   // the slab (16 customers x sumK dishes, contiguous) into LDS, 8 loads in flight
+      const mvc_d2 *src = (const mvc_d2 *)(lpb + (size_t)g * sumK * 16);
+      mvc_d2 *dst = (mvc_d2 *)s_slab;
+      const int ne = sumK * 8;
+      for (int e0 = 0; e0 < ne; e0 += 8 * 256) {
+        mvc_d2 q[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q[u] = src[min(e0 + u * 256 + tid, ne - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (e0 + u * 256 + tid < ne) dst[e0 + u * 256 + tid] = q[u];
+      }
+      __syncthreads();
+    }
+    const auto lp = [&] {
+      if constexpr (kLds) return LdsRow{s_slab + row};
+      else return LpRow(lpb, (int)(lpb_index(lic, 0, sumK) * 8));   // dish k of this customer: lp.at(k)
+    }();
     const int p0 = P.z[i];
     const bool alive = (P.n_t[p0] - 1) > 0;
     double s_new = mvc_log_nb(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
@@ -1143,9 +1164,6 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
       const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
       const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
       const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
-      double w0 = (double)l0p - sigma;
-      if (w0 < 0.0) w0 = 0.0;
-      if (!(l0p > 0)) w0 = -1.0;
       const double m = A.vmax[(size_t)v * n + i];
       // column c: included dishes j = 16 t + c in ascending t (an excluded
       // dish adds +0: its weight and argument are zeroed); the loads of 8
@@ -1158,8 +1176,10 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int j = 16 * (t0 + u) + c;
-          const double w = (j == j0) ? w0 : s_w[koff + min(j, K - 1)];
-          const bool in = j < K && w >= 0.0;
+          const int l = (j == j0) ? l0p : s_dl[koff + min(j, K - 1)];
+          double w = (double)l - sigma;                 // w_j = max(l - sigma, 0), included iff l > 0
+          if (w < 0.0) w = 0.0;
+          const bool in = j < K && l > 0;
           double xe = in ? x[u] - m : 0.0;
           asm volatile("" : "+v"(xe) : "v"(col));   // one exp in flight (registers)
           col = col + (in ? w : 0.0) * mvc_exp_le0_sk(xe);
@@ -1226,11 +1246,13 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
       pick = 16 * kb + pw16_select(a, r - prev);
     }
     if (ok && c == 0) A.choice[i] = pick;
-    wave_lds_sync();
+    if constexpr (kLds) __syncthreads();           // the slab is rewritten next round
+    else wave_lds_sync();
   }
 }
-__host__ __device__ inline size_t zdraw_row_shared_bytes(int V, int NB, int sumK) {
-  return 8 * ((size_t)16 * NB + (size_t)sumK + 256) + 4 * ((size_t)16 * NB * V + (size_t)V + 1 + (size_t)sumK) + 16;
+__host__ __device__ inline size_t zdraw_row_shared_bytes(int V, int NB, int sumK, bool lds) {
+  return 8 * ((size_t)16 * NB + 256 + (lds ? (size_t)16 * sumK : 0)) +
+         4 * ((size_t)16 * NB * V + (size_t)V + 1 + (size_t)sumK) + 16;
 }
 
 // ---------------------------------------------------------------------------
@@ -2085,6 +2107,7 @@ class ParallelSampler : public Sampler {
   int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   bool force_zdraw_row = false;   // MVC_ZDRAW_ROW=1: the row draw for every T <= 512 (default: 64 < T <= 512)
+  bool no_zrow_lds = false;       // MVC_ZROW_LDS=0: the row draw reads the lp buffer directly
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
   int shard_rank = 0, shard_world = 1;
@@ -2288,6 +2311,8 @@ class ParallelSampler : public Sampler {
     force_zdraw_lds = zl && zl[0] == '1';
     const char *zr = getenv("MVC_ZDRAW_ROW");
     force_zdraw_row = zr && zr[0] == '1';
+    const char *zrl = getenv("MVC_ZROW_LDS");
+    no_zrow_lds = zrl && zrl[0] == '0';
     if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
     {
       hipDeviceProp_t prop;
@@ -2317,6 +2342,9 @@ class ParallelSampler : public Sampler {
       no_big = e[0] == '0';
       force_big = e[0] == '1';
     }
+    for (const void *f : {(const void *)mvc_par_zdraw_row_kernel<4, true>, (const void *)mvc_par_zdraw_row_kernel<8, true>,
+                          (const void *)mvc_par_zdraw_row_kernel<16, true>, (const void *)mvc_par_zdraw_row_kernel<32, true>})
+      MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
     for (const void *f : {(const void *)mvc_par_lpbig_kernel<4>, (const void *)mvc_par_lpbig_kernel<2>,
                           (const void *)mvc_par_lpbig_kernel<1>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -2778,7 +2806,9 @@ class ParallelSampler : public Sampler {
     // the row draw (16 lanes per customer) where the register draw does not apply
     const int row_nb = c.T <= 64 ? 4 : c.T <= 128 ? 8 : c.T <= 256 ? 16 : 32;
     const bool use_zrow = !use_zreg && !force_zdraw_lds && c.T <= 512 &&
-                          zdraw_row_shared_bytes(V, row_nb, sk) <= 64 * 1024;
+                          zdraw_row_shared_bytes(V, row_nb, sk, false) <= 64 * 1024;
+    // the row draw with its slab in LDS where two blocks fit a CU
+    const bool zrow_lds = use_zrow && !no_zrow_lds && zdraw_row_shared_bytes(V, row_nb, sk, true) <= 80 * 1024;
     // phase A on the two-kernel path needs the draw's LDS tables; beyond them
     // the repair's eval kernel evaluates the sweep from customer 0 instead
     const bool phaseA = use_zreg || use_zrow || zdraw_shared_bytes(V, c.T, sk) <= 160 * 1024;
@@ -2880,14 +2910,20 @@ class ParallelSampler : public Sampler {
         hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<64>, zg, dim3(256), zdraw_reg_shared_bytes(V, 64, sk), stream, A,
                            (int)b0, nb, (const double *)lpb);
       else if (use_zrow) {
-        const dim3 rg(std::max(1, std::min((nb + 15) / 16, 8 * n_cu)));   // 16 customers per block and round
-        const size_t rl = zdraw_row_shared_bytes(V, row_nb, sk);
+        // 16 customers (one slab) per block and round
+        const dim3 rg(std::max(1, std::min((nb + 15) / 16, (zrow_lds ? 2 : 8) * n_cu)));
+        const size_t rl = zdraw_row_shared_bytes(V, row_nb, sk, zrow_lds);
+        const double *lc = lpb;
+#define MVC_ZROW(NBV)                                                                                      \
+  if (zrow_lds) hipLaunchKernelGGL((mvc_par_zdraw_row_kernel<NBV, true>), rg, dim3(256), rl, stream, A, (int)b0, nb, lc); \
+  else hipLaunchKernelGGL((mvc_par_zdraw_row_kernel<NBV, false>), rg, dim3(256), rl, stream, A, (int)b0, nb, lc);
         switch (row_nb) {
-          case 4: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<4>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
-          case 8: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<8>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
-          case 16: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<16>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
-          default: hipLaunchKernelGGL(mvc_par_zdraw_row_kernel<32>, rg, dim3(256), rl, stream, A, (int)b0, nb, (const double *)lpb); break;
+          case 4: MVC_ZROW(4) break;
+          case 8: MVC_ZROW(8) break;
+          case 16: MVC_ZROW(16) break;
+          default: MVC_ZROW(32) break;
         }
+#undef MVC_ZROW
       } else {
         // the table-score scratch (T x nb doubles) when it stays under 1 GiB
         const size_t scn = (size_t)c.T * (size_t)nb;

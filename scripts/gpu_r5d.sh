@@ -15,5 +15,5 @@ tail -1 gpurun_out/${TAG}_c5prof.log | cut -c1-400
 find gpurun_out/${TAG}_c5prof -name "*kernel_trace.csv" -delete
 timeout -k 10 300 python3 bench.py --leg configs4_full_gpu > gpurun_out/${TAG}_c5leg.json 2>&1 || { echo "c5 leg failed"; exit 1; }
 tail -1 gpurun_out/${TAG}_c5leg.json | cut -c1-600
-MVC_HIP_LIB=$PWD/build_variants/zrow3/libmvc_hip.so timeout -k 10 300 python3 bench.py --leg configs4_full_gpu > gpurun_out/${TAG}_c5leg_zrow3.json 2>&1 || { echo "c5 leg zrow3 failed"; exit 1; }
-tail -1 gpurun_out/${TAG}_c5leg_zrow3.json | cut -c1-400
+MVC_ZROW_LDS=0 timeout -k 10 300 python3 bench.py --leg configs4_full_gpu > gpurun_out/${TAG}_c5leg_global.json 2>&1 || { echo "c5 leg global failed"; exit 1; }
+tail -1 gpurun_out/${TAG}_c5leg_global.json | cut -c1-400

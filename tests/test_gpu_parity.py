@@ -369,7 +369,8 @@ def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=
     check the path taken on the first sweep."""
     monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
     monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
-    monkeypatch.setenv("MVC_ZDRAW_ROW", "1" if draw == "row" else "0")
+    monkeypatch.setenv("MVC_ZDRAW_ROW", "1" if draw.startswith("row") else "0")
+    monkeypatch.setenv("MVC_ZROW_LDS", "0" if draw == "row-global" else "1")
     monkeypatch.setenv("MVC_LPALL", "0" if draw.endswith("-perview") else "1")
     draw = draw.replace("-perview", "")
     s = m.Sampler(y, seed=seed, mode="parallel")
@@ -381,7 +382,7 @@ def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=
             zp = s.zpath()
             assert zp & 3 == path
             assert bool(zp & 4) == ((draw == "reg") if expect_reg is None else expect_reg)
-            if draw == "row":
+            if draw.startswith("row"):
                 assert zp & 128
             elif draw == "lds":
                 assert not zp & 128
@@ -412,7 +413,7 @@ ZPATH_SHAPES = [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96),
                 (1500, 3, 16, 32, 40), (2000, 2, 24, 8, 24), (4100, 4, 128, 64, 64), (777, 1, 32, 16, 16)]
 
 
-@pytest.mark.parametrize("draw", ["reg", "lds", "reg-perview", "row"])
+@pytest.mark.parametrize("draw", ["reg", "lds", "reg-perview", "row", "row-global"])
 @pytest.mark.parametrize("n,V,D,K,T", ZPATH_SHAPES)
 def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
     m = _mvc()
