@@ -1100,8 +1100,13 @@ struct LdsRow {
   __device__ __forceinline__ double at(int k) const { return p[16 * k]; }
 };
 
+// the row draw's exp: Horner coefficients in VGPRs where the register
+// budget allows (the LDS form, two waves per SIMD), else in SGPRs
+template <bool kV>
+__device__ __forceinline__ double zexp(double x) { return kV ? mvc_exp_le0(x) : mvc_exp_le0_sk(x); }
+
 template <int NB, bool kLds>
-__global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb,
+__global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void mvc_par_zdraw_row_kernel(Sweep A, int b0, int nb,
                                                                                             const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
@@ -1181,15 +1186,15 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
           if (w < 0.0) w = 0.0;
           const bool in = j < K && l > 0;
           double xe = in ? x[u] - m : 0.0;
-          asm volatile("" : "+v"(xe) : "v"(col));   // one exp in flight (registers)
-          col = col + (in ? w : 0.0) * mvc_exp_le0_sk(xe);
+          if constexpr (!kLds) asm volatile("" : "+v"(xe) : "v"(col));   // one exp in flight (4 waves per SIMD)
+          col = col + (in ? w : 0.0) * zexp<kLds>(xe);
         }
       }
       double S = row_pw16(col);
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = alpha + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
-      S = S + wn * mvc_exp_le0_sk(lfn - m);
+      S = S + wn * zexp<kLds>(lfn - m);
       const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
       const double lm = (denom <= 0.0) ? lfn : (m + mvc_log_nb(S)) - mvc_log_nb(denom);
       s_new = s_new + lm;
@@ -1222,11 +1227,11 @@ __global__ __launch_bounds__(256, NB >= 32 ? 2 : MVC_ZROW_MINB) void mvc_par_zdr
     double tot = 0.0, Cmine = 0.0;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
-      sp[k] = (16 * k + c < T) ? mvc_exp_le0_sk(sp[k] - M) : 0.0;   // excluded: exp(-inf) = +0
+      sp[k] = (16 * k + c < T) ? zexp<kLds>(sp[k] - M) : 0.0;   // excluded: exp(-inf) = +0
       tot = tot + row_pw16(sp[k]);
       if (c == k) Cmine = tot;
     }
-    const double W = mvc_exp_le0_sk(s_new - M) + tot;
+    const double W = zexp<kLds>(s_new - M) + tot;
     double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
     // the first block k with r < C_k: the lowest such lane of the row
     const uint64_t hit = __ballot(c < NB && r < Cmine);
