@@ -1162,12 +1162,11 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
     }();
     const int p0 = P.z[i];
     const bool alive = (P.n_t[p0] - 1) > 0;
-    double s_new = mvc_log_nb(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+    double Smine = 0.0;                            // lane v of the row keeps view v's column sum
     for (int v = 0; v < V; ++v) {
       const int koff = s_koff[v], K = s_koff[v + 1] - koff;
       const int j0 = s_tix[p0 * V + v] - koff;
-      const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+      const double sigma = P.hyper[2 * V + v];
       const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
       const double m = A.vmax[(size_t)v * n + i];
       // column c: included dishes j = 16 t + c in ascending t (an excluded
@@ -1190,15 +1189,29 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
           col = col + (in ? w : 0.0) * zexp<kLds>(xe);
         }
       }
-      double S = row_pw16(col);
+      const double S = row_pw16(col);
+      if (c == v) Smine = S;
+    }
+    // the per-view scalar terms, lane v of the row for view v (one wave
+    // instruction stream for all views instead of V), then the view-order sum
+    double lm = 0.0;
+    {
+      const int v = min(c, V - 1);
+      const int koff = s_koff[v], K = s_koff[v + 1] - koff;
+      const int j0 = s_tix[p0 * V + v] - koff;
+      const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
+      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+      const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
+      const double m = A.vmax[(size_t)v * n + i];
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = alpha + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
-      S = S + wn * zexp<kLds>(lfn - m);
+      const double S = Smine + wn * zexp<kLds>(lfn - m);
       const double denom = alpha + (double)(P.Ltot[v] - (alive ? 0 : 1));
-      const double lm = (denom <= 0.0) ? lfn : (m + mvc_log_nb(S)) - mvc_log_nb(denom);
-      s_new = s_new + lm;
+      lm = (denom <= 0.0) ? lfn : (m + mvc_log_nb(S)) - mvc_log_nb(denom);
     }
+    double s_new = mvc_log_nb(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
+    for (int v = 0; v < V; ++v) s_new = s_new + __shfl(lm, lane_row_base(row) + v, 64);
     // table scores of positions 16 k + c, view order
     const int np0 = P.n_t[p0] - 1;
     const double m0 = (double)np0 - sg;
@@ -2113,6 +2126,7 @@ class ParallelSampler : public Sampler {
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   bool force_zdraw_row = false;   // MVC_ZDRAW_ROW=1: the row draw for every T <= 512 (default: 64 < T <= 512)
   bool no_zrow_lds = false;       // MVC_ZROW_LDS=0: the row draw reads the lp buffer directly
+  size_t zsc_max_bytes = (size_t)1 << 30;   // the checkpoint draw's table-score scratch limit (MVC_ZSC_MAX_MB)
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
   int shard_rank = 0, shard_world = 1;
@@ -2318,6 +2332,7 @@ class ParallelSampler : public Sampler {
     force_zdraw_row = zr && zr[0] == '1';
     const char *zrl = getenv("MVC_ZROW_LDS");
     no_zrow_lds = zrl && zrl[0] == '0';
+    if (const char *e = getenv("MVC_ZSC_MAX_MB")) zsc_max_bytes = (size_t)std::max(0L, std::strtol(e, nullptr, 10)) << 20;
     if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
     {
       hipDeviceProp_t prop;
@@ -2932,7 +2947,7 @@ class ParallelSampler : public Sampler {
       } else {
         // the table-score scratch (T x nb doubles) when it stays under 1 GiB
         const size_t scn = (size_t)c.T * (size_t)nb;
-        const bool use_sc = scn * sizeof(double) <= ((size_t)1 << 30);
+        const bool use_sc = scn * sizeof(double) <= zsc_max_bytes;
         if (use_sc && scn > zsc_cap) {
           retire(zsc, sizeof(double) * zsc_cap);
           zsc_cap = scn + scn / 2;
