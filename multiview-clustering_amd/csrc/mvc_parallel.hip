@@ -1426,7 +1426,7 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
 // max over the included dishes and the new dish, oracle eval_view_seq) goes
 // to vmax, so the draw reads each lp row once.
 __device__ __forceinline__ void lpa_tile_end(const Sweep &A, const LpaLds &L, int b0, int li0, int nb, double y2,
-                                             double h, int pz, mvc_i4 rsrc, int tile_boff, int disc_boff,
+                                             double h, double cnew, int pz, mvc_i4 rsrc, int tile_boff, int disc_boff,
                                              const double *wsp, double *dslot) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63, row = lane & 15, v = lane >> 4;
@@ -1444,7 +1444,7 @@ __device__ __forceinline__ void lpa_tile_end(const Sweep &A, const LpaLds &L, in
   const int l0p = L.dl[kk] - (alive ? 0 : 1);
   double m = wsp[192 + vv * 16 + row];
   if (l0p > 0 && sv > m) m = sv;
-  const double lfn = A.cnew[vv] + h;
+  const double lfn = cnew + h;
   if (lfn > m) m = lfn;
   double *dm = ok ? A.vmax + (size_t)vv * n + b0 + li0 + row : dslot;
   *dm = m;
@@ -1545,23 +1545,32 @@ __global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep
   const int disc_boff = (int)((uint64_t)(discard - lpb) * 8) + 8 * lane;
   const int row = lane & 15, vl = lane >> 4;      // this lane's (row, view) in the tile start / end passes
   const int vq = min(vl, V - 1);
-  const double tau_l = P.hyper[vq];
+  const double tau_l = P.hyper[vq], cnew_l = A.cnew[vq];
+  // The tile's z and Y2 are loaded one tile ahead: vmcnt retires in order,
+  // so a load issued at the tile start would make its first use wait for
+  // every y prefetch in flight (the ring) as well.
+  auto rowof = [&](int mm) { return min(b0 + (gw + min(mm, nmy - 1) * NWT) * 16 + row, n - 1); };
+  int pz_next = P.z[rowof(0)];
+  double y2_next = A.Y2[(size_t)vq * n + rowof(0)];
   for (int m = 0; m < nmy; ++m) {
     const int li0 = (gw + m * NWT) * 16;
-    const int li_row = min(b0 + li0 + row, n - 1);
-    const int pz = P.z[li_row];
-    // tile start: y2 and h of (view vl, row) -- one division per lane per tile
-    const double y2 = A.Y2[(size_t)vq * n + li_row];
+    const int pz = pz_next;
+    const double y2 = y2_next;
+    pz_next = P.z[rowof(m + 1)];
+    y2_next = A.Y2[(size_t)vq * n + rowof(m + 1)];
+    // tile start: y2 and h of (view vl, row) -- one division per lane per
+    // tile; unconditional LDS writes (lanes of one row store the same z)
     const double h = (-0.5 * y2) / tau_l;
-    if (vl < V) { wsp[vl * 16 + row] = y2; wsp[64 + vl * 16 + row] = h; }
-    if (vl == 0) zs[row] = pz;
+    wsp[vl * 16 + row] = y2;
+    wsp[64 + vl * 16 + row] = h;
+    zs[row] = pz;
     wave_lds_sync();
     const int tile_boff = li0 * sumK * 8;           // (li0 >> 4) * sumK * 16 doubles
     lpa_views<SPPT, RP, PAT, 0>(A, L, li0, nb, ybase, vstride, toff(m), toff(m + 1), ring, rsrc, tile_boff, disc_boff,
                                 wsp, zs);
     wave_lds_sync();
 #ifndef MVC_ABL_LP_NOEPI
-    lpa_tile_end(A, L, b0, li0, nb, y2, h, pz, rsrc, tile_boff, disc_boff, wsp, dslot);
+    lpa_tile_end(A, L, b0, li0, nb, y2, h, cnew_l, pz, rsrc, tile_boff, disc_boff, wsp, dslot);
 #endif
     wave_lds_sync();
   }
