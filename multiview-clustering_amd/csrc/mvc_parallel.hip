@@ -1237,19 +1237,34 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
     if (s_new > M) M = s_new;
     // weights in place, block sums, running block totals C_k (block order,
     // formed in every lane of the row; lane k keeps C_k)
-    double tot = 0.0, Cmine = 0.0;
+    constexpr int NG = (NB + 15) / 16;             // lane c keeps C_k of blocks k = c + 16 g
+    double tot = 0.0, Cm[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) Cm[g] = 0.0;
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       sp[k] = (16 * k + c < T) ? zexp<kLds>(sp[k] - M) : 0.0;   // excluded: exp(-inf) = +0
       tot = tot + row_pw16(sp[k]);
-      if (c == k) Cmine = tot;
+      if (c == (k & 15)) Cm[k >> 4] = tot;
     }
     const double W = zexp<kLds>(s_new - M) + tot;
     double r = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z) * W;
-    // the first block k with r < C_k: the lowest such lane of the row
-    const uint64_t hit = __ballot(c < NB && r < Cmine);
-    const int kb = min(NB - 1, __builtin_ctzll(((hit >> (16 * (row & 3))) & 0xFFFFull) | 0x10000ull));
-    const double prev = kb > 0 ? __shfl(Cmine, (lane_row_base(row) + kb - 1), 64) : 0.0;
+    // the first block k with r < C_k: the lowest such lane of the row, group by group
+    int kb = NB - 1;
+#pragma unroll
+    for (int g = NG - 1; g >= 0; --g) {
+      const uint64_t hit = __ballot(16 * g + c < NB && r < Cm[g]);
+      const uint64_t mine = (hit >> lane_row_base(row)) & 0xFFFFull;
+      if (mine) kb = 16 * g + __builtin_ctzll(mine);
+    }
+    // C_{kb-1} from its lane (the whole wave takes part in the shuffle)
+    const int kp = max(kb - 1, 0);
+    double cv = Cm[0];
+#pragma unroll
+    for (int g = 1; g < NG; ++g)
+      if ((kp >> 4) == g) cv = Cm[g];
+    const double cprev = __shfl(cv, lane_row_base(row) + (kp & 15), 64);
+    const double prev = kb > 0 ? cprev : 0.0;
     double leaf = sp[0];
 #pragma unroll
     for (int k = 1; k < NB; ++k)

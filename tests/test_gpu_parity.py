@@ -410,6 +410,7 @@ def test_mfma_and_generic_paths_identical(monkeypatch):
 # phase 1 as lp buffer + register draw (T <= 64, K_v <= 64) or lp buffer +
 # LDS checkpoint draw (any T), the all-views producer or one launch per view
 ZPATH_SHAPES = [(3001, 4, 64, 16, 16), (50, 2, 20, 4, 4), (4000, 3, 32, 64, 96), (2500, 2, 128, 64, 64),
+                (5000, 3, 32, 32, 200), (6000, 2, 16, 64, 300),
                 (1500, 3, 16, 32, 40), (2000, 2, 24, 8, 24), (4100, 4, 128, 64, 64), (777, 1, 32, 16, 16)]
 
 
