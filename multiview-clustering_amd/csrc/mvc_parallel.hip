@@ -1424,6 +1424,7 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
       if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
     }
   }
+#ifndef MVC_ABL_LP_NOMAX   // timing ablation: no row maxima
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     double x = mx[r];
@@ -1433,6 +1434,7 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
     x = dmax(x, down_d<1>(x));
     if (col == 0) mrest[grp + 4 * r] = x;   // lane 0 of the row holds the row's max
   }
+#endif
 }
 
 // The own dish of every (view, row) of the tile, one lane each (lane = row +
@@ -1584,7 +1586,7 @@ __global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep
     lpa_views<SPPT, RP, PAT, 0>(A, L, li0, nb, ybase, vstride, toff(m), toff(m + 1), ring, rsrc, tile_boff, disc_boff,
                                 wsp, zs);
     wave_lds_sync();
-#ifndef MVC_ABL_LP_NOEPI
+#if !defined(MVC_ABL_LP_NOEPI) && !defined(MVC_ABL_LP_NOEND)
     lpa_tile_end(A, L, b0, li0, nb, y2, h, cnew_l, pz, rsrc, tile_boff, disc_boff, wsp, dslot);
 #endif
     wave_lds_sync();
