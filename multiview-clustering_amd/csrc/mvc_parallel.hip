@@ -63,7 +63,7 @@ typedef double mvc_d4 __attribute__((ext_vector_type(4)));
 //   1. an lp producer writes lp[i][Koff[v] + j] (frozen dish j of view v,
 //      self-removal applied to the customer's own dish) into the lp buffer,
 //      slabs of 16 customers, dish-major:  lpb[(li >> 4) * sumK * 16 +
-//      k * 16 + (li & 15)],  li = i - b0;
+//      k * 16 + lpb_slot(li & 15)],  li = i - b0;
 //        * MFMA producer (D % 4 == 0, D >= 16, K_v <= 64): G = Y S1^T tiles
 //          with v_mfma_f64_16x16x4_f64, S1 B-fragments staged through LDS by
 //          the block, y A-fragments streamed from the tiled copy yt;
@@ -75,8 +75,13 @@ typedef double mvc_d4 __attribute__((ext_vector_type(4)));
 #define MVC_Z_KMAX 64
 #define MVC_Z_VMAX 8
 
+// Within a slab, customer row rho sits at slot 4 (rho & 3) + (rho >> 2): the
+// rows one lane of the MFMA producer holds (grp, grp + 4, grp + 8, grp + 12 of
+// a 16 x 16 tile) are then 32 contiguous bytes, stored as two 16-byte
+// pieces, and a dish's 16 rows are still one 128-byte line.
+__host__ __device__ inline int lpb_slot(int rho) { return 4 * (rho & 3) + (rho >> 2); }
 __host__ __device__ inline size_t lpb_index(int li, int k, int sumK) {
-  return ((size_t)(li >> 4) * (size_t)sumK + (size_t)k) * 16 + (size_t)(li & 15);
+  return ((size_t)(li >> 4) * (size_t)sumK + (size_t)k) * 16 + (size_t)lpb_slot(li & 15);
 }
 
 // A-fragment layout, k-steps in pairs (one 16 B load per lane covers two):
@@ -1157,7 +1162,7 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
       __syncthreads();
     }
     const auto lp = [&] {
-      if constexpr (kLds) return LdsRow{s_slab + row};
+      if constexpr (kLds) return LdsRow{s_slab + lpb_slot(row)};
       else return LpRow(lpb, (int)(lpb_index(lic, 0, sumK) * 8));   // dish k of this customer: lp.at(k)
     }();
     const int p0 = P.z[i];
@@ -1352,6 +1357,8 @@ __device__ __forceinline__ void lpall_self_coef(int dn, double tau, double L2pt,
 
 extern "C" __device__ void mvc_raw_buffer_store_f64(double v, mvc_i4 rsrc, int voffset, int soffset, int aux)
     __asm("llvm.amdgcn.raw.buffer.store.f64");
+extern "C" __device__ void mvc_raw_buffer_store_v2f64(mvc_d2 v, mvc_i4 rsrc, int voffset, int soffset, int aux)
+    __asm("llvm.amdgcn.raw.buffer.store.v2f64");
 
 // One view of one 16-customer tile: the MFMA block, then the lp of every
 // (row, frozen dish) stored (buffer stores: a 32-bit lane offset, invalid
@@ -1403,26 +1410,30 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
   double mx[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) mx[r] = -MVC_PM_INF;
-  // byte offset of (row grp + 4 r, dish koff + 16 t + col) within the tile: 128 (koff + 16 t + col) + 8 (grp + 4 r)
-  const int lbase = tile_boff + 128 * (koff + col) + 8 * grp;
+  // byte offset of (row grp + 4 r, dish koff + 16 t + col) within the tile:
+  // 128 (koff + 16 t + col) + 8 lpb_slot(grp + 4 r) = ... + 32 grp + 8 r, so a
+  // lane's four rows are two 16-byte stores.  Rows past the batch end go to
+  // their own (unread) slots of the last slab; dishes past K_v to the discard.
+  const int lbase = tile_boff + 128 * (koff + col) + 32 * grp;
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int j = 16 * t + col;
     const int kc = koff + min(j, K - 1);
     const double c0j = L.c0[kc], cbj = L.cb[kc];
     const bool inc = j < K && L.dl[kc] > 0;
+    double val[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
-      const bool ok = j < K && li0 + grp + 4 * r < nb;
-      const int off = ok ? lbase + 2048 * t + 32 * r : disc_boff;
-#ifndef MVC_ABL_LP_NOSTORE   // timing ablation: no lp stores
-      mvc_raw_buffer_store_f64(val, rsrc, off, 0, 0);
-#else
-      (void)off;
-#endif
-      if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
+      val[r] = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+      if (inc && j != j0[r] && val[r] > mx[r]) mx[r] = val[r];
     }
+    const int off = j < K ? lbase + 2048 * t : disc_boff;
+#ifndef MVC_ABL_LP_NOSTORE   // timing ablation: no lp stores
+    mvc_raw_buffer_store_v2f64((mvc_d2){val[0], val[1]}, rsrc, off, 0, 0);
+    mvc_raw_buffer_store_v2f64((mvc_d2){val[2], val[3]}, rsrc, j < K ? off + 16 : disc_boff, 0, 0);
+#else
+    (void)off;
+#endif
   }
 #ifndef MVC_ABL_LP_NOMAX   // timing ablation: no row maxima
 #pragma unroll
@@ -1456,7 +1467,7 @@ __device__ __forceinline__ void lpa_tile_end(const Sweep &A, const LpaLds &L, in
   const double c0 = L.xs[kk] - (0.5 * Qp) / L.dens[kk];
   const double sv = __builtin_fma(Gp + 0.5 * y2, L.cbs[kk], c0) + h;
   const bool ok = v < V && li0 + row < nb;
-  mvc_raw_buffer_store_f64(sv, rsrc, ok ? tile_boff + 128 * kk + 8 * row : disc_boff, 0, 0);
+  mvc_raw_buffer_store_f64(sv, rsrc, ok ? tile_boff + 128 * kk + 8 * lpb_slot(row) : disc_boff, 0, 0);
   const bool alive = (L.nt[pz] - 1) > 0;
   const int l0p = L.dl[kk] - (alive ? 0 : 1);
   double m = wsp[192 + vv * 16 + row];
@@ -1559,7 +1570,7 @@ __global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep
   // buffer is < 2^31 bytes, kLpbBudget); the discard slots follow it
   const uint64_t lpa = (uint64_t)lpb;
   const mvc_i4 rsrc = (mvc_i4){(int)(uint32_t)lpa, (int)(uint32_t)(lpa >> 32), -1, 0x00020000};
-  const int disc_boff = (int)((uint64_t)(discard - lpb) * 8) + 8 * lane;
+  const int disc_boff = (int)((uint64_t)(discard - lpb) * 8) + 16 * lane;   // 16-byte stores
   const int row = lane & 15, vl = lane >> 4;      // this lane's (row, view) in the tile start / end passes
   const int vq = min(vl, V - 1);
   const double tau_l = P.hyper[vq], cnew_l = A.cnew[vq];
@@ -2874,9 +2885,9 @@ class ParallelSampler : public Sampler {
       default: pat_ok = false;
     }
     if (phaseA && need > lpb_cap) {
-      retire(lpb, sizeof(double) * (lpb_cap + 64));
+      retire(lpb, sizeof(double) * (lpb_cap + 128));
       lpb_cap = need;
-      lpb = dmalloc<double>(lpb_cap + 64);   // + 64: the producer's per-lane discard slots
+      lpb = dmalloc<double>(lpb_cap + 128);   // + 128: the producers' per-lane discard slots (16 B per lane)
     }
     bool zpath_lpall = false;
     timers.begin("zresample", &e0);
