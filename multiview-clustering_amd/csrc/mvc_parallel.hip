@@ -179,10 +179,15 @@ __device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2
 #pragma unroll
         for (int t = 0; t < 2 * NT; ++t) bn[t] = bk[t * 64];
       }
+#ifndef MVC_ABL_LP_NOMFMA
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bc[t], acc[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bc[NT + t], acc[t], 0, 0, 0);
+#else   // timing ablation: the stream and the epilogue without the matrix pipe
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t][q & 3] += a[0] + a[1] + bc[t] + bc[NT + t];
+#endif
       __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
 #pragma unroll
       for (int t = 0; t < 2 * NT; ++t) bc[t] = bn[t];
