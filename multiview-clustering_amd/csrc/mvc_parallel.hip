@@ -2184,6 +2184,7 @@ class ParallelSampler : public Sampler {
   bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
+  int small_n_no_windows = 4096;  // MVC_SMALL_N: chains up to this n never use grid windows
   // MVC_RUN_WAVES: customers the run kernel evaluates per step.  4 by default:
   // one evaluating wave per SIMD (a second wave on a SIMD halves the first
   // customer's issue rate, and with dense movers the first customer decides)
@@ -2411,6 +2412,7 @@ class ParallelSampler : public Sampler {
                           (const void *)mvc_par_lpbig_kernel<1>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
+    if (const char *e = getenv("MVC_SMALL_N")) small_n_no_windows = atoi(e);
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
@@ -3040,7 +3042,9 @@ class ParallelSampler : public Sampler {
     int kmax = 1;
     for (int v = 0; v < V; ++v) kmax = std::max(kmax, (int)Klist[v]);
     SeqLds L{};
-    L.limit = run_limit;
+    // small chains: the run kernel walks the whole sweep (a window round is a
+    // launch triple and a host read-back, more than the steps it saves)
+    L.limit = (n <= small_n_no_windows) ? kNoWindows : run_limit;
     // in order of preference: S1 cached with room to grow, then without S1,
     // then tight margins without S1
     for (int attempt = force_global ? 3 : 0; attempt < 3; ++attempt) {

@@ -1970,6 +1970,14 @@ __device__ bool seq_commit(SeqArgs &A, const SView &W, const SCache *cc, const C
   return true;
 }
 
+// seq_commit of a birth with every call inside it inlined (flatten): the
+// lane-column run kernels commit their births themselves, and an outlined
+// call there would pass the kernel's arguments through scratch memory.
+__device__ __attribute__((flatten, always_inline)) inline bool seq_commit_birth_inline(SeqArgs &A, int i, double *lpw,
+                                                                                        double *treew, int nwd) {
+  return seq_commit(A, global_view(A), nullptr, global_cust(A, i), i, A.P.z[i], -1, lpw, treew, &A.R->moves, nwd);
+}
+
 // A store to global memory as a global_store (not flat: a flat store also
 // counts on lgkmcnt, so every LDS-only barrier after it would wait for HBM).
 template <class T>
@@ -2132,8 +2140,9 @@ __device__ __forceinline__ void note_mover(int32_t &lastm, int32_t &gapq, int f)
   gapq = (3 * gapq + 16 * gap) >> 2;
   lastm = f;
 }
+constexpr int kNoWindows = 1 << 29;   // a limit this large: the run kernel never hands over to windows
 __device__ __forceinline__ int stay_limit(int limit, int gapq) {
-  return gapq > 16 * kSparseGap ? min(limit, kSparseLimit) : limit;
+  return (limit < kNoWindows && gapq > 16 * kSparseGap) ? min(limit, kSparseLimit) : limit;
 }
 
 // Resolve the grid window evaluated by the last mvc_seq_eval_kernel (thread 0).
@@ -3748,135 +3757,163 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
   if (tid < 12) mvc_prof_lds[tid] = 0;
 #endif
   if (tid < 8) mvc_run_bad[tid] = 0;   // (MVC_RUN_CHECK; published by the barrier below)
-  if (tid == 0) {
-    const int go = !(R->done || R->overflow || R->restride);
-    if (go && R->win1 > R->win0) {
-      seq_resolve_window(A, R);
-      if (R->pend) {
-        R->mode = kSeqRun;
-        R->streak = 0;
+  // The lane-column loops stop at a birth (its dish draws want the block's
+  // waves and the global state); the birth is committed here on the global
+  // state and the loop resumes at the next customer with its LDS cache
+  // re-staged, so a sweep with births is one launch, not one per birth (the
+  // mvc_seq_birth_kernel the host launches after this kernel is then a no-op).
+  for (;;) {
+    if (tid == 0) {
+      const int go = !(R->done || R->overflow || R->restride);
+      if (go && R->win1 > R->win0) {
+        seq_resolve_window(A, R);
+        if (R->pend) {
+          R->mode = kSeqRun;
+          R->streak = 0;
+        }
       }
+      if (go) R->rounds += 1;
+      U.go = go;
+      U.cur = R->cur;
+      U.pend = R->pend;
+      U.pc = R->pchoice;
+      U.pp0 = U.pend ? P.z[U.cur] : 0;
+      U.mode = R->mode;
+      U.streak = R->streak;
+      U.done = R->done;
+      U.fill = U.cur;   // nothing staged yet
+      U.landed = U.cur;
+      U.lpc = -1;
+      U.cnt[0] = R->moves;
+      U.cnt[1] = R->births;
+      U.cnt[2] = R->newdish;
+      U.lastm = R->lastm;
+      U.gapq = R->gapq;
     }
-    if (go) R->rounds += 1;
-    U.go = go;
-    U.cur = R->cur;
-    U.pend = R->pend;
-    U.pc = R->pchoice;
-    U.pp0 = U.pend ? P.z[U.cur] : 0;
-    U.mode = R->mode;
-    U.streak = R->streak;
-    U.done = R->done;
-    U.fill = U.cur;   // nothing staged yet
-    U.landed = U.cur;
-    U.lpc = -1;
-    U.cnt[0] = R->moves;
-    U.cnt[1] = R->births;
-    U.cnt[2] = R->newdish;
-    U.lastm = R->lastm;
-    U.gapq = R->gapq;
-  }
-  __syncthreads();
-  if (!U.go || !(U.mode == kSeqRun || U.pend)) {
-    if (tid == 0 && U.go && !(R->win1 > R->win0)) {   // scan mode: open the next grid window
-      if (R->cur >= n && !R->pend) {
+    __syncthreads();
+    if (!U.go || !(U.mode == kSeqRun || U.pend)) {
+      if (tid == 0 && U.go && !(R->win1 > R->win0)) {   // scan mode: open the next grid window
+        if (R->cur >= n && !R->pend) {
+          R->done = 1;
+        } else {
+          R->win0 = R->cur;
+          R->win1 = min(n, R->cur + R->W);
+          R->fmin = n;
+        }
+      }
+      return;
+    }
+    int flags = 0;   // kRunOvf | kRunRestride | kRunVpOff
+    double *tree = SeqScratch(A, w).tree;   // global per-wave scratch: the dish draws' tree64 levels
+    if (L.lds) {   // the state cache, from the global state at launch
+      const int ts = L.ts, ks = L.ks;
+      const SCache cc = lds_cache(V, D, ts, ks, L.s1);
+      // the sweep's hyperparameters and per-view constants (the evaluation and
+      // the commits read them from LDS; the MH changes them only after the repair)
+      for (int k = tid; k < 3 * V + 2; k += nt) mvc_seq_const[k] = P.hyper[k];
+      for (int k = tid; k < V; k += nt) {
+        mvc_seq_const[3 * MVC_MAXV + 2 + k] = A.cnew[k];
+        mvc_seq_const[4 * MVC_MAXV + 2 + k] = A.L2pt[k];
+      }
+      const int T = R->T;
+      for (int k = tid; k < T; k += nt) {
+        cc.n_t[k] = P.n_t[k];
+        cc.lmass[k] = P.lmass[k];
+      }
+      for (int k = tid; k < V * T; k += nt) {
+        const int v = k / T, p = k - v * T;
+        cc.dish[v * ts + p] = P.dish[v * TC + p];
+      }
+      for (int k = tid; k < V * ks; k += nt) {
+        const int v = k / ks, j = k - v * ks;
+        if (j < R->Klist[v]) {
+          cc.d_l[k] = P.d_l[v * KC + j];
+          cc.d_n[k] = P.d_n[v * KC + j];
+          cc.c0[k] = P.c0[v * KC + j];
+          cc.cb[k] = P.cb[v * KC + j];
+          cc.Q[k] = P.Q[v * KC + j];
+          cc.S2[k] = P.S2[v * KC + j];
+          self_coef_parts(cc.d_n[k], P.hyper[v], A.L2pt[v], D, cc.xm[k], cc.ym[k], cc.cbm[k]);
+        }
+      }
+      if (L.s1) {
+        for (int k = tid; k < V * D * ks; k += nt) {
+          const int row = k / ks, j = k - row * ks;
+          if (j < R->Klist[row / D]) cc.S1T[k] = P.S1T[(size_t)row * KC + j];
+        }
+      }
+      if (tid < V) {
+        cc.Klist[tid] = R->Klist[tid];
+        cc.Ltot[tid] = P.Ltot[tid];
+      }
+      if (tid == 0) {
+        *cc.T = R->T;
+        *cc.T_ne = R->T_ne;
+      }
+      __syncthreads();
+      Ring G;
+      G.n = L.ring;
+      G.slot = (int)seq_ring_slot(V, D);
+      G.base = mvc_seq_lds + L.cache_dbl + (int64_t)L.nws * L.stride;
+      if constexpr (kMode == 3)
+        flags = seq_run_loop_lc(A, L, G, U);
+      else if constexpr (kMode == 4)
+        flags = seq_run_loop_vp(A, L, G, U);
+      else
+        flags = seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
+                                          SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
+                                          G, tree, U);
+      __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
+    } else if constexpr (kMode < 3) {   // (the lane-column kernels always have the LDS layout)
+      Ring G{nullptr, 0, 0};
+      flags = seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U);
+    }
+    if (tid == 0) {   // write the cursor back; open a grid window when handing over
+  #ifdef MVC_RUN_PROF
+      for (int k = 0; k < 12; ++k) R->prof[k] += mvc_prof_lds[k];
+  #endif
+      R->cur = U.cur;
+      R->pend = U.pend;
+      R->pchoice = U.pc;
+      R->mode = U.mode;
+      R->streak = U.streak;
+      R->moves = U.cnt[0];
+      R->births = U.cnt[1];
+      R->newdish = U.cnt[2];
+      R->lastm = U.lastm;
+      R->gapq = U.gapq;
+      if (L.chk && mvc_run_bad[0])
+        for (int k = 0; k < 8; ++k) R->dbg[k] = mvc_run_bad[k];
+      if (flags & kRunRestride) R->restride = 1;
+      if (flags & kRunVpOff) R->vpoff = 1;
+      if (U.done && !U.pend) {
         R->done = 1;
-      } else {
-        R->win0 = R->cur;
-        R->win1 = min(n, R->cur + R->W);
+      } else if (!(flags & (kRunOvf | kRunRestride)) && U.mode == kSeqScan && !U.pend) {
+        R->win0 = U.cur;
+        R->win1 = min(n, U.cur + R->W);
         R->fmin = n;
       }
     }
-    return;
-  }
-  int flags = 0;   // kRunOvf | kRunRestride | kRunVpOff
-  double *tree = SeqScratch(A, w).tree;   // global per-wave scratch: the dish draws' tree64 levels
-  if (L.lds) {   // the state cache, from the global state at launch
-    const int ts = L.ts, ks = L.ks;
-    const SCache cc = lds_cache(V, D, ts, ks, L.s1);
-    // the sweep's hyperparameters and per-view constants (the evaluation and
-    // the commits read them from LDS; the MH changes them only after the repair)
-    for (int k = tid; k < 3 * V + 2; k += nt) mvc_seq_const[k] = P.hyper[k];
-    for (int k = tid; k < V; k += nt) {
-      mvc_seq_const[3 * MVC_MAXV + 2 + k] = A.cnew[k];
-      mvc_seq_const[4 * MVC_MAXV + 2 + k] = A.L2pt[k];
-    }
-    const int T = R->T;
-    for (int k = tid; k < T; k += nt) {
-      cc.n_t[k] = P.n_t[k];
-      cc.lmass[k] = P.lmass[k];
-    }
-    for (int k = tid; k < V * T; k += nt) {
-      const int v = k / T, p = k - v * T;
-      cc.dish[v * ts + p] = P.dish[v * TC + p];
-    }
-    for (int k = tid; k < V * ks; k += nt) {
-      const int v = k / ks, j = k - v * ks;
-      if (j < R->Klist[v]) {
-        cc.d_l[k] = P.d_l[v * KC + j];
-        cc.d_n[k] = P.d_n[v * KC + j];
-        cc.c0[k] = P.c0[v * KC + j];
-        cc.cb[k] = P.cb[v * KC + j];
-        cc.Q[k] = P.Q[v * KC + j];
-        cc.S2[k] = P.S2[v * KC + j];
-        self_coef_parts(cc.d_n[k], P.hyper[v], A.L2pt[v], D, cc.xm[k], cc.ym[k], cc.cbm[k]);
+    if constexpr (kMode >= 3) {
+      __shared__ int s_birth, s_bi;
+      __syncthreads();
+      if (tid == 0) {
+        s_birth = !(R->done || R->overflow || R->restride) && R->pend && R->pchoice < 0;
+        s_bi = R->cur;
       }
-    }
-    if (L.s1) {
-      for (int k = tid; k < V * D * ks; k += nt) {
-        const int row = k / ks, j = k - row * ks;
-        if (j < R->Klist[row / D]) cc.S1T[k] = P.S1T[(size_t)row * KC + j];
+      __syncthreads();
+      if (!s_birth) return;
+      const SeqScratch Sb(A, w);
+      if (!seq_commit_birth_inline(A, s_bi, Sb.lp, Sb.tree, nt >> 6)) return;   // overflow: the host grows and relaunches this step
+      if (tid == 0) {
+        R->cur = s_bi + 1;
+        R->pend = 0;
+        R->streak = 0;
+        if (R->cur >= n) R->done = 1;   // every customer is final (see mvc_seq_birth_kernel)
       }
-    }
-    if (tid < V) {
-      cc.Klist[tid] = R->Klist[tid];
-      cc.Ltot[tid] = P.Ltot[tid];
-    }
-    if (tid == 0) {
-      *cc.T = R->T;
-      *cc.T_ne = R->T_ne;
-    }
-    __syncthreads();
-    Ring G;
-    G.n = L.ring;
-    G.slot = (int)seq_ring_slot(V, D);
-    G.base = mvc_seq_lds + L.cache_dbl + (int64_t)L.nws * L.stride;
-    if constexpr (kMode == 3)
-      flags = seq_run_loop_lc(A, L, G, U);
-    else if constexpr (kMode == 4)
-      flags = seq_run_loop_vp(A, L, G, U);
-    else
-      flags = seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
-                                        SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
-                                        G, tree, U);
-    __builtin_amdgcn_s_waitcnt(0);   // no row request outlives the wave
-  } else if constexpr (kMode < 3) {   // (the lane-column kernels always have the LDS layout)
-    Ring G{nullptr, 0, 0};
-    flags = seq_run_loop<false, kMode == 2>(A, L, global_view(A), nullptr, SeqScratch(A, w), G, tree, U);
-  }
-  if (tid == 0) {   // write the cursor back; open a grid window when handing over
-#ifdef MVC_RUN_PROF
-    for (int k = 0; k < 12; ++k) R->prof[k] += mvc_prof_lds[k];
-#endif
-    R->cur = U.cur;
-    R->pend = U.pend;
-    R->pchoice = U.pc;
-    R->mode = U.mode;
-    R->streak = U.streak;
-    R->moves = U.cnt[0];
-    R->births = U.cnt[1];
-    R->newdish = U.cnt[2];
-    R->lastm = U.lastm;
-    R->gapq = U.gapq;
-    if (L.chk && mvc_run_bad[0])
-      for (int k = 0; k < 8; ++k) R->dbg[k] = mvc_run_bad[k];
-    if (flags & kRunRestride) R->restride = 1;
-    if (flags & kRunVpOff) R->vpoff = 1;
-    if (U.done && !U.pend) {
-      R->done = 1;
-    } else if (!(flags & (kRunOvf | kRunRestride)) && U.mode == kSeqScan && !U.pend) {
-      R->win0 = U.cur;
-      R->win1 = min(n, U.cur + R->W);
-      R->fmin = n;
+      __syncthreads();
+    } else {
+      return;
     }
   }
 }
