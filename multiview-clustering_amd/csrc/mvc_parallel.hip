@@ -2184,7 +2184,7 @@ class ParallelSampler : public Sampler {
   bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
-  int small_n_no_windows = 4096;  // MVC_SMALL_N: chains up to this n never use grid windows
+  int small_n_no_windows = 0;     // MVC_SMALL_N: chains up to this n never use grid windows (off: at N = 200 windows are faster)
   // MVC_RUN_WAVES: customers the run kernel evaluates per step.  4 by default:
   // one evaluating wave per SIMD (a second wave on a SIMD halves the first
   // customer's issue rate, and with dense movers the first customer decides)
@@ -2395,7 +2395,8 @@ class ParallelSampler : public Sampler {
     lpall_attr<16, 8>();
     // (instance 2 runs the global-scratch layout only: no dynamic LDS)
     for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>,
-                          (const void *)mvc_seq_run_kernel<4>})
+                          (const void *)mvc_seq_run_kernel<4>, (const void *)mvc_seq_run_kernel_b<0>,
+                          (const void *)mvc_seq_run_kernel_b<3>, (const void *)mvc_seq_run_kernel_b<4>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_wide_fin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kWideFinLds));
@@ -2835,6 +2836,13 @@ class ParallelSampler : public Sampler {
 #undef X
   }
   void sweep_chain(Chain &c, uint32_t s) {
+    bool phaseA = false;
+    if (sweep_pre(c, s, phaseA)) repair(c, s, phaseA);
+  }
+  // A sweep up to the repair: phase A (producer + draw) of this rank's
+  // customers and, when sharded, the exchange of the choices.  false: the
+  // caller stops here (mvc_sampler_phase_a).
+  bool sweep_pre(Chain &c, uint32_t s, bool &phaseA_out) {
     Sweep A = make_sweep(c, s);
     const SeqArgs Q0 = make_seq(c, s);
     hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
@@ -3013,7 +3021,7 @@ class ParallelSampler : public Sampler {
       phase_a_ran = phaseA;
       zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) | (use_big ? 64 : 0) |
                         (use_zrow ? 128 : 0)) : 32;
-      return;
+      return false;
     }
     if (phaseA && shard_world > 1) {
       // the other ranks' phase-A choices: this shard into the exchange buffer,
@@ -3031,7 +3039,8 @@ class ParallelSampler : public Sampler {
     }
     zpath = phaseA ? ((use_mfma ? 2 : 0) | (use_zreg ? 4 : 0) | (zpath_lpall ? 16 : 0) |
                       (use_big ? 64 : 0) | (use_zrow ? 128 : 0)) : 32;
-    repair(c, s, phaseA);
+    phaseA_out = phaseA;
+    return true;
   }
 
   // LDS layout of the run kernel's per-wave scratch for T tables and dish
@@ -3107,75 +3116,182 @@ class ParallelSampler : public Sampler {
   // and a grid window (sparse movers).  One host synchronisation per batch of
   // rounds; at steady state a single batch of one round.  A birth beyond the
   // capacity grows every chain and resumes.
-  void repair(Chain &c, uint32_t s, bool phaseA) {
+  // The in-order repair of one chain, in three parts so
+  // that a ChainSet can run the rounds of all its chains as batched launches:
+  // repair_start (first mover / first window), the rounds with the outcome
+  // read back per batch (repair_outcome), repair_finish (compaction, MH).
+  struct RepairRun {
+    SeqArgs Q;
+    SeqLds L;
+    dim3 eg;
+    bool vp_ok = true, early_mh = false;
+    int rounds = 1;
     hipEvent_t e1 = nullptr;
-    timers.begin("repair", &e1);
-    SeqArgs Q = make_seq(c, s);
-    dim3 eg(seq_waves / 4);   // the eval grid: one wave per scratch slot (re-read after a capacity growth)
+  };
+  void repair_start(Chain &c, uint32_t s, bool phaseA, RepairRun &rr, bool allow_early_mh = true) {
+    timers.begin("repair", &rr.e1);
+    rr.Q = make_seq(c, s);
+    rr.eg = dim3(seq_waves / 4);   // the eval grid: one wave per scratch slot (re-read after a capacity growth)
     const dim3 eb(256);
     if (phaseA)
       hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
                          stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
     else
-      hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
+      hipLaunchKernelGGL(mvc_seq_eval_kernel, rr.eg, eb, 0, stream, rr.Q);
     MVC_HIP(hipGetLastError());
     dbg("seq_first / eval", c, s);
-    bool vp_ok = true;   // value prediction until it stops itself in this sweep (R->vpoff)
-    SeqLds L = run_layout(c.T, c.K.data(), vp_ok);
+    rr.vp_ok = true;   // value prediction until it stops itself in this sweep (R->vpoff)
+    rr.L = run_layout(c.T, c.K.data(), rr.vp_ok);
     // the gated early MH (below) only where no per-phase timers bracket the
     // repair and the MH separately (they would time the MH as repair)
-    const bool early_mh = !early_mh_off && (!timers.on || timers.coarse);
-    if (early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
-    int rounds = 1;
-    for (;;) {
-      // the grid-wide evaluation where the state is on the global layout (L.lds = 0) and
-      // the block-wide evaluation applies (L.tw > 1): one customer over many CUs
-      const bool wgrid = !repair_grid_only && wide_grid && L.lds == 0 && L.tw > 1;
-      int wblk = 1;
-      if (wgrid) {
-        if (!wide_part) wide_part = dmalloc<double>((size_t)kWideGridMax * 2 * V);
-        // blocks for the dish list (plus the births a round may add): two 64-dish chunks per wave
-        int nk = 0;
-        for (int k : c.K) nk += k;
-        nk += nk / 4 + 64;
-        wblk = std::max(1, std::min(kWideGridMax, (nk + 2 * kWideGridThreads - 1) / (2 * kWideGridThreads)));
-      }
-      for (int r = 0; r < rounds; ++r) {
-        if (repair_grid_only)
-          hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, Q);
-        else if (wgrid) {
-          hipLaunchKernelGGL(mvc_seq_wide_begin_kernel, dim3(1), dim3(64), 0, stream, Q);
-          for (int b = 0; b < kWideBatch; ++b) {
-            hipLaunchKernelGGL(mvc_seq_wide_lp_kernel, dim3(wblk), dim3(kWideGridThreads), 0, stream, Q, wide_part);
-            hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), wide_fin_lds, stream, Q,
-                               (const double *)wide_part, wblk, L.limit, wide_fin_lds);
-          }
-          MVC_HIP(hipGetLastError());
-          dbg("seq_wide (begin + lp/fin pairs)", c, s);
-        } else {
-          L.dyn = L.lds ? 8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D) +
-                               (L.lc == 2 ? (int64_t)kVpE * D : 0))
-                        : 0;
-          L.fill = lds_fill_byte();
-          L.chk = run_check() ? 1 : 0;
-          hipLaunchKernelGGL(L.lc ? (L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
-                                  : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
-                             dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, Q, L);
+    rr.early_mh = allow_early_mh && !early_mh_off && (!timers.on || timers.coarse);
+    if (rr.early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
+    rr.rounds = 1;
+  }
+  // The run kernel's dynamic LDS for layout L.
+  int64_t run_dyn(const SeqLds &L) const {
+    return L.lds ? 8 * (L.cache_dbl + L.stride * L.nws + (int64_t)L.ring * seq_ring_slot(V, D) +
+                        (L.lc == 2 ? (int64_t)kVpE * D : 0))
+                 : 0;
+  }
+  // The grid-wide evaluation where the state is on the global layout (L.lds = 0) and
+  // the block-wide evaluation applies (L.tw > 1): one customer over many CUs
+  bool run_wgrid(const SeqLds &L) const { return !repair_grid_only && wide_grid && L.lds == 0 && L.tw > 1; }
+  // rr.rounds repair rounds of one chain on its stream
+  void repair_rounds(Chain &c, uint32_t s, RepairRun &rr) {
+    const dim3 eb(256);
+    SeqLds &L = rr.L;
+    const bool wgrid = run_wgrid(L);
+    int wblk = 1;
+    if (wgrid) {
+      if (!wide_part) wide_part = dmalloc<double>((size_t)kWideGridMax * 2 * V);
+      // blocks for the dish list (plus the births a round may add): two 64-dish chunks per wave
+      int nk = 0;
+      for (int k : c.K) nk += k;
+      nk += nk / 4 + 64;
+      wblk = std::max(1, std::min(kWideGridMax, (nk + 2 * kWideGridThreads - 1) / (2 * kWideGridThreads)));
+    }
+    for (int r = 0; r < rr.rounds; ++r) {
+      if (repair_grid_only)
+        hipLaunchKernelGGL(mvc_seq_apply_kernel, dim3(1), dim3(256), 0, stream, rr.Q);
+      else if (wgrid) {
+        hipLaunchKernelGGL(mvc_seq_wide_begin_kernel, dim3(1), dim3(64), 0, stream, rr.Q);
+        for (int b = 0; b < kWideBatch; ++b) {
+          hipLaunchKernelGGL(mvc_seq_wide_lp_kernel, dim3(wblk), dim3(kWideGridThreads), 0, stream, rr.Q, wide_part);
+          hipLaunchKernelGGL(mvc_seq_wide_fin_kernel, dim3(1), dim3(kSeqRunThreads), wide_fin_lds, stream, rr.Q,
+                             (const double *)wide_part, wblk, L.limit, wide_fin_lds);
         }
         MVC_HIP(hipGetLastError());
-        dbg(repair_grid_only ? "seq_apply" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
-        if (L.lc && !repair_grid_only) {   // its loop leaves births pending
-          hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, Q);
-          MVC_HIP(hipGetLastError());
-          dbg("seq_birth", c, s);
-        }
-        hipLaunchKernelGGL(mvc_seq_eval_kernel, eg, eb, 0, stream, Q);
-        MVC_HIP(hipGetLastError());
-        dbg("seq_eval", c, s);
+        dbg("seq_wide (begin + lp/fin pairs)", c, s);
+      } else {
+        L.dyn = run_dyn(L);
+        L.fill = lds_fill_byte();
+        L.chk = run_check() ? 1 : 0;
+        hipLaunchKernelGGL(L.lc ? (L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
+                                : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
+                           dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, rr.Q, L);
       }
       MVC_HIP(hipGetLastError());
+      dbg(repair_grid_only ? "seq_apply" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
+      if (L.lc && !repair_grid_only) {   // a birth the loop left pending (overflow retry only: births commit in the kernel)
+        hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, rr.Q);
+        MVC_HIP(hipGetLastError());
+        dbg("seq_birth", c, s);
+      }
+      hipLaunchKernelGGL(mvc_seq_eval_kernel, rr.eg, eb, 0, stream, rr.Q);
+      MVC_HIP(hipGetLastError());
+      dbg("seq_eval", c, s);
+    }
+    MVC_HIP(hipGetLastError());
+  }
+  // Acts on a batch's outcome rs (read back): 0 run the same rounds again
+  // (after a capacity growth / relayout), 1 done, 2 more rounds.
+  int repair_outcome(Chain &c, uint32_t s, RepairRun &rr, const Repair &rs) {
+    if (rs.dbg[0]) {   // MVC_RUN_CHECK: a run kernel's index check failed
+      std::string v;
+      for (int k = 1; k < 8; ++k) v += " " + std::to_string(rs.dbg[k]);
+      throw Error(MVC_ERR_STATE, "run kernel index check " + std::to_string(rs.dbg[0]) + " failed (chain " +
+                                     std::to_string(c.gid) + ", sweep " + std::to_string(s) + ", lc " +
+                                     std::to_string(rr.L.lc) + "):" + v);
+    }
+    if (rs.overflow) {
+      grow_capacity(rs.overflow);
+      rr.Q = make_seq(c, s);
+      rr.eg = dim3(seq_waves / 4);   // the scratch may have fewer slots now
+      return 0;
+    }
+    if (rs.vpoff && rr.vp_ok) {   // predictions missed (or a dish list outgrew them): plain lane columns
+      rr.vp_ok = false;
+      if (rr.L.lc == 2) rr.L.lc = 1;
+    }
+    if (rs.restride) {
+      rr.L = run_layout(rs.T, rs.Klist, rr.vp_ok);
+      MVC_HIP(hipMemsetAsync(&c.R->restride, 0, sizeof(int32_t), stream));
+      return 0;
+    }
+    if (rs.done) return 1;
+    rr.rounds = std::min(rr.rounds * 4, 1024);
+    return 2;
+  }
+  void repair_finish(Chain &c, uint32_t s, RepairRun &rr, const Repair &rs, bool sync_status = true) {
+    const bool moved = rs.moves > 0;
+    if (moved) {
+      hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, rr.Q, c.pos_new, c.jmap);
+      hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
+                         stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
+      MVC_HIP(hipGetLastError());
+      dbg("seq_compact + relabel", c, s, false);
+    }
+    timers.end("repair", rr.e1);
+#ifdef MVC_RUN_PROF
+    fprintf(stderr, "runprof moves %d iters %llu | lc: views %.2f tables+weights %.2f draw %.2f | commit %.2f check %.2f spec %.2f decide %.2f (us per iter)\n",
+            rs.moves, rs.prof[7], rs.prof[0] * 0.01 / std::max(1ull, rs.prof[7]),
+            rs.prof[1] * 0.01 / std::max(1ull, rs.prof[7]), rs.prof[2] * 0.01 / std::max(1ull, rs.prof[7]),
+            rs.prof[3] * 0.01 / std::max(1ull, rs.prof[7]), rs.prof[4] * 0.01 / std::max(1ull, rs.prof[7]),
+            rs.prof[5] * 0.01 / std::max(1ull, rs.prof[7]), rs.prof[6] * 0.01 / std::max(1ull, rs.prof[7]));
+    fprintf(stderr, "runprof decided %llu same-as-phase-A %llu | movers %llu same-as-phase-A %llu\n", rs.prof[8],
+            rs.prof[9], rs.prof[10], rs.prof[11]);
+    if (rs.prof[18] + rs.prof[19]) {
+      const double nd = (double)std::max(1ull, rs.prof[18]), nc = (double)std::max(1ull, rs.prof[19]);
+      fprintf(stderr, "wideprof decided %llu commits %llu | combine %.2f lm %.2f tables %.2f weights %.2f draw %.2f (us per decided) "
+              "commit %.2f (us per commit)\n", rs.prof[18], rs.prof[19], rs.prof[12] * 0.01 / nd,
+              rs.prof[13] * 0.01 / nd, rs.prof[14] * 0.01 / nd, rs.prof[15] * 0.01 / nd,
+              rs.prof[16] * 0.01 / nd, rs.prof[17] * 0.01 / nc);
+      fprintf(stderr, "wideprof effective shader clock %.0f MHz (%llu clocks over %llu ticks of 100 MHz)\n",
+              rs.prof[20] ? 100.0 * (double)rs.prof[21] / (double)rs.prof[20] : 0.0, rs.prof[21],
+              rs.prof[20]);
+    }
+#endif
+    if (vp_stats)   // MVC_VP_STATS=1: value prediction's steps and full hits of this sweep, on stderr
+      fprintf(stderr, "mvc vp steps %d hits %d off %d\n", rs.vpsteps, rs.vphits, rs.vpoff);
+    c.last[0] = rs.moves;
+    c.last[1] = rs.births;
+    c.last[2] = rs.rounds;
+    c.last[3] = rs.newdish;
+    if (!(rr.early_mh && !moved)) launch_hyper(c, 1, s);   // else the gated launch above ran it
+    if (moved) {   // new T and dish counts for the next sweep's launch shapes
+      MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
+      if (sync_status) repair_status(c);
+      else status_pending = true;
+    }
+  }
+  bool status_pending = false;
+  Repair last_rs{};                // the chain-batched sweep's final outcome of this chain
+  // the next sweep's launch shapes from the status copied back by repair_finish
+  void repair_status(Chain &c) {
+    MVC_HIP(hipStreamSynchronize(stream));
+    status_pending = false;
+    c.T = st_host[0];
+    for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
+    tile_s1(c);   // S1 changed: the next phase A's MFMA B-fragments
+  }
+  void repair(Chain &c, uint32_t s, bool phaseA) {
+    RepairRun rr;
+    repair_start(c, s, phaseA, rr);
+    for (;;) {
+      repair_rounds(c, s, rr);
       MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
-      if (early_mh) {
+      if (rr.early_mh) {
         // the MH goes into the stream behind the copy, gated on the device by
         // the repair's outcome (it runs iff the repair is done with no move),
         // so the GPU runs it while the host waits for the copy and decides the
@@ -3187,73 +3303,9 @@ class ParallelSampler : public Sampler {
       } else {
         MVC_HIP(hipStreamSynchronize(stream));
       }
-      if (rs_host->dbg[0]) {   // MVC_RUN_CHECK: a run kernel's index check failed
-        std::string v;
-        for (int k = 1; k < 8; ++k) v += " " + std::to_string(rs_host->dbg[k]);
-        throw Error(MVC_ERR_STATE, "run kernel index check " + std::to_string(rs_host->dbg[0]) + " failed (chain " +
-                                       std::to_string(c.gid) + ", sweep " + std::to_string(s) + ", lc " +
-                                       std::to_string(L.lc) + "):" + v);
-      }
-      if (rs_host->overflow) {
-        grow_capacity(rs_host->overflow);
-        Q = make_seq(c, s);
-        eg = dim3(seq_waves / 4);   // the scratch may have fewer slots now
-        continue;
-      }
-      if (rs_host->vpoff && vp_ok) {   // predictions missed (or a dish list outgrew them): plain lane columns
-        vp_ok = false;
-        if (L.lc == 2) L.lc = 1;
-      }
-      if (rs_host->restride) {
-        L = run_layout(rs_host->T, rs_host->Klist, vp_ok);
-        MVC_HIP(hipMemsetAsync(&c.R->restride, 0, sizeof(int32_t), stream));
-        continue;
-      }
-      if (rs_host->done) break;
-      rounds = std::min(rounds * 4, 1024);
+      if (repair_outcome(c, s, rr, *rs_host) == 1) break;
     }
-    const bool moved = rs_host->moves > 0;
-    if (moved) {
-      hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, Q, c.pos_new, c.jmap);
-      hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
-                         stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
-      MVC_HIP(hipGetLastError());
-      dbg("seq_compact + relabel", c, s, false);
-    }
-    timers.end("repair", e1);
-#ifdef MVC_RUN_PROF
-    fprintf(stderr, "runprof moves %d iters %llu | lc: views %.2f tables+weights %.2f draw %.2f | commit %.2f check %.2f spec %.2f decide %.2f (us per iter)\n",
-            rs_host->moves, rs_host->prof[7], rs_host->prof[0] * 0.01 / std::max(1ull, rs_host->prof[7]),
-            rs_host->prof[1] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[2] * 0.01 / std::max(1ull, rs_host->prof[7]),
-            rs_host->prof[3] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[4] * 0.01 / std::max(1ull, rs_host->prof[7]),
-            rs_host->prof[5] * 0.01 / std::max(1ull, rs_host->prof[7]), rs_host->prof[6] * 0.01 / std::max(1ull, rs_host->prof[7]));
-    fprintf(stderr, "runprof decided %llu same-as-phase-A %llu | movers %llu same-as-phase-A %llu\n", rs_host->prof[8],
-            rs_host->prof[9], rs_host->prof[10], rs_host->prof[11]);
-    if (rs_host->prof[18] + rs_host->prof[19]) {
-      const double nd = (double)std::max(1ull, rs_host->prof[18]), nc = (double)std::max(1ull, rs_host->prof[19]);
-      fprintf(stderr, "wideprof decided %llu commits %llu | combine %.2f lm %.2f tables %.2f weights %.2f draw %.2f (us per decided) "
-              "commit %.2f (us per commit)\n", rs_host->prof[18], rs_host->prof[19], rs_host->prof[12] * 0.01 / nd,
-              rs_host->prof[13] * 0.01 / nd, rs_host->prof[14] * 0.01 / nd, rs_host->prof[15] * 0.01 / nd,
-              rs_host->prof[16] * 0.01 / nd, rs_host->prof[17] * 0.01 / nc);
-      fprintf(stderr, "wideprof effective shader clock %.0f MHz (%llu clocks over %llu ticks of 100 MHz)\n",
-              rs_host->prof[20] ? 100.0 * (double)rs_host->prof[21] / (double)rs_host->prof[20] : 0.0, rs_host->prof[21],
-              rs_host->prof[20]);
-    }
-#endif
-    if (vp_stats)   // MVC_VP_STATS=1: value prediction's steps and full hits of this sweep, on stderr
-      fprintf(stderr, "mvc vp steps %d hits %d off %d\n", rs_host->vpsteps, rs_host->vphits, rs_host->vpoff);
-    c.last[0] = rs_host->moves;
-    c.last[1] = rs_host->births;
-    c.last[2] = rs_host->rounds;
-    c.last[3] = rs_host->newdish;
-    if (!(early_mh && !moved)) launch_hyper(c, 1, s);   // else the gated launch above ran it
-    if (moved) {   // new T and dish counts for the next sweep's launch shapes
-      MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
-      MVC_HIP(hipStreamSynchronize(stream));
-      c.T = st_host[0];
-      for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
-      tile_s1(c);   // S1 changed: the next phase A's MFMA B-fragments
-    }
+    repair_finish(c, s, rr, *rs_host);
   }
 
   // Double the table (flags & 1) and/or dish (flags & 2) capacity of every
@@ -3506,6 +3558,7 @@ class ChainSet : public Sampler {
     stream = subs[0]->stream;
   }
   ~ChainSet() override {
+    batch_free();
     while (!subs.empty()) subs.pop_back();   // the data owner (chain 0) last
   }
   template <class F>
@@ -3534,9 +3587,194 @@ class ChainSet : public Sampler {
       s->timers.on = timers.on;
       s->timers.coarse = timers.coarse;
     }
-    each([&](ParallelSampler &s) { s.sweep(n_sweeps); });
+    if (batch_on) {
+      for (int it = 0; it < n_sweeps; ++it) sweep_batched();
+    } else {
+      each([&](ParallelSampler &s) { s.sweep(n_sweeps); });
+    }
     sweeps_done += n_sweeps;
     zpath = subs[0]->zpath;
+  }
+
+  // ---- the chain-batched sweep ----
+  // Phase A of every chain on its own stream; then the in-order repair of all
+  // chains as batched launches on one stream (the run kernel with one block
+  // per chain, the window evaluation with a block range per chain) and one
+  // read-back of all chains' outcomes per batch of rounds; then compaction
+  // and the MH of every chain on its stream.  The same kernels run on the same
+  // state as a chain swept alone, so every chain is the same chain, bit for bit;
+  // concurrency no longer needs a hardware queue per chain.
+  bool batch_on = [] {
+    const char *e = getenv("MVC_CHAIN_BATCH");   // =0: one host thread and stream per chain
+    return !(e && e[0] == '0');
+  }();
+  SeqArgs *bA_dev = nullptr, *bA_host = nullptr, *bE_dev = nullptr, *bE_host = nullptr;
+  SeqLds *bL_dev = nullptr, *bL_host = nullptr;
+  Repair *bR_dev = nullptr, *bR_host = nullptr;
+  std::vector<hipEvent_t> b_ev;
+  hipEvent_t b_join = nullptr;
+  void batch_alloc() {
+    if (bA_dev) return;
+    const size_t C = subs.size();
+    MVC_HIP(hipMalloc(&bA_dev, sizeof(SeqArgs) * C));
+    MVC_HIP(hipMalloc(&bE_dev, sizeof(SeqArgs) * C));
+    MVC_HIP(hipMalloc(&bL_dev, sizeof(SeqLds) * C));
+    MVC_HIP(hipMalloc(&bR_dev, sizeof(Repair) * C));
+    MVC_HIP(hipHostMalloc((void **)&bA_host, sizeof(SeqArgs) * C, hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&bE_host, sizeof(SeqArgs) * C, hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&bL_host, sizeof(SeqLds) * C, hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&bR_host, sizeof(Repair) * C, hipHostMallocDefault));
+    b_ev.assign(C, nullptr);
+    for (auto &e : b_ev) MVC_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    MVC_HIP(hipEventCreateWithFlags(&b_join, hipEventDisableTiming));
+  }
+  void batch_free() {
+    if (!bA_dev) return;
+    for (void *p : {(void *)bA_dev, (void *)bE_dev, (void *)bL_dev, (void *)bR_dev}) hipFree(p);
+    for (void *p : {(void *)bA_host, (void *)bE_host, (void *)bL_host, (void *)bR_host}) hipHostFree(p);
+    for (auto &e : b_ev) hipEventDestroy(e);
+    hipEventDestroy(b_join);
+    bA_dev = nullptr;
+  }
+  void sweep_batched() {
+    batch_alloc();
+    const int C = (int)subs.size();
+    hipStream_t bs = subs[0]->stream;   // the batch stream
+    std::vector<ParallelSampler::RepairRun> rr(C);
+    std::vector<char> done(C, 0);
+    // 1. phase A and the first mover, every chain on its own stream
+    for (int c = 0; c < C; ++c) {
+      ParallelSampler &S = *subs[c];
+      auto &ch = S.chains[0];
+      const uint32_t s = (uint32_t)S.sweeps_done;
+      bool phaseA = false;
+      S.sweep_pre(ch, s, phaseA);
+      S.repair_start(ch, s, phaseA, rr[c], false);
+      if (c > 0) {
+        MVC_HIP(hipEventRecord(b_ev[c], S.stream));
+        MVC_HIP(hipStreamWaitEvent(bs, b_ev[c], 0));
+      }
+    }
+    // 2. rounds of every unfinished chain, batched by run-kernel instance
+    for (;;) {
+      std::vector<int> act;
+      for (int c = 0; c < C; ++c)
+        if (!done[c]) act.push_back(c);
+      if (act.empty()) break;
+      int rounds = 1, bpc = 1 << 30;
+      for (int c : act) {
+        rounds = std::max(rounds, rr[c].rounds);
+        bpc = std::min(bpc, std::max(1, subs[c]->seq_waves / 4));
+      }
+      // the instances: 4 / 3 lane columns (+ value prediction), 0 one wave per
+      // customer, 2 the block-wide evaluation; -1 launched per chain (grid-wide
+      // evaluation, grid-only repair)
+      std::vector<int> kinds(C, -1);
+      for (int c : act) {
+        const ParallelSampler &S = *subs[c];
+        const SeqLds &L = rr[c].L;
+        kinds[c] = (S.repair_grid_only || S.run_wgrid(L)) ? -1 : L.lc == 2 ? 4 : L.lc ? 3 : L.tw == 1 ? 0 : 2;
+      }
+      int nb = 0;   // batched members, grouped by kind
+      std::vector<std::pair<int, int>> groups;   // (kind, first index), each up to the next
+      std::vector<size_t> dyn;
+      for (int k : {4, 3, 0, 2}) {
+        const int first = nb;
+        size_t dmax = 0;
+        for (int c : act) {
+          if (kinds[c] != k) continue;
+          ParallelSampler &S = *subs[c];
+          SeqLds &L = rr[c].L;
+          L.dyn = S.run_dyn(L);
+          L.fill = lds_fill_byte();
+          L.chk = run_check() ? 1 : 0;
+          bA_host[nb] = rr[c].Q;
+          bL_host[nb] = L;
+          dmax = std::max(dmax, (size_t)L.dyn);
+          ++nb;
+        }
+        if (nb > first) {
+          groups.push_back({k, first});
+          dyn.push_back(dmax);
+        }
+      }
+      // every active chain's arguments for the window evaluation (its wave
+      // stride set to the batched grid's) and the outcome gather
+      for (size_t j = 0; j < act.size(); ++j) {
+        bE_host[j] = rr[act[j]].Q;
+        bE_host[j].G = 4 * bpc;
+      }
+      if (nb) {
+        MVC_HIP(hipMemcpyAsync(bA_dev, bA_host, sizeof(SeqArgs) * nb, hipMemcpyHostToDevice, bs));
+        MVC_HIP(hipMemcpyAsync(bL_dev, bL_host, sizeof(SeqLds) * nb, hipMemcpyHostToDevice, bs));
+      }
+      MVC_HIP(hipMemcpyAsync(bE_dev, bE_host, sizeof(SeqArgs) * act.size(), hipMemcpyHostToDevice, bs));
+      // the chains launched one by one run on their own streams after the batch stream's work so far
+      bool any_single = false;
+      for (int c : act)
+        if (kinds[c] < 0) any_single = true;
+      if (any_single) MVC_HIP(hipEventRecord(b_join, bs));
+      for (int r = 0; r < rounds; ++r) {
+        for (size_t g = 0; g < groups.size(); ++g) {
+          const int k = groups[g].first, f = groups[g].second;
+          const int m = (g + 1 < groups.size() ? groups[g + 1].second : nb) - f;
+          const dim3 grid(m);
+          const SeqArgs *a = bA_dev + f;
+          const SeqLds *l = bL_dev + f;
+          switch (k) {
+            case 4: hipLaunchKernelGGL(mvc_seq_run_kernel_b<4>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
+            case 3: hipLaunchKernelGGL(mvc_seq_run_kernel_b<3>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
+            case 0: hipLaunchKernelGGL(mvc_seq_run_kernel_b<0>, grid, dim3(kSeqRunThreads), dyn[g], bs, a, l); break;
+            default: hipLaunchKernelGGL(mvc_seq_run_kernel_b<2>, grid, dim3(kSeqRunThreads), dyn[g], bs, a, l); break;
+          }
+          MVC_HIP(hipGetLastError());
+        }
+        hipLaunchKernelGGL(mvc_seq_eval_kernel_b, dim3((unsigned)(act.size() * bpc)), dim3(256), 0, bs,
+                           (const SeqArgs *)bE_dev, bpc);
+        MVC_HIP(hipGetLastError());
+      }
+      for (int c : act) {   // the others, one by one on their streams
+        if (kinds[c] >= 0) continue;
+        ParallelSampler &S = *subs[c];
+        MVC_HIP(hipStreamWaitEvent(S.stream, b_join, 0));
+        const int keep = rr[c].rounds;
+        rr[c].rounds = rounds;
+        S.repair_rounds(S.chains[0], (uint32_t)S.sweeps_done, rr[c]);
+        rr[c].rounds = keep;
+        MVC_HIP(hipEventRecord(b_ev[c], S.stream));
+        MVC_HIP(hipStreamWaitEvent(bs, b_ev[c], 0));
+      }
+      // every chain's outcome in one copy
+      hipLaunchKernelGGL(mvc_seq_gather_repair_kernel, dim3((unsigned)act.size()), dim3(64), 0, bs,
+                         (const SeqArgs *)bE_dev, bR_dev);
+      MVC_HIP(hipGetLastError());
+      MVC_HIP(hipMemcpyAsync(bR_host, bR_dev, sizeof(Repair) * act.size(), hipMemcpyDeviceToHost, bs));
+      MVC_HIP(hipStreamSynchronize(bs));
+      for (size_t j = 0; j < act.size(); ++j) {
+        const int c = act[j];
+        ParallelSampler &S = *subs[c];
+        rr[c].rounds = rounds;
+        const int res = S.repair_outcome(S.chains[0], (uint32_t)S.sweeps_done, rr[c], bR_host[j]);
+        if (res == 1) {
+          done[c] = 1;
+          S.last_rs = bR_host[j];
+        } else if (res == 0) {
+          MVC_HIP(hipStreamSynchronize(S.stream));   // (a relayout's reset on the chain's stream)
+        }
+      }
+    }
+    // 3. compaction and the MH of every chain, on its stream after the batch
+    MVC_HIP(hipEventRecord(b_join, bs));
+    for (int c = 0; c < C; ++c) {
+      ParallelSampler &S = *subs[c];
+      if (c > 0) MVC_HIP(hipStreamWaitEvent(S.stream, b_join, 0));
+      S.repair_finish(S.chains[0], (uint32_t)S.sweeps_done, rr[c], S.last_rs, false);
+    }
+    for (int c = 0; c < C; ++c) {
+      ParallelSampler &S = *subs[c];
+      if (S.status_pending) S.repair_status(S.chains[0]);
+      S.sweeps_done += 1;
+    }
   }
   void synchronize() override {
     for (auto &s : subs) s->synchronize();

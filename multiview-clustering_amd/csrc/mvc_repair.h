@@ -3737,7 +3737,7 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
 // One instance per evaluation shape, compiled separately so each keeps its
 // own register allocation.
 template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc); 4: + value prediction
-__global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
+__device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, w = tid >> 6, nt = blockDim.x;
@@ -3918,12 +3918,26 @@ __global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void m
   }
 }
 
+template <int kMode>
+__global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
+  seq_run_body<kMode>(A, L);
+}
+// The same for several chains at once (one block per chain, its arguments
+// and LDS layout from device arrays): the chain-batched repair of a handle's
+// chains, one launch per round instead of one stream and launch per chain.
+template <int kMode>
+__global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel_b(const SeqArgs *As,
+                                                                                                 const SeqLds *Ls) {
+  SeqArgs A = As[blockIdx.x];
+  const SeqLds L = Ls[blockIdx.x];
+  seq_run_body<kMode>(A, L);
+}
+
 // The exact conditional of every customer of the pending window against the
 // current state, one wavefront per customer; the first mover by atomicMin.
-extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel(SeqArgs A) {
+__device__ __forceinline__ void seq_eval_body(const SeqArgs &A, int gw) {
   Repair *R = A.R;
   const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (R->done || R->overflow || R->restride) return;
   const int w0 = R->win0, w1 = R->win1;
   if (w1 <= w0) return;
@@ -3939,6 +3953,20 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel(SeqArgs A)
       if (c != p0) atomicMin(&R->fmin, i);
     }
   }
+}
+extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel(SeqArgs A) {
+  seq_eval_body(A, blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+}
+// Every batched chain's repair state into one array (one read-back per batch).
+extern "C" __global__ void mvc_seq_gather_repair_kernel(const SeqArgs *As, Repair *out) {
+  const uint32_t *src = (const uint32_t *)As[blockIdx.x].R;
+  uint32_t *dst = (uint32_t *)(out + blockIdx.x);
+  for (int k = threadIdx.x; k < (int)(sizeof(Repair) / 4); k += blockDim.x) dst[k] = src[k];
+}
+// Batched: bpc blocks per chain, chain = blockIdx.x / bpc.
+extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel_b(const SeqArgs *As, int bpc) {
+  const SeqArgs A = As[blockIdx.x / bpc];
+  seq_eval_body(A, (blockIdx.x % bpc) * (blockDim.x >> 6) + (threadIdx.x >> 6));
 }
 
 // After the last repair step of a sweep that moved someone: drop dead tables

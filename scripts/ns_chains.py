@@ -1,14 +1,14 @@
 """North-star literal (N = 1M, V = 4, D = 1, K = 64) with C chains on one GPU
-at once (ChainSet: one stream and host thread per chain): one
-sweep from the generating partition, aggregate chain-sweeps/s and device
-memory per chain.  Usage: python scripts/ns_chains.py C [C ...]"""
+at once (ChainSet, DESIGN.md §7: the chain-batched repair by default;
+MVC_CHAIN_BATCH=0 one stream and host thread per chain, which needs
+GPU_MAX_HW_QUEUES >= C): one sweep from the generating partition, aggregate
+chain-sweeps/s.  Usage: python scripts/ns_chains.py C [C ...]"""
 import json
 import os
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["GPU_MAX_HW_QUEUES"] = "32"   # C concurrent chains, one stream each; before HIP starts
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
 
 import bench  # noqa: E402
@@ -31,7 +31,9 @@ def main():
         dt = time.perf_counter() - t0
         s.close()
         print(json.dumps({"workload": desc.replace("1 chain/GPU", f"{C} chains on 1 GPU"), "chains": C,
-                          "sweep_s": round(dt, 2), "chain_sweeps_per_s": round(C / dt, 3)}), flush=True)
+                          "sweep_s": round(dt, 2), "chain_sweeps_per_s": round(C / dt, 3),
+                          "batched": os.environ.get("MVC_CHAIN_BATCH", "1") != "0",
+                          "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}), flush=True)
 
 
 if __name__ == "__main__":

@@ -659,32 +659,43 @@ import mvc_amd as m
 from mvc_amd import data
 y, _ = data.new_simulation(1999)
 C, M = 4, 8
-conc = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
+conc = m.Sampler(y, seed=21, mode="parallel", n_chains=C)          # chain-batched repair (default)
 conc.sweep(M)
-os.environ["MVC_CHAIN_THREADS"] = "0"
+os.environ["MVC_CHAIN_BATCH"] = "0"                               # one host thread and stream per chain
+thr = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
+thr.sweep(M)
+del os.environ["MVC_CHAIN_BATCH"]
+os.environ["MVC_CHAIN_THREADS"] = "0"                             # one handle, chains one after another
 ser = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
 ser.sweep(M)
 del os.environ["MVC_CHAIN_THREADS"]
+# batched with capacity growth inside the batch (16 tables, 15 dishes at the start)
+grow = m.Sampler(y, seed=21, mode="parallel", n_chains=C, table_cap=16, dish_cap=15)
+for _ in range(M):
+    grow.sweep(1)
+assert max(grow.state(chain=c)[1].shape[1] for c in range(C)) > 16
 for c in range(C):
     one = m.Sampler(y, seed=21, mode="parallel", first_chain=c)
     one.sweep(M)
     t1, d1, h1 = one.state()
-    for s in (conc, ser):
+    for s in (conc, thr, ser, grow):
         t, d, h = s.state(chain=c)
         assert np.array_equal(t, t1) and np.array_equal(d, d1), c
         assert h["sigma_global"] == h1["sigma_global"] and np.array_equal(h["tau_v"], h1["tau_v"])
     one.close()
-conc.close()
-ser.close()
+for s in (conc, thr, ser, grow):
+    s.close()
 print("chains OK")
 """
 
 
 def test_chains_concurrent_equal_serial():
-    """Several chains in one handle run concurrently (ChainSet: a stream and a
-    host thread per chain, shared device data); every chain equals the same
-    chain run alone (first_chain = c) and the serial loop (MVC_CHAIN_THREADS=0),
-    bit for bit, through a cold start with births."""
+    """Several chains in one handle (ChainSet, shared device data): the
+    chain-batched repair (one launch per round for all chains), the per-chain
+    streams and host threads (MVC_CHAIN_BATCH=0) and the serial loop
+    (MVC_CHAIN_THREADS=0) all equal the same chain run alone (first_chain =
+    c), bit for bit, through a cold start with births, also when the batch
+    grows the chains' capacities."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
