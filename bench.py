@@ -32,18 +32,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
 
-# The legs that run many chains at once (one HIP stream each) run in a child
-# process with GPU_MAX_HW_QUEUES = 32 (child_leg): HIP maps a process's
-# streams onto that many hardware queues (4 by default, and the GPU pool's
-# environment sets 4), beyond which streams share queues and their kernels
-# serialise.  Not in this process: once many queues are live,
-# every later launch-heavy leg runs slower (configs[1] cold sweep 0: 0.97 s
-# alone, 1.44 s after a 16-stream run, r3r), so the headline and the
-# single-chain legs keep the caller's setting.
-HW_QUEUES_MULTI = "32"
-# the caller's setting, recorded before the library loads (mvc_amd's loader
-# sets 32 when the variable is unset); the other legs run with it, or with
-# HIP's own default of 4 when the caller set none
+# Every GPU leg runs in a child process (child_leg) with the caller's
+# GPU_MAX_HW_QUEUES (HIP's default of 4 when unset): the multi-chain legs use
+# the chain-batched repair, which needs no hardware queue per chain
+# (DESIGN.md §7).  The value is recorded before the library loads.
 CALLER_HW_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")
 
 import numpy as np  # noqa: E402
@@ -191,11 +183,11 @@ def gpu_line(config, seed, device, steps=10, warmup=3):
             "moves_last_sweep": rep["moves"]}
 
 
-def gpu_chains_line(config, seed, device, chains=16, sweeps=1):
-    """Several chains of one config on one GPU at once (parallel-mode ChainSet:
-    one stream and host thread per chain, the data shared), warm
-    start at the generating partition: aggregate chain-sweeps/s.  Run through
-    child_leg (a process with 32 hardware queues), so the 16 chains overlap."""
+def gpu_chains_line(config, seed, device, chains=64, sweeps=1):
+    """Several chains of one config on one GPU at once (parallel-mode ChainSet,
+    the data shared; the chain-batched repair: one block per chain in each
+    repair launch), warm start at the generating partition:
+    aggregate chain-sweeps/s, with HIP's default hardware queues."""
     from mvc_amd import data
     from mvc_amd.sampler import Sampler
     N, V, D, K, desc = CONFIGS[config]
@@ -331,29 +323,25 @@ def newsim_chains_line(seed, device):
 
 
 CHILD_LEGS = {
-    # name: (function(seed, device) -> dict, needs many hardware queues)
-    "north_star_literal_gpu": (lambda seed, dev: gpu_line("ns", seed, dev, 1, 0), False),
-    "north_star_literal_gpu_16chains": (lambda seed, dev: gpu_chains_line("ns", seed, dev), True),
-    "configs1_gpu": (lambda seed, dev: gpu_line("c2", seed, dev), False),
-    "configs4_full_gpu": (lambda seed, dev: config5_line(seed, dev), False),
-    "exact_schedule_gpu": (lambda seed, dev: gpu_exact_line(seed, dev), False),
-    "newsim_call": (lambda seed, dev: newsim_call_line(seed, dev), False),
-    # HIP's default hardware queues: at N = 200 the launches are short and 32 queues
-    # halved these chains' throughput (r4v bench vs the leg alone, r4x / r4y)
-    "newsim_chains": (lambda seed, dev: newsim_chains_line(seed, dev), False),
-    "cold_start_gpu": (lambda seed, dev: cold_start(seed, dev), False),
+    # name: function(seed, device) -> dict
+    "north_star_literal_gpu": lambda seed, dev: gpu_line("ns", seed, dev, 1, 0),
+    "north_star_literal_gpu_64chains": lambda seed, dev: gpu_chains_line("ns", seed, dev, chains=64),
+    "configs1_gpu": lambda seed, dev: gpu_line("c2", seed, dev),
+    "configs4_full_gpu": lambda seed, dev: config5_line(seed, dev),
+    "exact_schedule_gpu": lambda seed, dev: gpu_exact_line(seed, dev),
+    "newsim_call": lambda seed, dev: newsim_call_line(seed, dev),
+    "newsim_chains": lambda seed, dev: newsim_chains_line(seed, dev),
+    "cold_start_gpu": lambda seed, dev: cold_start(seed, dev),
 }
 
 
 def child_leg(name, seed, device, timeout=300):
-    """Run CHILD_LEGS[name] in a child process (its own HIP runtime; 32
-    hardware queues for the multi-chain legs).  Never raises: a leg that
+    """Run CHILD_LEGS[name] in a child process (its own HIP runtime).  Never raises: a leg that
     fails, faults or times out is recorded as {"error": ...}, so no extra
     leg can take the headline line with it."""
     import subprocess
     env = dict(os.environ)
-    env["GPU_MAX_HW_QUEUES"] = (HW_QUEUES_MULTI if CHILD_LEGS[name][1] else
-                                CALLER_HW_QUEUES if CALLER_HW_QUEUES is not None else "4")
+    env["GPU_MAX_HW_QUEUES"] = CALLER_HW_QUEUES if CALLER_HW_QUEUES is not None else "4"
     t = time.perf_counter()
     try:
         r = subprocess.run([sys.executable, os.path.abspath(__file__), "--leg", name, "--seed", str(seed),
@@ -410,7 +398,7 @@ def cold_start(seed, device, sweeps=4):
 def main():
     args = parse()
     if args.leg:   # a child_leg process: one multi-chain leg, one JSON line
-        print(json.dumps(CHILD_LEGS[args.leg][0](args.seed, args.leg_device)), flush=True)
+        print(json.dumps(CHILD_LEGS[args.leg](args.seed, args.leg_device)), flush=True)
         return
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -588,7 +576,7 @@ def main():
             ex["reference_schedule_cpu"] = leg("reference_schedule_cpu", reference_schedule_cpu, args.seed)
             ex["newsim_call"]["reference_cpu_1core"] = leg("newsim_call_cpu", newsim_call_cpu, args.seed)
             try:   # the chains' comparator: min(chains, nproc) host cores, one chain each
-                ch = ex["north_star_literal_gpu_16chains"]
+                ch = ex["north_star_literal_gpu_64chains"]
                 ref1 = ex["reference_schedule_cpu"]["value"]
                 cores = min(ch["chains"], os.cpu_count() or 1)
                 ch["cpu_cores_compared"] = cores

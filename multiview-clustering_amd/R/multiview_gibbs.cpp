@@ -78,9 +78,8 @@ const Api &api() {
   static bool ready = false;
   if (ready) return a;
   const char *path = std::getenv("MVC_HIP_LIB");
-  // hardware queues for concurrent chains: HIP reads this once,
-  // when it starts, which is while the library loads; a value the user set is kept
-  if (env_int("GPU_MAX_HW_QUEUES", -1) < 0) setenv("GPU_MAX_HW_QUEUES", "32", 1);
+  // (no hardware-queue request: the chains of one call share a stream for
+  // their repair, so HIP's default queues serve them)
   void *h = dlopen(path ? path : "libmvc_hip.so", RTLD_NOW | RTLD_LOCAL);
   if (!h) Rcpp::stop(std::string("cannot load libmvc_hip.so: ") + dlerror());
   bind(h, "mvc_config_init", a.config_init);

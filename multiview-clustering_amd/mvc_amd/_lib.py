@@ -57,16 +57,6 @@ class Config(ctypes.Structure):
 
 
 _lib = None
-HW_QUEUES = 32   # hardware queues requested for concurrent chains (the GPU pool allows at most 32)
-
-
-def hw_queues(value):
-    """GPU_MAX_HW_QUEUES to run with: the user's value when it is an integer,
-    else HW_QUEUES (unset, empty or unparsable counts as unset)."""
-    try:
-        return int(str(value).strip()) if value is not None else HW_QUEUES
-    except ValueError:
-        return HW_QUEUES
 
 
 def lib():
@@ -77,13 +67,9 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise FileNotFoundError(
             f"{LIB_PATH} not found: build the HIP extension first (make, or __graft_entry__.build())")
-    # Concurrent chains (parallel mode, one stream each) overlap only as far
-    # as HIP gives the process hardware queues: GPU_MAX_HW_QUEUES, 4 by
-    # default, read once when HIP starts (at the latest while this library's
-    # kernels register at load).  Ask for 32 only when the variable is unset
-    # (or not an integer): a value the user chose is kept; a process that
-    # started HIP earlier keeps its own.
-    os.environ["GPU_MAX_HW_QUEUES"] = str(hw_queues(os.environ.get("GPU_MAX_HW_QUEUES")))
+    # No hardware-queue request: a handle's chains share one stream for
+    # their repair (the chain-batched repair), so HIP's default
+    # of 4 queues serves them; GPU_MAX_HW_QUEUES is left as the caller set it.
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u32, u64, sz = (ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint32,
                                   ctypes.c_uint64, ctypes.c_size_t)

@@ -14,7 +14,7 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multiview-clustering_amd")]
-os.environ["GPU_MAX_HW_QUEUES"] = "32"   # 8 concurrent chains, one stream each; before HIP starts
+
 
 import numpy as np  # noqa: E402
 

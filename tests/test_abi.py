@@ -12,6 +12,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "mvc.h")
+PKG = os.path.join(ROOT, "multiview-clustering_amd")
 
 
 @pytest.fixture(scope="module")
@@ -72,10 +73,17 @@ def test_shard_callback_returns_a_status(lib):
     assert "int (*all_gather)(void *)" in open(HEADER).read()
 
 
-def test_hw_queue_request_keeps_a_user_setting(lib):
-    assert lib.hw_queues(None) == lib.HW_QUEUES
-    assert lib.hw_queues("4") == 4 and lib.hw_queues(" 8 ") == 8
-    assert lib.hw_queues("") == lib.HW_QUEUES and lib.hw_queues("many") == lib.HW_QUEUES
+def test_loaders_leave_the_hardware_queues_alone(lib):
+    """The chain-batched repair needs no hardware queue per chain: neither the
+    Python loader nor the Rcpp drop-in sets GPU_MAX_HW_QUEUES any more."""
+    import subprocess
+    import sys
+    code = ("import os, sys; sys.path[:0] = [%r, %r]; os.environ.pop('GPU_MAX_HW_QUEUES', None); "
+            "import mvc_amd; mvc_amd.lib(); print(os.environ.get('GPU_MAX_HW_QUEUES'))" % (ROOT, PKG))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().splitlines()[-1] == "None", r.stderr[-800:]
+    src = open(os.path.join(PKG, "R", "multiview_gibbs.cpp")).read()
+    assert 'setenv("GPU_MAX_HW_QUEUES"' not in src
 
 
 def _call_run(lib, cfg, y):
