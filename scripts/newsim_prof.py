@@ -18,3 +18,14 @@ t0 = time.perf_counter()
 mvc_amd.run_gibbs_cpp(y, M, M - 1, 1, seed=1999, mode=mode, quiet=True)
 dt = time.perf_counter() - t0
 print(f"newsim {mode}: {M} sweeps in {dt:.3f} s = {M / dt:.1f} sweeps/s", flush=True)
+
+# the repair's counters per sweep (rounds = run-kernel passes) on a handle
+from mvc_amd.sampler import Sampler  # noqa: E402
+s = Sampler(y, seed=1999, mode=mode)
+s.sweep(300)
+rows = []
+for _ in range(8):
+    s.sweep(1)
+    rows.append(s.repair_stats())
+s.close()
+print("repair per sweep:", rows, flush=True)
