@@ -841,9 +841,6 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
   double col[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) col[c] = 0.0;
-  // an excluded dish (w = -1) adds +0; its argument is clamped at 0 (its lp
-  // may exceed m, which is over the included dishes, and exp would overflow:
-  // 0 * inf); an included dish has lp <= m, so the clamp changes nothing there
   if constexpr (KB > 0) {
     double x[KB];
 #pragma unroll
@@ -857,7 +854,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
     for (int j = 0; j < KB; ++j) {
       if (j < K) {
         const double w = (j == j0) ? w0 : sw[j];
-        double xe = __builtin_fmin(x[j] - m, 0.0);
+        double xe = x[j] - m;
         asm volatile("" : "+v"(xe) : "v"(col[(j + 16 - MVC_ZEXP_LAG) & 15]));    // MVC_ZEXP_LAG exps in flight (register pressure)
         col[j & 15] = col[j & 15] + __builtin_fmax(w, 0.0) * mvc_exp_le0(xe);   // dead dish (w = -1): + 0, exact
       }
@@ -871,7 +868,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        double xe = __builtin_fmin(x[u] - m, 0.0);
+        double xe = x[u] - m;
         asm volatile("" : "+v"(xe) : "v"(col[(u + 16 - MVC_ZEXP_LAG) & 15]));
         col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(xe);
       }
@@ -880,59 +877,8 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
     for (int u = 0; u < 16; ++u) {
       if (j + u < K) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(__builtin_fmin(row(koff + j + u) - m, 0.0));
+        col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(row(koff + j + u) - m);
       }
-    }
-  }
-  return pw16(col);
-}
-
-// A G-form row (the all-views producer's views with K_v > 16):
-// dish j holds the dot product G_ij and the customer's own dish its final
-// (self-removed) lp, so lp_j = fma(G + y2/2, cb_j, c0_j) + h is formed here,
-// the expression and operand order of the producer's epilogue; the view
-// maximum m (over the included dishes and the new dish) too, in a first pass
-// over the row.  cb / c0 by wave-uniform dish index (scalar loads).
-struct GForm {
-  const double *c0, *cb;   // the view's coefficient rows
-  double hy, h;            // y2 / 2 and (-y2 / 2) / tau of this customer
-  int j0;                  // its own dish
-  __device__ __forceinline__ double lp(double x, int j) const {
-    return (j == j0) ? x : __builtin_fma(x + hy, cb[j], c0[j]) + h;
-  }
-};
-__device__ __forceinline__ double zview_sum_g(const LpRow &row, int koff, int K, const GForm &g, double w0,
-                                              const double *sw, double lfn, double &m_out) {
-  double m = -MVC_PM_INF;
-  for (int j = 0; j < K; j += 16) {               // pass 1: the view maximum
-    double x[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = row(koff + min(j + u, K - 1));
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int jj = min(j + u, K - 1);
-      const double w = (jj == g.j0) ? w0 : sw[jj];
-      const double val = g.lp(x[u], jj);
-      if (j + u < K && w >= 0.0 && val > m) m = val;
-    }
-  }
-  if (lfn > m) m = lfn;
-  m_out = m;
-  double col[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) col[c] = 0.0;
-  for (int j = 0; j < K; j += 16) {               // pass 2: the column partials
-    double x[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) x[u] = row(koff + min(j + u, K - 1));
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int jj = min(j + u, K - 1);
-      const double w = (jj == g.j0) ? w0 : sw[jj];
-      const bool in = j + u < K && w >= 0.0;
-      double xe = in ? g.lp(x[u], jj) - m : 0.0;
-      asm volatile("" : "+v"(xe) : "v"(col[(u + 16 - MVC_ZEXP_LAG) & 15]));
-      col[u] = col[u] + (in ? w : 0.0) * mvc_exp_le0(xe);
     }
   }
   return pw16(col);
@@ -955,7 +901,7 @@ struct ZregLds {
 // read once; rows of K_v <= 16 in registers, staged rows kept in LDS for the
 // gathers), the table scores in view order, weights, block totals and the
 // pw16 descent.  Returns the choice (table position, -1 = birth).
-template <int TM, bool kG>
+template <int TM>
 __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, int i, const LpRow &row, double *s_stage,
                                              int lane) {
   const ParState &P = A.P;
@@ -977,17 +923,11 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     if (w0 < 0.0) w0 = 0.0;
     if (!(l0p > 0)) w0 = -1.0;
     const double *sw = Z.w + koff;
-    double m = 0.0;
+    const double m = A.vmax[(size_t)v * n + i];
     double S;
     const bool allv = __builtin_amdgcn_readfirstlane(Z.lmin[v]) != 0;
     const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
     double *stg = so >= 0 ? s_stage + (size_t)so * 64 + lane : nullptr;
-    if (kG && K > 16) {   // a G-form row (all-views producer): lp and the view maximum formed here
-      const double y2 = A.Y2[(size_t)v * n + i];
-      const GForm g{P.c0 + (size_t)v * P.KC, P.cb + (size_t)v * P.KC, 0.5 * y2, (-0.5 * y2) / P.hyper[v], j0};
-      S = zview_sum_g(row, koff, K, g, w0, sw, lfn, m);
-    } else {
-    m = A.vmax[(size_t)v * n + i];
 #ifdef MVC_ABL_DRAW_NOVIEW   // timing ablation: no view pass
     if (true) S = 1.0 + m; else
 #endif
@@ -995,7 +935,6 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     else if (K <= 8) S = zview_sum<8>(row, koff, K, j0, w0, sw, m, stg);     // row in registers
     else if (K <= 16) S = zview_sum<16>(row, koff, K, j0, w0, sw, m, stg);
     else S = zview_sum<0>(row, koff, K, j0, w0, sw, m);
-    }
     const int Kact = K - ((l0p == 0) ? 1 : 0);
     double wn = P.hyper[V + v] + (double)Kact * sigma;
     if (wn < 0.0) wn = 0.0;
@@ -1015,37 +954,6 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     sp[p] = p < T ? ((pc == p0) ? base_self : Z.base[pc]) : -MVC_PM_INF;
   }
 #ifndef MVC_ABL_DRAW_NOGATHER   // timing ablation: no table gathers
-  if constexpr (kG) {
-    // the G-form rows' gathered dot products become lp here (their
-    // conversion constants re-formed per 16 tables: registers hold the scores)
-#pragma unroll
-    for (int c = 0; c < TM; c += 16) {
-      for (int v = 0; v < V; ++v) {
-        const int koff = __builtin_amdgcn_readfirstlane(Z.koff[v]);
-        const int K = __builtin_amdgcn_readfirstlane(Z.koff[v + 1]) - koff;
-        const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
-        double x[16];
-        if (so >= 0) {                             // staged row: LDS [dish][lane], conflict-free
-          const double *st = s_stage + (size_t)(so - koff) * 64 + lane;
-#pragma unroll
-          for (int u = 0; u < 16; ++u) x[u] = st[(size_t)__builtin_amdgcn_readfirstlane(Z.tix[min(c + u, T - 1) * V + v]) * 64];
-        } else {
-#pragma unroll
-          for (int u = 0; u < 16; ++u) x[u] = row(__builtin_amdgcn_readfirstlane(Z.tix[min(c + u, T - 1) * V + v]));
-        }
-        if (K > 16) {
-          const double y2 = A.Y2[(size_t)v * n + i];
-          const GForm g{P.c0 + (size_t)v * P.KC, P.cb + (size_t)v * P.KC, 0.5 * y2, (-0.5 * y2) / P.hyper[v],
-                        Z.tix[p0 * V + v] - koff};
-#pragma unroll
-          for (int u = 0; u < 16; ++u)
-            x[u] = g.lp(x[u], __builtin_amdgcn_readfirstlane(Z.tix[min(c + u, T - 1) * V + v]) - koff);
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
-      }
-    }
-  } else {
 #pragma unroll
   for (int c = 0; c < TM; c += 16) {
     for (int v = 0; v < V; ++v) {
@@ -1062,7 +970,6 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
 #pragma unroll
       for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
     }
-  }
   }
 #endif
   double M = -MVC_PM_INF;
@@ -1113,15 +1020,11 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
   return pick;
 }
 
+template <int TM>
 #ifndef MVC_ZDRAW_MINB
 #define MVC_ZDRAW_MINB 3      // blocks of 4 waves per CU the register budget must allow
 #endif
-#ifndef MVC_ZDRAW_MINB_G
-#define MVC_ZDRAW_MINB_G 2    // the same for the G-form draw (it converts the gathered dot products)
-#endif
-// kG: the rows of views with K_v > 16 are in G form (the all-views producer's)
-template <int TM, bool kG>
-__global__ __launch_bounds__(256, kG ? MVC_ZDRAW_MINB_G : MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
+__global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(Sweep A, int b0, int nb, const double *lpb) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const ParState &P = A.P;
   const int V = P.V, KC = P.KC, TC = P.TC;
@@ -1173,7 +1076,7 @@ __global__ __launch_bounds__(256, kG ? MVC_ZDRAW_MINB_G : MVC_ZDRAW_MINB) void m
   const int li = blockIdx.x * blockDim.x + tid;   // one customer per thread (no loop-invariant hoisting)
   if (li >= nb) return;
   const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
-  A.choice[b0 + li] = zdraw_reg_one<TM, kG>(A, Z, b0 + li, row, s_stage, tid & 63);
+  A.choice[b0 + li] = zdraw_reg_one<TM>(A, Z, b0 + li, row, s_stage, tid & 63);
 }
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
   return 8 * ((size_t)TM + (size_t)sumK + (size_t)4 * MVC_ZSTAGE * 64) +
@@ -1467,7 +1370,7 @@ extern "C" __device__ void mvc_raw_buffer_store_v2f64(mvc_d2 v, mvc_i4 rsrc, int
 // lanes to their discard slot), the own dish's G and the max over the other
 // included dishes per row to LDS; the own dish itself is done for all views
 // at once at the end of the tile (lpa_tile_end).
-template <int NT, int SPPT, int RP, bool kG>
+template <int NT, int SPPT, int RP>
 __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v, int li0, int nb, const mvc_d2 *cur,
                                          const mvc_d2 *nxt, mvc_d2 (&ring)[RP], mvc_i4 rsrc, int tile_boff,
                                          int disc_boff, double *wsp, const int *zs) {
@@ -1505,19 +1408,6 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
     for (int t = 1; t < NT; ++t)
       if (jt == t) g = acc[t][r];
     if (col == (j0[r] & 15)) selfG[grp + 4 * r] = g;
-  }
-  if constexpr (kG && NT >= 2) {
-    // G form: the dot products themselves (the draw forms lp and the view
-    // maximum; the own dish's final lp is stored at the end of the tile)
-    const int lbase = tile_boff + 128 * (koff + col) + 32 * grp;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int j = 16 * t + col;
-      const int off = j < K ? lbase + 2048 * t : disc_boff;
-      mvc_raw_buffer_store_v2f64((mvc_d2){acc[t][0], acc[t][1]}, rsrc, off, 0, 0);
-      mvc_raw_buffer_store_v2f64((mvc_d2){acc[t][2], acc[t][3]}, rsrc, j < K ? off + 16 : disc_boff, 0, 0);
-    }
-    return;
   }
   // frozen-dish lp for every (row, dish): a fixed number of unconditional
   // stores (the own dish is overwritten at the end of the tile by this same
@@ -1570,7 +1460,7 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
 // to vmax, so the draw reads each lp row once.
 __device__ __forceinline__ void lpa_tile_end(const Sweep &A, const LpaLds &L, int b0, int li0, int nb, double y2,
                                              double h, double cnew, int pz, mvc_i4 rsrc, int tile_boff, int disc_boff,
-                                             const double *wsp, double *dslot, uint32_t gmask) {
+                                             const double *wsp, double *dslot) {
   const ParState &P = A.P;
   const int lane = threadIdx.x & 63, row = lane & 15, v = lane >> 4;
   const int V = P.V, n = P.n;
@@ -1589,37 +1479,30 @@ __device__ __forceinline__ void lpa_tile_end(const Sweep &A, const LpaLds &L, in
   if (l0p > 0 && sv > m) m = sv;
   const double lfn = cnew + h;
   if (lfn > m) m = lfn;
-  double *dm = (ok && !((gmask >> vv) & 1u)) ? A.vmax + (size_t)vv * n + b0 + li0 + row : dslot;   // G form: the draw's
+  double *dm = ok ? A.vmax + (size_t)vv * n + b0 + li0 + row : dslot;
   *dm = m;
 }
 
-template <int SPPT, int RP, uint32_t PAT, int VI, bool kG>
+template <int SPPT, int RP, uint32_t PAT, int VI>
 __device__ __forceinline__ void lpa_views(const Sweep &A, const LpaLds &L, int li0, int nb, const mvc_d2 *ybase,
                                           size_t vstride, size_t tcur, size_t tnext, mvc_d2 (&ring)[RP], mvc_i4 rsrc,
                                           int tile_boff, int disc_boff, double *wsp, const int *zs) {
   if constexpr (VI < fz_pat_v(PAT)) {
     const mvc_d2 *cur = ybase + (size_t)VI * vstride + tcur;
     const mvc_d2 *nxt = (VI + 1 < fz_pat_v(PAT)) ? ybase + (size_t)(VI + 1) * vstride + tcur : ybase + tnext;
-    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP, kG>(A, L, VI, li0, nb, cur, nxt, ring, rsrc, tile_boff, disc_boff, wsp, zs);
-    lpa_views<SPPT, RP, PAT, VI + 1, kG>(A, L, li0, nb, ybase, vstride, tcur, tnext, ring, rsrc, tile_boff, disc_boff,
-                                         wsp, zs);
+    lpa_view<fz_pat_nt(PAT, VI), SPPT, RP>(A, L, VI, li0, nb, cur, nxt, ring, rsrc, tile_boff, disc_boff, wsp, zs);
+    lpa_views<SPPT, RP, PAT, VI + 1>(A, L, li0, nb, ybase, vstride, tcur, tnext, ring, rsrc, tile_boff, disc_boff, wsp,
+                                     zs);
   }
 }
-// the views of pattern PAT that the G form stores as dot products (K_v > 16)
-__host__ __device__ constexpr uint32_t fz_pat_gmask(uint32_t pat) {
-  uint32_t m = 0;
-  for (int v = 0; v < fz_pat_v(pat); ++v)
-    if (fz_pat_nt(pat, v) >= 2) m |= 1u << v;
-  return m;
-}
 
+template <int SPPT, int RP, uint32_t PAT>
 #ifndef MVC_LPA_WAVES
 #define MVC_LPA_WAVES 8       // waves per block (one block per CU) of the all-views producer
 #endif
 #ifndef MVC_LPA_RP16
 #define MVC_LPA_RP16 8        // ring depth (k-step pairs in flight per wave) at D = 128
 #endif
-template <int SPPT, int RP, uint32_t PAT, bool kG>
 __global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep A, int b0, int nb, double *lpb,
                                                                           double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1716,12 +1599,11 @@ __global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep
     zs[row] = pz;
     wave_lds_sync();
     const int tile_boff = li0 * sumK * 8;           // (li0 >> 4) * sumK * 16 doubles
-    lpa_views<SPPT, RP, PAT, 0, kG>(A, L, li0, nb, ybase, vstride, toff(m), toff(m + 1), ring, rsrc, tile_boff,
-                                    disc_boff, wsp, zs);
+    lpa_views<SPPT, RP, PAT, 0>(A, L, li0, nb, ybase, vstride, toff(m), toff(m + 1), ring, rsrc, tile_boff, disc_boff,
+                                wsp, zs);
     wave_lds_sync();
 #if !defined(MVC_ABL_LP_NOEPI) && !defined(MVC_ABL_LP_NOEND)
-    lpa_tile_end(A, L, b0, li0, nb, y2, h, cnew_l, pz, rsrc, tile_boff, disc_boff, wsp, dslot,
-                 kG ? fz_pat_gmask(PAT) : 0u);
+    lpa_tile_end(A, L, b0, li0, nb, y2, h, cnew_l, pz, rsrc, tile_boff, disc_boff, wsp, dslot);
 #endif
     wave_lds_sync();
   }
@@ -2286,8 +2168,6 @@ class ParallelSampler : public Sampler {
   bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
   bool force_zdraw_row = false;   // MVC_ZDRAW_ROW=1: the row draw for every T <= 512 (default: 64 < T <= 512)
   bool no_zrow_lds = false;       // MVC_ZROW_LDS=0: the row draw reads the lp buffer directly
-  bool no_gform = false;          // MVC_GFORM=0: the all-views producer stores lp for every view
-  bool lpa_g = false;             // this batch: the producer's G form
   size_t zsc_max_bytes = (size_t)1 << 30;   // the checkpoint draw's table-score scratch limit (MVC_ZSC_MAX_MB)
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
@@ -2495,7 +2375,6 @@ class ParallelSampler : public Sampler {
     force_zdraw_row = zr && zr[0] == '1';
     const char *zrl = getenv("MVC_ZROW_LDS");
     no_zrow_lds = zrl && zrl[0] == '0';
-    if (const char *e = getenv("MVC_GFORM")) no_gform = e[0] == '0';
     if (const char *e = getenv("MVC_ZSC_MAX_MB")) zsc_max_bytes = (size_t)std::max(0L, std::strtol(e, nullptr, 10)) << 20;
     if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
     {
@@ -2936,13 +2815,12 @@ class ParallelSampler : public Sampler {
   }
 
   template <int SPPT, int RP>
-  void launch_lpall(uint32_t pat, bool g, dim3 grid, dim3 block, size_t lds, const Sweep &A, int b0, int nb) {
+  void launch_lpall(uint32_t pat, dim3 grid, dim3 block, size_t lds, const Sweep &A, int b0, int nb) {
     double *disc = lpb + lpb_cap;
     switch (pat) {
 #define X(p)                                                                                       \
   case p:                                                                                          \
-    if (g) hipLaunchKernelGGL((mvc_par_lpall_kernel<SPPT, RP, p, true>), grid, block, lds, stream, A, b0, nb, lpb, disc); \
-    else hipLaunchKernelGGL((mvc_par_lpall_kernel<SPPT, RP, p, false>), grid, block, lds, stream, A, b0, nb, lpb, disc); \
+    hipLaunchKernelGGL((mvc_par_lpall_kernel<SPPT, RP, p>), grid, block, lds, stream, A, b0, nb, lpb, disc); \
     break;
       MVC_FZ_PATS(X)
 #undef X
@@ -2952,9 +2830,7 @@ class ParallelSampler : public Sampler {
   template <int SPPT, int RP>
   static void lpall_attr() {
 #define X(p)                                                                                            \
-  MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_lpall_kernel<SPPT, RP, p, true>,                    \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));                  \
-  MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_lpall_kernel<SPPT, RP, p, false>,                   \
+  MVC_HIP(hipFuncSetAttribute((const void *)mvc_par_lpall_kernel<SPPT, RP, p>,                          \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     MVC_FZ_PATS(X)
 #undef X
@@ -3040,16 +2916,13 @@ class ParallelSampler : public Sampler {
       const size_t lpa_lds = lpall_shared_bytes(s1t_d, V, sk, MVC_LPA_WAVES);
       const bool use_lpall = !no_lpall && use_mfma && pat_ok && c.T <= 16 * MVC_FZ_TB &&
                              (spp == 4 || spp == 8 || spp == 16) && lpa_lds <= 160 * 1024;
-      // G form (the producer stores the dot products of its views with K_v >
-      // 16; the register draw forms their lp and view maxima)
-      lpa_g = use_lpall && use_zreg && !no_gform;
       if (use_lpall) {
         const int ntile = (nb + 15) / 16;
         const int grid = std::max(1, std::min(n_cu, (ntile + MVC_LPA_WAVES - 1) / MVC_LPA_WAVES));
         switch (spp) {
-          case 4: launch_lpall<4, 4>(fz_pat, lpa_g, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
-          case 8: launch_lpall<8, 8>(fz_pat, lpa_g, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
-          default: launch_lpall<16, MVC_LPA_RP16>(fz_pat, lpa_g, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
+          case 4: launch_lpall<4, 4>(fz_pat, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
+          case 8: launch_lpall<8, 8>(fz_pat, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
+          default: launch_lpall<16, MVC_LPA_RP16>(fz_pat, dim3(grid), dim3(64 * MVC_LPA_WAVES), lpa_lds, A, (int)b0, nb); break;
         }
         zpath_lpall = true;
       } else if (use_mfma) {
@@ -3099,19 +2972,15 @@ class ParallelSampler : public Sampler {
       timers.end("lp", el);
       timers.begin("draw", &ed);
       const dim3 zg((nb + 255) / 256);   // the register kernel takes one customer per thread
-#define MVC_ZREG(TMV)                                                                                         \
-  if (lpa_g) hipLaunchKernelGGL((mvc_par_zdraw_reg_kernel<TMV, true>), zg, dim3(256), zdraw_reg_shared_bytes(V, TMV, sk), \
-                                stream, A, (int)b0, nb, (const double *)lpb);                                       \
-  else hipLaunchKernelGGL((mvc_par_zdraw_reg_kernel<TMV, false>), zg, dim3(256), zdraw_reg_shared_bytes(V, TMV, sk),    \
-                          stream, A, (int)b0, nb, (const double *)lpb);
-      if (use_zreg && c.T <= 16) {
-        MVC_ZREG(16)
-      } else if (use_zreg && c.T <= 32) {
-        MVC_ZREG(32)
-      } else if (use_zreg) {
-        MVC_ZREG(64)
-      }
-#undef MVC_ZREG
+      if (use_zreg && c.T <= 16)
+        hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<16>, zg, dim3(256), zdraw_reg_shared_bytes(V, 16, sk), stream, A,
+                           (int)b0, nb, (const double *)lpb);
+      else if (use_zreg && c.T <= 32)
+        hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<32>, zg, dim3(256), zdraw_reg_shared_bytes(V, 32, sk), stream, A,
+                           (int)b0, nb, (const double *)lpb);
+      else if (use_zreg)
+        hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<64>, zg, dim3(256), zdraw_reg_shared_bytes(V, 64, sk), stream, A,
+                           (int)b0, nb, (const double *)lpb);
       else if (use_zrow) {
         // 16 customers (one slab) per block and round
         const dim3 rg(std::max(1, std::min((nb + 15) / 16, (zrow_lds ? 2 : 8) * n_cu)));
