@@ -841,6 +841,9 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
   double col[16];
 #pragma unroll
   for (int c = 0; c < 16; ++c) col[c] = 0.0;
+  // an excluded dish (w = -1) adds +0; its argument is clamped at 0 (its lp
+  // may exceed m, which is over the included dishes, and exp would overflow:
+  // 0 * inf); an included dish has lp <= m, so the clamp changes nothing there
   if constexpr (KB > 0) {
     double x[KB];
 #pragma unroll
@@ -854,7 +857,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
     for (int j = 0; j < KB; ++j) {
       if (j < K) {
         const double w = (j == j0) ? w0 : sw[j];
-        double xe = x[j] - m;
+        double xe = __builtin_fmin(x[j] - m, 0.0);
         asm volatile("" : "+v"(xe) : "v"(col[(j + 16 - MVC_ZEXP_LAG) & 15]));    // MVC_ZEXP_LAG exps in flight (register pressure)
         col[j & 15] = col[j & 15] + __builtin_fmax(w, 0.0) * mvc_exp_le0(xe);   // dead dish (w = -1): + 0, exact
       }
@@ -868,7 +871,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
 #pragma unroll
       for (int u = 0; u < 16; ++u) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        double xe = x[u] - m;
+        double xe = __builtin_fmin(x[u] - m, 0.0);
         asm volatile("" : "+v"(xe) : "v"(col[(u + 16 - MVC_ZEXP_LAG) & 15]));
         col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(xe);
       }
@@ -877,7 +880,7 @@ __device__ __forceinline__ double zview_sum(const LpRow &row, int koff, int K, i
     for (int u = 0; u < 16; ++u) {
       if (j + u < K) {
         const double w = (j + u == j0) ? w0 : sw[j + u];
-        col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(row(koff + j + u) - m);
+        col[u] = col[u] + __builtin_fmax(w, 0.0) * mvc_exp_le0(__builtin_fmin(row(koff + j + u) - m, 0.0));
       }
     }
   }
