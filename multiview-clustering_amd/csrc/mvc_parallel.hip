@@ -2199,6 +2199,7 @@ class ParallelSampler : public Sampler {
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
   bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
+  int run_grow_first = 0;         // MVC_RUN_GROW=0: the run kernel's LDS layout with room for T / 2 more tables only
   bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
   bool vp_stats = false;          // MVC_VP_STATS=1
 
@@ -2420,6 +2421,7 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
+    if (const char *e = getenv("MVC_RUN_GROW")) run_grow_first = e[0] == '0' ? 1 : 0;
     if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
     if (const char *e = getenv("MVC_VP_STATS")) vp_stats = e[0] == '1';
     if (const char *e = getenv("MVC_WIDE")) {
@@ -3057,18 +3059,21 @@ class ParallelSampler : public Sampler {
     // small chains: the run kernel walks the whole sweep (a window round is a
     // launch triple and a host read-back, more than the steps it saves)
     L.limit = (n <= small_n_no_windows) ? kNoWindows : run_limit;
-    // in order of preference: S1 cached with room to grow, then without S1,
+    // in order of preference: S1 cached with room to double (a cold sweep's
+    // births then rarely restride; in a chain batch a restride ends the round
+    // for every chain), S1 cached with room to grow by half, then without S1,
     // then tight margins without S1
-    for (int attempt = force_global ? 3 : 0; attempt < 3; ++attempt) {
-      const bool s1 = attempt == 0;
-      const int kgrow = attempt < 2 ? std::max(8, kmax / 2) : 4;
-      const int tgrow = attempt < 2 ? std::max(64, T / 2) : 16;
+    for (int attempt = force_global ? 4 : run_grow_first; attempt < 4; ++attempt) {
+      const bool s1 = attempt <= 1;
+      const int kgrow = attempt == 0 ? std::max(16, kmax) : attempt < 3 ? std::max(8, kmax / 2) : 4;
+      const int tgrow = attempt == 0 ? std::max(128, T) : attempt < 3 ? std::max(64, T / 2) : 16;
       // ks = 16 (mod 32): the lane-column evaluation's rows (views) read dish
       // j of [v][ks] arrays at v ks + j, so rows 0 / 1 (and 2 / 3) of a
       // ds_read_b64 lane group then fall on disjoint banks (2 ks dwords = 32
       // mod 64), and of a ds_read_b32 too (ks = 16 mod 32)
       L.ks = (kmax + kgrow + 15) / 32 * 32 + 16;
       L.ts = (T + tgrow + 63) / 64 * 64;   // whole 64-table chunks (the lane-column evaluation's e[] scratch)
+      if (attempt == 0 && use_lc && L.ts > 64 * kLcChunks) continue;   // doubling would leave the lane-column form
       L.s1 = s1 ? 1 : 0;
       L.cache_dbl = seq_lds_cache(V, D, L.ks, L.ts, s1);
       L.stride = seq_lds_stride(V, D, L.ks, L.ts);
