@@ -5,7 +5,8 @@ the output list of ``Rcpp::List run_gibbs_cpp(const Rcpp::List& data_views,
 int M, int burn_in, int thin)`` (/root/reference/Multiview/multiview_gibbs.cpp:
 105-131): a dict with ``table_of`` (list over saved iterations of int32[n],
 0-based table positions), ``dish_of`` (list over saved iterations of a list
-over views of int32[T_s], raw dish ids), ``loglik`` (empty: the reference
+over views of int32[T_s], raw dish ids) -- both read-only sequences whose
+items are built on access from one contiguous block per chain -- ``loglik`` (empty: the reference
 declares compute_log_likelihood but never defines it, multiview_gibbs.h:13),
 ``alpha_v``/``sigma_v``/``tau_v`` (list over views of float64[S]) and
 ``alpha_global``/``sigma_global`` (float64[S]).
@@ -17,6 +18,7 @@ raises R conditions via Rcpp::stop, multiview_utils.cpp:141,145).
 """
 import ctypes
 import time
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -65,6 +67,32 @@ def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_ch
     cfg.flags = _timing_flags(timing) | (L.FLAG_QUIET if quiet else 0)
     cfg.n_devices, cfg.chain_stride = n_devices, chain_stride
     return cfg
+
+
+class _Samples(Sequence):
+    """The saved samples of one chain as a read-only list: item s is built
+    from the chain's contiguous result block when it is read (the reference's
+    R list holds S small vectors per chain; materialising them eagerly for
+    thousands of chains cost more than the sampling)."""
+
+    def __init__(self, count, item):
+        self._n, self._item = count, item
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, s):
+        if isinstance(s, slice):
+            return [self._item(k) for k in range(*s.indices(self._n))]
+        k = s.__index__()
+        if k < 0:
+            k += self._n
+        if not 0 <= k < self._n:
+            raise IndexError("saved sample index out of range")
+        return self._item(k)
+
+    def __repr__(self):
+        return f"<{self._n} saved samples>"
 
 
 def _view_ptrs(y):
@@ -121,12 +149,14 @@ def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chain
             st = lib.mvc_result_copy_chain(res, c, tab.ctypes.data_as(ip), None, dsh.ctypes.data_as(ip))
             if st != L.MVC_OK:
                 raise L.MvcError(st, f"mvc_result_copy_chain(chain {c}) failed")
-            table_of = list(tab)
-            ends = np.cumsum(V * Ts.astype(np.int64))
-            dish_of = []
-            for s, blk in enumerate(np.split(dsh[: int(ends[-1]) if S else 0], ends[:-1]) if S else []):
-                d = blk.reshape(V, int(Ts[s]))
-                dish_of.append([d[v] for v in range(V)])
+            table_of = _Samples(S, tab.__getitem__)
+            starts = np.concatenate(([0], np.cumsum(V * Ts.astype(np.int64))))
+
+            def dishes(s, dsh=dsh, starts=starts, Ts=Ts):
+                d = dsh[starts[s]:starts[s + 1]].reshape(V, int(Ts[s]))
+                return [d[v] for v in range(V)]
+
+            dish_of = _Samples(S, dishes)
 
             def tr(which, per_view):
                 p = lib.mvc_result_trace(res, c, which)
