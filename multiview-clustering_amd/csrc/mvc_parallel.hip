@@ -1788,10 +1788,11 @@ struct MHArgs {
 
 }  // namespace
 
-// 5 waves: waves 0-3 run the per-view MH steps (views w, w + 4, ...); wave 4
-// runs the global pair at the same time when T is small (one-wave tree64 =
-// the block tree64's association), else the whole block runs it afterwards.
-constexpr int kHypWaves = 5, kHypThreads = 64 * kHypWaves, kHypGlobalWaveT = 512;
+// 8 waves (two per SIMD): waves 0-6 run the per-view MH steps (views w, w + 7,
+// ...: one view per wave for the reference's few views); wave 7 runs the
+// global pair at the same time when T is small (one-wave tree64 = the block
+// tree64's association), else the whole block runs it afterwards.
+constexpr int kHypWaves = 8, kHypViewWaves = kHypWaves - 1, kHypThreads = 64 * kHypWaves, kHypGlobalWaveT = 512;
 extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(MHArgs A) {
   ParState &P = A.P;
   const int tid = threadIdx.x;
@@ -1858,7 +1859,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     // Every MH step draws from its own window of the MH counter (oracle
     // update_hyper): tau of view v at 3v, alpha/sigma of view v at 3V + 6v,
     // the global pair at 9V.  The per-view steps are independent, so wave w
-    // runs views w, w + 4, ... with wavefront-level tree64 sums (same
+    // runs views w, w + 7, ... with wavefront-level tree64 sums (same
     // association as block_tree64); the global pair then runs on the block.
     auto unif_at = [&](uint32_t k) -> double { return mvc_uniform(A.seed, k, A.sweep, A.chain, MVC_TAG_MH); };
     auto rnorm_at = [&](uint32_t k, double mu, double sd) -> double {
@@ -1962,11 +1963,11 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
         }
         return root;
       };
-      if (wv == 4 && global_on_wave) {
+      if (wv == kHypViewWaves && global_on_wave) {
         const auto g = global_pair(wtree);
         if (lane == 0) { hyp[3 * V] = g.first; hyp[3 * V + 1] = g.second; }
       }
-      for (int v = wv; v < V && wv < 4; v += 4) {
+      for (int v = wv; v < V && wv < kHypViewWaves; v += kHypViewWaves) {
         const int Kv = P.Kact[v], Lv = P.Ltot[v];
         auto eppf_view = [&](double a, double s) -> double {
           if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
@@ -3133,6 +3134,7 @@ class ParallelSampler : public Sampler {
     SeqLds L;
     dim3 eg;
     bool vp_ok = true, early_mh = false;
+    bool birth_retry = false;   // a capacity growth interrupted a birth: the birth kernel follows the next run kernel
     int rounds = 1;
     hipEvent_t e1 = nullptr;
   };
@@ -3201,7 +3203,8 @@ class ParallelSampler : public Sampler {
       }
       MVC_HIP(hipGetLastError());
       dbg(repair_grid_only ? "seq_apply" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
-      if (L.lc && !repair_grid_only) {   // a birth the loop left pending (overflow retry only: births commit in the kernel)
+      if (L.lc && !repair_grid_only && rr.birth_retry) {   // a birth the loop left pending (births commit in the kernel)
+        rr.birth_retry = false;
         hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, rr.Q);
         MVC_HIP(hipGetLastError());
         dbg("seq_birth", c, s);
@@ -3223,6 +3226,7 @@ class ParallelSampler : public Sampler {
                                      std::to_string(rr.L.lc) + "):" + v);
     }
     if (rs.overflow) {
+      rr.birth_retry = true;
       grow_capacity(rs.overflow);
       rr.Q = make_seq(c, s);
       rr.eg = dim3(seq_waves / 4);   // the scratch may have fewer slots now
