@@ -376,6 +376,161 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
   }
 }
 
+// The dish-block producer's tiles with the k-steps unrolled (SPC = D / 4):
+// the same MFMA chain and epilogue as the runtime-SP loop of
+// mvc_par_lpbig_kernel, so the same bits.
+// Two k-steps of A-fragments from one 16-byte load per lane: lane (row, q)
+// holds y[row][8p + 2q], y[row][8p + 2q + 1] (x, y below, rows q = 0..3 of
+// the wave); k-step 2p needs d = 8p + k on lane (row, k), k-step 2p + 1
+// d = 8p + 4 + k.  permlane16_swap(x, y) makes the 16-lane rows (0,1 | 4,5)
+// and (2,3 | 6,7), permlane32_swap of those (0,1,2,3) and (4,5,6,7).
+__device__ __forceinline__ void lpbig_pair_ksteps(mvc_d2 xy, double &a0, double &a1) {
+  const long long bx = __double_as_longlong(xy[0]), by = __double_as_longlong(xy[1]);
+  const auto l16 = __builtin_amdgcn_permlane16_swap((unsigned)bx, (unsigned)by, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap((unsigned)(bx >> 32), (unsigned)(by >> 32), false, false);
+  const auto l32 = __builtin_amdgcn_permlane32_swap(l16[0], l16[1], false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(h16[0], h16[1], false, false);
+  a0 = __longlong_as_double(((long long)h32[0] << 32) | (unsigned)l32[0]);
+  a1 = __longlong_as_double(((long long)h32[1] << 32) | (unsigned)l32[1]);
+}
+
+// The dish-block producer's tiles with the k-steps unrolled (SPC = D / 4):
+// the same MFMA chain and epilogue as the runtime-SP loop of
+// mvc_par_lpbig_kernel, so the same bits.  A-fragments are read 16 bytes per
+// lane (two k-steps, lpbig_pair_ksteps), RP pair loads ahead.
+template <int NTB, int SPC>
+__device__ __forceinline__ void lpbig_tiles(const Sweep &A, int v, int jb0, int kb, int first, int b0, int nb,
+                                            double *lpb, double *dslot, const double *yv, const double *Bs, double *y2s,
+                                            double *selfG, double *mrest, const double *b_c0, const double *b_cb,
+                                            const double *b_Q, const int *b_l, const int *b_dn, const int *t_dish,
+                                            const int *t_n, int *zs, int gw, int NWT, int ntile, double tau,
+                                            double L2pt, double cnew) {
+#ifndef MVC_BIG_RP
+#define MVC_BIG_RP 8
+#endif
+  constexpr int NP = SPC / 2, RP = (NP % MVC_BIG_RP == 0) ? MVC_BIG_RP : 8;   // k-step pairs per tile, in flight
+  static_assert(NP >= RP && NP % RP == 0, "unrolled k-step pairs");
+  const ParState &P = A.P;
+  const int lane = threadIdx.x & 63, col = lane & 15, grp = lane >> 4;
+  const int V = P.V, D = 4 * SPC, n = P.n;
+  const int koff = A.Koff[v], sumK = A.Koff[V];
+  // this lane's pairs of row (col) of tile t (clamped to the batch: unconditional loads); pair p at [4 p]
+  auto rowp = [&](int t) -> const mvc_d2 * {
+    const int tt = t < ntile ? t : (ntile - 1);
+    return (const mvc_d2 *)(yv + (size_t)(b0 + min(tt * 16 + col, nb - 1)) * D) + grp;
+  };
+  mvc_d2 ar[RP];
+  const mvc_d2 *yr = rowp(gw);
+#pragma unroll
+  for (int u = 0; u < RP; ++u) ar[u] = yr[4 * u];
+  for (int tile = gw; tile < ntile; tile += NWT) {
+    const int li0 = tile * 16;
+    const int li_row = min(li0 + col, nb - 1);
+    const bool ok = lane < 16 && li0 + col < nb;
+    // the epilogue's global reads, issued ahead of this tile's MFMAs
+    const int pz = P.z[b0 + li_row];
+    const double y2 = A.Y2[(size_t)v * n + b0 + li_row];
+    double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
+    const double mprev = *dm;   // (unconditional load: read only when !first)
+    const mvc_d2 *yn = rowp(tile + NWT);
+    mvc_d4 acc[NTB];
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) acc[t] = (mvc_d4){0.0, 0.0, 0.0, 0.0};
+    double bc[NTB];
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) bc[t] = Bs[t * 64 + lane];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      double a2[2];
+      lpbig_pair_ksteps(ar[p % RP], a2[0], a2[1]);
+      ar[p % RP] = p + RP < NP ? yr[4 * (p + RP)] : yn[4 * (p + RP - NP)];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int s = 2 * p + h;
+        double bn[NTB];
+        const double *bk = Bs + (size_t)(s + 1 < SPC ? s + 1 : SPC - 1) * NTB * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) bn[t] = bk[t * 64];
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2[h], bc[t], acc[t], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NTB; ++t) bc[t] = bn[t];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep each refill RP pairs ahead (no sinking)
+    }
+    yr = yn;
+    // ---- epilogue (the runtime-SP loop's, with the own dish's Q / d_n from LDS)
+    if (grp == 0) { zs[col] = pz; y2s[col] = y2; }
+    wave_lds_sync();
+    double hy[4], hr[4];
+    int j0[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double y2r = y2s[grp + 4 * r];
+      hy[r] = 0.5 * y2r;
+      hr[r] = (-0.5 * y2r) / tau;
+      j0[r] = t_dish[zs[grp + 4 * r]];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int jl = j0[r] - jb0;
+      double g = acc[0][r];
+#pragma unroll
+      for (int t = 1; t < NTB; ++t)
+        if ((jl >> 4) == t) g = acc[t][r];
+      if (jl >= 0 && jl < kb && col == (jl & 15)) selfG[grp + 4 * r] = g;
+    }
+    double mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[r] = -MVC_PM_INF;
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) {
+      const int j = jb0 + 16 * t + col;
+      const double c0j = b_c0[16 * t + col], cbj = b_cb[16 * t + col];
+      const bool inj = j < jb0 + kb;
+      const bool inc = inj && b_l[16 * t + col] > 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double val = __builtin_fma(acc[t][r] + hy[r], cbj, c0j) + hr[r];
+        const int li = li0 + grp + 4 * r;
+        double *dst = (inj && li < nb) ? lpb + lpb_index(li, koff + j, sumK) : dslot;
+        *dst = val;
+        if (inc && j != j0[r] && val > mx[r]) mx[r] = val;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double mr = row16_max(mx[r]);
+      if (col == 0) mrest[grp + 4 * r] = mr;
+    }
+    wave_lds_sync();
+    {   // own dish (when in this block) and the view maximum, one row per lane
+      const int jj = t_dish[pz];
+      const int jl = jj - jb0;
+      const bool own = jl >= 0 && jl < kb;
+      const int jb = own ? jl : 0;
+      double m = mrest[col];
+      const double hself = (-0.5 * y2) / tau;
+      {   // (unconditional: lanes without their own dish here store to the discard slot)
+        const double G = selfG[col];
+        const double Gp = G - y2;
+        const double Qp = (b_Q[jb] - 2.0 * G) + y2;
+        const Coef cf = coef(b_dn[jb] - 1, Qp, tau, L2pt, D);
+        const double sv = __builtin_fma(Gp + 0.5 * y2, cf.cb, cf.c0) + hself;
+        double *dst = (ok && own) ? lpb + lpb_index(li0 + col, koff + jj, sumK) : dslot;
+        *dst = sv;
+        const int l0p = b_l[jb] - ((t_n[pz] - 1) > 0 ? 0 : 1);
+        if (own && l0p > 0 && sv > m) m = sv;
+      }
+      const double lfn = cnew + hself;
+      if (lfn > m) m = lfn;
+      if (!first) m = dmax(m, mprev);   // max is exact: the block order does not matter
+      *dm = m;
+    }
+    wave_lds_sync();
+  }
+}
+
 // MFMA lp producer for one block of up to 16*NTB dishes of view v (dishes
 // jb0 .. jb0 + kb), for views with K_v > 64 or when the tiled copy yt was not
 // built (BASELINE config 5: N = 10M, D = 256, K = 256 -- y alone is 164 GB).
@@ -386,7 +541,15 @@ __global__ __launch_bounds__(512) void mvc_par_lpview_kernel(Sweep A, int v, int
 // launch per dish block (y re-read per block: at D = 256, K = 256 the
 // arithmetic intensity stays ~16 flop/B, above the fp64 ridge).  The first
 // block writes the view maximum m_v of each customer, later blocks max it in.
-template <int NTB>
+//
+// SPC > 0 (= A.SP = D / 4, no padded k-steps): the tile is fully unrolled, so
+// every slot of the A-fragment ring is a fixed register and the loads are
+// unconditional (rows past the batch read the last row; their results go to
+// the discard slot), the ring runs on into the next tile (its first RA k-steps
+// are issued during this tile's last ones), and the epilogue reads nothing
+// from global memory but the tile's z / Y2 / previous view maximum, issued
+// at the tile start: no in-order vmcnt drain per k-step chunk or per tile.
+template <int NTB, int SPC>
 __global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int jb0, int kb, int first, int b0, int nb,
                                                             double *lpb, double *discard) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -405,16 +568,20 @@ __global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int 
   double *mrest = selfG + 16;
   double *b_c0 = wsp + BW * 48;                     // [16 NTB] the block's dish coefficients
   double *b_cb = b_c0 + 16 * NTB;
-  int *ip = (int *)(b_cb + 16 * NTB);
+  double *b_Q = b_cb + 16 * NTB;                    // [16 NTB] ||S1||^2 of the block's dishes
+  int *ip = (int *)(b_Q + 16 * NTB);
   int *b_l = ip;                                    // [16 NTB] table counts l of the block's dishes
-  int *t_dish = b_l + 16 * NTB;                     // [T]
+  int *b_dn = b_l + 16 * NTB;                       // [16 NTB] member counts of the block's dishes
+  int *t_dish = b_dn + 16 * NTB;                    // [T]
   int *t_n = t_dish + T;                            // [T]
   int *zs = t_n + T + w * 16;                       // per wave [16]
   for (int e = tid; e < 16 * NTB; e += blockDim.x) {
     const int jc = min(jb0 + e, K - 1);
     b_c0[e] = P.c0[v * KC + jc];
     b_cb[e] = P.cb[v * KC + jc];
+    b_Q[e] = P.Q[v * KC + jc];
     b_l[e] = P.d_l[v * KC + jc];
+    b_dn[e] = P.d_n[v * KC + jc];
   }
   {   // B-fragments of the dish block: Bs[(s * NTB + t) * 64 + lane] = S1[d = 4s + grp][j = jb0 + 16t + col]
     const double *S1v = P.S1T + (size_t)v * D * KC;
@@ -434,6 +601,11 @@ __global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int 
   const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
   double *const dslot = discard + lane;
   const double *yv = A.y + (size_t)v * n * D;
+  if constexpr (SPC > 0) {
+    lpbig_tiles<NTB, SPC>(A, v, jb0, kb, first, b0, nb, lpb, dslot, yv, Bs, y2s, selfG, mrest, b_c0, b_cb, b_Q, b_l,
+                          b_dn, t_dish, t_n, zs, gw, NWT, ntile, tau, L2pt, cnew);
+    return;
+  }
   for (int tile = gw; tile < ntile; tile += NWT) {
     const int li0 = tile * 16;
     const int li_row = min(li0 + col, nb - 1);
@@ -545,7 +717,7 @@ __global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int 
   }
 }
 __host__ inline size_t lpbig_shared_bytes(int SP, int NTB, int T, int waves) {
-  return 8 * ((size_t)SP * NTB * 64 + (size_t)waves * 48 + 32 * NTB) + 4 * (16 * NTB + 2 * (size_t)T + (size_t)waves * 16) + 64;
+  return 8 * ((size_t)SP * NTB * 64 + (size_t)waves * 48 + 48 * NTB) + 4 * (32 * NTB + 2 * (size_t)T + (size_t)waves * 16) + 64;
 }
 
 // Generic lp producer: one lane per customer (any D).
@@ -2187,6 +2359,8 @@ class ParallelSampler : public Sampler {
   bool early_mh_off = false;      // MVC_EARLY_MH=0: the MH launched only after the host has read the repair
   bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
   bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
+  bool big_runtime_sp = false;    // MVC_BIG_RUNTIME_SP=1: the dish-block producer's runtime k-step loop only (tests, A/B)
+  int big_bpc_narrow = 3;         // MVC_BIG_BPC: 4-wave blocks per CU of the dish-block producer's 16 / 32-dish instances
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
   int small_n_no_windows = 0;     // MVC_SMALL_N: chains up to this n never use grid windows (off: at N = 200 windows are faster)
   // MVC_RUN_WAVES: customers the run kernel evaluates per step.  4 by default:
@@ -2414,9 +2588,14 @@ class ParallelSampler : public Sampler {
     for (const void *f : {(const void *)mvc_par_zdraw_row_kernel<4, true>, (const void *)mvc_par_zdraw_row_kernel<8, true>,
                           (const void *)mvc_par_zdraw_row_kernel<16, true>, (const void *)mvc_par_zdraw_row_kernel<32, true>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
-    for (const void *f : {(const void *)mvc_par_lpbig_kernel<4>, (const void *)mvc_par_lpbig_kernel<2>,
-                          (const void *)mvc_par_lpbig_kernel<1>})
+#define MVC_LPBIG_FNS(NTB_)                                                                            \
+  (const void *)mvc_par_lpbig_kernel<NTB_, 0>, (const void *)mvc_par_lpbig_kernel<NTB_, 16>,             \
+      (const void *)mvc_par_lpbig_kernel<NTB_, 32>, (const void *)mvc_par_lpbig_kernel<NTB_, 64>
+    for (const void *f : {MVC_LPBIG_FNS(4), MVC_LPBIG_FNS(2), MVC_LPBIG_FNS(1)})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+#undef MVC_LPBIG_FNS
+    if (const char *e = getenv("MVC_BIG_RUNTIME_SP")) big_runtime_sp = e[0] == '1';
+    if (const char *e = getenv("MVC_BIG_BPC")) big_bpc_narrow = std::max(1, std::min(4, atoi(e)));
     if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
     if (const char *e = getenv("MVC_SMALL_N")) small_n_no_windows = atoi(e);
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
@@ -2957,15 +3136,32 @@ class ParallelSampler : public Sampler {
           for (int jb0 = 0, first = 1; jb0 < c.K[v]; jb0 += 16 * vntb, first = 0) {
             const int kb = std::min(16 * vntb, c.K[v] - jb0);
             const size_t lds = lpbig_shared_bytes(SPb, vntb, c.T, vwaves);
-            const int per_cu = vwaves == 8 ? 1 : 2;
+            // blocks per CU: the register budget allows three 4-wave blocks of the
+            // narrow instances (<= 168 VGPRs), two of the 64-dish one; LDS permitting
+            int per_cu = vwaves == 8 ? 1 : (vntb <= 2 ? big_bpc_narrow : 2);
+            per_cu = std::max(1, std::min<int>(per_cu, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
             const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + vwaves - 1) / vwaves));
             Sweep Ab = A;
             Ab.SP = SPb;
+            // the unrolled instance where D = 4 SP exactly (no padded k-steps)
+            const int spc = (4 * SPb == D && !big_runtime_sp && (SPb == 16 || SPb == 32 || SPb == 64)) ? SPb : 0;
+#define MVC_LPBIG(NTB_, SPC_)                                                                                   \
+  hipLaunchKernelGGL((mvc_par_lpbig_kernel<NTB_, SPC_>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, \
+                     first, (int)b0, nb, lpb, lpb + lpb_cap)
+#define MVC_LPBIG_SP(NTB_)         \
+  switch (spc) {                   \
+    case 16: MVC_LPBIG(NTB_, 16); break; \
+    case 32: MVC_LPBIG(NTB_, 32); break; \
+    case 64: MVC_LPBIG(NTB_, 64); break; \
+    default: MVC_LPBIG(NTB_, 0); break;  \
+  }
             switch (vntb) {
-              case 4: hipLaunchKernelGGL((mvc_par_lpbig_kernel<4>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
-              case 2: hipLaunchKernelGGL((mvc_par_lpbig_kernel<2>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
-              default: hipLaunchKernelGGL((mvc_par_lpbig_kernel<1>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, jb0, kb, first, (int)b0, nb, lpb, lpb + lpb_cap); break;
+              case 4: MVC_LPBIG_SP(4) break;
+              case 2: MVC_LPBIG_SP(2) break;
+              default: MVC_LPBIG_SP(1) break;
             }
+#undef MVC_LPBIG_SP
+#undef MVC_LPBIG
             MVC_HIP(hipGetLastError());
           }
         }

@@ -754,18 +754,22 @@ def test_last_customer_birth_with_poisoned_lds():
     assert int(r.stdout.split("last-birth OK")[1].split()[0]) >= 4
 
 
-@pytest.mark.parametrize("force", ["", "1"])
+@pytest.mark.parametrize("force", ["", "1", "d256", "d256-runtime"])
 def test_dish_block_producer(force, monkeypatch):
     """The dish-block MFMA producer (mvc_par_lpbig_kernel: A-fragments from y
     itself, dishes in blocks of 64, the view maximum combined over blocks):
-    K_v = 128 / 64 / 32 at D = 32 (two dish blocks in view 0), warm, and
-    forced onto a K <= 64 shape that the tiled producer would take; bitwise
-    vs the oracle."""
+    K_v = 128 / 64 / 32 at D = 32 (two dish blocks in view 0, the runtime
+    k-step loop), warm; forced onto a K <= 64 shape that the tiled producer
+    would take (D = 64: the unrolled tile); and configs[4]'s D = 256 with
+    K_v = 80 / 40 (a 64 + 16 dish split), unrolled and with the runtime loop
+    (MVC_BIG_RUNTIME_SP); bitwise vs the oracle."""
     if force:
         monkeypatch.setenv("MVC_BIG", "1")
+    if force == "d256-runtime":
+        monkeypatch.setenv("MVC_BIG_RUNTIME_SP", "1")
     m = _mvc()
     from mvc_amd import data
-    N, V, D, K = (6000, 3, 32, 128) if not force else (4100, 4, 64, 64)
+    N, V, D, K = {"": (6000, 3, 32, 128), "1": (4100, 4, 64, 64)}.get(force, (3000, 2, 256, 80))
     y, z = data.synthetic(N, V, D, K, seed=17)
     st = _warm_state(z, V, K)
     s = m.Sampler(y, seed=5, mode="parallel")
