@@ -1327,6 +1327,13 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
     const bool ok = li < nb;
     const int lic = min(li, nb - 1);
     const int i = b0 + lic;
+    // this customer's per-view scalars, lane c of the row holding view c,
+    // loaded together ahead of the slab (one memory latency per round instead
+    // of one per view)
+    const int vq = min(c, V - 1);
+    const int p0 = P.z[i];
+    const double m_lane = A.vmax[(size_t)vq * n + i];
+    const double y2_lane = A.Y2[(size_t)vq * n + i];
     if constexpr (kLds) {   // the slab (16 customers x sumK dishes, contiguous) into LDS, 8 loads in flight
       const mvc_d2 *src = (const mvc_d2 *)(lpb + (size_t)g * sumK * 16);
       mvc_d2 *dst = (mvc_d2 *)s_slab;
@@ -1345,7 +1352,6 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
       if constexpr (kLds) return LdsRow{s_slab + lpb_slot(row)};
       else return LpRow(lpb, (int)(lpb_index(lic, 0, sumK) * 8));   // dish k of this customer: lp.at(k)
     }();
-    const int p0 = P.z[i];
     const bool alive = (P.n_t[p0] - 1) > 0;
     double Smine = 0.0;                            // lane v of the row keeps view v's column sum
     for (int v = 0; v < V; ++v) {
@@ -1353,7 +1359,7 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
       const int j0 = s_tix[p0 * V + v] - koff;
       const double sigma = P.hyper[2 * V + v];
       const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
-      const double m = A.vmax[(size_t)v * n + i];
+      const double m = __shfl(m_lane, lane_row_base(row) + v, 64);
       // column c: included dishes j = 16 t + c in ascending t (an excluded
       // dish adds +0: its weight and argument are zeroed); the loads of 8
       // t at a time are issued before their exps
@@ -1362,8 +1368,10 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
         double x[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) x[u] = lp.at(koff + min(16 * (t0 + u) + c, K - 1));
+        const int tn = (K - 16 * t0 + 15) >> 4;   // dish blocks of this chunk with any dish (uniform)
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
+          if (u >= tn) break;                     // (a block past K_v would add +0 in every lane)
           const int j = 16 * (t0 + u) + c;
           const int l = (j == j0) ? l0p : s_dl[koff + min(j, K - 1)];
           double w = (double)l - sigma;                 // w_j = max(l - sigma, 0), included iff l > 0
@@ -1385,9 +1393,9 @@ __global__ __launch_bounds__(256, (NB >= 32 || kLds) ? 2 : MVC_ZROW_MINB) void m
       const int koff = s_koff[v], K = s_koff[v + 1] - koff;
       const int j0 = s_tix[p0 * V + v] - koff;
       const double alpha = P.hyper[V + v], sigma = P.hyper[2 * V + v];
-      const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+      const double lfn = A.cnew[v] + (-0.5 * y2_lane) / P.hyper[v];
       const int l0p = s_dl[koff + j0] - (alive ? 0 : 1);
-      const double m = A.vmax[(size_t)v * n + i];
+      const double m = m_lane;
       const int Kact = K - ((l0p == 0) ? 1 : 0);
       double wn = alpha + (double)Kact * sigma;
       if (wn < 0.0) wn = 0.0;
