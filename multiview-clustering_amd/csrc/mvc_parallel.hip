@@ -1084,21 +1084,29 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
   const int T = __builtin_amdgcn_readfirstlane(A.T);
   const double ag = P.hyper[3 * V], sg = P.hyper[3 * V + 1];
   const int T_ne = A.status[V + 3];
+  // view v's maximum and Y2 are loaded one view ahead (with z and the first
+  // view's row), not at the top of each view's iteration
+  double m_nx = A.vmax[i], y2_nx = A.Y2[i];
   const int p0 = P.z[i];
   const bool alive = (P.n_t[p0] - 1) > 0;
   double s_new = mvc_log(ag + sg * (double)(T_ne - (alive ? 0 : 1)));
   for (int v = 0; v < V; ++v) {
+    const double m = m_nx, y2v = y2_nx;
+    {
+      const size_t vn = (size_t)min(v + 1, V - 1) * n + i;
+      m_nx = A.vmax[vn];
+      y2_nx = A.Y2[vn];
+    }
     const int koff = __builtin_amdgcn_readfirstlane(Z.koff[v]);
     const int K = __builtin_amdgcn_readfirstlane(Z.koff[v + 1]) - koff;
     const int j0 = Z.tix[p0 * V + v] - koff;
     const double sigma = P.hyper[2 * V + v];
-    const double lfn = A.cnew[v] + (-0.5 * A.Y2[(size_t)v * n + i]) / P.hyper[v];
+    const double lfn = A.cnew[v] + (-0.5 * y2v) / P.hyper[v];
     const int l0p = Z.dl[koff + j0] - (alive ? 0 : 1);
     double w0 = (double)l0p - sigma;
     if (w0 < 0.0) w0 = 0.0;
     if (!(l0p > 0)) w0 = -1.0;
     const double *sw = Z.w + koff;
-    const double m = A.vmax[(size_t)v * n + i];
     double S;
     const bool allv = __builtin_amdgcn_readfirstlane(Z.lmin[v]) != 0;
     const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
