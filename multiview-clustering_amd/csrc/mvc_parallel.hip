@@ -1997,10 +1997,10 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
   // relabel, capacity growth) has to come between the repair and the MH
   if (A.gate && !(A.gate->done && A.gate->moves == 0 && A.gate->overflow == 0 && A.gate->restride == 0)) return;
   const int T = A.status[0];
+  __shared__ int s_koff[MVC_MAXV + 1];
   // ---- Q = ||S1||^2 per live dish (fma chain in d order), all views at once;
   //      the strided S1 loads are issued 16 ahead of the chain ----
   {
-    __shared__ int s_koff[MVC_MAXV + 1];
     if (tid == 0) {
       s_koff[0] = 0;
       for (int v = 0; v < V; ++v) s_koff[v + 1] = s_koff[v] + P.Kact[v];
@@ -2086,12 +2086,27 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     };
     // ---- per-view steps, one wavefront per view (multiview_hyper.cpp:211-266)
     const bool global_on_wave = T <= kHypGlobalWaveT;
+    // The tree64 leaves e of a thread are e = 64 c + (tid & 63) (wave and
+    // block trees alike), so each thread loads its leaves' table counts for
+    // c < 8 once, not once per EPPF evaluation (4 of them in the pair).
+    const int hl = tid & 63;
+    int nt_pre[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) nt_pre[c] = P.n_t[max(0, min(64 * c + hl, T - 1))];
+    auto nt_at = [&](int p) -> int {
+      if (p >= 512) return P.n_t[p];
+      int x = nt_pre[0];
+#pragma unroll
+      for (int c = 1; c < 8; ++c)
+        if ((p >> 6) == c) x = nt_pre[c];
+      return x;
+    };
     auto global_pair = [&](auto tree) {   // (:268-291), counters 9V ..
       auto eppf_global = [&](double a, double s) -> double {
         if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
         if (a <= -s) return -MVC_PM_INF;
         if (T <= 0) return 0.0;
-        return eppf(T, n, [&](int p) { return P.n_t[p]; }, a, s, tree);
+        return eppf(T, n, nt_at, a, s, tree);
       };
       const uint32_t k0 = 9u * (uint32_t)V;
       double ag_old = hyp[3 * V];
@@ -2157,16 +2172,28 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
       }
       for (int v = wv; v < V && wv < kHypViewWaves; v += kHypViewWaves) {
         const int Kv = P.Kact[v], Lv = P.Ltot[v];
+        // dish `lane` of the view (the wave tree's first chunk) loaded once for
+        // the six tree evaluations below; its tau-leaf parts are the same
+        // expressions as the leaf's, so the same values
+        const int jl = max(0, min(lane, Kv - 1));
+        const int dl_pre = P.d_l[v * KC + jl], nk_pre = P.d_n[v * KC + jl];
+        double sse_pre = 0.0;
+        if (nk_pre != 0) {
+          sse_pre = P.S2[v * KC + jl] - P.Q[v * KC + jl] / (double)nk_pre;
+          if (sse_pre < 0.0) sse_pre = 0.0;
+        }
+        const double a_pre = (-0.5 * (double)nk_pre) * (double)D;
         auto eppf_view = [&](double a, double s) -> double {
           if (!(s > kEps && s < 1.0 - kEps)) return -MVC_PM_INF;
           if (a <= -s) return -MVC_PM_INF;
           if (Lv == 0) return 0.0;
-          return eppf(Kv, Lv, [&](int j) { return P.d_l[v * KC + j]; }, a, s, wtree);
+          return eppf(Kv, Lv, [&](int j) { return j < 64 ? dl_pre : P.d_l[v * KC + j]; }, a, s, wtree);
         };
         auto post_tau = [&](double t) -> double {
           if (t <= 0.0) return -MVC_PM_INF;
           const double L = mvc_log((2.0 * MVC_PI) * t);
           const double ll = wtree(Kv, [&](int64_t j) {
+            if (j < 64) return nk_pre == 0 ? 0.0 : a_pre * L - 0.5 * (sse_pre / t);
             const int nk = P.d_n[v * KC + j];
             if (nk == 0) return 0.0;
             double sse = P.S2[v * KC + j] - P.Q[v * KC + j] / (double)nk;
@@ -2225,16 +2252,23 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     __syncthreads();
   }
   HYP_MARK("mh");
-  // ---- coefficients of the next sweep (frozen state) ----
-  for (int v = 0; v < V; ++v) {
-    const double tau = hyp[v];
-    const double L = mvc_log((2.0 * MVC_PI) * tau);
-    if (tid == 0) { A.L2pt[v] = L; A.cnew[v] = (double)D * (-0.5 * L); }
-    for (int j = tid; j < P.Kact[v]; j += kHypThreads) {
-      const Coef c = coef(P.d_n[v * KC + j], P.Q[v * KC + j], tau, L, D);
-      P.c0[v * KC + j] = c.c0;
-      P.cb[v * KC + j] = c.cb;
-    }
+  // ---- coefficients of the next sweep (frozen state): log(2 pi tau_v) on
+  //      thread v, then every dish of every view in one pass ----
+  __shared__ double s_L2pt[MVC_MAXV];
+  if (tid < V) {
+    const double L = mvc_log((2.0 * MVC_PI) * hyp[tid]);
+    s_L2pt[tid] = L;
+    A.L2pt[tid] = L;
+    A.cnew[tid] = (double)D * (-0.5 * L);
+  }
+  __syncthreads();
+  for (int k = tid; k < s_koff[V]; k += kHypThreads) {
+    int v = 0;
+    while (k >= s_koff[v + 1]) ++v;
+    const int j = k - s_koff[v];
+    const Coef c = coef(P.d_n[v * KC + j], P.Q[v * KC + j], hyp[v], s_L2pt[v], D);
+    P.c0[v * KC + j] = c.c0;
+    P.cb[v * KC + j] = c.cb;
   }
   const double sg = hyp[3 * V + 1];
   for (int p = tid; p < T; p += kHypThreads) P.lmass[p] = mvc_log((double)P.n_t[p] - sg);
