@@ -2412,6 +2412,7 @@ class ParallelSampler : public Sampler {
   bool big_runtime_sp = false;    // MVC_BIG_RUNTIME_SP=1: the dish-block producer's runtime k-step loop only (tests, A/B)
   int big_bpc_narrow = 3;         // MVC_BIG_BPC: 4-wave blocks per CU of the dish-block producer's 16 / 32-dish instances
   int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
+  bool run_limit_set = false;     // MVC_RUN_LIMIT given (it then applies to small chains too)
   int small_n_no_windows = 0;     // MVC_SMALL_N: chains up to this n never use grid windows (off: at N = 200 windows are faster)
   // MVC_RUN_WAVES: customers the run kernel evaluates per step.  4 by default:
   // one evaluating wave per SIMD (a second wave on a SIMD halves the first
@@ -2426,6 +2427,11 @@ class ParallelSampler : public Sampler {
   bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
   int run_grow_first = 0;         // MVC_RUN_GROW=0: the run kernel's LDS layout with room for T / 2 more tables only
   bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
+  // Small chains (n <= small_n_plain, MVC_SMALL_N_PLAIN): the lane-column loop without value
+  // prediction and a stay limit of 16. At the reference's own call (N = 200, V = 5) the
+  // prediction waves' overlay evaluation costs more per step than the steps it saves
+  // (1,578 -> 2,262 sweeps/s, profiles/r5af_*); at N = 1M (the literal) it is worth 1.5x.
+  int small_n_plain = 1024;
   bool vp_stats = false;          // MVC_VP_STATS=1
 
   // MVC_DEBUG_SYNC=1: wait for the launch just made and name it in the error;
@@ -2646,13 +2652,14 @@ class ParallelSampler : public Sampler {
 #undef MVC_LPBIG_FNS
     if (const char *e = getenv("MVC_BIG_RUNTIME_SP")) big_runtime_sp = e[0] == '1';
     if (const char *e = getenv("MVC_BIG_BPC")) big_bpc_narrow = std::max(1, std::min(4, atoi(e)));
-    if (const char *e = getenv("MVC_RUN_LIMIT")) run_limit = std::max(1, atoi(e));
+    if (const char *e = getenv("MVC_RUN_LIMIT")) { run_limit = std::max(1, atoi(e)); run_limit_set = true; }
     if (const char *e = getenv("MVC_SMALL_N")) small_n_no_windows = atoi(e);
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
     if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
     if (const char *e = getenv("MVC_RUN_GROW")) run_grow_first = e[0] == '0' ? 1 : 0;
     if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
+    if (const char *e = getenv("MVC_SMALL_N_PLAIN")) small_n_plain = atoi(e);
     if (const char *e = getenv("MVC_VP_STATS")) vp_stats = e[0] == '1';
     if (const char *e = getenv("MVC_WIDE")) {
       use_wide = e[0] != '0';
@@ -3305,7 +3312,7 @@ class ParallelSampler : public Sampler {
     SeqLds L{};
     // small chains: the run kernel walks the whole sweep (a window round is a
     // launch triple and a host read-back, more than the steps it saves)
-    L.limit = (n <= small_n_no_windows) ? kNoWindows : run_limit;
+    L.limit = (n <= small_n_no_windows) ? kNoWindows : (n <= small_n_plain && !run_limit_set) ? 16 : run_limit;
     // in order of preference: S1 cached with room to double (a cold sweep's
     // births then rarely restride; in a chain batch a restride ends the round
     // for every chain), S1 cached with room to grow by half, then without S1,
@@ -3345,7 +3352,7 @@ class ParallelSampler : public Sampler {
         // value prediction (lc == 2) where its overlay fits: V <= kVpV, every dish list <= 128, and the
         // overlay's S1 columns [kVpE][D] after the ring (which follows the clamped nws scratches)
         L.vpo = L.cache_dbl + (int64_t)L.nws * L.stride + (int64_t)rn * slot;
-        if (L.lc && use_vp && vp_ok && V <= kVpV && kmax <= 128 && L.nws >= kSeqLcThreads / 64 &&
+        if (L.lc && use_vp && vp_ok && n > small_n_plain && V <= kVpV && kmax <= 128 && L.nws >= kSeqLcThreads / 64 &&
             left - (int64_t)rn * slot >= (int64_t)kVpE * D)
           L.lc = 2;
         return L;

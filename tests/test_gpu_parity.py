@@ -727,7 +727,8 @@ print("last-birth OK", last)
 """
 
 
-def test_last_customer_birth_with_poisoned_lds():
+@pytest.mark.parametrize("vp", ["0", "1"])
+def test_last_customer_birth_with_poisoned_lds(vp):
     """Regression test of the round-3 multi-chain fault: a
     birth decided for the sweep's LAST customer is committed by the birth
     kernel, and the next repair round's run kernel then starts at cur == n.
@@ -745,7 +746,9 @@ def test_last_customer_birth_with_poisoned_lds():
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MVC_LDS_FILL="0xA5", MVC_RUN_CHECK="1")
+    # vp = "1": value prediction at N = 200 too (small chains run the plain
+    # lane-column loop by default, MVC_SMALL_N_PLAIN), the loop the fault was in
+    env = dict(os.environ, MVC_LDS_FILL="0xA5", MVC_RUN_CHECK="1", MVC_SMALL_N_PLAIN="0" if vp == "1" else "1024")
     env.pop("MVC_CHAIN_THREADS", None)
     env.pop("MVC_VP", None)
     r = subprocess.run([sys.executable, "-c", _LAST_BIRTH_CHILD, root], capture_output=True, text=True, timeout=240,
