@@ -1998,18 +1998,30 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
   if (A.gate && !(A.gate->done && A.gate->moves == 0 && A.gate->overflow == 0 && A.gate->restride == 0)) return;
   const int T = A.status[0];
   __shared__ int s_koff[MVC_MAXV + 1];
+  __shared__ int s_kact[MVC_MAXV];
+  __shared__ double s_hyp[3 * MVC_MAXV + 2];   // the sweep's hyperparameters (the MH's updates written through)
+  // The view offsets, the hyperparameters and this thread's first table
+  // count are loaded together (one memory latency, not one per view).
+  if (tid < V) s_kact[tid] = P.Kact[tid];
+  for (int k = tid; k < 3 * V + 2; k += kHypThreads) s_hyp[k] = P.hyper[k];
+  const int nt_me = P.n_t[max(0, min(tid, T - 1))];
+  __syncthreads();
+  if (tid == 0) {
+    s_koff[0] = 0;
+    for (int v = 0; v < V; ++v) s_koff[v + 1] = s_koff[v] + s_kact[v];
+  }
+  __syncthreads();
   // ---- Q = ||S1||^2 per live dish (fma chain in d order), all views at once;
-  //      the strided S1 loads are issued 16 ahead of the chain ----
+  //      the strided S1 loads are issued 16 ahead of the chain.  The thread's
+  //      first dish keeps Q and its member count for the coefficients below ----
+  double q_me = 0.0;
+  int dn_me = 0;
   {
-    if (tid == 0) {
-      s_koff[0] = 0;
-      for (int v = 0; v < V; ++v) s_koff[v + 1] = s_koff[v] + P.Kact[v];
-    }
-    __syncthreads();
     for (int k = tid; k < s_koff[V]; k += kHypThreads) {
       int v = 0;
       while (k >= s_koff[v + 1]) ++v;
       const int j = k - s_koff[v];
+      if (k == tid) dn_me = P.d_n[v * KC + j];
       const double *col = P.S1T + (size_t)v * D * KC + j;
       double q = 0.0;
       int d = 0;
@@ -2025,12 +2037,13 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
         q = __builtin_fma(x, x, q);
       }
       P.Q[v * KC + j] = q;
+      if (k == tid) q_me = q;
     }
   }
   {   // integer sums (order-free): L_v = sum of the view's table counts, tables non-empty
     const int lane = tid & 63, w = tid >> 6;
     for (int v = w; v <= V; v += kHypWaves) {
-      const int m = v < V ? P.Kact[v] : T;
+      const int m = v < V ? s_kact[v] : T;
       int acc = 0;
       for (int j = lane; j < m; j += 64) acc += v < V ? P.d_l[v * KC + j] : (P.n_t[j] > 0 ? 1 : 0);
       for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -2042,7 +2055,8 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
   }
   __syncthreads();
   HYP_MARK("q+sums");
-  double *hyp = P.hyper;
+  const double *hyp = s_hyp;
+  auto put_hyp = [&](int k, double x) { s_hyp[k] = x; P.hyper[k] = x; };
   if (A.do_mh) {
     // Every MH step draws from its own window of the MH counter (oracle
     // update_hyper): tau of view v at 3v, alpha/sigma of view v at 3V + 6v,
@@ -2078,10 +2092,15 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
       if (a <= -s) return -MVC_PM_INF;
       // any term a + j s <= 0 ?  (monotone in j for s > 0: check j = 0)
       if (K > 0 && !(a + 0.0 * s > 0.0)) return -MVC_PM_INF;
-      const double P1 = tree(K, [&](int64_t j) { return mvc_log(a + (double)j * s); });
-      const double P2 = mvc_lgamma_pos(a + (double)tot) - mvc_lgamma_pos(a + 1.0);
-      const double lg1 = mvc_lgamma_pos(1.0 - s);
-      const double P3 = tree(K, [&](int64_t j) { return mvc_lgamma_pos((double)size((int)j) - s) - lg1; });
+      const double P1 = tree(K, [&](int64_t j) { return mvc_log_nb(a + (double)j * s); });
+      // the three scalar log-gammas on lanes 0 / 1 / 2 of one branch-free
+      // evaluation (the same arguments and function, so the same values)
+      const int ql = threadIdx.x & 63;
+      const double qa = ql == 0 ? a + (double)tot : (ql == 1 ? a + 1.0 : 1.0 - s);
+      const double qg = mvc_lgamma_pos_nb(qa);
+      const double P2 = readlane_d(qg, 0) - readlane_d(qg, 1);
+      const double lg1 = readlane_d(qg, 2);
+      const double P3 = tree(K, [&](int64_t j) { return mvc_lgamma_pos_nb((double)size((int)j) - s) - lg1; });
       return (P1 - P2) + P3;
     };
     // ---- per-view steps, one wavefront per view (multiview_hyper.cpp:211-266)
@@ -2168,7 +2187,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
       };
       if (wv == kHypViewWaves && global_on_wave) {
         const auto g = global_pair(wtree);
-        if (lane == 0) { hyp[3 * V] = g.first; hyp[3 * V + 1] = g.second; }
+        if (lane == 0) { put_hyp(3 * V, g.first); put_hyp(3 * V + 1, g.second); }
       }
       for (int v = wv; v < V && wv < kHypViewWaves; v += kHypViewWaves) {
         const int Kv = P.Kact[v], Lv = P.Ltot[v];
@@ -2204,6 +2223,9 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
           return ll + prior;
         };
         // tau (multiview_hyper.cpp:211-231), counters 3v ..
+#ifdef MVC_HYP_PROF
+        const uint64_t tw0 = wall_clock64();
+#endif
         double tau_v = hyp[v];
         {
           const uint32_t k0 = 3u * (uint32_t)v;
@@ -2218,6 +2240,10 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
           }
         }
         // alpha_v, sigma_v (:239-266), counters 3V + 6v ..
+#ifdef MVC_HYP_PROF
+        const uint64_t tw1 = wall_clock64();
+        uint64_t tw2 = 0;
+#endif
         double a_v = hyp[V + v], s_v = hyp[2 * V + v];
         {
           const uint32_t k0 = 3u * (uint32_t)V + 6u * (uint32_t)v;
@@ -2230,6 +2256,9 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
           const double ln = (a_prop <= 0.0) ? -MVC_PM_INF : eppf_view(a_prop, s_v) + prior_alpha(a_prop);
           const double lq = mvc_log(a_prop) - mvc_log(a_old);
           if (mvc_log(unif_at(k0 + 2)) < (ln - lo) + lq) a_v = a_prop;
+#ifdef MVC_HYP_PROF
+          tw2 = wall_clock64();
+#endif
           const double s_old = s_v;
           const double s_prop = reflect_unit(s_old + rnorm_at(k0 + 3, 0.0, 0.05));
           const double u2 = unif_at(k0 + 5);
@@ -2237,7 +2266,12 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
           const double po = (s_old <= kEps || s_old >= 1.0 - kEps) ? -MVC_PM_INF : eppf_view(a_v, s_old) + prior_sigma(s_old);
           if (mvc_log(u2) < pn - po) s_v = s_prop;
         }
-        if (lane == 0) { hyp[v] = tau_v; hyp[V + v] = a_v; hyp[2 * V + v] = s_v; }
+        if (lane == 0) { put_hyp(v, tau_v); put_hyp(V + v, a_v); put_hyp(2 * V + v, s_v); }
+#ifdef MVC_HYP_PROF
+        if (lane == 0 && A.sweep == 5)
+          printf("hyp view %d: start %llu tau %llu alpha %llu sigma %llu\n", v, (unsigned long long)(tw0 - t0),
+                 (unsigned long long)(tw1 - t0), (unsigned long long)(tw2 - t0), (unsigned long long)(wall_clock64() - t0));
+#endif
       }
     }
     __syncthreads();
@@ -2247,7 +2281,7 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
       auto btree = [&](int64_t nn, auto leaf) -> double { return block_tree64(nn, leaf); };
       const auto g = global_pair(btree);
       __syncthreads();
-      if (tid == 0) { hyp[3 * V] = g.first; hyp[3 * V + 1] = g.second; }
+      if (tid == 0) { put_hyp(3 * V, g.first); put_hyp(3 * V + 1, g.second); }
     }
     __syncthreads();
   }
@@ -2266,12 +2300,13 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
     int v = 0;
     while (k >= s_koff[v + 1]) ++v;
     const int j = k - s_koff[v];
-    const Coef c = coef(P.d_n[v * KC + j], P.Q[v * KC + j], hyp[v], s_L2pt[v], D);
+    const bool mine = k == tid;   // (the Q loop's first dish of this thread)
+    const Coef c = coef(mine ? dn_me : P.d_n[v * KC + j], mine ? q_me : P.Q[v * KC + j], hyp[v], s_L2pt[v], D);
     P.c0[v * KC + j] = c.c0;
     P.cb[v * KC + j] = c.cb;
   }
   const double sg = hyp[3 * V + 1];
-  for (int p = tid; p < T; p += kHypThreads) P.lmass[p] = mvc_log((double)P.n_t[p] - sg);
+  for (int p = tid; p < T; p += kHypThreads) P.lmass[p] = mvc_log((double)(p == tid ? nt_me : P.n_t[p]) - sg);
   HYP_MARK("coef");
 #undef HYP_MARK
 }

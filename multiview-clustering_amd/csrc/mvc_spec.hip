@@ -21,6 +21,7 @@ extern "C" __global__ void mvc_spec_math_kernel(int op, const double *x, double 
       case 5: r = mvc_exp_sk(a); break;            // the fused kernel's variants
       case 6: r = mvc_log_nb(a); break;
       case 7: r = mvc_exp_le0(a); break;           // the draw's a - max form
+      case 8: r = mvc_lgamma_pos_nb(a); break;     // the MH kernel's EPPF form
       default: r = __builtin_sqrt(a); break;
     }
     o[i] = r;

@@ -425,7 +425,7 @@ def ari(a, b, device=0):
 
 
 def device_math(op, x, device=0):
-    ops = {"exp": 0, "log": 1, "lgamma": 2, "qnorm": 3, "sqrt": 4, "exp_sk": 5, "log_nb": 6, "exp_le0": 7}
+    ops = {"exp": 0, "log": 1, "lgamma": 2, "qnorm": 3, "sqrt": 4, "exp_sk": 5, "log_nb": 6, "exp_le0": 7, "lgamma_nb": 8}
     x = np.ascontiguousarray(x, dtype=np.float64)
     o = np.empty_like(x)
     buf = L.errbuf()

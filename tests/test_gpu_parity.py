@@ -46,6 +46,12 @@ def test_device_lgamma_qnorm_sqrt_bitwise():
     rng = np.random.default_rng(1)
     x = np.concatenate([rng.uniform(1e-6, 30, 100000), rng.uniform(30, 2e6, 100000)])
     assert np.array_equal(m.device_math("lgamma", x), O.pm_lgamma(x))
+    # the branch-free form (MH kernel): every recurrence length, tiny and huge arguments, the edges
+    xb = np.concatenate([x, rng.uniform(0, 13, 100000), 10.0 ** rng.uniform(-300, 300, 20000),
+                         [1e-320, 5e-324, 1.0, 2.0, 11.0, 11.999999999999998, 12.0, 12.000000000000002, 1e308]])
+    assert np.array_equal(m.device_math("lgamma_nb", xb), O.pm_lgamma(xb))
+    edge = np.array([0.0, -0.0, -1.0, np.inf, -np.inf, np.nan])
+    assert np.array_equal(m.device_math("lgamma_nb", edge), m.device_math("lgamma", edge), equal_nan=True)
     p = np.concatenate([rng.uniform(0, 1, 100000), 10.0 ** rng.uniform(-30, -1, 10000)])
     assert np.array_equal(m.device_math("qnorm", p), O.pm_qnorm(p))
     s = rng.uniform(0, 1e6, 100000)
