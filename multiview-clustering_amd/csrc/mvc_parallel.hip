@@ -3029,7 +3029,9 @@ class ParallelSampler : public Sampler {
     A.R = c.R;
     A.scr = seq_scr;
     A.scr_stride = seq_stride;
-    A.G = seq_waves;
+    // eval grid waves: one per scratch slot, and no more than one per customer
+    // (a small chain's windows cover the whole sweep; idle blocks cost dispatch)
+    A.G = std::min(seq_waves, std::max(4, (n + 3) / 4 * 4));
     A.Wmin = kSeqWmin;
     A.Wmax = kSeqWmax;
     A.seed = cfg.seed;
@@ -3429,7 +3431,7 @@ class ParallelSampler : public Sampler {
   void repair_start(Chain &c, uint32_t s, bool phaseA, RepairRun &rr, bool allow_early_mh = true) {
     timers.begin("repair", &rr.e1);
     rr.Q = make_seq(c, s);
-    rr.eg = dim3(seq_waves / 4);   // the eval grid: one wave per scratch slot (re-read after a capacity growth)
+    rr.eg = dim3(rr.Q.G / 4);   // the eval grid: SeqArgs.G waves (re-read after a capacity growth)
     const dim3 eb(256);
     if (phaseA)
       hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
@@ -3444,7 +3446,9 @@ class ParallelSampler : public Sampler {
     // repair and the MH separately (they would time the MH as repair)
     rr.early_mh = allow_early_mh && !early_mh_off && (!timers.on || timers.coarse);
     if (rr.early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
-    rr.rounds = 1;
+    // the first batch of rounds: one; small chains four (their repair
+    // usually takes 2-5 rounds, and a batch costs a host round trip)
+    rr.rounds = n <= small_n_plain ? 4 : 1;
   }
   // The run kernel's dynamic LDS for layout L.
   int64_t run_dyn(const SeqLds &L) const {
@@ -3517,7 +3521,7 @@ class ParallelSampler : public Sampler {
       rr.birth_retry = true;
       grow_capacity(rs.overflow);
       rr.Q = make_seq(c, s);
-      rr.eg = dim3(seq_waves / 4);   // the scratch may have fewer slots now
+      rr.eg = dim3(rr.Q.G / 4);   // the scratch may have fewer slots now
       return 0;
     }
     if (rs.vpoff && rr.vp_ok) {   // predictions missed (or a dish list outgrew them): plain lane columns
@@ -3964,7 +3968,7 @@ class ChainSet : public Sampler {
       int rounds = 1, bpc = 1 << 30;
       for (int c : act) {
         rounds = std::max(rounds, rr[c].rounds);
-        bpc = std::min(bpc, std::max(1, subs[c]->seq_waves / 4));
+        bpc = std::min(bpc, std::max(1, rr[c].Q.G / 4));
       }
       // the instances: 4 / 3 lane columns (+ value prediction), 0 one wave per
       // customer, 2 the block-wide evaluation; -1 launched per chain (grid-wide
