@@ -8,9 +8,9 @@ cat gpurun_out/${TAG}_newsim.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_nsprof -o run --output-format csv -- \
   python3 scripts/newsim_prof.py > gpurun_out/${TAG}_nsprof.log 2>&1 || { echo "ns prof failed"; exit 1; }
 grep newsim gpurun_out/${TAG}_nsprof.log
-python3 - <<'PY'
-import csv, glob, collections
-f = [p for p in glob.glob("gpurun_out/r5u_nsprof/**/*kernel_trace.csv", recursive=True)][0]
+TAG=$TAG python3 - <<'PY'
+import csv, glob, collections, os
+f = [p for p in glob.glob("gpurun_out/%s_nsprof/**/*kernel_trace.csv" % os.environ["TAG"], recursive=True)][0]
 rows = list(csv.DictReader(open(f)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 # the timed call's last 200 sweeps: kernel sequence and gaps between launches
