@@ -1267,6 +1267,66 @@ __device__ __forceinline__ void lc_view_terms(const SView &W, const double *yv, 
     cs = cs + w * mvc_exp_le0(lj[u] > 0 ? lp[u] - m : -MVC_PM_INF);
   }
 }
+// 8-lane rows (every K_v <= 8, V <= 8): one view per 8 lanes, so every view
+// of a customer in one pass instead of a pass per 4 views.  The values are
+// the 16-lane evaluation's: lanes 8..15 of a 16-lane row hold no dish there,
+// so their column partials are +0 and their maxima -inf and counts 0; the
+// row's pw16 is then the pw8 of columns 0..7 plus +0 (a non-negative sum:
+// the same value), its maximum and count those of the 8 lanes.
+__device__ __forceinline__ double row8_max_all(double x) {   // xor butterfly: every lane of the 8-group
+  x = dmax(x, dpp_d<0xB1>(x));    // quad_perm [1,0,3,2]
+  x = dmax(x, dpp_d<0x4E>(x));    // quad_perm [2,3,0,1]
+  x = dmax(x, dpp_d<0x141>(x));   // row_half_mirror: the sibling quad
+  return x;
+}
+__device__ __forceinline__ int row8_isum_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, true);
+  return x;
+}
+// pw8 of the 8-group's column partials (pairs (c, c + h), h = 1, 2, 4), valid
+// in the group's first lane
+__device__ __forceinline__ double row8_pw_head(double x) {
+  x = x + down_d<1>(x);
+  x = x + down_d<2>(x);
+  x = x + down_d<4>(x);
+  return x;
+}
+// lc_view_terms<1> on an 8-lane row (col = lane & 7, dish j = col)
+__device__ __forceinline__ void lc_view_terms8(const SView &W, const double *yv, const double *S1v, int s1s, int D, int vv,
+                                               int ks, int col, int K, int j0, int l0p, double hy, double h, double Y2i,
+                                               double lfn, double sigma, const int *dl, double *lpv, double &mx, int &cnt,
+                                               double &cs) {
+  const int jc = min(col, ks - 1);
+  double G = 0.0;
+  constexpr int DB = 16;
+  int d = 0;
+  for (; d + DB <= D; d += DB) {
+    double yd[DB], sd[DB];
+#pragma unroll
+    for (int k = 0; k < DB; ++k) {
+      yd[k] = yv[d + k];
+      sd[k] = S1v[(d + k) * s1s + jc];
+    }
+#pragma unroll
+    for (int k = 0; k < DB; ++k) G = __builtin_fma(yd[k], sd[k], G);
+  }
+  for (; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + jc], G);
+  const bool valid = col < K, own = col == j0;
+  const double self = lc_self<false>(W, vv, ks, j0, own ? G : 0.0, Y2i, hy, h, -1);
+  const double fr = __builtin_fma(G + hy, W.cb[vv * ks + jc], W.c0[vv * ks + jc]) + h;
+  const double lp = own ? self : fr;
+  const int lj = valid ? (own ? l0p : dl[jc]) : 0;
+  if (valid) lpv[lc_lpx(col)] = lp;
+  mx = row8_max_all((lj > 0 && lp > -MVC_PM_INF) ? lp : -MVC_PM_INF);   // (lc_view_terms: if (lp > mx) mx = lp)
+  cnt = row8_isum_dpp(lj > 0 ? 1 : 0);
+  const double m = lfn > mx ? lfn : mx;
+  double w = (double)lj - sigma;
+  if (w < 0.0) w = 0.0;
+  cs = 0.0 + w * mvc_exp_le0(lj > 0 ? lp - m : -MVC_PM_INF);
+}
+
 // The same for any K (more than 8 dishes per lane): one dish at a time.
 __device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double *yv, const double *S1v, int s1s, int D,
                                                 int vv, int ks, int col, int K, int j0, int l0p, double hy, double h,
@@ -1422,6 +1482,42 @@ __device__ __forceinline__ int seq_resample_lc(const SeqArgs &A, const SView &W,
   double s_new = 0.0, lmass0 = 0.0;
   const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);   // independent of the rest
   RUN_T0();
+  int kmx = 0;
+  for (int v = 0; v < V; ++v) kmx = max(kmx, W.Klist[v]);
+  if (!kVp && V <= 8 && kmx <= 8) {   // every view in one pass on 8-lane rows (the same values)
+    const int r8 = lane >> 3, c8 = lane & 7;
+    const int v = r8;
+    const bool vok = v < V;
+    const int vv = vok ? v : V - 1;
+    const int K = vok ? W.Klist[vv] : 0;
+    const double tau = hyp[vv], alpha = hyp[V + vv], sigma = hyp[2 * V + vv];
+    const double Y2i = C.Y2[vv * (int)C.y2stride];
+    const double hy = 0.5 * Y2i;
+    const double h = (-0.5 * Y2i) / tau;
+    const double lfn = cnewv[vv] + h;
+    const int j0 = W.dish[vv * ts + p0];
+    const int *dl = W.d_l + vv * ks;
+    const int l0p = dl[j0] - (alive ? 0 : 1);
+    double mx, cs;
+    int cnt;
+    lc_view_terms8(W, C.y + vv * (int)C.ystride, W.S1T + vv * D * s1s, s1s, D, vv, ks, c8, K, j0, l0p, hy, h, Y2i, lfn,
+                   sigma, dl, S.lp + vv * lps, mx, cnt, cs);
+    const double m = lfn > mx ? lfn : mx;
+    double Sv = row8_pw_head(cs);
+    double wn = alpha + (double)cnt * sigma;
+    if (wn < 0.0) wn = 0.0;
+    Sv = Sv + wn * mvc_exp_le0(lfn - m);
+    const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
+    double arg = c8 == 0 ? Sv : (c8 == 1 ? denom : 1.0);
+    if (r8 == 0 && c8 == 2) arg = ag + sg * (double)Tne_i;
+    if (r8 == 0 && c8 == 3) arg = mass0;
+    const double Lg = mvc_log(arg);
+    const double logden = down_d<1>(Lg);   // column 1's log, in column 0
+    const double lm = (denom <= 0.0) ? lfn : (m + Lg) - logden;   // valid in column 0
+    s_new = readlane_d(Lg, 2);
+    lmass0 = readlane_d(Lg, 3);
+    for (int r = 0; r < V; ++r) s_new = s_new + readlane_d(lm, 8 * r);   // view order
+  } else
   for (int g = 0; g < V; g += 4) {
     const int v = g + row;
     const bool vok = v < V;
