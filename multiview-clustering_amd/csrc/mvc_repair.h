@@ -1369,7 +1369,7 @@ __device__ __forceinline__ void lc_view_terms_loop(const SView &W, const double 
 // scratch e[]; block sums pw16 per row and running block totals C_b kept in
 // lane b.  kOne: one step covers every table (nch <= QB), so the scores stay
 // in registers between the two passes.  Same operations and order for every QB.
-template <int QB, bool kOne, bool kVp = false>
+template <int QB, bool kOne, bool kVp = false, int VC = 4>   // VC: views whose dish indices are loaded per round
 __device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScratch &S, int V, int ts, int lps, int p0,
                                                   int T, double sg, double lmass0, double s_new, double &M,
                                                   double &tot, double &Cb, const VpCtx &X) {
@@ -1393,22 +1393,22 @@ __device__ __forceinline__ void lc_scores_weights(const SView &W, const SeqScrat
       inc[h2] = p < T && np >= 1 && mass > 0.0;
       x[h2] = inc[h2] ? (p == p0 ? lmass0 : lmp) : -MVC_PM_INF;
     }
-    for (int v0 = 0; v0 < V; v0 += 4) {
-      int dj[QB][4];
+    for (int v0 = 0; v0 < V; v0 += VC) {
+      int dj[QB][VC];
 #pragma unroll
       for (int h2 = 0; h2 < QB; ++h2)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < VC; ++u)
           dj[h2][u] = (inc[h2] && v0 + u < V) ? W.dish[(v0 + u) * ts + pp[h2]] : 0;
-      double lv[QB][4];
+      double lv[QB][VC];
 #pragma unroll
       for (int h2 = 0; h2 < QB; ++h2)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + lc_lpx(dj[h2][u])];
+        for (int u = 0; u < VC; ++u) lv[h2][u] = S.lp[min(v0 + u, V - 1) * lps + lc_lpx(dj[h2][u])];
 #pragma unroll
       for (int h2 = 0; h2 < QB; ++h2)
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < VC; ++u)
           if (inc[h2] && v0 + u < V) x[h2] = x[h2] + lv[h2][u];   // view order
     }
 #pragma unroll
@@ -1581,7 +1581,9 @@ __device__ __forceinline__ int seq_resample_lc(const SeqArgs &A, const SView &W,
   // -inf when excluded; to the wave's scratch e[]
   const int T = *W.T, TB = (T + 15) >> 4, nch = (T + 63) >> 6;
   double M, tot, Cb;
-  if (nch <= 2)
+  if (nch <= 1)   // T <= 64: one chunk, every view's dish indices in one round when V <= 8
+    lc_scores_weights<1, true, kVp, 8>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb, X);
+  else if (nch <= 2)
     lc_scores_weights<2, true, kVp>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb, X);
   else if (nch <= 4)
     lc_scores_weights<4, true, kVp>(W, S, V, ts, lps, p0, T, sg, lmass0, s_new, M, tot, Cb, X);
