@@ -3193,8 +3193,16 @@ __device__ __forceinline__ int seq_run_loop_lc(SeqArgs &A, const SeqLds &L, cons
     __syncthreads();
     fill = landed = cur + 1;
   }
+  {   // the LDS layout must hold the current lists plus one birth.  Checked once:
+      // this loop commits moves only (a birth ends it), which add no table and
+      // no dish, so T and the dish lists stay as they are until it returns
+    bool bad = *cc.T >= L.ts;
+    for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks;
+    if (bad) flags |= kRunRestride;
+  }
   for (;;) {
     RUN_T0();
+    if (flags & kRunRestride) break;
     if (pend) {
       if (pc < 0) break;   // a birth: left pending for mvc_seq_birth_kernel (inlined here, the
                            // general commit costs the loop 184 B of scratch and flat accesses)
@@ -3211,14 +3219,6 @@ __device__ __forceinline__ int seq_run_loop_lc(SeqArgs &A, const SeqLds &L, cons
       }
       seq_bar(true);   // the commit, visible to every wave
       if (L.chk && mvc_run_bad[0]) break;
-    }
-    {   // the LDS layout must hold the current lists plus one birth
-      bool bad = *cc.T >= L.ts;
-      for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks;
-      if (bad) {
-        flags |= kRunRestride;
-        break;
-      }
     }
     RUN_MARK(4);
     const int i0 = cur;
@@ -3254,14 +3254,20 @@ __device__ __forceinline__ int seq_run_loop_lc(SeqArgs &A, const SeqLds &L, cons
     }
     seq_bar(true);
     RUN_MARK(5);
-    // every wave: the first customer whose choice is not its table
+    // every wave: the first customer whose choice is not its table (the step's
+    // choices read together, then the first mismatch below m by selects)
     const int m = min(L.nws, n - i0);
+    constexpr int kW = kSeqLcThreads / 64;
+    int chs[kW], p0s[kW];
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+      chs[k] = U.chb[par][k];
+      p0s[k] = U.p0b[par][k];
+    }
     int f = -1;
-    for (int k = 0; k < m; ++k)
-      if (U.chb[par][k] != U.p0b[par][k]) {
-        f = k;
-        break;
-      }
+#pragma unroll
+    for (int k = kW - 1; k >= 0; --k)
+      if (k < m && chs[k] != p0s[k]) f = k;
     if (f >= 0) {
       cur = i0 + f;
       pend = 1;
