@@ -4079,49 +4079,82 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel_b(const Se
 extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArgs A, int32_t *pos_new, int32_t *jmap) {
   Repair *R = A.R;
   ParState &P = A.P;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
   const int V = P.V, D = P.D, KC = P.KC, TC = P.TC;
   __shared__ int s_T, s_K[MVC_MAXV];
   if (!(R->done && R->moves > 0)) return;
   const int T = R->T;
-  if (tid == 0) {
-    int Tn = 0;
-    for (int p = 0; p < T; ++p) pos_new[p] = P.n_t[p] > 0 ? Tn++ : -1;
-    s_T = Tn;
-  } else if (tid <= V) {
-    const int v = tid - 1, K = R->Klist[v];
-    int Kn = 0;
-    for (int j = 0; j < K; ++j) {
-      const int e = v * KC + j;
-      if (P.d_l[e] > 0) {
-        jmap[e] = Kn;
-        const int o = v * KC + Kn;
-        P.d_id[o] = P.d_id[e];
-        P.d_n[o] = P.d_n[e];
-        P.d_l[o] = P.d_l[e];
-        P.S2[o] = P.S2[e];
-        ++Kn;
-      } else {
-        jmap[e] = -1;
-      }
+  const uint64_t below = (1ull << lane) - 1;   // lanes before this one
+  // In-place compactions in chunks of 64 entries per wave: each chunk's
+  // entries are read into registers before any of its writes, and an entry
+  // only moves down (its new position <= its old one), so no write of a
+  // chunk reaches an entry not yet read.  The surviving order is kept.
+  // 1. wave 0: the surviving tables' new positions; waves 1..: the dish
+  //    lists of the views (order kept), their rows moved down
+  if (w == 0) {
+    int base = 0;
+    for (int p0 = 0; p0 < T; p0 += 64) {
+      const int p = p0 + lane;
+      const bool alive = p < T && P.n_t[p] > 0;
+      const uint64_t m = __ballot(alive);
+      if (p < T) pos_new[p] = alive ? base + __builtin_popcountll(m & below) : -1;
+      base += __builtin_popcountll(m);
     }
-    s_K[v] = Kn;
+    if (lane == 0) s_T = base;
+  } else {
+    for (int v = w - 1; v < V; v += nw - 1) {
+      const int K = R->Klist[v];
+      int base = 0;
+      for (int j0 = 0; j0 < K; j0 += 64) {
+        const int j = j0 + lane, e = v * KC + j;
+        const bool in = j < K;
+        const int dl = in ? P.d_l[e] : 0;
+        const bool alive = in && dl > 0;
+        const int id = alive ? P.d_id[e] : 0, dn = alive ? P.d_n[e] : 0;
+        const double s2 = alive ? P.S2[e] : 0.0;
+        const uint64_t m = __ballot(alive);
+        const int o = base + __builtin_popcountll(m & below);
+        __builtin_amdgcn_s_waitcnt(0);   // the chunk read before it is written
+        if (in) jmap[e] = alive ? o : -1;
+        if (alive) {
+          const int eo = v * KC + o;
+          P.d_id[eo] = id;
+          P.d_n[eo] = dn;
+          P.d_l[eo] = dl;
+          P.S2[eo] = s2;
+        }
+        base += __builtin_popcountll(m);
+      }
+      if (lane == 0) s_K[v] = base;
+    }
   }
   __syncthreads();
-  for (int row = tid; row < V * D; row += blockDim.x) {
+  // 2. the S1 columns of the surviving dishes, one wave per (view, d) row
+  for (int row = w; row < V * D; row += nw) {
     const int v = row / D, K = R->Klist[v];
     double *col = P.S1T + (size_t)row * KC;
     const int32_t *jm = jmap + v * KC;
-    for (int j = 0; j < K; ++j)
-      if (jm[j] >= 0) col[jm[j]] = col[j];
+    for (int j0 = 0; j0 < K; j0 += 64) {
+      const int j = j0 + lane;
+      const int t = j < K ? jm[j] : -1;
+      const double x = t >= 0 ? col[j] : 0.0;
+      __builtin_amdgcn_s_waitcnt(0);
+      if (t >= 0) col[t] = x;
+    }
   }
-  if (tid < V) {
-    const int v = tid;
-    for (int p = 0; p < T; ++p)
-      if (pos_new[p] >= 0) P.dish[v * TC + pos_new[p]] = jmap[v * KC + P.dish[v * TC + p]];
-  } else if (tid == V) {
-    for (int p = 0; p < T; ++p)
-      if (pos_new[p] >= 0) P.n_t[pos_new[p]] = P.n_t[p];
+  // 3. the surviving tables' dishes (view v) and counts (task V)
+  for (int task = w; task <= V; task += nw) {
+    for (int p0 = 0; p0 < T; p0 += 64) {
+      const int p = p0 + lane;
+      const int q = p < T ? pos_new[p] : -1;
+      int x = 0;
+      if (q >= 0) x = task < V ? jmap[task * KC + P.dish[task * TC + p]] : P.n_t[p];
+      __builtin_amdgcn_s_waitcnt(0);
+      if (q >= 0) {
+        if (task < V) P.dish[task * TC + q] = x;
+        else P.n_t[q] = x;
+      }
+    }
   }
   __syncthreads();
   if (tid == 0) {
