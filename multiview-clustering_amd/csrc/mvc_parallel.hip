@@ -3444,7 +3444,9 @@ class ParallelSampler : public Sampler {
     rr.L = run_layout(c.T, c.K.data(), rr.vp_ok);
     // the gated early MH (below) only where no per-phase timers bracket the
     // repair and the MH separately (they would time the MH as repair)
-    rr.early_mh = allow_early_mh && !early_mh_off && (!timers.on || timers.coarse);
+    // (not for small chains: nearly every sweep of theirs moves someone, so the
+    // gated launch would be a no-op launch per sweep)
+    rr.early_mh = allow_early_mh && !early_mh_off && (!timers.on || timers.coarse) && n > small_n_plain;
     if (rr.early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
     // the first batch of rounds: one; small chains four (their repair
     // usually takes 2-5 rounds, and a batch costs a host round trip)
@@ -3540,9 +3542,13 @@ class ParallelSampler : public Sampler {
   void repair_finish(Chain &c, uint32_t s, RepairRun &rr, const Repair &rs, bool sync_status = true) {
     const bool moved = rs.moves > 0;
     if (moved) {
-      hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, rr.Q, c.pos_new, c.jmap);
-      hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
-                         stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
+      // small chains: the compaction block relabels z itself (one launch less per sweep)
+      const int relabel_in_block = n <= 16384 ? 1 : 0;
+      hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, rr.Q, c.pos_new, c.jmap,
+                         relabel_in_block);
+      if (!relabel_in_block)
+        hipLaunchKernelGGL(mvc_seq_relabel_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
+                           stream, n, c.P.z, (const int32_t *)c.pos_new, (const Repair *)c.R);
       MVC_HIP(hipGetLastError());
       dbg("seq_compact + relabel", c, s, false);
     }

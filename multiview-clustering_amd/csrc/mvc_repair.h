@@ -4076,7 +4076,10 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel_b(const Se
 // After the last repair step of a sweep that moved someone: drop dead tables
 // (order kept) and dead dishes (l = 0, order kept) in place (oracle
 // SeqSampler::compact).  pos_new [TC], jmap [V*KC].
-extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArgs A, int32_t *pos_new, int32_t *jmap) {
+// relabel != 0 (small n): the block also relabels z (mvc_seq_relabel_kernel's
+// work, without its launch).
+extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArgs A, int32_t *pos_new, int32_t *jmap,
+                                                                          int relabel) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
@@ -4156,6 +4159,8 @@ extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArg
       }
     }
   }
+  if (relabel)   // pos_new is complete (step 1, before the barrier above)
+    for (int i = tid; i < P.n; i += blockDim.x) P.z[i] = pos_new[P.z[i]];
   __syncthreads();
   if (tid == 0) {
     A.status[0] = s_T;
