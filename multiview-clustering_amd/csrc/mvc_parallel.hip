@@ -52,6 +52,7 @@ struct Sweep {
   int32_t T, sumK;
   uint64_t seed;
   uint32_t chain, sweep;
+  int32_t *fmin;          // non-null: the register draw reduces the first mover into it (mvc_seq_first_kernel's work)
 };
 
 }  // namespace
@@ -1259,7 +1260,12 @@ __global__ __launch_bounds__(256, MVC_ZDRAW_MINB) void mvc_par_zdraw_reg_kernel(
   const int li = blockIdx.x * blockDim.x + tid;   // one customer per thread (no loop-invariant hoisting)
   if (li >= nb) return;
   const LpRow row(lpb, (int)(lpb_index(li, 0, sumK) * 8));
-  A.choice[b0 + li] = zdraw_reg_one<TM>(A, Z, b0 + li, row, s_stage, tid & 63);
+  const int pick = zdraw_reg_one<TM>(A, Z, b0 + li, row, s_stage, tid & 63);
+  A.choice[b0 + li] = pick;
+  if (A.fmin) {   // the wave's first customer whose choice is not its table (a wave's customers are consecutive)
+    const uint64_t mv = __ballot(pick != P.z[b0 + li]);
+    if (mv && (tid & 63) == (int)__ffsll((long long)mv) - 1) atomicMin(A.fmin, b0 + li);
+  }
 }
 __host__ __device__ inline size_t zdraw_reg_shared_bytes(int V, int TM, int sumK) {
   return 8 * ((size_t)TM + (size_t)sumK + (size_t)4 * MVC_ZSTAGE * 64) +
@@ -2433,6 +2439,7 @@ class ParallelSampler : public Sampler {
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
   int shard_rank = 0, shard_world = 1;
+  bool first_in_draw = false;     // this sweep's register draw reduced the first mover into Repair::fmin
   int32_t *shard_exch = nullptr;
   int (*shard_cb)(void *) = nullptr;
   void *shard_user = nullptr;
@@ -3042,6 +3049,7 @@ class ParallelSampler : public Sampler {
 
   Sweep make_sweep(Chain &c, uint32_t s) {
     Sweep A;
+    A.fmin = nullptr;
     A.P = c.P;
     A.y = y;
     A.Y2 = Y2;
@@ -3268,6 +3276,9 @@ class ParallelSampler : public Sampler {
       timers.end("lp", el);
       timers.begin("draw", &ed);
       const dim3 zg((nb + 255) / 256);   // the register kernel takes one customer per thread
+      // the register draw finds the first mover itself when it sees every customer (no shard)
+      first_in_draw = use_zreg && shard_world == 1;
+      A.fmin = first_in_draw ? &c.R->fmin : nullptr;
       if (use_zreg && c.T <= 16)
         hipLaunchKernelGGL(mvc_par_zdraw_reg_kernel<16>, zg, dim3(256), zdraw_reg_shared_bytes(V, 16, sk), stream, A,
                            (int)b0, nb, (const double *)lpb);
@@ -3433,10 +3444,11 @@ class ParallelSampler : public Sampler {
     rr.Q = make_seq(c, s);
     rr.eg = dim3(rr.Q.G / 4);   // the eval grid: SeqArgs.G waves (re-read after a capacity growth)
     const dim3 eb(256);
-    if (phaseA)
-      hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
-                         stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
-    else
+    if (phaseA) {
+      if (!first_in_draw)
+        hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
+                           stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
+    } else
       hipLaunchKernelGGL(mvc_seq_eval_kernel, rr.eg, eb, 0, stream, rr.Q);
     MVC_HIP(hipGetLastError());
     dbg("seq_first / eval", c, s);
