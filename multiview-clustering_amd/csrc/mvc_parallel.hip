@@ -2474,6 +2474,7 @@ class ParallelSampler : public Sampler {
   // prediction waves' overlay evaluation costs more per step than the steps it saves
   // (1,578 -> 2,262 sweeps/s, profiles/r5af_*); at N = 1M (the literal) it is worth 1.5x.
   int small_n_plain = 1024;
+  int small_first_rounds = 4;     // MVC_SMALL_ROUNDS: the first batch of repair rounds of a small chain
   bool vp_stats = false;          // MVC_VP_STATS=1
 
   // MVC_DEBUG_SYNC=1: wait for the launch just made and name it in the error;
@@ -2702,6 +2703,7 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_RUN_GROW")) run_grow_first = e[0] == '0' ? 1 : 0;
     if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
     if (const char *e = getenv("MVC_SMALL_N_PLAIN")) small_n_plain = atoi(e);
+    if (const char *e = getenv("MVC_SMALL_ROUNDS")) small_first_rounds = std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("MVC_VP_STATS")) vp_stats = e[0] == '1';
     if (const char *e = getenv("MVC_WIDE")) {
       use_wide = e[0] != '0';
@@ -3462,7 +3464,7 @@ class ParallelSampler : public Sampler {
     if (rr.early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
     // the first batch of rounds: one; small chains four (their repair
     // usually takes 2-5 rounds, and a batch costs a host round trip)
-    rr.rounds = n <= small_n_plain ? 4 : 1;
+    rr.rounds = n <= small_n_plain ? small_first_rounds : 1;
   }
   // The run kernel's dynamic LDS for layout L.
   int64_t run_dyn(const SeqLds &L) const {
