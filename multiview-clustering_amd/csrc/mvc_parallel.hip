@@ -1969,6 +1969,36 @@ __device__ double block_tree64(int64_t n, F leaf) {
   return r;
 }
 
+// Four EPPF evaluations at once on one wave (the MH's speculative form for
+// small states, mvc_par_hyper_kernel): row r of the wave (lanes 16 r ..
+// 16 r + 15) evaluates the EPPF of a partition of K <= 16
+// blocks of sizes size(j) and total tot at (a[r], s[r]), exactly as the
+// kernel's eppf does with one wave: its tree64 sums have their leaves in
+// lanes 0..K-1 and +0 above (no partial sum is -0), so the row tree
+// (offsets 8, 4, 2, 1) is the wave tree's value (whose offsets 32 and 16 add
+// +0 there); the three scalar log-gammas on lanes 0 / 1 / 2 of the row.  E[r]
+// is the row's value, wave-uniform.  Only the arithmetic part: the callers
+// apply eppf's early returns per row.
+template <class F>
+__device__ __forceinline__ void eppf_rows4(int K, int tot, F size, const double (&a)[4], const double (&s)[4],
+                                           double (&E)[4]) {
+  const int lane = threadIdx.x & 63, r = lane >> 4, j = lane & 15;
+  double ar = a[0], sr = s[0];
+#pragma unroll
+  for (int q = 1; q < 4; ++q)
+    if (r == q) { ar = a[q]; sr = s[q]; }
+  const double l1 = j < K ? mvc_log_nb(ar + (double)j * sr) : 0.0;
+  const double qa = j == 0 ? ar + (double)tot : (j == 1 ? ar + 1.0 : 1.0 - sr);
+  const double qg = mvc_lgamma_pos_nb(qa);
+  const double P2 = row_bcast_d<0>(qg) - row_bcast_d<1>(qg);
+  const double lg1 = row_bcast_d<2>(qg);
+  const double l3 = j < K ? mvc_lgamma_pos_nb((double)size(min(j, K - 1)) - sr) - lg1 : 0.0;
+  const double P1 = row16_tree_sum(l1), P3 = row16_tree_sum(l3);
+  const double e = (P1 - P2) + P3;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) E[q] = readlane_d(e, 16 * q);
+}
+
 struct MHArgs {
   ParState P;
   int32_t *status;        // [V+3]: T, K[V], err, NB  -> we add T_ne at status[V+3]
@@ -2154,7 +2184,105 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
       if (mvc_log(u2) < pn - po) s_g = sg_prop;
       return std::make_pair(a_g, s_g);
     };
-    {
+    // The speculative form for small states (every dish list and the tables
+    // <= 16, V <= 7, every alpha > 0, the reference's own call at steady
+    // state): a step's two EPPF evaluations and the sigma step's two, for
+    // both outcomes of the alpha step, run at once on the four rows of one
+    // wave (eppf_rows4), the tau step's two posteriors on two rows; then the
+    // same accept decisions on the same values.  With alpha > 0 the alpha
+    // step's "old" value is the current alpha, so the sigma step's EPPFs are
+    // two of the four rows whichever way the alpha step went.
+    bool fast = V <= kHypViewWaves && T <= 16 && hyp[3 * V] > 0.0;
+    for (int v = 0; v < V; ++v) fast = fast && s_kact[v] <= 16 && hyp[V + v] > 0.0;
+    if (fast) {
+      const int lane = tid & 63, wv = tid >> 6, row = lane >> 4, j = lane & 15;
+      if (wv < V) {   // view wv
+        const int v = wv;
+        const int Kv = s_kact[v], Lv = P.Ltot[v];
+        const uint32_t kt = 3u * (uint32_t)v, ka = 3u * (uint32_t)V + 6u * (uint32_t)v;
+        const double zt = rnorm_at(kt, 0.0, 0.3), za = rnorm_at(ka, 0.0, 0.1), zs = rnorm_at(ka + 3, 0.0, 0.05);
+        // tau (multiview_hyper.cpp:211-231): rows 0 / 1 the posterior at t_old / t_prop
+        double tau_v = hyp[v];
+        double t_old = tau_v;
+        if (t_old <= 0.0) t_old = kEps;
+        const double t_prop = mvc_exp(mvc_log(t_old) + zt);
+        {
+          const double t = row == 0 ? t_old : t_prop;
+          const double L = mvc_log((2.0 * MVC_PI) * t);
+          const int jj = min(j, max(Kv - 1, 0));
+          const int nk = P.d_n[v * KC + jj];
+          double leaf = 0.0;
+          if (j < Kv && nk != 0) {
+            double sse = P.S2[v * KC + jj] - P.Q[v * KC + jj] / (double)nk;
+            if (sse < 0.0) sse = 0.0;
+            leaf = ((-0.5 * (double)nk) * (double)D) * L - 0.5 * (sse / t);
+          }
+          const double ll = row16_tree_sum(leaf);
+          const double post = ll + ((-3.0 * mvc_log(t)) - 1.0 / t);
+          const double l_old = readlane_d(post, 0), l_new = readlane_d(post, 16);
+          if (t_prop > 0.0) {
+            const double acc = (l_new - l_old) + (mvc_log(t_prop) - mvc_log(t_old));
+            if (mvc_log(unif_at(kt + 2)) < acc) tau_v = t_prop;
+          }
+        }
+        // alpha_v, sigma_v (:239-266)
+        const double a_orig = hyp[V + v], s_v0 = hyp[2 * V + v];
+        const double a_old = a_orig;   // > 0 (the fast form's condition)
+        double a_prop = mvc_exp(mvc_log(a_old > kEps ? a_old : kEps) + za);
+        if (!(a_prop > kEps)) a_prop = kEps;
+        const double s_prop = reflect_unit(s_v0 + zs);
+        const double ar[4] = {a_old, a_prop, a_orig, a_prop}, sr[4] = {s_v0, s_v0, s_prop, s_prop};
+        double E[4];
+        eppf_rows4(Kv, Lv, [&](int jj) { return P.d_l[v * KC + jj]; }, ar, sr, E);
+        auto ev = [&](int q) -> double {   // eppf_view's early returns
+          if (!(sr[q] > kEps && sr[q] < 1.0 - kEps)) return -MVC_PM_INF;
+          if (ar[q] <= -sr[q]) return -MVC_PM_INF;
+          if (Lv == 0) return 0.0;
+          if (Kv > 0 && !(ar[q] + 0.0 * sr[q] > 0.0)) return -MVC_PM_INF;
+          return E[q];
+        };
+        double a_v = a_orig, s_v = s_v0;
+        const double lo = ev(0) + prior_alpha(a_old);
+        const double ln = ev(1) + prior_alpha(a_prop);
+        const double lq = mvc_log(a_prop) - mvc_log(a_old);
+        const bool took = mvc_log(unif_at(ka + 2)) < (ln - lo) + lq;
+        if (took) a_v = a_prop;
+        const double u2 = unif_at(ka + 5);
+        const double pn = (s_prop <= kEps || s_prop >= 1.0 - kEps) ? -MVC_PM_INF : ev(took ? 3 : 2) + prior_sigma(s_prop);
+        const double po = (s_v0 <= kEps || s_v0 >= 1.0 - kEps) ? -MVC_PM_INF : ev(took ? 1 : 0) + prior_sigma(s_v0);
+        if (mvc_log(u2) < pn - po) s_v = s_prop;
+        if (lane == 0) { put_hyp(v, tau_v); put_hyp(V + v, a_v); put_hyp(2 * V + v, s_v); }
+      } else if (wv == kHypViewWaves) {   // the global pair (:268-291), counters 9V ..
+        const uint32_t k0 = 9u * (uint32_t)V;
+        const double za = rnorm_at(k0, 0.0, 0.1), zs = rnorm_at(k0 + 3, 0.0, 0.05);
+        const double ag_orig = hyp[3 * V], sg0 = hyp[3 * V + 1];
+        const double ag_old = ag_orig;   // > 0
+        double ag_prop = mvc_exp(mvc_log(ag_old > kEps ? ag_old : kEps) + za);
+        if (!(ag_prop > kEps)) ag_prop = kEps;
+        const double sg_prop = reflect_unit(sg0 + zs);
+        const double ar[4] = {ag_old, ag_prop, ag_orig, ag_prop}, sr[4] = {sg0, sg0, sg_prop, sg_prop};
+        double E[4];
+        eppf_rows4(T, n, [&](int p) { return P.n_t[p]; }, ar, sr, E);
+        auto eg = [&](int q) -> double {   // eppf_global's and eppf's early returns
+          if (!(sr[q] > kEps && sr[q] < 1.0 - kEps)) return -MVC_PM_INF;
+          if (ar[q] <= -sr[q]) return -MVC_PM_INF;
+          if (T <= 0) return 0.0;
+          if (!(ar[q] + 0.0 * sr[q] > 0.0)) return -MVC_PM_INF;
+          return E[q];
+        };
+        const double lo = eg(0) + prior_alpha(ag_old);
+        const double ln = eg(1) + prior_alpha(ag_prop);
+        const double lq = mvc_log(ag_prop) - mvc_log(ag_old);
+        double a_g = ag_orig, s_g = sg0;
+        const bool took = mvc_log(unif_at(k0 + 2)) < (ln - lo) + lq;
+        if (took) a_g = ag_prop;
+        const double u2 = unif_at(k0 + 5);
+        const double pn = (sg_prop <= kEps || sg_prop >= 1.0 - kEps) ? -MVC_PM_INF : eg(took ? 3 : 2) + prior_sigma(sg_prop);
+        const double po = (sg0 <= kEps || sg0 >= 1.0 - kEps) ? -MVC_PM_INF : eg(took ? 1 : 0) + prior_sigma(sg0);
+        if (mvc_log(u2) < pn - po) s_g = sg_prop;
+        if (lane == 0) { put_hyp(3 * V, a_g); put_hyp(3 * V + 1, s_g); }
+      }
+    } else {
       __shared__ double s_wpart[kHypWaves][64];
       __shared__ double s_wpart2[kHypWaves][64];
       const int lane = tid & 63, wv = tid >> 6;
@@ -2342,6 +2470,9 @@ constexpr int kSeqWmin = 1024;     // repair window after a mover
 constexpr int kSeqWmax = 1 << 16;  // cap of the window doubling over mover-free stretches
 constexpr int kSeqRunLimit = 64;   // stays in a row after which the run kernel hands over to grid windows
 constexpr size_t kSeqLdsBudget = 150 * 1024;   // run kernel: per-wave LDS scratch of all its waves
+// the lane-per-customer loop of small chains (mvc_seq_run_kernel<5>): customers,
+// dims, tables (its evaluation's registers) and dishes per view it takes on
+constexpr int kLaneMaxN = 1024, kLaneMaxD = 16, kLaneMaxV = 8, kLaneTM = 32, kLaneMaxK = 32;   // (V: one view per lane of 8)
 constexpr int kWideGridMax = 256;  // grid-wide evaluation: at most this many blocks per customer
 constexpr int kWideBatch = 32;     // grid-wide evaluation: customers (lp + fin pairs) per repair round
 constexpr int kWideFinLds = 152 * 1024;   // the fin kernel's dynamic LDS (wide_fin_resample: dish list, block totals)
@@ -2467,6 +2598,8 @@ class ParallelSampler : public Sampler {
   bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
   bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
   bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
+  bool use_lane = true;           // MVC_LC=col: no lane-per-customer loop for small chains (lane columns instead)
+  bool lane_now = false;          // this sweep runs the lane-per-customer loop (sweep_pre)
   int run_grow_first = 0;         // MVC_RUN_GROW=0: the run kernel's LDS layout with room for T / 2 more tables only
   bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
   // Small chains (n <= small_n_plain, MVC_SMALL_N_PLAIN): the lane-column loop without value
@@ -2673,8 +2806,9 @@ class ParallelSampler : public Sampler {
     lpall_attr<16, 8>();
     // (instance 2 runs the global-scratch layout only: no dynamic LDS)
     for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>,
-                          (const void *)mvc_seq_run_kernel<4>, (const void *)mvc_seq_run_kernel_b<0>,
-                          (const void *)mvc_seq_run_kernel_b<3>, (const void *)mvc_seq_run_kernel_b<4>})
+                          (const void *)mvc_seq_run_kernel<4>, (const void *)mvc_seq_run_kernel<5>,
+                          (const void *)mvc_seq_run_kernel_b<0>, (const void *)mvc_seq_run_kernel_b<3>,
+                          (const void *)mvc_seq_run_kernel_b<4>, (const void *)mvc_seq_run_kernel_b<5>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_wide_fin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kWideFinLds));
@@ -2699,7 +2833,10 @@ class ParallelSampler : public Sampler {
     if (const char *e = getenv("MVC_SMALL_N")) small_n_no_windows = atoi(e);
     if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
     if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
-    if (const char *e = getenv("MVC_LC")) use_lc = e[0] != '0';
+    if (const char *e = getenv("MVC_LC")) {   // 0: neither lane-column nor lane loop; col: lane columns only
+      use_lc = e[0] != '0';
+      use_lane = use_lc && e[0] != 'c';
+    }
     if (const char *e = getenv("MVC_RUN_GROW")) run_grow_first = e[0] == '0' ? 1 : 0;
     if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
     if (const char *e = getenv("MVC_SMALL_N_PLAIN")) small_n_plain = atoi(e);
@@ -3134,9 +3271,17 @@ class ParallelSampler : public Sampler {
   bool sweep_pre(Chain &c, uint32_t s, bool &phaseA_out) {
     Sweep A = make_sweep(c, s);
     const SeqArgs Q0 = make_seq(c, s);
-    hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0);
+    // small chains: the run kernel's lane-per-customer loop runs the whole
+    // sweep from customer 0 (its first step is phase A)
+    lane_now = lane_sweep(c);
+    hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0, lane_now ? 1 : 0);
     MVC_HIP(hipGetLastError());
     dbg("seq_init", c, s);
+    if (lane_now) {
+      zpath = 32 | 256;
+      phaseA_out = false;
+      return true;
+    }
     hipEvent_t e0 = nullptr;
     // phase 1 in customer batches: lp producer (MFMA or generic), then draw
     int Kmax = 0, Kmin = 1 << 30;
@@ -3164,9 +3309,10 @@ class ParallelSampler : public Sampler {
     const size_t need = (nbatch_sz / 64) * per64;
     const bool use_zreg = !force_zdraw_lds && !force_zdraw_row && c.T <= 64 && Kmax <= 64 && sk <= MVC_Z_VMAX * 64 &&
                           zdraw_reg_shared_bytes(V, 64, sk) <= 64 * 1024;
-    // the row draw (16 lanes per customer) where the register draw does not apply
+    // the row draw (16 lanes per customer) where the register draw does not
+    // apply; lane v of a customer's row holds view v's scalars, so V <= 16
     const int row_nb = c.T <= 64 ? 4 : c.T <= 128 ? 8 : c.T <= 256 ? 16 : 32;
-    const bool use_zrow = !use_zreg && !force_zdraw_lds && c.T <= 512 &&
+    const bool use_zrow = !use_zreg && !force_zdraw_lds && c.T <= 512 && V <= 16 &&
                           zdraw_row_shared_bytes(V, row_nb, sk, false) <= 64 * 1024;
     // the row draw with its slab in LDS where two blocks fit a CU
     const bool zrow_lds = use_zrow && !no_zrow_lds && zdraw_row_shared_bytes(V, row_nb, sk, true) <= 80 * 1024;
@@ -3352,6 +3498,40 @@ class ParallelSampler : public Sampler {
     return true;
   }
 
+  // The small chains' lane-per-customer loop (mvc_seq_run_kernel<5>, L.lc ==
+  // 3): the state cache with S1, tables up to kLaneTM (the evaluation's
+  // registers), dish lists with room to double, and a ring holding the whole
+  // sweep's rows; no per-wave scratch.  L.lc == 0: it does not fit.
+  SeqLds lane_layout(int T, const int32_t *Klist) const {
+    int kmax = 1;
+    for (int v = 0; v < V; ++v) kmax = std::max(kmax, (int)Klist[v]);
+    SeqLds L{};
+    L.limit = kNoWindows;
+    L.ks = (kmax + std::max(16, kmax) + 15) / 32 * 32 + 16;
+    L.ts = kLaneTM;
+    L.s1 = 1;
+    L.cache_dbl = seq_lds_cache(V, D, L.ks, L.ts, true);
+    L.stride = 0;
+    L.nws = kSeqLcThreads / 64;
+    int rn = 2;
+    while (rn < n) rn *= 2;
+    if (T >= L.ts || 8 * (L.cache_dbl + (int64_t)rn * seq_ring_slot(V, D)) > (int64_t)kSeqLdsBudget) return L;
+    L.lds = 1;
+    L.tw = 1;
+    L.ring = rn;
+    L.pfn = 0;
+    L.vpo = 0;
+    L.lc = 3;
+    return L;
+  }
+  bool lane_sweep(const Chain &c) const {
+    if (!use_lane || force_global || repair_grid_only || phase_a_only || shard_world > 1) return false;
+    if (n > kLaneMaxN || D > kLaneMaxD || V > kLaneMaxV || c.T >= kLaneTM) return false;
+    for (int k : c.K)
+      if (k > kLaneMaxK) return false;
+    return lane_layout(c.T, c.K.data()).lc == 3;
+  }
+
   // LDS layout of the run kernel's per-wave scratch for T tables and dish
   // lists Klist, with room for growth (a birth past it makes the kernel exit
   // with R->restride; the host then relaunches with a new layout).  Falls back
@@ -3450,12 +3630,12 @@ class ParallelSampler : public Sampler {
       if (!first_in_draw)
         hipLaunchKernelGGL(mvc_seq_first_kernel, dim3(std::max(1, std::min(1024, (n + 255) / 256))), dim3(256), 0,
                            stream, n, (const int32_t *)c.choice, (const int32_t *)c.P.z, c.R);
-    } else
+    } else if (!lane_now)
       hipLaunchKernelGGL(mvc_seq_eval_kernel, rr.eg, eb, 0, stream, rr.Q);
     MVC_HIP(hipGetLastError());
     dbg("seq_first / eval", c, s);
     rr.vp_ok = true;   // value prediction until it stops itself in this sweep (R->vpoff)
-    rr.L = run_layout(c.T, c.K.data(), rr.vp_ok);
+    rr.L = lane_now ? lane_layout(c.T, c.K.data()) : run_layout(c.T, c.K.data(), rr.vp_ok);
     // the gated early MH (below) only where no per-phase timers bracket the
     // repair and the MH separately (they would time the MH as repair)
     // (not for small chains: nearly every sweep of theirs moves someone, so the
@@ -3464,7 +3644,7 @@ class ParallelSampler : public Sampler {
     if (rr.early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
     // the first batch of rounds: one; small chains four (their repair
     // usually takes 2-5 rounds, and a batch costs a host round trip)
-    rr.rounds = n <= small_n_plain ? small_first_rounds : 1;
+    rr.rounds = (n <= small_n_plain && !lane_now) ? small_first_rounds : 1;
   }
   // The run kernel's dynamic LDS for layout L.
   int64_t run_dyn(const SeqLds &L) const {
@@ -3505,21 +3685,23 @@ class ParallelSampler : public Sampler {
         L.dyn = run_dyn(L);
         L.fill = lds_fill_byte();
         L.chk = run_check() ? 1 : 0;
-        hipLaunchKernelGGL(L.lc ? (L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
+        hipLaunchKernelGGL(L.lc ? (L.lc == 3 ? mvc_seq_run_kernel<5> : L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
                                 : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
                            dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, rr.Q, L);
       }
       MVC_HIP(hipGetLastError());
-      dbg(repair_grid_only ? "seq_apply" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
+      dbg(repair_grid_only ? "seq_apply" : L.lc == 3 ? "seq_run<5>" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
       if (L.lc && !repair_grid_only && rr.birth_retry) {   // a birth the loop left pending (births commit in the kernel)
         rr.birth_retry = false;
         hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, rr.Q);
         MVC_HIP(hipGetLastError());
         dbg("seq_birth", c, s);
       }
-      hipLaunchKernelGGL(mvc_seq_eval_kernel, rr.eg, eb, 0, stream, rr.Q);
-      MVC_HIP(hipGetLastError());
-      dbg("seq_eval", c, s);
+      if (!(L.lc == 3 && !repair_grid_only)) {   // (the lane loop opens no windows)
+        hipLaunchKernelGGL(mvc_seq_eval_kernel, rr.eg, eb, 0, stream, rr.Q);
+        MVC_HIP(hipGetLastError());
+        dbg("seq_eval", c, s);
+      }
     }
     MVC_HIP(hipGetLastError());
   }
@@ -3961,9 +4143,13 @@ class ChainSet : public Sampler {
     bA_dev = nullptr;
   }
   void sweep_batched() {
+    MVC_HIP(hipSetDevice(cfg.device));
     batch_alloc();
     const int C = (int)subs.size();
     hipStream_t bs = subs[0]->stream;   // the batch stream
+    Timers &tm = subs[0]->timers;       // the handle's "sweep" timer: batch stream, joined by every chain
+    hipEvent_t ev_sweep = nullptr;
+    tm.begin("sweep", &ev_sweep);
     std::vector<ParallelSampler::RepairRun> rr(C);
     std::vector<char> done(C, 0);
     // 1. phase A and the first mover, every chain on its own stream
@@ -3997,12 +4183,12 @@ class ChainSet : public Sampler {
       for (int c : act) {
         const ParallelSampler &S = *subs[c];
         const SeqLds &L = rr[c].L;
-        kinds[c] = (S.repair_grid_only || S.run_wgrid(L)) ? -1 : L.lc == 2 ? 4 : L.lc ? 3 : L.tw == 1 ? 0 : 2;
+        kinds[c] = (S.repair_grid_only || S.run_wgrid(L)) ? -1 : L.lc == 3 ? 5 : L.lc == 2 ? 4 : L.lc ? 3 : L.tw == 1 ? 0 : 2;
       }
       int nb = 0;   // batched members, grouped by kind
       std::vector<std::pair<int, int>> groups;   // (kind, first index), each up to the next
       std::vector<size_t> dyn;
-      for (int k : {4, 3, 0, 2}) {
+      for (int k : {5, 4, 3, 0, 2}) {
         const int first = nb;
         size_t dmax = 0;
         for (int c : act) {
@@ -4022,11 +4208,23 @@ class ChainSet : public Sampler {
           dyn.push_back(dmax);
         }
       }
-      // every active chain's arguments for the window evaluation (its wave
-      // stride set to the batched grid's) and the outcome gather
-      for (size_t j = 0; j < act.size(); ++j) {
-        bE_host[j] = rr[act[j]].Q;
-        bE_host[j].G = 4 * bpc;
+      // every active chain's arguments for the outcome gather, the batched
+      // chains first: only they take part in the batched window evaluation
+      // (its wave stride set to the batched grid's).  A chain launched on its
+      // own stream runs its own window evaluation inside repair_rounds; the
+      // batched one must not evaluate it concurrently.
+      // (the lane loop's chains, kind 5, open no windows: after the others)
+      std::vector<int> ord;
+      for (int c : act)
+        if (kinds[c] >= 0 && kinds[c] != 5) ord.push_back(c);
+      const int n_bat = (int)ord.size();
+      for (int c : act)
+        if (kinds[c] == 5) ord.push_back(c);
+      for (int c : act)
+        if (kinds[c] < 0) ord.push_back(c);
+      for (size_t j = 0; j < ord.size(); ++j) {
+        bE_host[j] = rr[ord[j]].Q;
+        if ((int)j < n_bat) bE_host[j].G = 4 * bpc;
       }
       if (nb) {
         MVC_HIP(hipMemcpyAsync(bA_dev, bA_host, sizeof(SeqArgs) * nb, hipMemcpyHostToDevice, bs));
@@ -4046,6 +4244,7 @@ class ChainSet : public Sampler {
           const SeqArgs *a = bA_dev + f;
           const SeqLds *l = bL_dev + f;
           switch (k) {
+            case 5: hipLaunchKernelGGL(mvc_seq_run_kernel_b<5>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
             case 4: hipLaunchKernelGGL(mvc_seq_run_kernel_b<4>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
             case 3: hipLaunchKernelGGL(mvc_seq_run_kernel_b<3>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
             case 0: hipLaunchKernelGGL(mvc_seq_run_kernel_b<0>, grid, dim3(kSeqRunThreads), dyn[g], bs, a, l); break;
@@ -4053,9 +4252,11 @@ class ChainSet : public Sampler {
           }
           MVC_HIP(hipGetLastError());
         }
-        hipLaunchKernelGGL(mvc_seq_eval_kernel_b, dim3((unsigned)(act.size() * bpc)), dim3(256), 0, bs,
-                           (const SeqArgs *)bE_dev, bpc);
-        MVC_HIP(hipGetLastError());
+        if (n_bat) {
+          hipLaunchKernelGGL(mvc_seq_eval_kernel_b, dim3((unsigned)(n_bat * bpc)), dim3(256), 0, bs,
+                             (const SeqArgs *)bE_dev, bpc);
+          MVC_HIP(hipGetLastError());
+        }
       }
       for (int c : act) {   // the others, one by one on their streams
         if (kinds[c] >= 0) continue;
@@ -4074,8 +4275,8 @@ class ChainSet : public Sampler {
       MVC_HIP(hipGetLastError());
       MVC_HIP(hipMemcpyAsync(bR_host, bR_dev, sizeof(Repair) * act.size(), hipMemcpyDeviceToHost, bs));
       MVC_HIP(hipStreamSynchronize(bs));
-      for (size_t j = 0; j < act.size(); ++j) {
-        const int c = act[j];
+      for (size_t j = 0; j < ord.size(); ++j) {
+        const int c = ord[j];
         ParallelSampler &S = *subs[c];
         rr[c].rounds = rounds;
         const int res = S.repair_outcome(S.chains[0], (uint32_t)S.sweeps_done, rr[c], bR_host[j]);
@@ -4099,6 +4300,13 @@ class ChainSet : public Sampler {
       if (S.status_pending) S.repair_status(S.chains[0]);
       S.sweeps_done += 1;
     }
+    if (tm.on && ev_sweep) {
+      for (int c = 1; c < C; ++c) {
+        MVC_HIP(hipEventRecord(b_ev[c], subs[c]->stream));
+        MVC_HIP(hipStreamWaitEvent(bs, b_ev[c], 0));
+      }
+    }
+    tm.end("sweep", ev_sweep);
   }
   void synchronize() override {
     for (auto &s : subs) s->synchronize();

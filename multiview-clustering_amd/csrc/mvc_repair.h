@@ -1742,14 +1742,17 @@ __device__ int seq_dish_draw_leaves(const SeqArgs &A, const SView &W, int i, int
 }  // namespace
 
 // Before phase A: the whole sweep is one pending window [0, n).
-extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
+// run_start: the sweep starts in the run kernel at customer 0 (the small
+// chains' lane-per-customer loop, whose first step is phase A) instead of a
+// window over the whole sweep.
+extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A, int run_start) {
   if (threadIdx.x != 0) return;
   Repair *R = A.R;
   const int V = A.P.V, n = A.P.n;
   R->cur = 0;
   R->pend = 0;
   R->win0 = 0;
-  R->win1 = n;
+  R->win1 = run_start ? 0 : n;
   R->fmin = n;
   R->W = A.Wmin;
   R->lastm = 0;
@@ -1759,7 +1762,7 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A) {
   R->vphits = 0;
   R->done = 0;
   R->overflow = 0;
-  R->mode = kSeqScan;
+  R->mode = run_start ? kSeqRun : kSeqScan;
   R->pchoice = 0;
   R->streak = 0;
   R->restride = 0;
@@ -3826,6 +3829,333 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
   return flags;
 }
 
+// ---- small chains: eight lanes per customer (L.lc == 3) ----
+//
+// The logs an evaluation shares with every other customer of the step,
+// computed once per wave, one per lane, into the wave's LDS row (the same
+// expressions, so the same values): k = v < V log(alpha_v + L_v), k = V + v
+// log(alpha_v + L_v - 1) (the own table dies), k = 2V / 2V + 1 log(ag + sg
+// T_ne) / log(ag + sg (T_ne - 1)), k = 2V + 2 + p log((n_p - 1) - sg) (the
+// own table without the customer).  Needs 2V + 2 + T <= 128.
+constexpr int kLanePre = 128;
+__shared__ double mvc_lane_pre[kSeqLcThreads / 64][kLanePre];
+struct LanePre {
+  const double *pre;   // this wave's row
+  __device__ __forceinline__ double at(int k) const { return pre[k]; }
+};
+__device__ __forceinline__ LanePre lane_pre(const SView &W, int V, const double *hyp) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double ag = hyp[3 * V], sg = hyp[3 * V + 1];
+  const int T = *W.T, T_ne = *W.T_ne;
+  double *row = mvc_lane_pre[w];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = 64 * h + lane;
+    double arg = 1.0;
+    if (k < 2 * V) {
+      const int v = k < V ? k : k - V;
+      arg = hyp[V + v] + (double)(W.Ltot[v] - (k < V ? 0 : 1));
+    } else if (k < 2 * V + 2) {
+      arg = ag + sg * (double)(T_ne - (k == 2 * V ? 0 : 1));
+    } else if (k < 2 * V + 2 + T) {
+      arg = (double)(W.n_t[k - 2 * V - 2] - 1) - sg;
+    }
+    row[k] = mvc_log(arg);
+  }
+  wave_lds_sync();
+  return LanePre{row};
+}
+
+// seq_resample for one customer on an 8-lane group of a wave, lane v of the
+// group owning view v (V <= 8), against the run kernel's LDS state: the same
+// decision, bit for bit, as the wave-shaped forms above,
+// because every reduction of the spec is either sequential per column or a
+// fixed tree that one lane walks itself, or a sum in view order taken over
+// the group's lanes in that order:
+//   * lane v, view v: the lp of every listed dish (the own dish j0
+//     self-removed, lc_self), the max over the included ones and the new
+//     dish, K_act; the column partials col_c = sum over j = c mod 16 in
+//     ascending j of w_j exp(lp_j - m) (excluded dishes add +0, as a lane
+//     column does), pw16 of the columns (pw16_seq: row_pw16's association),
+//     the new dish, lm_v; and lp of the dish of every table p < T;
+//   * every lane of the group: s_new and the table scores as sums in view
+//     order of the lanes' values (broadcast from lane v of the group), the
+//     weights exp(sp - M), block sums pw16 per 16 tables, running block
+//     totals in block order, the draw: the first block with r < C_b, then
+//     pw16_select inside it.  The group's lanes agree; lane 0's is used.
+// Every lane of the wave calls it (customers past n with a clamped index):
+// the broadcasts read other lanes.
+template <int TM>
+__device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0,
+                                                  const double *hyp, const double *cnewv, const LanePre &LP) {
+  static_assert(TM % 16 == 0 && TM <= 64, "TM: tables in registers, whole blocks of 16");
+  constexpr int NBk = TM / 16;
+  const int lane = threadIdx.x & 63, gb = lane & ~7, v = lane & 7;
+  const int V = A.P.V, D = A.P.D, ts = W.ts, ks = W.ks, s1s = W.s1s;
+  const bool vok = v < V;
+  const int vv = vok ? v : V - 1;
+  const double sg = hyp[3 * V + 1];
+  const int np0 = W.n_t[p0] - 1;
+  const bool alive = np0 > 0;
+  const int T = *W.T;
+  // ---- lane v: view v's terms and the lp of every table's dish
+  const int K = W.Klist[vv];
+  const double tau = hyp[vv], alpha = hyp[V + vv], sigma = hyp[2 * V + vv];
+  const double Y2i = C.Y2[vv * (int)C.y2stride];
+  const double hy = 0.5 * Y2i;
+  const double h = (-0.5 * Y2i) / tau;
+  const double lfn = cnewv[vv] + h;
+  const int j0 = W.dish[vv * ts + p0];
+  const int *dl = W.d_l + vv * ks;
+  const int l0p = dl[j0] - (alive ? 0 : 1);
+  const double *yv = C.y + vv * (int)C.ystride;
+  const double *S1v = W.S1T + (size_t)vv * D * s1s;
+  const double *cbv = W.cb + vv * ks, *c0v = W.c0 + vv * ks;
+  auto dot = [&](int j) {   // G = y . S1[:, j], one fma chain in ascending d
+    double G = 0.0;
+    for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j], G);
+    return G;
+  };
+  const double self = lc_self(W, vv, ks, j0, dot(j0), Y2i, hy, h);
+  auto lpj = [&](int j) { return j == j0 ? self : __builtin_fma(dot(j) + hy, cbv[j], c0v[j]) + h; };
+  double lm;
+  {
+    // pass 1: max over the included dishes, K_act; the first 16 lp kept
+    double lr[16];
+    double mx = -MVC_PM_INF;
+    int cnt = 0;
+    for (int t0 = 0; t0 < K; t0 += 16) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int j = t0 + c;
+        if (j < K) {
+          const double x = lpj(j);
+          if (t0 == 0) lr[c] = x;
+          const int l = j == j0 ? l0p : dl[j];
+          if (l > 0) {
+            ++cnt;
+            if (x > mx) mx = x;
+          }
+        }
+      }
+    }
+    const double m = lfn > mx ? lfn : mx;
+    // pass 2: column partials in ascending j
+    double col[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) col[c] = 0.0;
+    for (int t0 = 0; t0 < K; t0 += 16) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int j = t0 + c;
+        if (j < K) {
+          const double x = t0 == 0 ? lr[c] : lpj(j);
+          const int l = j == j0 ? l0p : dl[j];
+          double w = (double)l - sigma;
+          if (w < 0.0) w = 0.0;
+          col[c] = col[c] + w * mvc_exp_le0(l > 0 ? x - m : -MVC_PM_INF);
+        }
+      }
+    }
+    double Sv = pw16_seq(col);
+    double wn = alpha + (double)cnt * sigma;
+    if (wn < 0.0) wn = 0.0;
+    Sv = Sv + wn * mvc_exp_le0(lfn - m);
+    const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
+    const double logden = LP.at(alive ? vv : V + vv);
+    lm = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - logden;
+  }
+  double lt[TM];   // lp of table p's dish in this lane's view
+#pragma unroll
+  for (int p = 0; p < TM; ++p) lt[p] = p < T ? lpj(W.dish[vv * ts + p]) : 0.0;
+  // ---- the group: sums in view order over its lanes
+  double s_new = LP.at(alive ? 2 * V : 2 * V + 1);   // log(ag + sg T_ne')
+  for (int u = 0; u < V; ++u) s_new = s_new + __shfl(lm, gb + u, 64);
+  const double mass0 = (double)np0 - sg;
+  const double lmass0 = LP.at(2 * V + 2 + p0);   // log(mass0)
+  double sp[TM];
+  uint64_t inc = 0;   // tables included in the draw (n_p' >= 1, n_p' - sigma_g > 0)
+#pragma unroll
+  for (int p = 0; p < TM; ++p) {
+    sp[p] = -MVC_PM_INF;
+    if (p < T) {
+      const int np = W.n_t[p] - (p == p0 ? 1 : 0);
+      const double mass = (double)np - sg;
+      if (np >= 1 && mass > 0.0) {
+        sp[p] = (p == p0) ? lmass0 : W.lmass[p];
+        inc |= 1ull << p;
+      }
+    }
+  }
+  (void)mass0;
+  for (int u = 0; u < V; ++u) {
+#pragma unroll
+    for (int p = 0; p < TM; ++p) {
+      if (p < T) {
+        const double x = __shfl(lt[p], gb + u, 64);
+        if ((inc >> p) & 1ull) sp[p] = sp[p] + x;
+      }
+    }
+  }
+  double M = -MVC_PM_INF;
+#pragma unroll
+  for (int p = 0; p < TM; ++p)
+    if (p < T && sp[p] > M) M = sp[p];
+  if (s_new > M) M = s_new;
+  // weights in place (excluded tables and padding: +0), block sums, running block totals C_b
+  double tot = 0.0, Cb[NBk];
+#pragma unroll
+  for (int b = 0; b < NBk; ++b) {
+    Cb[b] = 0.0;
+    if (16 * b < T) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int p = 16 * b + q;
+        sp[p] = (p < T) ? mvc_exp_le0(sp[p] - M) : 0.0;   // excluded: exp(-inf) = +0
+      }
+      tot = tot + pw16_seq(sp + 16 * b);
+      Cb[b] = tot;
+    }
+  }
+  const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);
+  const double Wt = mvc_exp_le0(s_new - M) + tot;
+  double r = u_i * Wt;
+  if (!(r < tot)) return -1;   // the new table
+  int bsel = NBk - 1;
+#pragma unroll
+  for (int b = NBk - 1; b >= 0; --b)
+    if (16 * b < T && r < Cb[b]) bsel = b;
+  double cprev = 0.0;
+#pragma unroll
+  for (int b = 1; b < NBk; ++b)
+    if (b == bsel) cprev = Cb[b - 1];
+  r = r - (bsel > 0 ? cprev : 0.0);
+  double x16[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    x16[q] = sp[q];
+#pragma unroll
+    for (int b = 1; b < NBk; ++b)
+      if (b == bsel) x16[q] = sp[16 * b + q];
+  }
+  return 16 * bsel + pw16_select_seq(x16, r);
+}
+
+// The run kernel's loop for small chains (L.lc == 3): the whole sweep staged
+// in the ring (ring >= n), every 8-lane group of the block one customer of
+// the next 32, so a step evaluates 32 customers against the current state
+// (the first steps are phase A: no separate producer / draw / window
+// launches).  The first customer whose choice is not its table is the mover;
+// the ones before it are final.  Step = {commit; barrier; evaluate; barrier;
+// decide}, the cursor in registers (every wave derives it from the same LDS
+// values), the per-wave candidates double-buffered by step parity.  Moves are
+// committed by the four waves (seq_commit_move_split); a birth ends the loop
+// and seq_run_body commits it on the global state, then resumes here.
+constexpr int kLaneCust = kSeqLcThreads / 8;   // customers per step
+__device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U) {
+  constexpr int kW = kSeqLcThreads / 64;
+  int flags = 0;
+  const ParState &P = A.P;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int V = P.V, D = P.D, n = P.n;
+  const SCache cc = lds_cache(V, D, L.ts, L.ks, 1);
+  SView Wv = cache_view(cc, A);
+  Wv.S1T = cc.S1T;
+  Wv.s1s = cc.ks;
+  __shared__ int s_mv[2][kW][5];   // per wave: first mover (offset in the step, -1: none), its choice, table, n_t of both
+  int cur = U.cur, pend = U.pend, pc = U.pc, pp0 = U.pp0, done = U.done, par = 0;
+  int pnt0 = 0, pntc = 0;
+  if (pend && pc >= 0) {
+    pnt0 = cc.n_t[pp0];
+    pntc = cc.n_t[pc];
+  }
+  if (cur < n) {   // every remaining customer's row (ring >= n: one pass)
+    ring_fill_async<kW>(A, G, cur, n);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+  }
+  {   // the layout holds the lists plus one birth (moves add no table and no dish)
+    bool bad = *cc.T >= L.ts;
+    for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks;
+    if (bad) flags |= kRunRestride;
+  }
+  for (;;) {
+    if (flags & kRunRestride) break;
+    if (cur >= n) {
+      done = 1;
+      break;
+    }
+    if (pend) {
+      if (pc < 0) break;   // a birth: committed by seq_run_body
+      seq_commit_move_split(A, cc, G.cust(cur, V, D), cur, pp0, pc, pnt0, pntc, U.cnt, L.chk);
+      cur = cur + 1;
+      pend = 0;
+      if (cur >= n) {
+        done = 1;
+        break;
+      }
+      seq_bar(true);
+      if (L.chk && mvc_run_bad[0]) break;
+    }
+    const int q = tid >> 3;            // this group's customer in the step
+    const int i = cur + q;
+    const int ic = min(i, n - 1);      // (past n: a clamped customer, result unused)
+    const int p0 = ring_z(G, ic, V, D);
+    const LanePre LP = lane_pre(Wv, V, cc.hyp);
+    const int T = *cc.T;
+    int c;
+    if (T <= 16)
+      c = seq_resample_lane8<16>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+    else
+      c = seq_resample_lane8<32>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+    const bool mv = (lane & 7) == 0 && i < n && c != p0;
+    const uint64_t hit = __ballot(mv);
+    const int first = hit ? (int)__builtin_ctzll(hit) : 0;
+    if (lane == first) {
+      int *sm = s_mv[par][w];
+      sm[0] = hit ? q : -1;
+      sm[1] = c;
+      sm[2] = p0;
+      if (mv && c >= 0) {
+        sm[3] = cc.n_t[p0];
+        sm[4] = cc.n_t[c];
+      }
+    }
+    seq_bar(true);
+    int f = -1, fw = 0;
+#pragma unroll
+    for (int k = kW - 1; k >= 0; --k)
+      if (s_mv[par][k][0] >= 0) {
+        f = s_mv[par][k][0];
+        fw = k;
+      }
+    if (f >= 0) {
+      cur = cur + f;
+      pend = 1;
+      pc = s_mv[par][fw][1];
+      pp0 = s_mv[par][fw][2];
+      if (pc >= 0) {
+        pnt0 = s_mv[par][fw][3];
+        pntc = s_mv[par][fw][4];
+      }
+    } else {
+      cur = cur + kLaneCust;
+    }
+    par ^= 1;
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (tid == 0) {
+    U.cur = cur;
+    U.pend = pend;
+    U.pc = pc;
+    U.pp0 = pp0;
+    U.done = done;
+    U.fill = U.landed = n;
+  }
+  return flags;
+}
+
 }  // namespace
 
 // The run kernel (one block of kSeqRunThreads = 8 waves): the
@@ -3840,7 +4170,9 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
 // window (mvc_seq_eval_kernel) and exits; the next launch resolves it.
 // One instance per evaluation shape, compiled separately so each keeps its
 // own register allocation.
-template <int kMode>   // 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc); 4: + value prediction
+// kMode 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc == 1);
+// 4: + value prediction (L.lc == 2); 5: one customer per lane, small chains (L.lc == 3)
+template <int kMode>
 __device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
   Repair *R = A.R;
   ParState &P = A.P;
@@ -3963,6 +4295,8 @@ __device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
         flags = seq_run_loop_lc(A, L, G, U);
       else if constexpr (kMode == 4)
         flags = seq_run_loop_vp(A, L, G, U);
+      else if constexpr (kMode == 5)
+        flags = seq_run_loop_lane(A, L, G, U);
       else
         flags = seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
                                           SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),

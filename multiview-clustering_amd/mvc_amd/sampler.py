@@ -70,13 +70,30 @@ def make_config(n, V, D, M=0, burn_in=0, thin=1, seed=1999, n_chains=1, first_ch
 
 
 class _Samples(Sequence):
-    """The saved samples of one chain as a read-only list: item s is built
+    """The saved samples of one chain as a read-only sequence: item s is built
     from the chain's contiguous result block when it is read (the reference's
     R list holds S small vectors per chain; materialising them eagerly for
-    thousands of chains cost more than the sampling)."""
+    thousands of chains cost more than the sampling).
 
-    def __init__(self, count, item):
-        self._n, self._item = count, item
+    table_of: `block` is the [S, n] array, item s its row s.  dish_of:
+    `block` is the flat dish block, `starts` the offsets of the samples and
+    `Ts` their table counts, item s the list of V rows.  Items are read-only
+    views of the block; pickling (or `list(...)`) gives plain lists."""
+
+    def __init__(self, block, starts=None, Ts=None, V=0):
+        self._block = block
+        self._block.flags.writeable = False
+        self._starts, self._Ts, self._V = starts, Ts, V
+        self._n = block.shape[0] if starts is None else len(Ts)
+
+    def _item(self, k):
+        if self._starts is None:
+            return self._block[k]
+        d = self._block[self._starts[k]:self._starts[k + 1]].reshape(self._V, int(self._Ts[k]))
+        return [d[v] for v in range(self._V)]
+
+    def __reduce__(self):
+        return (list, (list(self),))
 
     def __len__(self):
         return self._n
@@ -149,14 +166,9 @@ def run_gibbs_cpp(data_views, M, burn_in, thin, seed=1999, mode="exact", n_chain
             st = lib.mvc_result_copy_chain(res, c, tab.ctypes.data_as(ip), None, dsh.ctypes.data_as(ip))
             if st != L.MVC_OK:
                 raise L.MvcError(st, f"mvc_result_copy_chain(chain {c}) failed")
-            table_of = _Samples(S, tab.__getitem__)
+            table_of = _Samples(tab)
             starts = np.concatenate(([0], np.cumsum(V * Ts.astype(np.int64))))
-
-            def dishes(s, dsh=dsh, starts=starts, Ts=Ts):
-                d = dsh[starts[s]:starts[s + 1]].reshape(V, int(Ts[s]))
-                return [d[v] for v in range(V)]
-
-            dish_of = _Samples(S, dishes)
+            dish_of = _Samples(dsh, starts, Ts, V)
 
             def tr(which, per_view):
                 p = lib.mvc_result_trace(res, c, which)

@@ -442,6 +442,36 @@ def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
         assert h["sigma_global"] == ref["sigma_global"][it]
 
 
+def test_many_views_row_draw_gate(monkeypatch):
+    """More than 16 views with 64 < T <= 512: the row draw keeps one view per
+    lane of a customer's 16-lane row, so it must not be selected (even under
+    MVC_ZDRAW_ROW=1); the checkpoint draw runs and the chain is bitwise the
+    oracle's."""
+    m = _mvc()
+    from mvc_amd import data
+    V, K = 18, 8
+    y, z = data.synthetic(1200, V, 16, 96, seed=77)
+    uniq, table_of = np.unique(z, return_inverse=True)
+    table_of = table_of.astype(np.int32)
+    T = uniq.size
+    assert 64 < T <= 512
+    dish = np.stack([np.arange(T) % max(1, K // (2 ** min(v, 3))) for v in range(V)]).astype(np.int32)
+    hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
+    st = (table_of, dish, hyper)
+    monkeypatch.setenv("MVC_ZDRAW_ROW", "1")
+    s = m.Sampler(y, seed=41, mode="parallel")
+    s.set_state(*st)
+    ref = O.run(y, 2, 0, 1, seed=41, mode=O.PARALLEL, state=st)
+    for it in range(2):
+        s.sweep(1)
+        if it == 0:
+            assert not s.zpath() & 128
+        t, d, h = s.state()
+        assert np.array_equal(t, ref["table_of"][it]), it
+        assert np.array_equal(d, ref["dish_of"][it]), it
+    s.close()
+
+
 # Phase A alone (mvc_sampler_phase_a) against the oracle's phase-A
 # conditional: ragged tile groups (n % 64 != 0), fewer tiles than waves,
 # T <= 16 / 64, the bench's dish pattern (64, 32, 16, 8) at D = 128 and
@@ -707,6 +737,40 @@ def test_chains_concurrent_equal_serial():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", _CHAINS_CHILD, root], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "chains OK" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
+
+
+@pytest.mark.parametrize("env", [
+    {"MVC_LC": "0"},                                  # batched kind 0: one wave per customer, LDS cache
+    {"MVC_RUN_LDS": "0", "MVC_WIDE": "0"},            # kind 0 on the global layout
+    {"MVC_RUN_LDS": "0", "MVC_WIDE": "block"},        # kind 2: the block-wide evaluation
+    {"MVC_RUN_LDS": "0"},                             # grid-wide evaluation: every chain on its own stream
+    {"MVC_REPAIR": "grid"},                           # grid windows only: every chain on its own stream
+], ids=["lc0", "global_tw1", "wide_block", "wide_grid", "grid_only"])
+def test_chains_batched_kinds_equal_alone(env, monkeypatch):
+    """The chain-batched repair with every run-kernel instance it can batch
+    (kinds 0 and 2) and with the chains it launches one by one on their own
+    streams (grid-wide evaluation, grid-only repair: their window evaluation
+    must not also run in the batched window launch) gives every chain bit for
+    bit as the same chain swept alone, through a cold start with births."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(1999)
+    C, M = 3, 6
+    conc = m.Sampler(y, seed=31, mode="parallel", n_chains=C)
+    conc.sweep(M)
+    for c in range(C):
+        one = m.Sampler(y, seed=31, mode="parallel", first_chain=c)
+        one.sweep(M)
+        t1, d1, h1 = one.state()
+        t, d, h = conc.state(chain=c)
+        assert np.array_equal(t, t1) and np.array_equal(d, d1), c
+        assert h["sigma_global"] == h1["sigma_global"] and np.array_equal(h["tau_v"], h1["tau_v"]), c
+        one.close()
+    ref = O.run(y, M, 0, 1, seed=31, chain=1, mode=O.PARALLEL)
+    assert np.array_equal(conc.state(chain=1)[0], ref["table_of"][-1])
+    conc.close()
 
 
 _LAST_BIRTH_CHILD = r"""

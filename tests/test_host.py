@@ -76,3 +76,27 @@ def test_bench_leg_failure_is_recorded_not_raised():
     import bench
     r = bench.child_leg("configs1_gpu", 1, 99, timeout=240)
     assert isinstance(r, dict) and "error" in r
+
+
+def test_saved_samples_are_read_only_and_picklable():
+    """run_gibbs_cpp's table_of / dish_of sequences (mvc_amd.sampler._Samples):
+    items are read-only views of the result block, and pickling gives plain
+    lists with the same values."""
+    import pickle
+    from mvc_amd.sampler import _Samples
+    tab = np.arange(12, dtype=np.int32).reshape(3, 4)
+    Ts = np.array([1, 2, 1], dtype=np.int32)
+    V = 2
+    dsh = np.arange(V * int(Ts.sum()), dtype=np.int32)
+    starts = np.concatenate(([0], np.cumsum(V * Ts.astype(np.int64))))
+    t, d = _Samples(tab), _Samples(dsh, starts, Ts, V)
+    assert len(t) == 3 and len(d) == 3
+    assert np.array_equal(t[-1], [8, 9, 10, 11]) and not t[0].flags.writeable
+    assert [x.tolist() for x in d[1]] == [[2, 3], [4, 5]]
+    with pytest.raises(ValueError):
+        t[0][0] = 5
+    t2, d2 = pickle.loads(pickle.dumps(t)), pickle.loads(pickle.dumps(d))
+    assert isinstance(t2, list) and all(np.array_equal(a, b) for a, b in zip(t2, t))
+    assert [[x.tolist() for x in s] for s in d2] == [[x.tolist() for x in s] for s in d]
+    with pytest.raises(IndexError):
+        t[3]
