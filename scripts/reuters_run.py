@@ -31,12 +31,14 @@ def main():
     ap.add_argument("--budget-s", type=float, default=150.0)
     ap.add_argument("--drop-topics", action="store_true",
                     help="zero the TOPICS columns of the third view (the ARI truth; mvc_amd.reuters)")
+    ap.add_argument("--standardize", action="store_true",
+                    help="every projected dimension centred and scaled to unit variance (mvc_amd.reuters.views)")
     ap.add_argument("--save", default=None, help="write every chain's state here (npz) at the end")
     ap.add_argument("--resume", default=None,
                     help="start every chain from a state --save wrote (the chains continue with fresh sweep "
                          "counters: a valid continuation of each chain, not the bitwise one)")
     a = ap.parse_args()
-    y = reuters.views(drop_topics=a.drop_topics)
+    y = reuters.views(drop_topics=a.drop_topics, standardize=a.standardize)
     lab, names, _ = reuters.topic_truth()
     sel = lab >= 0
     s = mvc_amd.Sampler(y, seed=a.seed, mode="parallel", n_chains=a.chains)
@@ -53,7 +55,7 @@ def main():
         s.sweep(1)
         s.synchronize()
         dt = time.perf_counter() - t0
-        rec = {"sweep": start + it, "s": round(dt, 4), "drop_topics": a.drop_topics}
+        rec = {"sweep": start + it, "s": round(dt, 4), "drop_topics": a.drop_topics, "standardize": a.standardize}
         Ts, aris, moves, taus = [], [], [], []
         for c in range(a.chains):
             t, d, h = s.state(chain=c)

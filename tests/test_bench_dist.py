@@ -23,13 +23,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _two_ranks(extra):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2",
+def _ranks(world, extra):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
                LOCAL_RANK="0", MVC_BENCH_BACKEND="gloo")
-    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config", "c2", "--steps", "3",
-           "--warmup", "1", "--no-extras", "--no-cpu-baseline"] + extra
+    cmd = [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--config", "c2", "--steps",
+           "3", "--warmup", "1", "--no-extras", "--no-cpu-baseline"] + extra
     procs = [subprocess.Popen(cmd, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                              text=True) for r in (1, 0)]
+                              text=True) for r in range(world - 1, -1, -1)]
     outs = []
     for p in procs:
         try:
@@ -40,10 +40,15 @@ def _two_ranks(extra):
             raise
         assert p.returncode == 0, e[-2000:]
         outs.append(o)
-    lines = [ln for ln in outs[1].strip().splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, outs[1][-2000:]
-    assert not [ln for ln in outs[0].strip().splitlines() if ln.startswith("{")], "only rank 0 prints"
+    lines = [ln for ln in outs[-1].strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, outs[-1][-2000:]
+    for o in outs[:-1]:
+        assert not [ln for ln in o.strip().splitlines() if ln.startswith("{")], "only rank 0 prints"
     return json.loads(lines[0])
+
+
+def _two_ranks(extra):
+    return _ranks(2, extra)
 
 
 def test_bench_two_ranks_chains_mode():
@@ -55,6 +60,17 @@ def test_bench_two_ranks_chains_mode():
     # the reported cross-chain reduce pooled both ranks' chains
     assert r["hyper_pooled"]["chains"] == 2
     assert r["roofline"]["bound"] in ("hbm", "mfma")
+
+
+def test_bench_four_ranks_chains_mode():
+    """Four ranks (the driver's 8-GPU launch has the same shape): one chain
+    per rank, the line's value is all ranks' sweeps over the max-over-ranks
+    time, and the pooled reduce holds four chains."""
+    r = _ranks(4, [])
+    assert r["n_gpus"] == 4 and r["scaling"] == "weak"
+    assert r["config"]["chains"] == 4 and r["config"]["parallelism"] == "chains4"
+    assert abs(r["value"] - 4 * r["steps"] / (r["ms_per_step"] * r["steps"] / 1e3)) <= 0.01 * r["value"]
+    assert r["hyper_pooled"]["chains"] == 4
 
 
 def test_bench_two_ranks_shard_mode():

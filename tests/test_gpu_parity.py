@@ -1012,6 +1012,29 @@ def test_run_n_devices_split_on_one_gpu(mode, monkeypatch):
         m.run_gibbs_cpp(y, 2, 0, 1, seed=7, mode=mode, n_chains=2, n_devices=2)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["exact", "parallel"])
+def test_run_eight_logical_devices_on_one_gpu(mode, monkeypatch):
+    """mvc_run's 8-way split (the driver's 8-GPU node shape) on one MI355X:
+    n_devices = 8 with every logical device mapped to device 0
+    (MVC_DEVICE_MAP=0,...,0), 16 chains striped two per device.  Every chain
+    equals the same chain run on one logical device, bit for bit, and so
+    does the pooled summary."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(11)
+    M, burn, C = 12, 6, 16
+    s1, s8 = {}, {}
+    single = m.run_gibbs_cpp(y, M, burn, 1, seed=9, mode=mode, n_chains=C, summary=s1)
+    monkeypatch.setenv("MVC_DEVICE_MAP", ",".join(["0"] * 8))
+    multi = m.run_gibbs_cpp(y, M, burn, 1, seed=9, mode=mode, n_chains=C, n_devices=8, summary=s8)
+    assert len(multi) == C
+    for c in range(C):
+        _compare(multi[c], single[c])
+    assert np.array_equal(s1["mean"], s8["mean"])
+    assert np.array_equal(s1["rhat"], s8["rhat"], equal_nan=True)
+
+
 def test_shard_exchange_failure_leaves_the_chain_unchanged():
     """A failing all_gather (the callback returns nonzero) stops the sweep
     with MVC_ERR_CALLBACK before the exchange buffer is read: the state is

@@ -43,6 +43,15 @@ def test_views_deterministic():
     assert np.isfinite(a).all()
 
 
+def test_standardized_views():
+    z = reuters.views(standardize=True)
+    assert z.shape == (3, 21578, 64) and np.isfinite(z).all()
+    assert np.allclose(z.mean(axis=1), 0.0, atol=1e-12)
+    assert np.allclose(z.std(axis=1), 1.0, atol=1e-12)
+    raw = reuters.views()
+    assert float(raw[1:].std(axis=1).max()) < 0.25   # title / <D> projections: far below the N(0, 1) prior's scale
+
+
 def _oracle_chain(args):
     y, chain, sweeps = args
     from oracle import oracle as O
@@ -51,7 +60,8 @@ def _oracle_chain(args):
 
 
 @pytest.mark.gpu
-def test_config3_full_corpus_eight_chains_one_gpu():
+@pytest.mark.parametrize("standardize", [False, True], ids=["raw", "standardized"])
+def test_config3_full_corpus_eight_chains_one_gpu(standardize):
     """BASELINE configs[2] at its workload: the full 21,578-document corpus,
     8 concurrent chains (ChainSet) on one MI355X, one cold sweep from the
     reference initialisation (nearly every document opens a table: the
@@ -62,7 +72,7 @@ def test_config3_full_corpus_eight_chains_one_gpu():
     from multiprocessing import get_context
     import mvc_amd
     from oracle import oracle as O
-    y = np.ascontiguousarray(reuters.views())
+    y = np.ascontiguousarray(reuters.views(standardize=standardize))
     lab, _, _ = reuters.topic_truth()
     sel = lab >= 0
     sweeps = 1
@@ -77,7 +87,7 @@ def test_config3_full_corpus_eight_chains_one_gpu():
     pool.close()
     for c in (0, 5):
         t, d, h = s.state(chain=c)
-        assert d.shape[1] == ref[c][2][-1] > 10000, c      # thousands of tables after the cold sweep
+        assert d.shape[1] == ref[c][2][-1] > 1000, c      # thousands of tables after the cold sweep
         assert np.array_equal(t, ref[c][0]) and np.array_equal(d, ref[c][1]), c
     for c in range(8):
         t, _, _ = s.state(chain=c)
@@ -87,13 +97,14 @@ def test_config3_full_corpus_eight_chains_one_gpu():
 
 
 @pytest.mark.gpu
-def test_config3_prefix_two_sweeps():
+@pytest.mark.parametrize("standardize", [False, True], ids=["raw", "standardized"])
+def test_config3_prefix_two_sweeps(standardize):
     """The first 2,000 documents, 8 chains, two cold sweeps: chains 0 and 5
     bit for bit vs the oracle's SeqSampler."""
     import mvc_amd
     from oracle import oracle as O
     n = 2000
-    y = np.ascontiguousarray(reuters.views()[:, :n])
+    y = np.ascontiguousarray(reuters.views(standardize=standardize)[:, :n])
     s = mvc_amd.Sampler(y, seed=3, mode="parallel", n_chains=8)
     s.sweep(2)
     for c in (0, 5):
