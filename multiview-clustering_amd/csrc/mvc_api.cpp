@@ -19,6 +19,33 @@
 
 namespace mvc {
 
+const char *path_opt(const char *key) {
+  // MVC_PATH is re-read on every call (tests change it between handles), and
+  // the value returned lives in a thread-local copy until the next call
+  thread_local std::string val;
+  const char *e = std::getenv("MVC_PATH");
+  if (!e) return nullptr;
+  const std::string s(e), k(key);
+  size_t pos = 0;
+  while (pos <= s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    const std::string item = s.substr(pos, end - pos);
+    const size_t eq = item.find('=');
+    if (eq != std::string::npos && item.substr(0, eq) == k) {
+      val = item.substr(eq + 1);
+      return val.c_str();
+    }
+    pos = end + 1;
+  }
+  return nullptr;
+}
+int path_int(const char *key, int dflt) {
+  const char *v = path_opt(key);
+  return (v && v[0]) ? std::atoi(v) : dflt;
+}
+
+
 InitState draw_initial_draws(int n, int V, uint64_t seed, uint32_t chain) {
   // multiview_gibbs.cpp:12-62: T0 = 4 tables drawn for i ascending, then per
   // view K0 = 2 dishes for t ascending, all from R::runif(0, K).

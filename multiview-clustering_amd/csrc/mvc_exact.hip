@@ -1253,7 +1253,7 @@ class ExactSampler : public Sampler {
       part = std::max(part, (size_t)((char *)A.h.mhbuf - (char *)A.h.n_t));
     }
     int m = full <= kExactLds ? 2 : (part <= kExactLds ? 1 : 0);
-    if (const char *e = getenv("MVC_EXACT_MODE"); e && e[0] >= '0' && e[0] <= '2') m = std::min(m, e[0] - '0');   // tests
+    if (const char *e = path_opt("exact_lds"); e && e[0] >= '0' && e[0] <= '2') m = std::min(m, e[0] - '0');   // tests (MVC_PATH)
     if (mode) *mode = m;
     return (int)(m == 2 ? full : (m == 1 ? part : 0));
   }

@@ -47,6 +47,14 @@ int lds_fill_byte();    // MVC_LDS_FILL, -1: off
 bool run_check();       // MVC_RUN_CHECK
 bool debug_sync();
 
+// MVC_PATH: the execution-path overrides of the tests and A/B runs, one
+// variable of comma-separated key=value items (e.g. "lc=0,waves=3"), read
+// when a sampler is created.  Every key selects a path that is bitwise the
+// default's and is pinned by a test (DESIGN.md §9 lists them).  path_opt
+// returns the value of key, or nullptr when it is not set.
+const char *path_opt(const char *key);
+int path_int(const char *key, int dflt);   // the value as an int, dflt when unset
+
 // Initial state draws of multiview_gibbs.cpp:12-62 on the sequential Philox
 // stream (shared by both schedules), plus tau_v of :78-94.
 struct InitState {

@@ -165,7 +165,6 @@ template <int NT, int SPPT, int RP>
 __device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2 *nxt, int SPP, const double *Bl,
                                                  mvc_d2 (&ring)[RP], mvc_d4 (&acc)[4]) {
   if constexpr (SPPT > 0) {
-#ifndef MVC_BPIPE_OFF
     // B-fragments one k-step pair ahead (LDS latency off the MFMA issue path)
     double bc[2 * NT], bn[2 * NT];
 #pragma unroll
@@ -180,34 +179,14 @@ __device__ __forceinline__ void lpview_tile_mfma(const mvc_d2 *cur, const mvc_d2
 #pragma unroll
         for (int t = 0; t < 2 * NT; ++t) bn[t] = bk[t * 64];
       }
-#ifndef MVC_ABL_LP_NOMFMA
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bc[t], acc[t], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bc[NT + t], acc[t], 0, 0, 0);
-#else   // timing ablation: the stream and the epilogue without the matrix pipe
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t][q & 3] += a[0] + a[1] + bc[t] + bc[NT + t];
-#endif
       __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
 #pragma unroll
       for (int t = 0; t < 2 * NT; ++t) bc[t] = bn[t];
     }
-#else   // MVC_BPIPE_OFF (tuning builds): B-fragments read at their k-step
-#pragma unroll
-    for (int q = 0; q < SPPT; ++q) {
-      const int u = q % RP;
-      const mvc_d2 a = ring[u];
-      ring[u] = (q + RP < SPPT) ? cur[(q + RP) * 64] : nxt[(q + RP - SPPT) * 64];
-      const double *bk = Bl + (size_t)(2 * q) * NT * 64;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], bk[t * 64], acc[t], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], bk[(NT + t) * 64], acc[t], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);           // keep each refill RP pairs ahead (no sinking)
-    }
-#endif
   } else {
     for (int s0 = 0; s0 < SPP; s0 += RP) {
 #pragma unroll
@@ -1112,9 +1091,6 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     const bool allv = __builtin_amdgcn_readfirstlane(Z.lmin[v]) != 0;
     const int so = __builtin_amdgcn_readfirstlane(Z.soff[v]);
     double *stg = so >= 0 ? s_stage + (size_t)so * 64 + lane : nullptr;
-#ifdef MVC_ABL_DRAW_NOVIEW   // timing ablation: no view pass
-    if (true) S = 1.0 + m; else
-#endif
     if (!allv) S = zview_sum<0>(row, koff, K, j0, w0, sw, m);           // general: streamed
     else if (K <= 8) S = zview_sum<8>(row, koff, K, j0, w0, sw, m, stg);     // row in registers
     else if (K <= 16) S = zview_sum<16>(row, koff, K, j0, w0, sw, m, stg);
@@ -1137,7 +1113,6 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
     const int pc = min(p, T - 1);
     sp[p] = p < T ? ((pc == p0) ? base_self : Z.base[pc]) : -MVC_PM_INF;
   }
-#ifndef MVC_ABL_DRAW_NOGATHER   // timing ablation: no table gathers
 #pragma unroll
   for (int c = 0; c < TM; c += 16) {
     for (int v = 0; v < V; ++v) {
@@ -1155,7 +1130,6 @@ __device__ __forceinline__ int zdraw_reg_one(const Sweep &A, const ZregLds &Z, i
       for (int u = 0; u < 16; ++u) sp[c + u] = sp[c + u] + x[u];
     }
   }
-#endif
   double M = -MVC_PM_INF;
 #pragma unroll
   for (int p = 0; p < TM; ++p)
@@ -1580,15 +1554,6 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
   lpview_tile_mfma<NT, SPPT, RP>(cur, nxt, SPPT, L.Bs + L.boff[v] + lane, ring, acc);
   const double *y2t = wsp + v * 16, *ht = wsp + 64 + v * 16;
   double *selfG = wsp + 128 + v * 16, *mrest = wsp + 192 + v * 16;
-#ifdef MVC_ABL_LP_NOEPI   // timing ablation (scripts/zprobe.py): the MFMA stream alone
-  {
-    double t = 0.0;
-#pragma unroll
-    for (int q = 0; q < NT; ++q) t += acc[q][0] + acc[q][1] + acc[q][2] + acc[q][3];
-    if (t == 1.2345) selfG[col] = t;
-    return;
-  }
-#endif
   double hy[4], hr[4];
   int j0[4];
 #pragma unroll
@@ -1630,14 +1595,9 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
       if (inc && j != j0[r] && val[r] > mx[r]) mx[r] = val[r];
     }
     const int off = j < K ? lbase + 2048 * t : disc_boff;
-#ifndef MVC_ABL_LP_NOSTORE   // timing ablation: no lp stores
     mvc_raw_buffer_store_v2f64((mvc_d2){val[0], val[1]}, rsrc, off, 0, 0);
     mvc_raw_buffer_store_v2f64((mvc_d2){val[2], val[3]}, rsrc, j < K ? off + 16 : disc_boff, 0, 0);
-#else
-    (void)off;
-#endif
   }
-#ifndef MVC_ABL_LP_NOMAX   // timing ablation: no row maxima
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     double x = mx[r];
@@ -1647,7 +1607,6 @@ __device__ __forceinline__ void lpa_view(const Sweep &A, const LpaLds &L, int v,
     x = dmax(x, down_d<1>(x));
     if (col == 0) mrest[grp + 4 * r] = x;   // lane 0 of the row holds the row's max
   }
-#endif
 }
 
 // The own dish of every (view, row) of the tile, one lane each (lane = row +
@@ -1799,9 +1758,7 @@ __global__ __launch_bounds__(64 * MVC_LPA_WAVES) void mvc_par_lpall_kernel(Sweep
     lpa_views<SPPT, RP, PAT, 0>(A, L, li0, nb, ybase, vstride, toff(m), toff(m + 1), ring, rsrc, tile_boff, disc_boff,
                                 wsp, zs);
     wave_lds_sync();
-#if !defined(MVC_ABL_LP_NOEPI) && !defined(MVC_ABL_LP_NOEND)
     lpa_tile_end(A, L, b0, li0, nb, y2, h, cnew_l, pz, rsrc, tile_boff, disc_boff, wsp, dslot);
-#endif
     wave_lds_sync();
   }
 }
@@ -2513,13 +2470,15 @@ bool run_check() {
   }();
   return on;
 }
-bool debug_sync() {
-  static const bool on = [] {
+// MVC_DEBUG_SYNC=1|2 (see ParallelSampler::dbg): the level, 0 when unset
+int debug_sync_level() {
+  static const int l = [] {
     const char *e = getenv("MVC_DEBUG_SYNC");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 0;
   }();
-  return on;
+  return l;
 }
+bool debug_sync() { return debug_sync_level() >= 1; }
 
 class ParallelSampler : public Sampler {
  public:
@@ -2562,11 +2521,10 @@ class ParallelSampler : public Sampler {
   size_t part_cap = 0;             // sumK capacity of partials
   int32_t *st_host = nullptr;   // pinned [2V+4]: the per-sweep status readback
   bool force_generic = false;
-  int lpv_waves = 0, lpv_bpc = 0;  // MVC_LPV_WAVES / MVC_LPV_BPC: producer block shape overrides (tuning)
-  bool force_zdraw_lds = false;   // MVC_ZDRAW_LDS=1: the LDS-checkpoint draw kernel for every T
-  bool force_zdraw_row = false;   // MVC_ZDRAW_ROW=1: the row draw for every T <= 512 (default: 64 < T <= 512)
-  bool no_zrow_lds = false;       // MVC_ZROW_LDS=0: the row draw reads the lp buffer directly
-  size_t zsc_max_bytes = (size_t)1 << 30;   // the checkpoint draw's table-score scratch limit (MVC_ZSC_MAX_MB)
+  bool force_zdraw_lds = false;   // MVC_PATH zdraw=lds: the LDS-checkpoint draw kernel for every T
+  bool force_zdraw_row = false;   // zdraw=row: the row draw for every T <= 512 (default: 64 < T <= 512)
+  bool no_zrow_lds = false;       // zdraw=row-global: the row draw reads the lp buffer directly
+  static constexpr size_t zsc_max_bytes = (size_t)1 << 30;   // the checkpoint draw's table-score scratch limit
   // within-chain N-sharding (mvc_sampler_set_shard): phase A covers this
   // rank's customers only; exch_cb all-gathers the choices into shard_exch
   int shard_rank = 0, shard_world = 1;
@@ -2574,41 +2532,35 @@ class ParallelSampler : public Sampler {
   int32_t *shard_exch = nullptr;
   int (*shard_cb)(void *) = nullptr;
   void *shard_user = nullptr;
-  bool no_lpall = false;          // MVC_LPALL=0: per-view producer launches even where the all-views producer applies
+  bool no_lpall = false;          // MVC_PATH lpall=0: per-view producer launches even where the all-views producer applies
   bool phase_a_only = false;      // sweep_chain stops after phase A (mvc_sampler_phase_a)
   bool phase_a_ran = false;
   int n_cu = 256;
-  bool repair_grid_only = false;  // MVC_REPAIR=grid: every mover through a grid window round (no run kernel)
-  bool early_mh_off = false;      // MVC_EARLY_MH=0: the MH launched only after the host has read the repair
-  bool no_big = false;            // MVC_BIG=0: the generic producer instead of the dish-block MFMA producer
-  bool force_big = false;         // MVC_BIG=1: the dish-block producer even where the tiled one applies (tests)
-  bool big_runtime_sp = false;    // MVC_BIG_RUNTIME_SP=1: the dish-block producer's runtime k-step loop only (tests, A/B)
-  int big_bpc_narrow = 3;         // MVC_BIG_BPC: 4-wave blocks per CU of the dish-block producer's 16 / 32-dish instances
-  int run_limit = kSeqRunLimit;   // MVC_RUN_LIMIT
-  bool run_limit_set = false;     // MVC_RUN_LIMIT given (it then applies to small chains too)
-  int small_n_no_windows = 0;     // MVC_SMALL_N: chains up to this n never use grid windows (off: at N = 200 windows are faster)
-  // MVC_RUN_WAVES: customers the run kernel evaluates per step.  4 by default:
+  bool repair_grid_only = false;  // MVC_PATH repair=grid: every mover through a grid window round (no run kernel)
+  bool force_big = false;         // big=1: the dish-block producer even where the tiled one applies (tests)
+  bool big_runtime_sp = false;    // big_sp=runtime: the dish-block producer's runtime k-step loop only (tests)
+  static constexpr int big_bpc_narrow = 3;   // 4-wave blocks per CU of the dish-block producer's 16 / 32-dish instances
+  static constexpr int run_limit = kSeqRunLimit;
+  // waves=N: customers the run kernel evaluates per step.  4 by default:
   // one evaluating wave per SIMD (a second wave on a SIMD halves the first
   // customer's issue rate, and with dense movers the first customer decides)
   int run_waves = 4;
-  bool use_wide = true;           // MVC_WIDE=0: global-scratch run kernel speculates one customer per wave
-  bool wide_grid = true;          // MVC_WIDE=block: the wide evaluation on the run kernel's one block instead of the grid
+  bool use_wide = true;           // wide=0: global-scratch run kernel speculates one customer per wave
+  bool wide_grid = true;          // wide=block: the wide evaluation on the run kernel's one block instead of the grid
   double *wide_part = nullptr;    // grid-wide evaluation: per-block partials [kWideGridMax][2V]
-  int wide_fin_lds = kWideFinLds; // the fin kernel's LDS evaluation up to this many bytes (MVC_WIDE_FIN=0: off)
-  bool force_global = false;      // MVC_RUN_LDS=0: the run kernel's global-scratch layout (tests)
-  bool use_ring = true;           // MVC_RUN_RING=0: stage each step's rows synchronously (no prefetch ring)
-  bool use_lc = true;             // MVC_LC=0: the run kernel's per-wave evaluation without the lane-column form
-  bool use_lane = true;           // MVC_LC=col: no lane-per-customer loop for small chains (lane columns instead)
+  int wide_fin_lds = kWideFinLds; // the fin kernel's LDS evaluation up to this many bytes (wide_fin=0: off)
+  bool force_global = false;      // run_lds=0: the run kernel's global-scratch layout (tests)
+  bool use_lc = true;             // lc=0: the run kernel's per-wave evaluation without the lane-column form
+  bool use_lane = true;           // lc=col: no lane-per-customer loop for small chains (lane columns instead)
   bool lane_now = false;          // this sweep runs the lane-per-customer loop (sweep_pre)
-  int run_grow_first = 0;         // MVC_RUN_GROW=0: the run kernel's LDS layout with room for T / 2 more tables only
-  bool use_vp = true;             // MVC_VP=0: the lane-column kernel without value prediction
-  // Small chains (n <= small_n_plain, MVC_SMALL_N_PLAIN): the lane-column loop without value
+  bool use_vp = true;             // vp=0: the lane-column kernel without value prediction
+  // Small chains (n <= small_n_plain, MVC_PATH small_plain=N): the lane-column loop without value
   // prediction and a stay limit of 16. At the reference's own call (N = 200, V = 5) the
   // prediction waves' overlay evaluation costs more per step than the steps it saves
   // (1,578 -> 2,262 sweeps/s, profiles/r5af_*); at N = 1M (the literal) it is worth 1.5x.
   int small_n_plain = 1024;
-  int small_first_rounds = 4;     // MVC_SMALL_ROUNDS: the first batch of repair rounds of a small chain
-  bool vp_stats = false;          // MVC_VP_STATS=1
+  static constexpr int small_first_rounds = 4;   // the first batch of repair rounds of a small chain
+  bool vp_stats = false;          // vp_stats=1: value prediction's steps and hits per sweep on stderr
 
   // MVC_DEBUG_SYNC=1: wait for the launch just made and name it in the error;
   // =2: also read the chain state back and check its invariants (z against
@@ -2626,13 +2578,7 @@ class ParallelSampler : public Sampler {
       if (!bad.empty()) throw Error(MVC_ERR_STATE, "state check after " + where + ": " + bad);
     }
   }
-  static int debug_level() {
-    static const int l = [] {
-      const char *e = getenv("MVC_DEBUG_SYNC");
-      return e ? atoi(e) : 0;
-    }();
-    return l;
-  }
+  static int debug_level() { return debug_sync_level(); }
   // Invariants of a chain's state between launches:
   // positions p < T (R->T; table slots are stable within a sweep), dishes
   // j < Klist[v]; every customer in a table, n_t = members, d_l = live tables
@@ -2727,8 +2673,7 @@ class ParallelSampler : public Sampler {
         // instead of yielding so the GPU idles as briefly as possible.  The
         // flag applies to the current device (set just above), and only
         // before that device's context exists; otherwise it is left as is.
-      const char *e = getenv("MVC_SPIN");
-      if (!(e && e[0] == '0')) (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
+      (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
       (void)hipGetLastError();
     }
     MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -2776,18 +2721,14 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipHostMalloc((void **)&rs_host, sizeof(Repair), hipHostMallocDefault));
     alloc_seq_scratch();
     std::fill(st_host, st_host + 2 * V + 4, 0);
-    const char *fg = getenv("MVC_FORCE_GENERIC");
-    force_generic = fg && fg[0] == '1';
-    if (const char *e = getenv("MVC_LPV_WAVES")) lpv_waves = std::max(0, std::min(8, atoi(e)));
-    if (const char *e = getenv("MVC_LPV_BPC")) lpv_bpc = std::max(0, std::min(8, atoi(e)));
-    const char *zl = getenv("MVC_ZDRAW_LDS");
-    force_zdraw_lds = zl && zl[0] == '1';
-    const char *zr = getenv("MVC_ZDRAW_ROW");
-    force_zdraw_row = zr && zr[0] == '1';
-    const char *zrl = getenv("MVC_ZROW_LDS");
-    no_zrow_lds = zrl && zrl[0] == '0';
-    if (const char *e = getenv("MVC_ZSC_MAX_MB")) zsc_max_bytes = (size_t)std::max(0L, std::strtol(e, nullptr, 10)) << 20;
-    if (const char *e = getenv("MVC_LPALL")) no_lpall = e[0] == '0';
+    // execution-path overrides (MVC_PATH, tests and A/B runs)
+    force_generic = path_int("generic", 0) == 1;
+    if (const char *e = path_opt("zdraw")) {
+      force_zdraw_lds = std::strcmp(e, "lds") == 0;
+      force_zdraw_row = std::strncmp(e, "row", 3) == 0;
+      no_zrow_lds = std::strcmp(e, "row-global") == 0;
+    }
+    no_lpall = path_int("lpall", 1) == 0;
     {
       hipDeviceProp_t prop;
       MVC_HIP(hipGetDeviceProperties(&prop, cf.device));
@@ -2812,12 +2753,9 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_wide_fin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kWideFinLds));
-    if (const char *e = getenv("MVC_WIDE_FIN")) wide_fin_lds = e[0] == '0' ? 0 : kWideFinLds;   // 0: the global-scratch evaluation
-    if (const char *e = getenv("MVC_REPAIR")) repair_grid_only = e[0] == 'g';
-    if (const char *e = getenv("MVC_BIG")) {
-      no_big = e[0] == '0';
-      force_big = e[0] == '1';
-    }
+    if (path_int("wide_fin", 1) == 0) wide_fin_lds = 0;   // the global-scratch evaluation
+    if (const char *e = path_opt("repair")) repair_grid_only = std::strcmp(e, "grid") == 0;
+    force_big = path_int("big", 0) == 1;
     for (const void *f : {(const void *)mvc_par_zdraw_row_kernel<4, true>, (const void *)mvc_par_zdraw_row_kernel<8, true>,
                           (const void *)mvc_par_zdraw_row_kernel<16, true>, (const void *)mvc_par_zdraw_row_kernel<32, true>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
@@ -2827,27 +2765,20 @@ class ParallelSampler : public Sampler {
     for (const void *f : {MVC_LPBIG_FNS(4), MVC_LPBIG_FNS(2), MVC_LPBIG_FNS(1)})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #undef MVC_LPBIG_FNS
-    if (const char *e = getenv("MVC_BIG_RUNTIME_SP")) big_runtime_sp = e[0] == '1';
-    if (const char *e = getenv("MVC_BIG_BPC")) big_bpc_narrow = std::max(1, std::min(4, atoi(e)));
-    if (const char *e = getenv("MVC_RUN_LIMIT")) { run_limit = std::max(1, atoi(e)); run_limit_set = true; }
-    if (const char *e = getenv("MVC_SMALL_N")) small_n_no_windows = atoi(e);
-    if (const char *e = getenv("MVC_RUN_WAVES")) run_waves = std::max(1, std::min(kSeqRunWaves, atoi(e)));
-    if (const char *e = getenv("MVC_RUN_RING")) use_ring = e[0] != '0';
-    if (const char *e = getenv("MVC_LC")) {   // 0: neither lane-column nor lane loop; col: lane columns only
+    big_runtime_sp = path_opt("big_sp") && std::strcmp(path_opt("big_sp"), "runtime") == 0;
+    run_waves = std::max(1, std::min(kSeqRunWaves, path_int("waves", run_waves)));
+    if (const char *e = path_opt("lc")) {   // 0: neither lane-column nor lane loop; col: lane columns only
       use_lc = e[0] != '0';
       use_lane = use_lc && e[0] != 'c';
     }
-    if (const char *e = getenv("MVC_RUN_GROW")) run_grow_first = e[0] == '0' ? 1 : 0;
-    if (const char *e = getenv("MVC_VP")) use_vp = e[0] != '0';
-    if (const char *e = getenv("MVC_SMALL_N_PLAIN")) small_n_plain = atoi(e);
-    if (const char *e = getenv("MVC_SMALL_ROUNDS")) small_first_rounds = std::max(1, std::min(64, atoi(e)));
-    if (const char *e = getenv("MVC_VP_STATS")) vp_stats = e[0] == '1';
-    if (const char *e = getenv("MVC_WIDE")) {
+    use_vp = path_int("vp", 1) != 0;
+    small_n_plain = path_int("small_plain", small_n_plain);
+    vp_stats = path_int("vp_stats", 0) == 1;
+    if (const char *e = path_opt("wide")) {
       use_wide = e[0] != '0';
       wide_grid = e[0] != 'b';
     }
-    if (const char *e = getenv("MVC_EARLY_MH")) early_mh_off = e[0] == '0';
-    if (const char *e = getenv("MVC_RUN_LDS")) force_global = e[0] == '0';
+    force_global = path_int("run_lds", 1) == 0;
     chains.resize(cf.n_chains);
     for (int c = 0; c < cf.n_chains; ++c) init_chain(chains[c], chain_gid(cf, c), yh_in);
     MVC_HIP(hipStreamSynchronize(stream));
@@ -3213,7 +3144,7 @@ class ParallelSampler : public Sampler {
   // SIMD.  Measured (scripts/lpv_sweep.py, D = 128, K = 64/32/16/8): more
   // waves per SIMD only contend for the f64 MFMA pipe and the load queue
   // (lp 1.11 ms at 4x2, 1.12 at 4x3 / 4x4, 1.22 at 6x2, 1.36 at 2x4).
-  int lpview_waves(int) const { return lpv_waves > 0 ? lpv_waves : 4; }
+  int lpview_waves(int) const { return 4; }
   template <int SPPT, int RP>
   void launch_lpview_nt(int NT, dim3 grid, dim3 block, size_t lds, const Sweep &A, int v, int b0, int nb) {
     double *disc = lpb + lpb_cap;
@@ -3300,7 +3231,7 @@ class ParallelSampler : public Sampler {
       if (lpbig_shared_bytes(SPb, nt, c.T, 4) <= 80 * 1024) { big_ntb = nt; big_waves = 4; }
       else if (lpbig_shared_bytes(SPb, nt, c.T, 8) <= 150 * 1024) { big_ntb = nt; big_waves = 8; }
     }
-    const bool use_big = !use_mfma && !force_generic && !no_big && D % 4 == 0 && D >= 16 && Kmin >= 1 && big_ntb > 0;
+    const bool use_big = !use_mfma && !force_generic && D % 4 == 0 && D >= 16 && Kmin >= 1 && big_ntb > 0;
     // batch: multiple of 64 customers, lp buffer <= kLpbBudget doubles
     const size_t per64 = (size_t)std::max(1, sk) * 64;
     size_t nb_max = std::max<size_t>(64, (kLpbBudget / per64) * 64);
@@ -3365,7 +3296,7 @@ class ParallelSampler : public Sampler {
         for (int v = 0; v < V; ++v) {
           const int NT = (c.K[v] + 15) / 16;
           const size_t lds = lpview_shared_bytes(SP, NT, c.K[v], c.T);
-          const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(lpv_bpc > 0 ? lpv_bpc : 2, (160 * 1024) / std::max<size_t>(lds, 1)));
+          const int per_cu = (int)std::max<size_t>(1, std::min<size_t>(2, (160 * 1024) / std::max<size_t>(lds, 1)));
           const int bw = lpview_waves(NT);
           const int grid = std::max(1, std::min(per_cu * n_cu, (ntile + bw - 1) / bw));
           launch_lpview(NT, dim3(grid), dim3(64 * bw), lds, A, v, (int)b0, nb);
@@ -3542,12 +3473,12 @@ class ParallelSampler : public Sampler {
     SeqLds L{};
     // small chains: the run kernel walks the whole sweep (a window round is a
     // launch triple and a host read-back, more than the steps it saves)
-    L.limit = (n <= small_n_no_windows) ? kNoWindows : (n <= small_n_plain && !run_limit_set) ? 16 : run_limit;
+    L.limit = n <= small_n_plain ? 16 : run_limit;
     // in order of preference: S1 cached with room to double (a cold sweep's
     // births then rarely restride; in a chain batch a restride ends the round
     // for every chain), S1 cached with room to grow by half, then without S1,
     // then tight margins without S1
-    for (int attempt = force_global ? 4 : run_grow_first; attempt < 4; ++attempt) {
+    for (int attempt = force_global ? 4 : 0; attempt < 4; ++attempt) {
       const bool s1 = attempt <= 1;
       const int kgrow = attempt == 0 ? std::max(16, kmax) : attempt < 3 ? std::max(8, kmax / 2) : 4;
       const int tgrow = attempt == 0 ? std::max(128, T) : attempt < 3 ? std::max(64, T / 2) : 16;
@@ -3572,9 +3503,8 @@ class ParallelSampler : public Sampler {
         const int64_t slot = seq_ring_slot(V, D);
         const int64_t left = room - (int64_t)L.nws * L.stride;
         int rn = 0;
-        if (use_ring)
-          for (int r = 256; r >= 2 * L.nws; r >>= 1)
-            if ((int64_t)r * slot <= left) { rn = r; break; }
+        for (int r = 256; r >= 2 * L.nws; r >>= 1)
+          if ((int64_t)r * slot <= left) { rn = r; break; }
         L.ring = rn;
         L.pfn = rn ? std::max(1, rn / 2) : 0;
         L.lc = (use_lc && s1 && rn > 0 && L.ts <= 64 * kLcChunks) ? 1 : 0;
@@ -3640,7 +3570,7 @@ class ParallelSampler : public Sampler {
     // repair and the MH separately (they would time the MH as repair)
     // (not for small chains: nearly every sweep of theirs moves someone, so the
     // gated launch would be a no-op launch per sweep)
-    rr.early_mh = allow_early_mh && !early_mh_off && (!timers.on || timers.coarse) && n > small_n_plain;
+    rr.early_mh = allow_early_mh && (!timers.on || timers.coarse) && n > small_n_plain;
     if (rr.early_mh && !rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
     // the first batch of rounds: one; small chains four (their repair
     // usually takes 2-5 rounds, and a batch costs a host round trip)
@@ -3822,7 +3752,7 @@ class ParallelSampler : public Sampler {
     // the table limit: the MH's three-level tree64 over the table sizes
     // (64^3 = 262,144); MVC_MAX_TABLES lowers it (tests of the limit's error)
     int max_tc = kParTC;
-    if (const char *e = getenv("MVC_MAX_TABLES")) max_tc = std::max(16, std::min(kParTC, atoi(e)));
+    max_tc = std::max(16, std::min(kParTC, path_int("max_tables", kParTC)));
     const int TC2 = (flags & 1) ? std::min(max_tc, 2 * TC) : TC;
     const int KC2 = (flags & 2) ? std::min(kParKC, 2 * KC + 1) : KC;
     if (TC2 == TC && KC2 == KC)
@@ -4111,8 +4041,7 @@ class ChainSet : public Sampler {
   // state as a chain swept alone, so every chain is the same chain, bit for bit;
   // concurrency no longer needs a hardware queue per chain.
   bool batch_on = [] {
-    const char *e = getenv("MVC_CHAIN_BATCH");   // =0: one host thread and stream per chain
-    return !(e && e[0] == '0');
+    return path_int("chain_batch", 1) != 0;   // chain_batch=0: one host thread and stream per chain
   }();
   SeqArgs *bA_dev = nullptr, *bA_host = nullptr, *bE_dev = nullptr, *bE_host = nullptr;
   SeqLds *bL_dev = nullptr, *bL_host = nullptr;
@@ -4347,14 +4276,13 @@ class ChainSet : public Sampler {
 };
 
 Sampler *make_parallel_sampler_device(const mvc_config &cfg, DeviceData &&dd) {
-  const char *e = getenv("MVC_CHAIN_THREADS");
-  if (cfg.n_chains > 1 && !(e && e[0] == '0')) return new ChainSet(cfg, std::move(dd));
+  if (cfg.n_chains > 1 && path_int("chain_threads", 1) != 0) return new ChainSet(cfg, std::move(dd));
   return new ParallelSampler(cfg, std::move(dd));
 }
 
 Sampler *make_parallel_sampler(const mvc_config &cfg, const double *const *views) {
-  const char *e = getenv("MVC_CHAIN_THREADS");   // =0: one handle runs its chains one after another
-  if (cfg.n_chains > 1 && !(e && e[0] == '0')) return new ChainSet(cfg, views);
+  // chain_threads=0 (MVC_PATH): one handle runs its chains one after another
+  if (cfg.n_chains > 1 && path_int("chain_threads", 1) != 0) return new ChainSet(cfg, views);
   return new ParallelSampler(cfg, views);
 }
 

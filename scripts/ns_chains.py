@@ -1,6 +1,6 @@
 """North-star literal (N = 1M, V = 4, D = 1, K = 64) with C chains on one GPU
 at once (ChainSet, DESIGN.md §7: the chain-batched repair by default;
-MVC_CHAIN_BATCH=0 one stream and host thread per chain, which needs
+MVC_PATH=chain_batch=0 one stream and host thread per chain, which needs
 GPU_MAX_HW_QUEUES >= C): one sweep from the generating partition, aggregate
 chain-sweeps/s.  Usage: python scripts/ns_chains.py C [C ...]"""
 import json
@@ -32,7 +32,7 @@ def main():
         s.close()
         print(json.dumps({"workload": desc.replace("1 chain/GPU", f"{C} chains on 1 GPU"), "chains": C,
                           "sweep_s": round(dt, 2), "chain_sweeps_per_s": round(C / dt, 3),
-                          "batched": os.environ.get("MVC_CHAIN_BATCH", "1") != "0",
+                          "batched": "chain_batch=0" not in os.environ.get("MVC_PATH", ""),
                           "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}), flush=True)
 
 

@@ -16,6 +16,12 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
+def _path(monkeypatch, **kw):
+    """Execution-path overrides of the library (MVC_PATH): one
+    variable of key=value items, read when a sampler is created."""
+    monkeypatch.setenv("MVC_PATH", ",".join(f"{k}={v}" for k, v in kw.items()))
+
+
 def _mvc():
     import mvc_amd
     return mvc_amd
@@ -168,10 +174,10 @@ def test_exact_run_many_chains_threaded_samples():
 @pytest.mark.parametrize("mode", ["0", "1", "2"])
 def test_exact_storage_modes(mode, monkeypatch):
     """The sweep kernel's three storage instances (every chain array in global
-    memory / all but z in LDS / all in LDS; MVC_EXACT_MODE caps the one the
+    memory / all but z in LDS / all in LDS; MVC_PATH exact_lds caps the one the
     sizes allow) give the oracle's chain through New_Simulation's cold
     transient (T ~ 170 of n = 200)."""
-    monkeypatch.setenv("MVC_EXACT_MODE", mode)
+    _path(monkeypatch, exact_lds=mode)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.new_simulation(11)
@@ -373,11 +379,8 @@ def _run_path(m, y, st, seed, sweeps, path, monkeypatch, draw="reg", expect_reg=
     2 MFMA) and the phase-1 kernels ("reg" lp buffer + register draw, "lds"
     lp buffer + checkpoint draw; "-perview" one producer launch per view);
     check the path taken on the first sweep."""
-    monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
-    monkeypatch.setenv("MVC_ZDRAW_LDS", "1" if draw == "lds" else "0")
-    monkeypatch.setenv("MVC_ZDRAW_ROW", "1" if draw.startswith("row") else "0")
-    monkeypatch.setenv("MVC_ZROW_LDS", "0" if draw == "row-global" else "1")
-    monkeypatch.setenv("MVC_LPALL", "0" if draw.endswith("-perview") else "1")
+    _path(monkeypatch, generic="1" if path == 0 else "0", zdraw=draw.replace("-perview", ""),
+          lpall="0" if draw.endswith("-perview") else "1")
     draw = draw.replace("-perview", "")
     s = m.Sampler(y, seed=seed, mode="parallel")
     s.set_state(*st)
@@ -445,7 +448,7 @@ def test_zpath2_vs_oracle(n, V, D, K, T, draw, monkeypatch):
 def test_many_views_row_draw_gate(monkeypatch):
     """More than 16 views with 64 < T <= 512: the row draw keeps one view per
     lane of a customer's 16-lane row, so it must not be selected (even under
-    MVC_ZDRAW_ROW=1); the checkpoint draw runs and the chain is bitwise the
+    MVC_PATH zdraw=row); the checkpoint draw runs and the chain is bitwise the
     oracle's."""
     m = _mvc()
     from mvc_amd import data
@@ -458,7 +461,7 @@ def test_many_views_row_draw_gate(monkeypatch):
     dish = np.stack([np.arange(T) % max(1, K // (2 ** min(v, 3))) for v in range(V)]).astype(np.int32)
     hyper = np.array([1.69] * V + [1.0] * V + [0.5] * V + [1.0, 0.6])
     st = (table_of, dish, hyper)
-    monkeypatch.setenv("MVC_ZDRAW_ROW", "1")
+    _path(monkeypatch, zdraw="row")
     s = m.Sampler(y, seed=41, mode="parallel")
     s.set_state(*st)
     ref = O.run(y, 2, 0, 1, seed=41, mode=O.PARALLEL, state=st)
@@ -582,7 +585,7 @@ def test_parallel_stats_bitwise_vs_oracle(D, path, monkeypatch):
     V, K = 3, 16
     y, z = data.synthetic(4000, V, D, K, seed=40 + D)
     st = _warm_state(z, V, K)
-    monkeypatch.setenv("MVC_FORCE_GENERIC", "1" if path == 0 else "0")
+    _path(monkeypatch, generic="1" if path == 0 else "0")
     s = m.Sampler(y, seed=13, mode="parallel")
     s.set_state(*st)
     s.sweep(6)
@@ -654,12 +657,10 @@ def test_repair_shapes_same_chain(waves, repair, lc, monkeypatch):
     """The repair's execution shape does not change the chain: the run kernel
     evaluating 1, 3 or 8 customers per step (fewer waves than the V = 5
     views, so birth dish draws wrap over the waves; the lane-column
-    evaluation, or MVC_LC=0 the one-wave-per-pass form), and the grid-window
-    path alone (MVC_REPAIR=grid), all bitwise vs oracle SeqSampler through the
+    evaluation, or lc=0 the one-wave-per-pass form), and the grid-window
+    path alone (repair=grid), all bitwise vs oracle SeqSampler through the
     births of a cold start."""
-    monkeypatch.setenv("MVC_RUN_WAVES", waves)
-    monkeypatch.setenv("MVC_REPAIR", repair)
-    monkeypatch.setenv("MVC_LC", lc)
+    _path(monkeypatch, waves=waves, repair=repair, lc=lc)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.new_simulation(1999)
@@ -675,7 +676,7 @@ def test_repair_run_shapes_d16(waves, V, monkeypatch):
     """The run kernel evaluating 8, 3 or 1 customers per step (one wave each)
     gives the oracle SeqSampler chain bit for bit, through the births of a
     cold start (D = 16: S1 in the LDS cache)."""
-    monkeypatch.setenv("MVC_RUN_WAVES", waves)
+    _path(monkeypatch, waves=waves)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.synthetic(3000, V, 16, 6, seed=60 + V)
@@ -697,14 +698,13 @@ y, _ = data.new_simulation(1999)
 C, M = 4, 8
 conc = m.Sampler(y, seed=21, mode="parallel", n_chains=C)          # chain-batched repair (default)
 conc.sweep(M)
-os.environ["MVC_CHAIN_BATCH"] = "0"                               # one host thread and stream per chain
+os.environ["MVC_PATH"] = "chain_batch=0"                          # one host thread and stream per chain
 thr = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
 thr.sweep(M)
-del os.environ["MVC_CHAIN_BATCH"]
-os.environ["MVC_CHAIN_THREADS"] = "0"                             # one handle, chains one after another
+os.environ["MVC_PATH"] = "chain_threads=0"                        # one handle, chains one after another
 ser = m.Sampler(y, seed=21, mode="parallel", n_chains=C)
 ser.sweep(M)
-del os.environ["MVC_CHAIN_THREADS"]
+del os.environ["MVC_PATH"]
 # batched with capacity growth inside the batch (16 tables, 15 dishes at the start)
 grow = m.Sampler(y, seed=21, mode="parallel", n_chains=C, table_cap=16, dish_cap=15)
 for _ in range(M):
@@ -728,8 +728,8 @@ print("chains OK")
 def test_chains_concurrent_equal_serial():
     """Several chains in one handle (ChainSet, shared device data): the
     chain-batched repair (one launch per round for all chains), the per-chain
-    streams and host threads (MVC_CHAIN_BATCH=0) and the serial loop
-    (MVC_CHAIN_THREADS=0) all equal the same chain run alone (first_chain =
+    streams and host threads (MVC_PATH chain_batch=0) and the serial loop
+    (chain_threads=0) all equal the same chain run alone (first_chain =
     c), bit for bit, through a cold start with births, also when the batch
     grows the chains' capacities."""
     import subprocess
@@ -740,20 +740,21 @@ def test_chains_concurrent_equal_serial():
 
 
 @pytest.mark.parametrize("env", [
-    {"MVC_LC": "0"},                                  # batched kind 0: one wave per customer, LDS cache
-    {"MVC_RUN_LDS": "0", "MVC_WIDE": "0"},            # kind 0 on the global layout
-    {"MVC_RUN_LDS": "0", "MVC_WIDE": "block"},        # kind 2: the block-wide evaluation
-    {"MVC_RUN_LDS": "0"},                             # grid-wide evaluation: every chain on its own stream
-    {"MVC_REPAIR": "grid"},                           # grid windows only: every chain on its own stream
-], ids=["lc0", "global_tw1", "wide_block", "wide_grid", "grid_only"])
+    {"lc": "0"},                                      # batched kind 0: one wave per customer, LDS cache
+    {"lc": "col"},                                    # batched kind 3: lane columns (no lane loop)
+    {},                                               # batched kind 5: the small chains' lane loop
+    {"run_lds": "0", "wide": "0"},                    # kind 0 on the global layout
+    {"run_lds": "0", "wide": "block"},                # kind 2: the block-wide evaluation
+    {"run_lds": "0"},                                 # grid-wide evaluation: every chain on its own stream
+    {"repair": "grid"},                               # grid windows only: every chain on its own stream
+], ids=["lc0", "lane_columns", "lane8", "global_tw1", "wide_block", "wide_grid", "grid_only"])
 def test_chains_batched_kinds_equal_alone(env, monkeypatch):
     """The chain-batched repair with every run-kernel instance it can batch
     (kinds 0 and 2) and with the chains it launches one by one on their own
     streams (grid-wide evaluation, grid-only repair: their window evaluation
     must not also run in the batched window launch) gives every chain bit for
     bit as the same chain swept alone, through a cold start with births."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    _path(monkeypatch, **env)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.new_simulation(1999)
@@ -797,7 +798,7 @@ print("last-birth OK", last)
 """
 
 
-@pytest.mark.parametrize("vp", ["0", "1"])
+@pytest.mark.parametrize("vp", ["0", "1", "col"])
 def test_last_customer_birth_with_poisoned_lds(vp):
     """Regression test of the round-3 multi-chain fault: a
     birth decided for the sweep's LAST customer is committed by the birth
@@ -816,11 +817,11 @@ def test_last_customer_birth_with_poisoned_lds(vp):
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    # vp = "1": value prediction at N = 200 too (small chains run the plain
-    # lane-column loop by default, MVC_SMALL_N_PLAIN), the loop the fault was in
-    env = dict(os.environ, MVC_LDS_FILL="0xA5", MVC_RUN_CHECK="1", MVC_SMALL_N_PLAIN="0" if vp == "1" else "1024")
-    env.pop("MVC_CHAIN_THREADS", None)
-    env.pop("MVC_VP", None)
+    # vp = "1": value prediction at N = 200 too (small chains run the lane
+    # loop by default, MVC_PATH small_plain), the loop the fault was in; "col":
+    # the plain lane-column loop; "0": the small chains' default (lane loop)
+    path = {"1": "small_plain=0", "col": "lc=col", "0": ""}[vp]
+    env = dict(os.environ, MVC_LDS_FILL="0xA5", MVC_RUN_CHECK="1", MVC_PATH=path)
     r = subprocess.run([sys.executable, "-c", _LAST_BIRTH_CHILD, root], capture_output=True, text=True, timeout=240,
                        env=env)
     assert r.returncode == 0 and "last-birth OK" in r.stdout, (r.stdout[-1000:], r.stderr[-2000:])
@@ -835,11 +836,9 @@ def test_dish_block_producer(force, monkeypatch):
     k-step loop), warm; forced onto a K <= 64 shape that the tiled producer
     would take (D = 64: the unrolled tile); and configs[4]'s D = 256 with
     K_v = 80 / 40 (a 64 + 16 dish split), unrolled and with the runtime loop
-    (MVC_BIG_RUNTIME_SP); bitwise vs the oracle."""
+    (MVC_PATH big_sp=runtime); bitwise vs the oracle."""
     if force:
-        monkeypatch.setenv("MVC_BIG", "1")
-    if force == "d256-runtime":
-        monkeypatch.setenv("MVC_BIG_RUNTIME_SP", "1")
+        _path(monkeypatch, big="1", **({"big_sp": "runtime"} if force == "d256-runtime" else {}))
     m = _mvc()
     from mvc_amd import data
     N, V, D, K = {"": (6000, 3, 32, 128), "1": (4100, 4, 64, 64)}.get(force, (3000, 2, 256, 80))
@@ -894,16 +893,14 @@ def test_shard_ranks_equal_unsharded(world, tmp_path):
 @pytest.mark.parametrize("wide,V,fin", [("1", 3, "1"), ("1", 3, "0"), ("0", 3, "1"), ("1", 5, "1"), ("1", 5, "0"),
                                         ("block", 3, "1"), ("block", 5, "1")])
 def test_repair_global_wide(wide, V, fin, monkeypatch):
-    """The run kernel on its global-scratch layout (MVC_RUN_LDS=0, as when
-    the state outgrows the LDS): one customer over the grid (MVC_WIDE=1: lp
-    kernel + fin kernel, the fin kernel's evaluation in LDS or, MVC_WIDE_FIN=0,
+    """The run kernel on its global-scratch layout (MVC_PATH run_lds=0, as
+    when the state outgrows the LDS): one customer over the grid (wide=1: lp
+    kernel + fin kernel, the fin kernel's evaluation in LDS or, wide_fin=0,
     in the global scratch), over the whole block (seq_resample_wide: dishes,
     tables and scans split over the 8 waves) or one customer per wave
-    (MVC_WIDE=0); bitwise vs oracle SeqSampler through the births of a cold
+    (wide=0); bitwise vs oracle SeqSampler through the births of a cold
     start."""
-    monkeypatch.setenv("MVC_RUN_LDS", "0")
-    monkeypatch.setenv("MVC_WIDE", wide)
-    monkeypatch.setenv("MVC_WIDE_FIN", fin)
+    _path(monkeypatch, run_lds="0", wide=wide, wide_fin=fin)
     m = _mvc()
     from mvc_amd import data
     y, _ = data.synthetic(3000, V, 16, 6, seed=80 + V)
@@ -1077,11 +1074,11 @@ def test_shard_exchange_failure_leaves_the_chain_unchanged():
 def test_table_limit_is_a_clean_error(monkeypatch):
     """A cold start that needs more tables than the parallel mode's limit
     (262,144 = 64^3, the MH's three-level tree64; lowered here with
-    MVC_MAX_TABLES) fails with MVC_ERR_UNSUPPORTED and a message naming the
+    MVC_PATH max_tables) fails with MVC_ERR_UNSUPPORTED and a message naming the
     limit, not a wrong answer (configs[3] at N = 1M from the
     reference initialisation would reach it: nearly every customer opens a
     table in sweep 0, multiview_gibbs.cpp:94)."""
-    monkeypatch.setenv("MVC_MAX_TABLES", "32")
+    _path(monkeypatch, max_tables="32")
     m = _mvc()
     from mvc_amd import data
     y, _ = data.new_simulation(1999)          # opens ~70 tables in sweep 0
@@ -1098,9 +1095,8 @@ def test_value_prediction_same_chain(V, D, K, vp, monkeypatch, capfd):
     i+3 against the state with the phase-A choices of the ones before applied,
     mvc_repair.h seq_run_loop_vp) gives the oracle SeqSampler chain bit for
     bit from a warm state where most customers move (overlapping clusters) and
-    through births; MVC_VP=0 is the plain lane-column loop on the same chain."""
-    monkeypatch.setenv("MVC_VP", vp)
-    monkeypatch.setenv("MVC_VP_STATS", "1")
+    through births; MVC_PATH vp=0 is the plain lane-column loop on the same chain."""
+    _path(monkeypatch, vp=vp, vp_stats="1")
     m = _mvc()
     import bench
     from mvc_amd import data
