@@ -3885,11 +3885,19 @@ __device__ __forceinline__ LanePre lane_pre(const SView &W, int V, const double 
 //     pw16_select inside it.  The group's lanes agree; lane 0's is used.
 // Every lane of the wave calls it (customers past n with a clamped index):
 // the broadcasts read other lanes.
-template <int TM>
+// KB: dishes per view handled as straight-line code (every K_v <= KB: the
+// lp values, counts and exps of all of them issued together, the ones past
+// K_v masked to the same +0 a skipped dish adds), 0: the general loop over
+// blocks of 16.  TR: table registers (T <= TR); positions past TR are the
+// compile-time +0 of the last block's padding.
+template <int KB, int TR>
 __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0,
                                                   const double *hyp, const double *cnewv, const LanePre &LP) {
-  static_assert(TM % 16 == 0 && TM <= 64, "TM: tables in registers, whole blocks of 16");
-  constexpr int NBk = TM / 16;
+  static_assert(TR <= 64 && (TR % 16 == 0 || TR < 16), "TR: whole blocks of 16, or part of one");
+  static_assert(KB == 0 || KB <= 16, "KB: the straight-line dishes");
+  constexpr int NBk = (TR + 15) / 16;
+  constexpr int TM = 16 * NBk;
+  RUN_T0();
   const int lane = threadIdx.x & 63, gb = lane & ~7, v = lane & 7;
   const int V = A.P.V, D = A.P.D, ts = W.ts, ks = W.ks, s1s = W.s1s;
   const bool vok = v < V;
@@ -3912,18 +3920,47 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
   const double *S1v = W.S1T + (size_t)vv * D * s1s;
   const double *cbv = W.cb + vv * ks, *c0v = W.c0 + vv * ks;
   auto dot = [&](int j) {   // G = y . S1[:, j], one fma chain in ascending d
+    if (D == 1) return __builtin_fma(yv[0], S1v[j], 0.0);
     double G = 0.0;
     for (int d = 0; d < D; ++d) G = __builtin_fma(yv[d], S1v[d * s1s + j], G);
     return G;
   };
   const double self = lc_self(W, vv, ks, j0, dot(j0), Y2i, hy, h);
   auto lpj = [&](int j) { return j == j0 ? self : __builtin_fma(dot(j) + hy, cbv[j], c0v[j]) + h; };
-  double lm;
-  {
+  double col[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) col[c] = 0.0;
+  double mx = -MVC_PM_INF;
+  int cnt = 0;
+  double m;
+  if constexpr (KB > 0) {
+    // every dish of the view at once: lp, max over the included ones, K_act,
+    // then the column terms (a dish past K_v: l = 0, its term w exp(-inf) =
+    // 0 * 0 = +0, the value col[c] keeps when the general loop skips it)
+    double x[KB];
+    int l[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      const int jc = min(u, K - 1);
+      x[u] = lpj(jc);
+      l[u] = u < K ? (u == j0 ? l0p : dl[jc]) : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (l[u] > 0) {
+        ++cnt;
+        if (x[u] > mx) mx = x[u];
+      }
+    m = lfn > mx ? lfn : mx;
+#pragma unroll
+    for (int u = 0; u < KB; ++u) {
+      double w = (double)l[u] - sigma;
+      if (w < 0.0) w = 0.0;
+      col[u] = col[u] + w * mvc_exp_le0(l[u] > 0 ? x[u] - m : -MVC_PM_INF);
+    }
+  } else {
     // pass 1: max over the included dishes, K_act; the first 16 lp kept
     double lr[16];
-    double mx = -MVC_PM_INF;
-    int cnt = 0;
     for (int t0 = 0; t0 < K; t0 += 16) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -3939,11 +3976,8 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
         }
       }
     }
-    const double m = lfn > mx ? lfn : mx;
+    m = lfn > mx ? lfn : mx;
     // pass 2: column partials in ascending j
-    double col[16];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) col[c] = 0.0;
     for (int t0 = 0; t0 < K; t0 += 16) {
 #pragma unroll
       for (int c = 0; c < 16; ++c) {
@@ -3957,6 +3991,9 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
         }
       }
     }
+  }
+  double lm;
+  {
     double Sv = pw16_seq(col);
     double wn = alpha + (double)cnt * sigma;
     if (wn < 0.0) wn = 0.0;
@@ -3965,20 +4002,20 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
     const double logden = LP.at(alive ? vv : V + vv);
     lm = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - logden;
   }
-  double lt[TM];   // lp of table p's dish in this lane's view
+  RUN_MARK(2);
+  double lt[TR];   // lp of table p's dish in this lane's view
 #pragma unroll
-  for (int p = 0; p < TM; ++p) lt[p] = p < T ? lpj(W.dish[vv * ts + p]) : 0.0;
+  for (int p = 0; p < TR; ++p) lt[p] = lpj(W.dish[vv * ts + min(p, T - 1)]);
   // ---- the group: sums in view order over its lanes
   double s_new = LP.at(alive ? 2 * V : 2 * V + 1);   // log(ag + sg T_ne')
   for (int u = 0; u < V; ++u) s_new = s_new + __shfl(lm, gb + u, 64);
-  const double mass0 = (double)np0 - sg;
-  const double lmass0 = LP.at(2 * V + 2 + p0);   // log(mass0)
+  const double lmass0 = LP.at(2 * V + 2 + p0);   // log((n_p0 - 1) - sg)
   double sp[TM];
   uint64_t inc = 0;   // tables included in the draw (n_p' >= 1, n_p' - sigma_g > 0)
 #pragma unroll
   for (int p = 0; p < TM; ++p) {
     sp[p] = -MVC_PM_INF;
-    if (p < T) {
+    if (p < TR && p < T) {
       const int np = W.n_t[p] - (p == p0 ? 1 : 0);
       const double mass = (double)np - sg;
       if (np >= 1 && mass > 0.0) {
@@ -3987,19 +4024,19 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
       }
     }
   }
-  (void)mass0;
   for (int u = 0; u < V; ++u) {
 #pragma unroll
-    for (int p = 0; p < TM; ++p) {
-      if (p < T) {
+    for (int p = 0; p < TR; ++p) {
+      if (TR <= 4 || p < T) {
         const double x = __shfl(lt[p], gb + u, 64);
         if ((inc >> p) & 1ull) sp[p] = sp[p] + x;
       }
     }
   }
+  RUN_MARK(4);
   double M = -MVC_PM_INF;
 #pragma unroll
-  for (int p = 0; p < TM; ++p)
+  for (int p = 0; p < TR; ++p)
     if (p < T && sp[p] > M) M = sp[p];
   if (s_new > M) M = s_new;
   // weights in place (excluded tables and padding: +0), block sums, running block totals C_b
@@ -4011,7 +4048,7 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int p = 16 * b + q;
-        sp[p] = (p < T) ? mvc_exp_le0(sp[p] - M) : 0.0;   // excluded: exp(-inf) = +0
+        sp[p] = (p < TR && p < T) ? mvc_exp_le0(sp[p] - M) : 0.0;   // excluded: exp(-inf) = +0
       }
       tot = tot + pw16_seq(sp + 16 * b);
       Cb[b] = tot;
@@ -4020,7 +4057,10 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
   const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);
   const double Wt = mvc_exp_le0(s_new - M) + tot;
   double r = u_i * Wt;
-  if (!(r < tot)) return -1;   // the new table
+  if (!(r < tot)) {
+    RUN_MARK(5);
+    return -1;   // the new table
+  }
   int bsel = NBk - 1;
 #pragma unroll
   for (int b = NBk - 1; b >= 0; --b)
@@ -4038,7 +4078,9 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
     for (int b = 1; b < NBk; ++b)
       if (b == bsel) x16[q] = sp[16 * b + q];
   }
-  return 16 * bsel + pw16_select_seq(x16, r);
+  const int pick = 16 * bsel + pw16_select_seq(x16, r);
+  RUN_MARK(5);
+  return pick;
 }
 
 // The run kernel's loop for small chains (L.lc == 3): the whole sweep staged
@@ -4080,6 +4122,7 @@ __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, co
     if (bad) flags |= kRunRestride;
   }
   for (;;) {
+    RUN_T0();
     if (flags & kRunRestride) break;
     if (cur >= n) {
       done = 1;
@@ -4097,17 +4140,24 @@ __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, co
       seq_bar(true);
       if (L.chk && mvc_run_bad[0]) break;
     }
+    RUN_MARK(3);
     const int q = tid >> 3;            // this group's customer in the step
     const int i = cur + q;
     const int ic = min(i, n - 1);      // (past n: a clamped customer, result unused)
     const int p0 = ring_z(G, ic, V, D);
     const LanePre LP = lane_pre(Wv, V, cc.hyp);
+    RUN_MARK(0);
     const int T = *cc.T;
     int c;
-    if (T <= 16)
-      c = seq_resample_lane8<16>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+    int kmx = 0;
+    for (int v = 0; v < V; ++v) kmx = max(kmx, cc.Klist[v]);
+    if (T <= 4 && kmx <= 4)   // the reference's own call at steady state
+      c = seq_resample_lane8<4, 4>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+    else if (T <= 16)
+      c = seq_resample_lane8<0, 16>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
     else
-      c = seq_resample_lane8<32>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+      c = seq_resample_lane8<0, 32>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+    RUN_MARK(1);
     const bool mv = (lane & 7) == 0 && i < n && c != p0;
     const uint64_t hit = __ballot(mv);
     const int first = hit ? (int)__builtin_ctzll(hit) : 0;
@@ -4142,6 +4192,10 @@ __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, co
       cur = cur + kLaneCust;
     }
     par ^= 1;
+    RUN_MARK(6);
+#ifdef MVC_RUN_PROF
+    if (tid == 0) mvc_prof_lds[7] += 1;
+#endif
   }
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
