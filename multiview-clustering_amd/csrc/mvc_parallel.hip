@@ -2748,8 +2748,9 @@ class ParallelSampler : public Sampler {
     // (instance 2 runs the global-scratch layout only: no dynamic LDS)
     for (const void *f : {(const void *)mvc_seq_run_kernel<0>, (const void *)mvc_seq_run_kernel<3>,
                           (const void *)mvc_seq_run_kernel<4>, (const void *)mvc_seq_run_kernel<5>,
-                          (const void *)mvc_seq_run_kernel_b<0>, (const void *)mvc_seq_run_kernel_b<3>,
-                          (const void *)mvc_seq_run_kernel_b<4>, (const void *)mvc_seq_run_kernel_b<5>})
+                          (const void *)mvc_seq_run_kernel<6>, (const void *)mvc_seq_run_kernel_b<0>,
+                          (const void *)mvc_seq_run_kernel_b<3>, (const void *)mvc_seq_run_kernel_b<4>,
+                          (const void *)mvc_seq_run_kernel_b<6>})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSeqLdsBudget));   // + the kernel's static LDS <= 160 KB
     MVC_HIP(hipFuncSetAttribute((const void *)mvc_seq_wide_fin_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 kWideFinLds));
@@ -3453,7 +3454,21 @@ class ParallelSampler : public Sampler {
     L.pfn = 0;
     L.vpo = 0;
     L.lc = 3;
+    L.small = (T <= kLaneSmall && kmax <= kLaneSmall) ? 1 : 0;
     return L;
+  }
+  // the layout of a repair round: the lane loop while this sweep runs it and
+  // the state still fits it, else the run kernels' (run_layout)
+  SeqLds pick_layout(int T, const int32_t *Klist, bool vp_ok) const {
+    if (lane_now) {
+      bool ok = T < kLaneTM;
+      for (int v = 0; v < V; ++v) ok = ok && Klist[v] <= kLaneMaxK;
+      if (ok) {
+        const SeqLds L = lane_layout(T, Klist);
+        if (L.lc == 3) return L;
+      }
+    }
+    return run_layout(T, Klist, vp_ok);
   }
   bool lane_sweep(const Chain &c) const {
     if (!use_lane || force_global || repair_grid_only || phase_a_only || shard_world > 1) return false;
@@ -3565,7 +3580,7 @@ class ParallelSampler : public Sampler {
     MVC_HIP(hipGetLastError());
     dbg("seq_first / eval", c, s);
     rr.vp_ok = true;   // value prediction until it stops itself in this sweep (R->vpoff)
-    rr.L = lane_now ? lane_layout(c.T, c.K.data()) : run_layout(c.T, c.K.data(), rr.vp_ok);
+    rr.L = pick_layout(c.T, c.K.data(), rr.vp_ok);
     // the gated early MH (below) only where no per-phase timers bracket the
     // repair and the MH separately (they would time the MH as repair)
     // (not for small chains: nearly every sweep of theirs moves someone, so the
@@ -3615,13 +3630,20 @@ class ParallelSampler : public Sampler {
         L.dyn = run_dyn(L);
         L.fill = lds_fill_byte();
         L.chk = run_check() ? 1 : 0;
-        hipLaunchKernelGGL(L.lc ? (L.lc == 3 ? mvc_seq_run_kernel<5> : L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
+        if (L.lc == 3 && L.small && rr.birth_retry) {   // the small lane loop left a birth pending: commit it first
+          rr.birth_retry = false;
+          hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, rr.Q);
+          MVC_HIP(hipGetLastError());
+          dbg("seq_birth", c, s);
+        }
+        hipLaunchKernelGGL(L.lc ? (L.lc == 3 ? (L.small ? mvc_seq_run_kernel<5> : mvc_seq_run_kernel<6>)
+                                             : L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
                                 : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
                            dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, rr.Q, L);
       }
       MVC_HIP(hipGetLastError());
-      dbg(repair_grid_only ? "seq_apply" : L.lc == 3 ? "seq_run<5>" : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
-      if (L.lc && !repair_grid_only && rr.birth_retry) {   // a birth the loop left pending (births commit in the kernel)
+      dbg(repair_grid_only ? "seq_apply" : L.lc == 3 ? (L.small ? "seq_run<5>" : "seq_run<6>") : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);
+      if (L.lc && !(L.lc == 3 && L.small) && !repair_grid_only && rr.birth_retry) {   // a birth the loop left pending (births commit in the kernel)
         rr.birth_retry = false;
         hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, rr.Q);
         MVC_HIP(hipGetLastError());
@@ -3657,11 +3679,12 @@ class ParallelSampler : public Sampler {
       if (rr.L.lc == 2) rr.L.lc = 1;
     }
     if (rs.restride) {
-      rr.L = run_layout(rs.T, rs.Klist, rr.vp_ok);
+      rr.L = pick_layout(rs.T, rs.Klist, rr.vp_ok);
       MVC_HIP(hipMemsetAsync(&c.R->restride, 0, sizeof(int32_t), stream));
       return 0;
     }
     if (rs.done) return 1;
+    if (rr.L.lc == 3 && rr.L.small && rs.pend && rs.pchoice < 0) rr.birth_retry = true;   // (committed before the next launch)
     rr.rounds = std::min(rr.rounds * 4, 1024);
     return 2;
   }
@@ -4112,12 +4135,13 @@ class ChainSet : public Sampler {
       for (int c : act) {
         const ParallelSampler &S = *subs[c];
         const SeqLds &L = rr[c].L;
-        kinds[c] = (S.repair_grid_only || S.run_wgrid(L)) ? -1 : L.lc == 3 ? 5 : L.lc == 2 ? 4 : L.lc ? 3 : L.tw == 1 ? 0 : 2;
+        // (lane loops batched in the general instance <6>: births commit in the kernel)
+        kinds[c] = (S.repair_grid_only || S.run_wgrid(L)) ? -1 : L.lc == 3 ? 6 : L.lc == 2 ? 4 : L.lc ? 3 : L.tw == 1 ? 0 : 2;
       }
       int nb = 0;   // batched members, grouped by kind
       std::vector<std::pair<int, int>> groups;   // (kind, first index), each up to the next
       std::vector<size_t> dyn;
-      for (int k : {5, 4, 3, 0, 2}) {
+      for (int k : {6, 4, 3, 0, 2}) {
         const int first = nb;
         size_t dmax = 0;
         for (int c : act) {
@@ -4142,13 +4166,13 @@ class ChainSet : public Sampler {
       // (its wave stride set to the batched grid's).  A chain launched on its
       // own stream runs its own window evaluation inside repair_rounds; the
       // batched one must not evaluate it concurrently.
-      // (the lane loop's chains, kind 5, open no windows: after the others)
+      // (the lane loop's chains, kind 6, open no windows: after the others)
       std::vector<int> ord;
       for (int c : act)
-        if (kinds[c] >= 0 && kinds[c] != 5) ord.push_back(c);
+        if (kinds[c] >= 0 && kinds[c] != 6) ord.push_back(c);
       const int n_bat = (int)ord.size();
       for (int c : act)
-        if (kinds[c] == 5) ord.push_back(c);
+        if (kinds[c] == 6) ord.push_back(c);
       for (int c : act)
         if (kinds[c] < 0) ord.push_back(c);
       for (size_t j = 0; j < ord.size(); ++j) {
@@ -4173,7 +4197,7 @@ class ChainSet : public Sampler {
           const SeqArgs *a = bA_dev + f;
           const SeqLds *l = bL_dev + f;
           switch (k) {
-            case 5: hipLaunchKernelGGL(mvc_seq_run_kernel_b<5>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
+            case 6: hipLaunchKernelGGL(mvc_seq_run_kernel_b<6>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
             case 4: hipLaunchKernelGGL(mvc_seq_run_kernel_b<4>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
             case 3: hipLaunchKernelGGL(mvc_seq_run_kernel_b<3>, grid, dim3(kSeqLcThreads), dyn[g], bs, a, l); break;
             case 0: hipLaunchKernelGGL(mvc_seq_run_kernel_b<0>, grid, dim3(kSeqRunThreads), dyn[g], bs, a, l); break;

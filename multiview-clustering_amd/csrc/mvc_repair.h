@@ -89,6 +89,7 @@ struct SeqLds {
   int32_t lc;           // 1: the lane-column evaluation (seq_resample_lc; LDS layout with S1 cached, ts <= 512); 2: + value prediction
   int64_t vpo;          // lc == 2: offset (doubles) of the overlay's S1 columns [kVpE][D] in the dynamic LDS
   int64_t dyn;          // bytes of dynamic LDS of the launch
+  int32_t small;        // lc == 3: every dish list and the tables <= kLaneSmall (mvc_seq_run_kernel<5>)
   int32_t fill;         // MVC_LDS_FILL diagnostics: >= 0 fills the block's LDS with this byte at launch
   int32_t chk;          // MVC_RUN_CHECK diagnostics: check every index a commit writes through (R->dbg)
 };
@@ -3843,11 +3844,17 @@ struct LanePre {
   const double *pre;   // this wave's row
   __device__ __forceinline__ double at(int k) const { return pre[k]; }
 };
-__device__ __forceinline__ LanePre lane_pre(const SView &W, int V, const double *hyp) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// The values, one per lane and half (k = 64 h + lane), computed by the
+// evaluation itself (interleaved with its own work), then published into the
+// wave's row (lane_pre_publish) before the first read.
+struct LanePreVals {
+  double x[2];
+};
+__device__ __forceinline__ LanePreVals lane_pre_vals(const SView &W, int V, const double *hyp) {
+  const int lane = threadIdx.x & 63;
   const double ag = hyp[3 * V], sg = hyp[3 * V + 1];
   const int T = *W.T, T_ne = *W.T_ne;
-  double *row = mvc_lane_pre[w];
+  LanePreVals P;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int k = 64 * h + lane;
@@ -3860,10 +3867,33 @@ __device__ __forceinline__ LanePre lane_pre(const SView &W, int V, const double 
     } else if (k < 2 * V + 2 + T) {
       arg = (double)(W.n_t[k - 2 * V - 2] - 1) - sg;
     }
-    row[k] = mvc_log(arg);
+    P.x[h] = mvc_log(arg);
   }
+  return P;
+}
+__device__ __forceinline__ LanePre lane_pre_publish(const LanePreVals &P) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double *row = mvc_lane_pre[w];
+  row[lane] = P.x[0];
+  row[64 + lane] = P.x[1];
   wave_lds_sync();
   return LanePre{row};
+}
+
+// Lane u of every 8-lane group broadcast to its group (u < 8 compile-time
+// after unrolling): DPP row_newbcast of lane u / 8 + u of the 16-lane row.
+__device__ __forceinline__ double group8_bcast(double x, int u) {
+  const bool hi = (threadIdx.x & 8) != 0;
+  switch (u) {
+    case 0: return hi ? row_bcast_d<8>(x) : row_bcast_d<0>(x);
+    case 1: return hi ? row_bcast_d<9>(x) : row_bcast_d<1>(x);
+    case 2: return hi ? row_bcast_d<10>(x) : row_bcast_d<2>(x);
+    case 3: return hi ? row_bcast_d<11>(x) : row_bcast_d<3>(x);
+    case 4: return hi ? row_bcast_d<12>(x) : row_bcast_d<4>(x);
+    case 5: return hi ? row_bcast_d<13>(x) : row_bcast_d<5>(x);
+    case 6: return hi ? row_bcast_d<14>(x) : row_bcast_d<6>(x);
+    default: return hi ? row_bcast_d<15>(x) : row_bcast_d<7>(x);
+  }
 }
 
 // seq_resample for one customer on an 8-lane group of a wave, lane v of the
@@ -3892,13 +3922,13 @@ __device__ __forceinline__ LanePre lane_pre(const SView &W, int V, const double 
 // compile-time +0 of the last block's padding.
 template <int KB, int TR>
 __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView &W, const Cust &C, int i, int p0,
-                                                  const double *hyp, const double *cnewv, const LanePre &LP) {
+                                                  const double *hyp, const double *cnewv) {
   static_assert(TR <= 64 && (TR % 16 == 0 || TR < 16), "TR: whole blocks of 16, or part of one");
   static_assert(KB == 0 || KB <= 16, "KB: the straight-line dishes");
   constexpr int NBk = (TR + 15) / 16;
   constexpr int TM = 16 * NBk;
   RUN_T0();
-  const int lane = threadIdx.x & 63, gb = lane & ~7, v = lane & 7;
+  const int v = threadIdx.x & 7;
   const int V = A.P.V, D = A.P.D, ts = W.ts, ks = W.ks, s1s = W.s1s;
   const bool vok = v < V;
   const int vv = vok ? v : V - 1;
@@ -3906,6 +3936,8 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
   const int np0 = W.n_t[p0] - 1;
   const bool alive = np0 > 0;
   const int T = *W.T;
+  const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);   // independent of the rest
+  const LanePreVals PV = lane_pre_vals(W, V, hyp);                                     // (interleaved with the views)
   // ---- lane v: view v's terms and the lp of every table's dish
   const int K = W.Klist[vv];
   const double tau = hyp[vv], alpha = hyp[V + vv], sigma = hyp[2 * V + vv];
@@ -3992,23 +4024,29 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
       }
     }
   }
-  double lm;
+  double Sv = pw16_seq(col);
   {
-    double Sv = pw16_seq(col);
     double wn = alpha + (double)cnt * sigma;
     if (wn < 0.0) wn = 0.0;
     Sv = Sv + wn * mvc_exp_le0(lfn - m);
-    const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
-    const double logden = LP.at(alive ? vv : V + vv);
-    lm = (denom <= 0.0) ? lfn : (m + mvc_log(Sv)) - logden;
   }
+  const double logS = mvc_log(Sv);
   RUN_MARK(2);
   double lt[TR];   // lp of table p's dish in this lane's view
 #pragma unroll
   for (int p = 0; p < TR; ++p) lt[p] = lpj(W.dish[vv * ts + min(p, T - 1)]);
-  // ---- the group: sums in view order over its lanes
+  const LanePre LP = lane_pre_publish(PV);
+  double lm;
+  {
+    const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
+    const double logden = LP.at(alive ? vv : V + vv);
+    lm = (denom <= 0.0) ? lfn : (m + logS) - logden;
+  }
+  // ---- the group: sums in view order over its lanes (DPP broadcasts from lane u of the group)
   double s_new = LP.at(alive ? 2 * V : 2 * V + 1);   // log(ag + sg T_ne')
-  for (int u = 0; u < V; ++u) s_new = s_new + __shfl(lm, gb + u, 64);
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (u < V) s_new = s_new + group8_bcast(lm, u);
   const double lmass0 = LP.at(2 * V + 2 + p0);   // log((n_p0 - 1) - sg)
   double sp[TM];
   uint64_t inc = 0;   // tables included in the draw (n_p' >= 1, n_p' - sigma_g > 0)
@@ -4024,12 +4062,15 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
       }
     }
   }
-  for (int u = 0; u < V; ++u) {
 #pragma unroll
-    for (int p = 0; p < TR; ++p) {
-      if (TR <= 4 || p < T) {
-        const double x = __shfl(lt[p], gb + u, 64);
-        if ((inc >> p) & 1ull) sp[p] = sp[p] + x;
+  for (int u = 0; u < 8; ++u) {
+    if (u < V) {
+#pragma unroll
+      for (int p = 0; p < TR; ++p) {
+        if (TR <= 4 || p < T) {
+          const double x = group8_bcast(lt[p], u);
+          if ((inc >> p) & 1ull) sp[p] = sp[p] + x;
+        }
       }
     }
   }
@@ -4054,7 +4095,6 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
       Cb[b] = tot;
     }
   }
-  const double u_i = mvc_uniform(A.seed, (uint32_t)i, A.sweep, A.chain, MVC_TAG_Z);
   const double Wt = mvc_exp_le0(s_new - M) + tot;
   double r = u_i * Wt;
   if (!(r < tot)) {
@@ -4094,6 +4134,12 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
 // committed by the four waves (seq_commit_move_split); a birth ends the loop
 // and seq_run_body commits it on the global state, then resumes here.
 constexpr int kLaneCust = kSeqLcThreads / 8;   // customers per step
+// kSmall (mvc_seq_run_kernel<5>, L.small): every dish list and the tables <= 8,
+// one straight-line evaluation instance and no birth commit in the kernel
+// (a birth ends the launch; mvc_seq_birth_kernel commits it), so the loop's
+// registers are the small evaluation's (a larger state exits with restride).
+constexpr int kLaneSmall = 8;
+template <bool kSmall>
 __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U) {
   constexpr int kW = kSeqLcThreads / 64;
   int flags = 0;
@@ -4117,8 +4163,8 @@ __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, co
     __syncthreads();
   }
   {   // the layout holds the lists plus one birth (moves add no table and no dish)
-    bool bad = *cc.T >= L.ts;
-    for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks;
+    bool bad = *cc.T >= L.ts || (kSmall && *cc.T > kLaneSmall);
+    for (int v = 0; v < V; ++v) bad = bad || cc.Klist[v] >= L.ks || (kSmall && cc.Klist[v] > kLaneSmall);
     if (bad) flags |= kRunRestride;
   }
   for (;;) {
@@ -4145,18 +4191,21 @@ __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, co
     const int i = cur + q;
     const int ic = min(i, n - 1);      // (past n: a clamped customer, result unused)
     const int p0 = ring_z(G, ic, V, D);
-    const LanePre LP = lane_pre(Wv, V, cc.hyp);
     RUN_MARK(0);
     const int T = *cc.T;
     int c;
-    int kmx = 0;
-    for (int v = 0; v < V; ++v) kmx = max(kmx, cc.Klist[v]);
-    if (T <= 4 && kmx <= 4)   // the reference's own call at steady state
-      c = seq_resample_lane8<4, 4>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
-    else if (T <= 16)
-      c = seq_resample_lane8<0, 16>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
-    else
-      c = seq_resample_lane8<0, 32>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew, LP);
+    if constexpr (kSmall) {   // the reference's own call at steady state
+      c = seq_resample_lane8<kLaneSmall, kLaneSmall>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew);
+    } else {
+      int kmx = 0;
+      for (int v = 0; v < V; ++v) kmx = max(kmx, cc.Klist[v]);
+      if (T <= kLaneSmall && kmx <= kLaneSmall)
+        c = seq_resample_lane8<kLaneSmall, kLaneSmall>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew);
+      else if (T <= 16)
+        c = seq_resample_lane8<0, 16>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew);
+      else
+        c = seq_resample_lane8<0, 32>(A, Wv, G.cust(ic, V, D), ic, p0, cc.hyp, cc.cnew);
+    }
     RUN_MARK(1);
     const bool mv = (lane & 7) == 0 && i < n && c != p0;
     const uint64_t hit = __ballot(mv);
@@ -4225,7 +4274,8 @@ __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, co
 // One instance per evaluation shape, compiled separately so each keeps its
 // own register allocation.
 // kMode 0: one wave per customer; 2: wide (L.tw > 1, global layout); 3: lane columns (L.lc == 1);
-// 4: + value prediction (L.lc == 2); 5: one customer per lane, small chains (L.lc == 3)
+// 4: + value prediction (L.lc == 2); 5 / 6: eight lanes per customer, small chains (L.lc == 3;
+// 5: small states, L.small)
 template <int kMode>
 __device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
   Repair *R = A.R;
@@ -4350,7 +4400,9 @@ __device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
       else if constexpr (kMode == 4)
         flags = seq_run_loop_vp(A, L, G, U);
       else if constexpr (kMode == 5)
-        flags = seq_run_loop_lane(A, L, G, U);
+        flags = seq_run_loop_lane<true>(A, L, G, U);
+      else if constexpr (kMode == 6)
+        flags = seq_run_loop_lane<false>(A, L, G, U);
       else
         flags = seq_run_loop<true, false>(A, L, cache_view(cc, A), &cc,
                                           SeqScratch(mvc_seq_lds + L.cache_dbl + (int64_t)w * L.stride, V, L.ks, L.ts),
@@ -4386,7 +4438,7 @@ __device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
         R->fmin = n;
       }
     }
-    if constexpr (kMode >= 3) {
+    if constexpr (kMode >= 3 && kMode != 5) {   // (the small lane loop leaves births to mvc_seq_birth_kernel)
       __shared__ int s_birth, s_bi;
       __syncthreads();
       if (tid == 0) {

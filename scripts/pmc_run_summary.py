@@ -1,4 +1,4 @@
-"""Summary of scripts/gpu_pmc_run.sh: the run kernel's SQ counters summed over
+"""Summary of scripts/gpu_pmc_run.sh / gpu_pmc_lane.sh: the run kernel's SQ counters summed over
 its launches in one warm north-star-literal sweep, per repair iteration
 (the iteration count is the run's own, from the probe log's first sweep)."""
 import csv
@@ -9,12 +9,12 @@ from collections import defaultdict
 
 tag = sys.argv[1]
 out = {"tag": tag, "kernel": "mvc_seq_run_kernel (every instance the sweep launched)", "counters": {}}
-for grp in ("a", "b", "c"):
+for grp in ("a", "b", "c", "d"):
     tot = defaultdict(float)
     launches = set()
     for f in glob.glob(f"gpurun_out/pmcr_{tag}_{grp}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "mvc_seq_run_kernel" not in r["Kernel_Name"]:
+            if "mvc_seq_run_kernel" not in r["Kernel_Name"] or (len(sys.argv) > 2 and sys.argv[2] not in r["Kernel_Name"]):
                 continue
             launches.add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
             tot[r["Counter_Name"]] += float(r["Counter_Value"])
