@@ -374,12 +374,28 @@ __device__ __forceinline__ void lpbig_pair_ksteps(mvc_d2 xy, double &a0, double 
   a1 = __longlong_as_double(((long long)h32[1] << 32) | (unsigned)l32[1]);
 }
 
+// A dish block's view maximum of a customer: vmode 0 writes it (the view's
+// first block), 1 maxes it into the earlier blocks' value (launches in block
+// order), 2 is an atomic max into a row pre-filled with -inf (every block of
+// the view in one launch, mvc_par_lpbig_group_kernel).  Max is exact, so the
+// block order does not matter: the same bits every way.  Lanes without a
+// customer (!ok) store to their discard slot, but never atomically: those
+// slots are shared by every wave of the grid.
+__device__ __forceinline__ void lpbig_vmax_put(int vmode, bool ok, double *dm, double m, double mprev) {
+  if (vmode == 2) {
+    if (ok) __builtin_amdgcn_flat_atomic_fmax_f64(dm, m);
+  } else {
+    if (vmode == 1) m = dmax(m, mprev);
+    *dm = m;
+  }
+}
+
 // The dish-block producer's tiles with the k-steps unrolled (SPC = D / 4):
 // the same MFMA chain and epilogue as the runtime-SP loop of
 // mvc_par_lpbig_kernel, so the same bits.  A-fragments are read 16 bytes per
 // lane (two k-steps, lpbig_pair_ksteps), RP pair loads ahead.
 template <int NTB, int SPC>
-__device__ __forceinline__ void lpbig_tiles(const Sweep &A, int v, int jb0, int kb, int first, int b0, int nb,
+__device__ __forceinline__ void lpbig_tiles(const Sweep &A, int v, int jb0, int kb, int vmode, int b0, int nb,
                                             double *lpb, double *dslot, const double *yv, const double *Bs, double *y2s,
                                             double *selfG, double *mrest, const double *b_c0, const double *b_cb,
                                             const double *b_Q, const int *b_l, const int *b_dn, const int *t_dish,
@@ -411,7 +427,7 @@ __device__ __forceinline__ void lpbig_tiles(const Sweep &A, int v, int jb0, int 
     const int pz = P.z[b0 + li_row];
     const double y2 = A.Y2[(size_t)v * n + b0 + li_row];
     double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
-    const double mprev = *dm;   // (unconditional load: read only when !first)
+    const double mprev = *dm;   // (unconditional load: read only when vmode == 1)
     const mvc_d2 *yn = rowp(tile + NWT);
     mvc_d4 acc[NTB];
 #pragma unroll
@@ -504,8 +520,7 @@ __device__ __forceinline__ void lpbig_tiles(const Sweep &A, int v, int jb0, int 
       }
       const double lfn = cnew + hself;
       if (lfn > m) m = lfn;
-      if (!first) m = dmax(m, mprev);   // max is exact: the block order does not matter
-      *dm = m;
+      lpbig_vmax_put(vmode, ok, dm, m, mprev);
     }
     wave_lds_sync();
   }
@@ -530,9 +545,8 @@ __device__ __forceinline__ void lpbig_tiles(const Sweep &A, int v, int jb0, int 
 // from global memory but the tile's z / Y2 / previous view maximum, issued
 // at the tile start: no in-order vmcnt drain per k-step chunk or per tile.
 template <int NTB, int SPC>
-__global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int jb0, int kb, int first, int b0, int nb,
-                                                            double *lpb, double *discard) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void lpbig_run(const Sweep &A, int v, int jb0, int kb, int vmode, int b0, int nb,
+                                          double *lpb, double *discard, int gw, int NWT, char *smem) {
   const ParState &P = A.P;
   const int tid = threadIdx.x;
   const int lane = tid & 63, w = tid >> 6, BW = blockDim.x >> 6;
@@ -578,11 +592,10 @@ __global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int 
   __syncthreads();
   const double cnew = A.cnew[v];
   const int ntile = (nb + 15) >> 4;
-  const int gw = blockIdx.x * BW + w, NWT = gridDim.x * BW;
   double *const dslot = discard + lane;
   const double *yv = A.y + (size_t)v * n * D;
   if constexpr (SPC > 0) {
-    lpbig_tiles<NTB, SPC>(A, v, jb0, kb, first, b0, nb, lpb, dslot, yv, Bs, y2s, selfG, mrest, b_c0, b_cb, b_Q, b_l,
+    lpbig_tiles<NTB, SPC>(A, v, jb0, kb, vmode, b0, nb, lpb, dslot, yv, Bs, y2s, selfG, mrest, b_c0, b_cb, b_Q, b_l,
                           b_dn, t_dish, t_n, zs, gw, NWT, ntile, tau, L2pt, cnew);
     return;
   }
@@ -690,11 +703,45 @@ __global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int 
       const double lfn = cnew + hself;
       if (lfn > m) m = lfn;
       double *dm = ok ? A.vmax + (size_t)v * n + b0 + li0 + col : dslot;
-      if (!first && ok) m = dmax(m, *dm);   // max is exact: the block order does not matter
-      *dm = m;
+      lpbig_vmax_put(vmode, ok, dm, m, vmode == 1 && ok ? *dm : m);
     }
     wave_lds_sync();
   }
+}
+// one dish block per launch, blocks of a view in order (vmode 0 for the first)
+template <int NTB, int SPC>
+__global__ __launch_bounds__(512) void mvc_par_lpbig_kernel(Sweep A, int v, int jb0, int kb, int first, int b0, int nb,
+                                                            double *lpb, double *discard) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int BW = blockDim.x >> 6, w = threadIdx.x >> 6;
+  lpbig_run<NTB, SPC>(A, v, jb0, kb, first ? 0 : 1, b0, nb, lpb, discard, blockIdx.x * BW + w, gridDim.x * BW, smem);
+}
+// Every dish block of view v in one launch (nblk blocks of 16 NTB dishes, one
+// workgroup per CU): the workgroups that share an XCD (b and b + 8, dealt
+// round-robin over the 8 XCDs -- for speed only, any placement is correct)
+// form groups of nblk, one per dish block, and the members of a group walk the
+// same customer tiles in the same order, so each y tile is fetched from HBM
+// once and re-read by the group's other dish blocks from the XCD's L2 (or the
+// Infinity Cache) instead of once per dish-block launch.  The view maximum is
+// an atomic max into the pre-filled row (lpbig_vmax_put, vmode 2).  gridDim.x is
+// a multiple of 8; workgroups beyond the last whole group per XCD, and dish
+// blocks past K_v, have no work.
+template <int NTB, int SPC>
+__global__ __launch_bounds__(512) void mvc_par_lpbig_group_kernel(Sweep A, int v, int nblk, int b0, int nb,
+                                                                  double *lpb, double *discard) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int L = gridDim.x >> 3, local = blockIdx.x >> 3, xs = blockIdx.x & 7;
+  const int GL = L / nblk, gi = local / nblk, db = local - gi * nblk;
+  const int K = A.Koff[v + 1] - A.Koff[v];
+  const int jb0 = 16 * NTB * db, kb = min(16 * NTB, K - jb0);
+  if (gi >= GL || kb <= 0) return;   // whole workgroup, before any barrier
+  const int BW = blockDim.x >> 6, w = threadIdx.x >> 6;
+  const int group = xs + 8 * gi, G = 8 * GL;
+  lpbig_run<NTB, SPC>(A, v, jb0, kb, 2, b0, nb, lpb, discard, group * BW + w, G * BW, smem);
+}
+// vmax[v][b0 .. b0 + nb) = -inf before a grouped launch
+__global__ void mvc_par_vmax_fill_kernel(double *row, int nb) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) row[i] = -MVC_PM_INF;
 }
 __host__ inline size_t lpbig_shared_bytes(int SP, int NTB, int T, int waves) {
   return 8 * ((size_t)SP * NTB * 64 + (size_t)waves * 48 + 48 * NTB) + 4 * (32 * NTB + 2 * (size_t)T + (size_t)waves * 16) + 64;
@@ -2539,6 +2586,7 @@ class ParallelSampler : public Sampler {
   bool repair_grid_only = false;  // MVC_PATH repair=grid: every mover through a grid window round (no run kernel)
   bool force_big = false;         // big=1: the dish-block producer even where the tiled one applies (tests)
   bool big_runtime_sp = false;    // big_sp=runtime: the dish-block producer's runtime k-step loop only (tests)
+  bool big_group = true;          // big_group=0: one launch per dish block (y re-read per block) instead of the XCD-grouped launch
   static constexpr int big_bpc_narrow = 3;   // 4-wave blocks per CU of the dish-block producer's 16 / 32-dish instances
   static constexpr int run_limit = kSeqRunLimit;
   // waves=N: customers the run kernel evaluates per step.  4 by default:
@@ -2762,11 +2810,14 @@ class ParallelSampler : public Sampler {
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024));
 #define MVC_LPBIG_FNS(NTB_)                                                                            \
   (const void *)mvc_par_lpbig_kernel<NTB_, 0>, (const void *)mvc_par_lpbig_kernel<NTB_, 16>,             \
-      (const void *)mvc_par_lpbig_kernel<NTB_, 32>, (const void *)mvc_par_lpbig_kernel<NTB_, 64>
+      (const void *)mvc_par_lpbig_kernel<NTB_, 32>, (const void *)mvc_par_lpbig_kernel<NTB_, 64>,      \
+      (const void *)mvc_par_lpbig_group_kernel<NTB_, 0>, (const void *)mvc_par_lpbig_group_kernel<NTB_, 16>, \
+      (const void *)mvc_par_lpbig_group_kernel<NTB_, 32>, (const void *)mvc_par_lpbig_group_kernel<NTB_, 64>
     for (const void *f : {MVC_LPBIG_FNS(4), MVC_LPBIG_FNS(2), MVC_LPBIG_FNS(1)})
       MVC_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
 #undef MVC_LPBIG_FNS
     big_runtime_sp = path_opt("big_sp") && std::strcmp(path_opt("big_sp"), "runtime") == 0;
+    big_group = path_int("big_group", 1) != 0;
     run_waves = std::max(1, std::min(kSeqRunWaves, path_int("waves", run_waves)));
     if (const char *e = path_opt("lc")) {   // 0: neither lane-column nor lane loop; col: lane columns only
       use_lc = e[0] != '0';
@@ -3315,6 +3366,40 @@ class ParallelSampler : public Sampler {
           while (vntb > 1 && 16 * (vntb / 2) >= c.K[v]) vntb /= 2;
           int vwaves = big_waves;
           if (vntb != big_ntb) vwaves = lpbig_shared_bytes(SPb, vntb, c.T, 4) <= 80 * 1024 ? 4 : 8;
+          const int nblk = (c.K[v] + 16 * vntb - 1) / (16 * vntb);
+          if (big_group && nblk >= 2) {
+            // every dish block of the view in one launch, XCD-grouped (y read once)
+            const size_t lds = lpbig_shared_bytes(SPb, vntb, c.T, vwaves);
+            int per_cu = vwaves == 8 ? 1 : (vntb <= 2 ? big_bpc_narrow : 2);
+            per_cu = std::max(1, std::min<int>(per_cu, (int)((160 * 1024) / std::max<size_t>(lds, 1))));
+            const int grid = per_cu * n_cu;
+            if (n_cu % 8 == 0 && grid / 8 >= nblk) {
+              hipLaunchKernelGGL(mvc_par_vmax_fill_kernel, dim3(std::min(1024, (nb + 255) / 256)), dim3(256), 0, stream,
+                                 A.vmax + (size_t)v * n + b0, nb);
+              Sweep Ab = A;
+              Ab.SP = SPb;
+              const int spc = (4 * SPb == D && !big_runtime_sp && (SPb == 16 || SPb == 32 || SPb == 64)) ? SPb : 0;
+#define MVC_LPBIG(NTB_, SPC_)                                                                                        \
+  hipLaunchKernelGGL((mvc_par_lpbig_group_kernel<NTB_, SPC_>), dim3(grid), dim3(64 * vwaves), lds, stream, Ab, v, nblk, \
+                     (int)b0, nb, lpb, lpb + lpb_cap)
+#define MVC_LPBIG_SP(NTB_)         \
+  switch (spc) {                   \
+    case 16: MVC_LPBIG(NTB_, 16); break; \
+    case 32: MVC_LPBIG(NTB_, 32); break; \
+    case 64: MVC_LPBIG(NTB_, 64); break; \
+    default: MVC_LPBIG(NTB_, 0); break;  \
+  }
+              switch (vntb) {
+                case 4: MVC_LPBIG_SP(4) break;
+                case 2: MVC_LPBIG_SP(2) break;
+                default: MVC_LPBIG_SP(1) break;
+              }
+#undef MVC_LPBIG_SP
+#undef MVC_LPBIG
+              MVC_HIP(hipGetLastError());
+              continue;
+            }
+          }
           for (int jb0 = 0, first = 1; jb0 < c.K[v]; jb0 += 16 * vntb, first = 0) {
             const int kb = std::min(16 * vntb, c.K[v] - jb0);
             const size_t lds = lpbig_shared_bytes(SPb, vntb, c.T, vwaves);

@@ -828,7 +828,7 @@ def test_last_customer_birth_with_poisoned_lds(vp):
     assert int(r.stdout.split("last-birth OK")[1].split()[0]) >= 4
 
 
-@pytest.mark.parametrize("force", ["", "1", "d256", "d256-runtime"])
+@pytest.mark.parametrize("force", ["", "1", "d256", "d256-runtime", "d256-separate"])
 def test_dish_block_producer(force, monkeypatch):
     """The dish-block MFMA producer (mvc_par_lpbig_kernel: A-fragments from y
     itself, dishes in blocks of 64, the view maximum combined over blocks):
@@ -836,9 +836,13 @@ def test_dish_block_producer(force, monkeypatch):
     k-step loop), warm; forced onto a K <= 64 shape that the tiled producer
     would take (D = 64: the unrolled tile); and configs[4]'s D = 256 with
     K_v = 80 / 40 (a 64 + 16 dish split), unrolled and with the runtime loop
-    (MVC_PATH big_sp=runtime); bitwise vs the oracle."""
+    (MVC_PATH big_sp=runtime).  A view with two or more dish blocks runs them
+    in one XCD-grouped launch (mvc_par_lpbig_group_kernel, the view maximum
+    an atomic max) unless MVC_PATH big_group=0 ("d256-separate": one launch
+    per block, the maximum combined in block order); bitwise vs the oracle."""
     if force:
-        _path(monkeypatch, big="1", **({"big_sp": "runtime"} if force == "d256-runtime" else {}))
+        _path(monkeypatch, big="1", **({"big_sp": "runtime"} if force == "d256-runtime" else
+                                       {"big_group": "0"} if force == "d256-separate" else {}))
     m = _mvc()
     from mvc_amd import data
     N, V, D, K = {"": (6000, 3, 32, 128), "1": (4100, 4, 64, 64)}.get(force, (3000, 2, 256, 80))
