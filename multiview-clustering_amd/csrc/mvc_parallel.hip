@@ -2021,7 +2021,7 @@ struct MHArgs {
 // global pair at the same time when T is small (one-wave tree64 = the block
 // tree64's association), else the whole block runs it afterwards.
 constexpr int kHypWaves = 8, kHypViewWaves = kHypWaves - 1, kHypThreads = 64 * kHypWaves, kHypGlobalWaveT = 512;
-extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(MHArgs A) {
+__device__ __forceinline__ void hyper_body(MHArgs &A) {
   ParState &P = A.P;
   const int tid = threadIdx.x;
   const int V = P.V, D = P.D, KC = P.KC, n = P.n;
@@ -2448,6 +2448,37 @@ extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(M
   HYP_MARK("coef");
 #undef HYP_MARK
 }
+extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel(MHArgs A) { hyper_body(A); }
+// The same for several chains (one block per chain): the chain-batched sweep
+extern "C" __global__ __launch_bounds__(kHypThreads) void mvc_par_hyper_kernel_b(const MHArgs *As) {
+  MHArgs A = As[blockIdx.x];
+  hyper_body(A);
+}
+
+// Every chain's sample of a chain set in one snapshot (blockIdx.y = chain):
+// z [n], the tables' raw dish ids d_id[v][dish[v][p]] for p < T (T from the
+// status row), the hyperparameters [3V + 2] and T.
+struct SnapArgs {
+  const int32_t *z, *dish, *did, *status;
+  const double *hyp;
+  int32_t TC, KC;
+};
+extern "C" __global__ void mvc_par_snapshot_all_kernel(const SnapArgs *As, int n, int V, int dcap, int32_t *dz,
+                                                       int32_t *ddish, int32_t *dT, double *dhyp) {
+  const int c = blockIdx.y;
+  const SnapArgs S = As[c];
+  const int T = S.status[0];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dz[(size_t)c * n + i] = S.z[i];
+  if (blockIdx.x == 0) {
+    const int H = 3 * V + 2;
+    for (int k = threadIdx.x; k < V * dcap; k += blockDim.x) {
+      const int v = k / dcap, p = k - v * dcap;
+      ddish[(size_t)c * V * dcap + k] = p < T ? S.did[(size_t)v * S.KC + S.dish[(size_t)v * S.TC + p]] : 0;
+    }
+    for (int k = threadIdx.x; k < H; k += blockDim.x) dhyp[(size_t)c * H + k] = S.hyp[k];
+    if (threadIdx.x == 0) dT[c] = T;
+  }
+}
 
 // ===========================================================================
 // Host side of the parallel schedule.
@@ -2548,6 +2579,7 @@ class ParallelSampler : public Sampler {
     // sweep's status synchronisation, so they outlive the copies.
     int32_t *hpin = nullptr;
     bool s1t_ok = false;
+    bool s1t_stale = false;        // S1 changed in a chain-batched lane sweep: S1t rebuilt before the next phase A
     int T = 0;
     std::vector<int32_t> K;
     uint32_t gid = 0;
@@ -3092,6 +3124,7 @@ class ParallelSampler : public Sampler {
   }
 
   void tile_s1(Chain &c) {
+    c.s1t_stale = false;
     int Kmax = 1;
     for (int k : c.K) Kmax = std::max(Kmax, k);
     c.s1t_ok = false;
@@ -3114,7 +3147,7 @@ class ParallelSampler : public Sampler {
     timers.end("stats", ev);
   }
 
-  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr) {
+  MHArgs mh_args(const Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr) const {
     MHArgs A;
     A.P = c.P;
     A.status = c.status;
@@ -3126,6 +3159,10 @@ class ParallelSampler : public Sampler {
     A.sweep = sweep_ix;
     A.do_mh = do_mh;
     A.gate = gate;
+    return A;
+  }
+  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr) {
+    const MHArgs A = mh_args(c, do_mh, sweep_ix, gate);
     hipEvent_t ev = nullptr;
     timers.begin("hyper", &ev);
     hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(kHypThreads), 0, stream, A);
@@ -3252,11 +3289,15 @@ class ParallelSampler : public Sampler {
   // customers and, when sharded, the exchange of the choices.  false: the
   // caller stops here (mvc_sampler_phase_a).
   bool sweep_pre(Chain &c, uint32_t s, bool &phaseA_out) {
-    Sweep A = make_sweep(c, s);
-    const SeqArgs Q0 = make_seq(c, s);
     // small chains: the run kernel's lane-per-customer loop runs the whole
     // sweep from customer 0 (its first step is phase A)
     lane_now = lane_sweep(c);
+    if (!lane_now && c.s1t_stale) {   // after chain-batched lane sweeps (ChainSet::sweep_batched)
+      c.s1t_stale = false;
+      tile_s1(c);
+    }
+    Sweep A = make_sweep(c, s);
+    const SeqArgs Q0 = make_seq(c, s);
     hipLaunchKernelGGL(mvc_seq_init_kernel, dim3(1), dim3(64), 0, stream, Q0, lane_now ? 1 : 0);
     MVC_HIP(hipGetLastError());
     dbg("seq_init", c, s);
@@ -4102,6 +4143,13 @@ class ChainSet : public Sampler {
     stream = subs[0]->stream;
   }
   ~ChainSet() override {
+    if (set_cstream) hipStreamSynchronize(set_cstream);
+    for (auto &q : set_saves) {
+      if (q.snap) hipEventDestroy(q.snap);
+      if (q.done) hipEventDestroy(q.done);
+      set_slot_free(q);
+    }
+    if (set_cstream) hipStreamDestroy(set_cstream);
     batch_free();
     while (!subs.empty()) subs.pop_back();   // the data owner (chain 0) last
   }
@@ -4154,11 +4202,26 @@ class ChainSet : public Sampler {
   SeqArgs *bA_dev = nullptr, *bA_host = nullptr, *bE_dev = nullptr, *bE_host = nullptr;
   SeqLds *bL_dev = nullptr, *bL_host = nullptr;
   Repair *bR_dev = nullptr, *bR_host = nullptr;
+  // the lane sweeps' batched launches: init arguments, compaction, MH, status rows
+  SeqArgs *bI_dev = nullptr, *bI_host = nullptr;
+  CompactArgs *bC_dev = nullptr, *bC_host = nullptr;
+  MHArgs *bM_dev = nullptr, *bM_host = nullptr;
+  int32_t *bS_dev = nullptr, *bS_host = nullptr;
   std::vector<hipEvent_t> b_ev;
   hipEvent_t b_join = nullptr;
+  bool last_lane_batch = false;   // the last sweep ran every chain's work on the batch stream (lane_batch)
   void batch_alloc() {
     if (bA_dev) return;
     const size_t C = subs.size();
+    const size_t SL = 2 * (size_t)cfg.n_views + 4;
+    MVC_HIP(hipMalloc(&bI_dev, sizeof(SeqArgs) * C));
+    MVC_HIP(hipMalloc(&bC_dev, sizeof(CompactArgs) * C));
+    MVC_HIP(hipMalloc(&bM_dev, sizeof(MHArgs) * C));
+    MVC_HIP(hipMalloc(&bS_dev, sizeof(int32_t) * C * SL));
+    MVC_HIP(hipHostMalloc((void **)&bI_host, sizeof(SeqArgs) * C, hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&bC_host, sizeof(CompactArgs) * C, hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&bM_host, sizeof(MHArgs) * C, hipHostMallocDefault));
+    MVC_HIP(hipHostMalloc((void **)&bS_host, sizeof(int32_t) * C * SL, hipHostMallocDefault));
     MVC_HIP(hipMalloc(&bA_dev, sizeof(SeqArgs) * C));
     MVC_HIP(hipMalloc(&bE_dev, sizeof(SeqArgs) * C));
     MVC_HIP(hipMalloc(&bL_dev, sizeof(SeqLds) * C));
@@ -4173,8 +4236,12 @@ class ChainSet : public Sampler {
   }
   void batch_free() {
     if (!bA_dev) return;
-    for (void *p : {(void *)bA_dev, (void *)bE_dev, (void *)bL_dev, (void *)bR_dev}) hipFree(p);
-    for (void *p : {(void *)bA_host, (void *)bE_host, (void *)bL_host, (void *)bR_host}) hipHostFree(p);
+    for (void *p : {(void *)bA_dev, (void *)bE_dev, (void *)bL_dev, (void *)bR_dev, (void *)bI_dev, (void *)bC_dev,
+                    (void *)bM_dev, (void *)bS_dev})
+      hipFree(p);
+    for (void *p : {(void *)bA_host, (void *)bE_host, (void *)bL_host, (void *)bR_host, (void *)bI_host,
+                    (void *)bC_host, (void *)bM_host, (void *)bS_host})
+      hipHostFree(p);
     for (auto &e : b_ev) hipEventDestroy(e);
     hipEventDestroy(b_join);
     bA_dev = nullptr;
@@ -4189,6 +4256,43 @@ class ChainSet : public Sampler {
     tm.begin("sweep", &ev_sweep);
     std::vector<ParallelSampler::RepairRun> rr(C);
     std::vector<char> done(C, 0);
+    // Every chain in the small chains' lane loop (and no per-phase timers or
+    // debug synchronisation): the whole sweep of every chain on the batch
+    // stream, each per-chain launch (the repair's init, compaction, MH,
+    // status read-back) one batched launch for all chains -- the same kernels
+    // on the same arguments, so the same chains, with ~10 host calls per
+    // sweep instead of ~10 per chain.
+    bool lane_batch = (!tm.on || tm.coarse) && debug_sync_level() == 0;
+    for (int c = 0; c < C && lane_batch; ++c) {
+      ParallelSampler &S = *subs[c];
+      lane_batch = !S.repair_grid_only && S.lane_sweep(S.chains[0]);
+    }
+    if (!lane_batch && last_lane_batch) {   // the chains' streams after the batch stream's last sweep and saves
+      MVC_HIP(hipEventRecord(b_join, bs));
+      for (int c = 1; c < C; ++c) MVC_HIP(hipStreamWaitEvent(subs[c]->stream, b_join, 0));
+    }
+    if (lane_batch && !last_lane_batch) {   // the batch stream after each chain's last work on its own stream
+      for (int c = 1; c < C; ++c) {
+        MVC_HIP(hipEventRecord(b_ev[c], subs[c]->stream));
+        MVC_HIP(hipStreamWaitEvent(bs, b_ev[c], 0));
+      }
+    }
+    last_lane_batch = lane_batch;
+    if (lane_batch) {
+      // 1. the repair state of every chain (mvc_seq_init_kernel, run_start: the lane loop starts at customer 0)
+      for (int c = 0; c < C; ++c) {
+        ParallelSampler &S = *subs[c];
+        auto &ch = S.chains[0];
+        const uint32_t s = (uint32_t)S.sweeps_done;
+        S.lane_now = true;
+        S.zpath = 32 | 256;
+        S.repair_start(ch, s, false, rr[c], false);   // (host only for a lane sweep)
+        bI_host[c] = rr[c].Q;
+      }
+      MVC_HIP(hipMemcpyAsync(bI_dev, bI_host, sizeof(SeqArgs) * C, hipMemcpyHostToDevice, bs));
+      hipLaunchKernelGGL(mvc_seq_init_kernel_b, dim3(C), dim3(64), 0, bs, (const SeqArgs *)bI_dev, 1);
+      MVC_HIP(hipGetLastError());
+    } else {
     // 1. phase A and the first mover, every chain on its own stream
     for (int c = 0; c < C; ++c) {
       ParallelSampler &S = *subs[c];
@@ -4201,6 +4305,7 @@ class ChainSet : public Sampler {
         MVC_HIP(hipEventRecord(b_ev[c], S.stream));
         MVC_HIP(hipStreamWaitEvent(bs, b_ev[c], 0));
       }
+    }
     }
     // 2. rounds of every unfinished chain, batched by run-kernel instance
     for (;;) {
@@ -4326,6 +4431,43 @@ class ChainSet : public Sampler {
         }
       }
     }
+    if (lane_batch) {
+      // 3. compaction (a chain that did not move returns at once) and the MH
+      // of every chain, then every chain's status row in one read-back: the
+      // next sweep's shapes (S1t, only needed by a phase A, is re-tiled when
+      // a chain leaves the lane loop: Chain::s1t_stale)
+      const int SL = 2 * cfg.n_views + 4;
+      for (int c = 0; c < C; ++c) {
+        ParallelSampler &S = *subs[c];
+        auto &ch = S.chains[0];
+        const Repair &rs = S.last_rs;
+        ch.last[0] = rs.moves;
+        ch.last[1] = rs.births;
+        ch.last[2] = rs.rounds;
+        ch.last[3] = rs.newdish;
+        bC_host[c] = CompactArgs{rr[c].Q, ch.pos_new, ch.jmap, 1};   // (n <= 1,024: the block relabels z)
+        bM_host[c] = S.mh_args(ch, 1, (uint32_t)S.sweeps_done);
+      }
+      MVC_HIP(hipMemcpyAsync(bC_dev, bC_host, sizeof(CompactArgs) * C, hipMemcpyHostToDevice, bs));
+      MVC_HIP(hipMemcpyAsync(bM_dev, bM_host, sizeof(MHArgs) * C, hipMemcpyHostToDevice, bs));
+      hipLaunchKernelGGL(mvc_seq_compact_kernel_b, dim3(C), dim3(1024), 0, bs, (const CompactArgs *)bC_dev);
+      hipLaunchKernelGGL(mvc_par_hyper_kernel_b, dim3(C), dim3(kHypThreads), 0, bs, (const MHArgs *)bM_dev);
+      hipLaunchKernelGGL(mvc_seq_gather_status_kernel, dim3(C), dim3(64), 0, bs, (const CompactArgs *)bC_dev, SL, bS_dev);
+      MVC_HIP(hipGetLastError());
+      MVC_HIP(hipMemcpyAsync(bS_host, bS_dev, sizeof(int32_t) * C * SL, hipMemcpyDeviceToHost, bs));
+      MVC_HIP(hipStreamSynchronize(bs));
+      for (int c = 0; c < C; ++c) {
+        ParallelSampler &S = *subs[c];
+        auto &ch = S.chains[0];
+        if (S.last_rs.moves > 0) {
+          const int32_t *st = bS_host + (size_t)c * SL;
+          ch.T = st[0];
+          for (int v = 0; v < cfg.n_views; ++v) ch.K[v] = st[1 + v];
+          ch.s1t_stale = true;
+        }
+        S.sweeps_done += 1;
+      }
+    } else {
     // 3. compaction and the MH of every chain, on its stream after the batch
     MVC_HIP(hipEventRecord(b_join, bs));
     for (int c = 0; c < C; ++c) {
@@ -4337,6 +4479,7 @@ class ChainSet : public Sampler {
       ParallelSampler &S = *subs[c];
       if (S.status_pending) S.repair_status(S.chains[0]);
       S.sweeps_done += 1;
+    }
     }
     if (tm.on && ev_sweep) {
       for (int c = 1; c < C; ++c) {
@@ -4360,12 +4503,109 @@ class ChainSet : public Sampler {
     at(chain).set_state(0, t, T, d, h);
   }
   bool save_async(int chain, const SampleFn &fn) override {
+    flush_set_saves();   // (older samples of save_all_async first)
     return at(chain).save_async(0, [fn, chain](int, int T, const int32_t *t, const int32_t *d, const double *h) {
       fn(chain, T, t, d, h);
     });
   }
   void flush_saves() override {
+    flush_set_saves();
     for (auto &s : subs) s->flush_saves();
+  }
+
+  // ---- every chain's sample in one snapshot (after a lane_batch sweep) ----
+  // One snapshot kernel for all chains on the batch stream, one read-back on
+  // a copy stream; the samples reach fn chain by chain, in order, when the
+  // slot is reused or at flush_saves (as the exact schedule's save_all_async).
+  // After other sweeps the chains' own save_async runs (false here).
+  struct SetSlot {
+    SnapArgs *args_dev = nullptr, *args_host = nullptr;
+    int32_t *dz = nullptr, *ddish = nullptr, *dT = nullptr, *hz = nullptr, *hdish = nullptr, *hT = nullptr;
+    double *dhyp = nullptr, *hhyp = nullptr;
+    int dcap = 0;
+    hipEvent_t snap = nullptr, done = nullptr;
+    bool busy = false;
+    SampleFn fn;
+  };
+  static constexpr int kSetSlots = 4;
+  SetSlot set_saves[kSetSlots];
+  int set_next = 0;
+  hipStream_t set_cstream = nullptr;
+  void set_slot_free(SetSlot &q) {
+    for (void *p : {(void *)q.args_dev, (void *)q.dz, (void *)q.ddish, (void *)q.dT, (void *)q.dhyp}) hipFree(p);
+    for (void *p : {(void *)q.args_host, (void *)q.hz, (void *)q.hdish, (void *)q.hT, (void *)q.hhyp}) hipHostFree(p);
+    q = SetSlot();
+  }
+  void set_slot_finish(SetSlot &q) {
+    MVC_HIP(hipEventSynchronize(q.done));
+    const int C = (int)subs.size(), V = cfg.n_views, n = cfg.n, H = 3 * V + 2;
+    std::vector<int32_t> d;
+    for (int c = 0; c < C; ++c) {
+      const int T = q.hT[c];
+      d.assign((size_t)V * std::max(T, 1), 0);
+      for (int v = 0; v < V; ++v)
+        std::copy(q.hdish + ((size_t)c * V + v) * q.dcap, q.hdish + ((size_t)c * V + v) * q.dcap + T,
+                  d.begin() + (size_t)v * T);
+      q.fn(c, T, q.hz + (size_t)c * n, d.data(), q.hhyp + (size_t)c * H);
+    }
+    q.busy = false;
+  }
+  void flush_set_saves() {
+    for (int k = 0; k < kSetSlots; ++k) {
+      SetSlot &q = set_saves[(set_next + k) % kSetSlots];   // oldest first
+      if (q.busy) set_slot_finish(q);
+    }
+  }
+  bool save_all_async(const SampleFn &fn) override {
+    if (!last_lane_batch) return false;
+    for (auto &s : subs) s->flush_saves();   // (older samples of the chains' own save_async first)
+    MVC_HIP(hipSetDevice(cfg.device));
+    if (!set_cstream) MVC_HIP(hipStreamCreateWithFlags(&set_cstream, hipStreamNonBlocking));
+    SetSlot &q = set_saves[set_next];
+    if (q.busy) set_slot_finish(q);
+    const int C = (int)subs.size(), V = cfg.n_views, n = cfg.n, H = 3 * V + 2;
+    int dcap = 1;
+    for (auto &sp : subs) dcap = std::max(dcap, sp->chains[0].T);
+    if (q.dcap < dcap) {
+      if (q.dz) set_slot_free(q);
+      dcap = std::max(dcap, 2 * q.dcap);   // (room to grow)
+      MVC_HIP(hipMalloc(&q.args_dev, sizeof(SnapArgs) * C));
+      MVC_HIP(hipMalloc(&q.dz, sizeof(int32_t) * (size_t)C * std::max(n, 1)));
+      MVC_HIP(hipMalloc(&q.ddish, sizeof(int32_t) * (size_t)C * V * dcap));
+      MVC_HIP(hipMalloc(&q.dT, sizeof(int32_t) * C));
+      MVC_HIP(hipMalloc(&q.dhyp, sizeof(double) * (size_t)C * H));
+      MVC_HIP(hipHostMalloc((void **)&q.args_host, sizeof(SnapArgs) * C, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hz, sizeof(int32_t) * (size_t)C * std::max(n, 1), hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hdish, sizeof(int32_t) * (size_t)C * V * dcap, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hT, sizeof(int32_t) * C, hipHostMallocDefault));
+      MVC_HIP(hipHostMalloc((void **)&q.hhyp, sizeof(double) * (size_t)C * H, hipHostMallocDefault));
+      q.dcap = dcap;
+    }
+    if (!q.snap) {
+      MVC_HIP(hipEventCreateWithFlags(&q.snap, hipEventDisableTiming));
+      MVC_HIP(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+    }
+    for (int c = 0; c < C; ++c) {
+      const ParallelSampler &S = *subs[c];
+      const auto &ch = S.chains[0];
+      q.args_host[c] = SnapArgs{ch.P.z, ch.P.dish, ch.P.d_id, ch.status, ch.P.hyper, (int32_t)ch.P.TC, (int32_t)ch.P.KC};
+    }
+    // (the slot's pinned arguments are rewritten only after set_slot_finish: this copy has run)
+    MVC_HIP(hipMemcpyAsync(q.args_dev, q.args_host, sizeof(SnapArgs) * C, hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(mvc_par_snapshot_all_kernel, dim3(std::min(64, (n + 255) / 256 + 1), C), dim3(256), 0, stream,
+                       (const SnapArgs *)q.args_dev, n, V, q.dcap, q.dz, q.ddish, q.dT, q.dhyp);
+    MVC_HIP(hipGetLastError());
+    MVC_HIP(hipEventRecord(q.snap, stream));
+    MVC_HIP(hipStreamWaitEvent(set_cstream, q.snap, 0));
+    MVC_HIP(hipMemcpyAsync(q.hz, q.dz, sizeof(int32_t) * (size_t)C * n, hipMemcpyDeviceToHost, set_cstream));
+    MVC_HIP(hipMemcpyAsync(q.hdish, q.ddish, sizeof(int32_t) * (size_t)C * V * q.dcap, hipMemcpyDeviceToHost, set_cstream));
+    MVC_HIP(hipMemcpyAsync(q.hT, q.dT, sizeof(int32_t) * C, hipMemcpyDeviceToHost, set_cstream));
+    MVC_HIP(hipMemcpyAsync(q.hhyp, q.dhyp, sizeof(double) * (size_t)C * H, hipMemcpyDeviceToHost, set_cstream));
+    MVC_HIP(hipEventRecord(q.done, set_cstream));
+    q.busy = true;
+    q.fn = fn;
+    set_next = (set_next + 1) % kSetSlots;
+    return true;
   }
   const int32_t *device_labels(int chain) override { return at(chain).device_labels(0); }
   void copy_rows(int view, const int32_t *idx, int64_t m, double *out) override { subs[0]->copy_rows(view, idx, m, out); }

@@ -1746,7 +1746,7 @@ __device__ int seq_dish_draw_leaves(const SeqArgs &A, const SView &W, int i, int
 // run_start: the sweep starts in the run kernel at customer 0 (the small
 // chains' lane-per-customer loop, whose first step is phase A) instead of a
 // window over the whole sweep.
-extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A, int run_start) {
+__device__ __forceinline__ void seq_init_body(const SeqArgs &A, int run_start) {
   if (threadIdx.x != 0) return;
   Repair *R = A.R;
   const int V = A.P.V, n = A.P.n;
@@ -1773,6 +1773,11 @@ extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A, int run_start) {
   for (int k = 0; k < 22; ++k) R->prof[k] = 0;
   for (int k = 0; k < 8; ++k) R->dbg[k] = 0;
   for (int v = 0; v < V; ++v) R->Klist[v] = A.P.Kact[v];
+}
+extern "C" __global__ void mvc_seq_init_kernel(SeqArgs A, int run_start) { seq_init_body(A, run_start); }
+// The same for several chains (one block per chain): the chain-batched sweep
+extern "C" __global__ void mvc_seq_init_kernel_b(const SeqArgs *As, int run_start) {
+  seq_init_body(As[blockIdx.x], run_start);
 }
 
 // After phase A: the first customer whose choice is not its own table.
@@ -4518,8 +4523,7 @@ extern "C" __global__ __launch_bounds__(256) void mvc_seq_eval_kernel_b(const Se
 // SeqSampler::compact).  pos_new [TC], jmap [V*KC].
 // relabel != 0 (small n): the block also relabels z (mvc_seq_relabel_kernel's
 // work, without its launch).
-extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArgs A, int32_t *pos_new, int32_t *jmap,
-                                                                          int relabel) {
+__device__ __forceinline__ void seq_compact_body(SeqArgs &A, int32_t *pos_new, int32_t *jmap, int relabel) {
   Repair *R = A.R;
   ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
@@ -4616,6 +4620,26 @@ extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArg
       A.Koff[v + 1] = acc;
     }
   }
+}
+extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel(SeqArgs A, int32_t *pos_new, int32_t *jmap,
+                                                                          int relabel) {
+  seq_compact_body(A, pos_new, jmap, relabel);
+}
+// The same for several chains (one block per chain; a chain that did not
+// move returns at once): the chain-batched sweep
+struct CompactArgs {
+  SeqArgs Q;
+  int32_t *pos_new, *jmap;
+  int32_t relabel;
+};
+extern "C" __global__ __launch_bounds__(1024) void mvc_seq_compact_kernel_b(const CompactArgs *As) {
+  SeqArgs A = As[blockIdx.x].Q;
+  seq_compact_body(A, As[blockIdx.x].pos_new, As[blockIdx.x].jmap, As[blockIdx.x].relabel);
+}
+// Every chain's status row [2V + 4] into out[chain][2V + 4] (one read-back)
+extern "C" __global__ void mvc_seq_gather_status_kernel(const CompactArgs *As, int len, int32_t *out) {
+  const int32_t *src = As[blockIdx.x].Q.status;
+  for (int k = threadIdx.x; k < len; k += blockDim.x) out[(size_t)blockIdx.x * len + k] = src[k];
 }
 
 extern "C" __global__ void mvc_seq_relabel_kernel(int n, int32_t *z, const int32_t *pos_new, const Repair *R) {

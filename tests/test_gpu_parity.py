@@ -742,7 +742,7 @@ def test_chains_concurrent_equal_serial():
 @pytest.mark.parametrize("env", [
     {"lc": "0"},                                      # batched kind 0: one wave per customer, LDS cache
     {"lc": "col"},                                    # batched kind 3: lane columns (no lane loop)
-    {},                                               # batched kind 5: the small chains' lane loop
+    {},                                               # batched kind 6: the small chains' lane loop (lane_batch)
     {"run_lds": "0", "wide": "0"},                    # kind 0 on the global layout
     {"run_lds": "0", "wide": "block"},                # kind 2: the block-wide evaluation
     {"run_lds": "0"},                                 # grid-wide evaluation: every chain on its own stream
@@ -772,6 +772,42 @@ def test_chains_batched_kinds_equal_alone(env, monkeypatch):
     ref = O.run(y, M, 0, 1, seed=31, chain=1, mode=O.PARALLEL)
     assert np.array_equal(conc.state(chain=1)[0], ref["table_of"][-1])
     conc.close()
+
+
+def test_lane_batch_transitions_equal_alone():
+    """ChainSet's lane_batch sweeps (every chain in the lane loop: the repair's
+    init, compaction, MH and status read-back batched over the chains on one
+    stream) and its other sweeps alternate through the reference call's cold
+    start (the tables outgrow the lane loop, then shrink back into it); every
+    chain stays bit for bit the chain swept alone, sweep by sweep, and
+    mvc_run's samples (save_all_async after lane_batch sweeps, the chains' own
+    saves after the others) equal the one-chain calls'."""
+    m = _mvc()
+    from mvc_amd import data
+    y, _ = data.new_simulation(7)
+    C, M = 4, 24
+    conc = m.Sampler(y, seed=13, mode="parallel", n_chains=C)
+    alone = [m.Sampler(y, seed=13, mode="parallel", first_chain=c) for c in range(C)]
+    lane, other = 0, 0
+    for it in range(M):
+        conc.sweep(1)
+        if conc.zpath() & 256:
+            lane += 1
+        else:
+            other += 1
+        for c in range(C):
+            alone[c].sweep(1)
+            t1, d1, h1 = alone[c].state()
+            t, d, h = conc.state(chain=c)
+            assert np.array_equal(t, t1) and np.array_equal(d, d1), (it, c)
+            assert np.array_equal(h["tau_v"], h1["tau_v"]) and h["alpha_global"] == h1["alpha_global"], (it, c)
+    assert lane > 0 and other > 0, (lane, other)
+    conc.close()
+    for a in alone:
+        a.close()
+    multi = m.run_gibbs_cpp(y, M, M // 3, 1, seed=13, mode="parallel", n_chains=C, quiet=True)
+    for c, res in enumerate(multi):
+        _compare(res, m.run_gibbs_cpp(y, M, M // 3, 1, seed=13, mode="parallel", first_chain=c, quiet=True))
 
 
 _LAST_BIRTH_CHILD = r"""
