@@ -2738,6 +2738,7 @@ class ParallelSampler : public Sampler {
   }
 
   bool owns_y = true;
+  bool owns_stream = true;
   std::vector<double> tau0;        // device data: initial tau_v per view (host data: from the views)
   void init(const mvc_config &cf, const double *yh_in, const ParallelSampler *share, bool dev_data = false) {
     cfg = cf;
@@ -2756,7 +2757,16 @@ class ParallelSampler : public Sampler {
       (void)hipSetDeviceFlags(hipDeviceScheduleSpin);
       (void)hipGetLastError();
     }
-    MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    if (share && n <= kLaneMaxN) {
+      // a chain of a set of small chains (ChainSet) works on the set's first
+      // chain's stream: their sweeps are one batched stream of launches
+      // (ChainSet::sweep_batched, lane_batch) and a stream costs ~20 ms to
+      // create, which a short call of many small chains would pay per chain
+      stream = share->stream;
+      owns_stream = false;
+    } else {
+      MVC_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    }
     timers.stream = stream;
     timers.on = (cf.flags & MVC_FLAG_TIMING) != 0;
     timers.coarse = (cf.flags & MVC_FLAG_TIMING_COARSE) != 0;
@@ -2990,7 +3000,7 @@ class ParallelSampler : public Sampler {
     if (st_host) hipHostFree(st_host);
     if (rs_host) hipHostFree(rs_host);
     if (rs_ev) hipEventDestroy(rs_ev);
-    if (stream) hipStreamDestroy(stream);
+    if (stream && owns_stream) hipStreamDestroy(stream);
   }
 
   // capacity-sized arrays of a chain (TC tables, KC dishes per view)
