@@ -2012,6 +2012,7 @@ struct MHArgs {
   uint32_t chain, sweep;
   int do_mh;
   const Repair *gate;     // non-null: run only if the sweep's repair is done with no move
+  int gate_mode;          // 1: with gate, run iff the repair is done (moves or not; its compaction ran before)
 };
 
 }  // namespace
@@ -2035,7 +2036,9 @@ __device__ __forceinline__ void hyper_body(MHArgs &A) {
   // gated launch (enqueued before the host has read the repair's outcome):
   // runs only for a finished repair with no move, where nothing (compaction,
   // relabel, capacity growth) has to come between the repair and the MH
-  if (A.gate && !(A.gate->done && A.gate->moves == 0 && A.gate->overflow == 0 && A.gate->restride == 0)) return;
+  if (A.gate && !(A.gate->done && (A.gate_mode == 1 || A.gate->moves == 0) && A.gate->overflow == 0 &&
+                  A.gate->restride == 0))
+    return;
   const int T = A.status[0];
   __shared__ int s_koff[MVC_MAXV + 1];
   __shared__ int s_kact[MVC_MAXV];
@@ -3157,7 +3160,7 @@ class ParallelSampler : public Sampler {
     timers.end("stats", ev);
   }
 
-  MHArgs mh_args(const Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr) const {
+  MHArgs mh_args(const Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr, int gate_mode = 0) const {
     MHArgs A;
     A.P = c.P;
     A.status = c.status;
@@ -3169,10 +3172,11 @@ class ParallelSampler : public Sampler {
     A.sweep = sweep_ix;
     A.do_mh = do_mh;
     A.gate = gate;
+    A.gate_mode = gate_mode;
     return A;
   }
-  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr) {
-    const MHArgs A = mh_args(c, do_mh, sweep_ix, gate);
+  void launch_hyper(Chain &c, int do_mh, uint32_t sweep_ix, const Repair *gate = nullptr, int gate_mode = 0) {
+    const MHArgs A = mh_args(c, do_mh, sweep_ix, gate, gate_mode);
     hipEvent_t ev = nullptr;
     timers.begin("hyper", &ev);
     hipLaunchKernelGGL(mvc_par_hyper_kernel, dim3(1), dim3(kHypThreads), 0, stream, A);
@@ -3883,6 +3887,12 @@ class ParallelSampler : public Sampler {
   void repair(Chain &c, uint32_t s, bool phaseA) {
     RepairRun rr;
     repair_start(c, s, phaseA, rr);
+#ifndef MVC_RUN_PROF
+    if (lane_now && (!timers.on || timers.coarse)) {
+      repair_lane_tail(c, s, rr);
+      return;
+    }
+#endif
     for (;;) {
       repair_rounds(c, s, rr);
       MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
@@ -3901,6 +3911,39 @@ class ParallelSampler : public Sampler {
       if (repair_outcome(c, s, rr, *rs_host) == 1) break;
     }
     repair_finish(c, s, rr, *rs_host);
+  }
+  // A small chain's lane sweep (one chain swept alone): the sweep's tail --
+  // compaction (a no-op on the device unless the repair is done with moves),
+  // the status and outcome read-backs, then the MH (gated on the device: it
+  // runs iff the repair is done) -- enqueued behind every batch of rounds, so
+  // a sweep is one host synchronisation, and the MH runs while the host reads
+  // the outcome and prepares the next sweep's launches.  The same kernels on
+  // the same state in the same order as repair_finish's.
+  void repair_lane_tail(Chain &c, uint32_t s, RepairRun &rr) {
+    if (!rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
+    for (;;) {
+      repair_rounds(c, s, rr);
+      hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, rr.Q, c.pos_new, c.jmap, 1);
+      MVC_HIP(hipMemcpyAsync(st_host, c.status, sizeof(int32_t) * (2 * V + 4), hipMemcpyDeviceToHost, stream));
+      MVC_HIP(hipMemcpyAsync(rs_host, c.R, sizeof(Repair), hipMemcpyDeviceToHost, stream));
+      MVC_HIP(hipEventRecord(rs_ev, stream));
+      launch_hyper(c, 1, s, c.R, 1);
+      MVC_HIP(hipEventSynchronize(rs_ev));
+      dbg("lane tail (compaction, gated hyper)", c, s);
+      if (repair_outcome(c, s, rr, *rs_host) == 1) break;
+    }
+    const Repair &rs = *rs_host;
+    timers.end("repair", rr.e1);
+    if (vp_stats) fprintf(stderr, "mvc vp steps %d hits %d off %d\n", rs.vpsteps, rs.vphits, rs.vpoff);
+    c.last[0] = rs.moves;
+    c.last[1] = rs.births;
+    c.last[2] = rs.rounds;
+    c.last[3] = rs.newdish;
+    if (rs.moves > 0) {   // new T and dish counts for the next sweep's launch shapes (S1t: s1t_stale)
+      c.T = st_host[0];
+      for (int v = 0; v < V; ++v) c.K[v] = st_host[1 + v];
+      c.s1t_stale = true;
+    }
   }
 
   // Double the table (flags & 1) and/or dish (flags & 2) capacity of every
