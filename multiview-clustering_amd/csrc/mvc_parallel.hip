@@ -4465,12 +4465,38 @@ class ChainSet : public Sampler {
         MVC_HIP(hipEventRecord(b_ev[c], S.stream));
         MVC_HIP(hipStreamWaitEvent(bs, b_ev[c], 0));
       }
+      const int SL = 2 * cfg.n_views + 4;
+      const unsigned na = (unsigned)act.size();
+      if (lane_batch) {
+        // the sweep's tail of the chains still active, gated on the device per
+        // chain: compaction (a no-op unless its repair is done with moves),
+        // the status rows, and behind the read-back's event the MH, which runs
+        // iff the repair is done -- one host synchronisation per batch of rounds
+        for (unsigned j = 0; j < na; ++j) {
+          ParallelSampler &S = *subs[ord[j]];
+          auto &ch = S.chains[0];
+          bC_host[j] = CompactArgs{rr[ord[j]].Q, ch.pos_new, ch.jmap, 1};   // (n <= 1,024: the block relabels z)
+          bM_host[j] = S.mh_args(ch, 1, (uint32_t)S.sweeps_done, ch.R, 1);
+        }
+        MVC_HIP(hipMemcpyAsync(bC_dev, bC_host, sizeof(CompactArgs) * na, hipMemcpyHostToDevice, bs));
+        hipLaunchKernelGGL(mvc_seq_compact_kernel_b, dim3(na), dim3(1024), 0, bs, (const CompactArgs *)bC_dev);
+        hipLaunchKernelGGL(mvc_seq_gather_status_kernel, dim3(na), dim3(64), 0, bs, (const CompactArgs *)bC_dev, SL,
+                           bS_dev);
+      }
       // every chain's outcome in one copy
-      hipLaunchKernelGGL(mvc_seq_gather_repair_kernel, dim3((unsigned)act.size()), dim3(64), 0, bs,
-                         (const SeqArgs *)bE_dev, bR_dev);
+      hipLaunchKernelGGL(mvc_seq_gather_repair_kernel, dim3(na), dim3(64), 0, bs, (const SeqArgs *)bE_dev, bR_dev);
       MVC_HIP(hipGetLastError());
-      MVC_HIP(hipMemcpyAsync(bR_host, bR_dev, sizeof(Repair) * act.size(), hipMemcpyDeviceToHost, bs));
-      MVC_HIP(hipStreamSynchronize(bs));
+      MVC_HIP(hipMemcpyAsync(bR_host, bR_dev, sizeof(Repair) * na, hipMemcpyDeviceToHost, bs));
+      if (lane_batch) {
+        MVC_HIP(hipMemcpyAsync(bS_host, bS_dev, sizeof(int32_t) * na * SL, hipMemcpyDeviceToHost, bs));
+        MVC_HIP(hipMemcpyAsync(bM_dev, bM_host, sizeof(MHArgs) * na, hipMemcpyHostToDevice, bs));
+        MVC_HIP(hipEventRecord(b_join, bs));
+        hipLaunchKernelGGL(mvc_par_hyper_kernel_b, dim3(na), dim3(kHypThreads), 0, bs, (const MHArgs *)bM_dev);
+        MVC_HIP(hipGetLastError());
+        MVC_HIP(hipEventSynchronize(b_join));
+      } else {
+        MVC_HIP(hipStreamSynchronize(bs));
+      }
       for (size_t j = 0; j < ord.size(); ++j) {
         const int c = ord[j];
         ParallelSampler &S = *subs[c];
@@ -4479,47 +4505,28 @@ class ChainSet : public Sampler {
         if (res == 1) {
           done[c] = 1;
           S.last_rs = bR_host[j];
+          if (lane_batch) {   // the outcome, and the next sweep's shapes from the status row
+            auto &ch = S.chains[0];
+            const Repair &rs = bR_host[j];
+            ch.last[0] = rs.moves;
+            ch.last[1] = rs.births;
+            ch.last[2] = rs.rounds;
+            ch.last[3] = rs.newdish;
+            if (rs.moves > 0) {
+              const int32_t *st = bS_host + j * SL;
+              ch.T = st[0];
+              for (int v = 0; v < cfg.n_views; ++v) ch.K[v] = st[1 + v];
+              ch.s1t_stale = true;   // (S1t, only read by a phase A, is re-tiled when the chain leaves the lane loop)
+            }
+          }
         } else if (res == 0) {
           MVC_HIP(hipStreamSynchronize(S.stream));   // (a relayout's reset on the chain's stream)
         }
       }
     }
     if (lane_batch) {
-      // 3. compaction (a chain that did not move returns at once) and the MH
-      // of every chain, then every chain's status row in one read-back: the
-      // next sweep's shapes (S1t, only needed by a phase A, is re-tiled when
-      // a chain leaves the lane loop: Chain::s1t_stale)
-      const int SL = 2 * cfg.n_views + 4;
-      for (int c = 0; c < C; ++c) {
-        ParallelSampler &S = *subs[c];
-        auto &ch = S.chains[0];
-        const Repair &rs = S.last_rs;
-        ch.last[0] = rs.moves;
-        ch.last[1] = rs.births;
-        ch.last[2] = rs.rounds;
-        ch.last[3] = rs.newdish;
-        bC_host[c] = CompactArgs{rr[c].Q, ch.pos_new, ch.jmap, 1};   // (n <= 1,024: the block relabels z)
-        bM_host[c] = S.mh_args(ch, 1, (uint32_t)S.sweeps_done);
-      }
-      MVC_HIP(hipMemcpyAsync(bC_dev, bC_host, sizeof(CompactArgs) * C, hipMemcpyHostToDevice, bs));
-      MVC_HIP(hipMemcpyAsync(bM_dev, bM_host, sizeof(MHArgs) * C, hipMemcpyHostToDevice, bs));
-      hipLaunchKernelGGL(mvc_seq_compact_kernel_b, dim3(C), dim3(1024), 0, bs, (const CompactArgs *)bC_dev);
-      hipLaunchKernelGGL(mvc_par_hyper_kernel_b, dim3(C), dim3(kHypThreads), 0, bs, (const MHArgs *)bM_dev);
-      hipLaunchKernelGGL(mvc_seq_gather_status_kernel, dim3(C), dim3(64), 0, bs, (const CompactArgs *)bC_dev, SL, bS_dev);
-      MVC_HIP(hipGetLastError());
-      MVC_HIP(hipMemcpyAsync(bS_host, bS_dev, sizeof(int32_t) * C * SL, hipMemcpyDeviceToHost, bs));
-      MVC_HIP(hipStreamSynchronize(bs));
-      for (int c = 0; c < C; ++c) {
-        ParallelSampler &S = *subs[c];
-        auto &ch = S.chains[0];
-        if (S.last_rs.moves > 0) {
-          const int32_t *st = bS_host + (size_t)c * SL;
-          ch.T = st[0];
-          for (int v = 0; v < cfg.n_views; ++v) ch.K[v] = st[1 + v];
-          ch.s1t_stale = true;
-        }
-        S.sweeps_done += 1;
-      }
+      // 3. (the compaction and the MH ran behind each chain's last batch of rounds)
+      for (int c = 0; c < C; ++c) subs[c]->sweeps_done += 1;
     } else {
     // 3. compaction and the MH of every chain, on its stream after the batch
     MVC_HIP(hipEventRecord(b_join, bs));
