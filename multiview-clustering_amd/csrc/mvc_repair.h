@@ -4037,6 +4037,83 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
   }
   const double logS = mvc_log(Sv);
   RUN_MARK(2);
+  if constexpr (TR <= 8) {
+    // ---- every table in its own lane (T <= 8): lane q of the group forms
+    // table q's score from the views' lp of its dish, in view order, with
+    // view u's per-customer values (the self-removed value of the own dish,
+    // hy, h, the own dish) broadcast from lane u -- the same lpj expression on
+    // the same inputs as lane u's, so the same values; then one exp per lane,
+    // and the block's 16 leaves (tables 8..15 the padding's +0) broadcast for
+    // the spec's pw16 sum and descent
+    const int q = v;
+    const LanePre LP = lane_pre_publish(PV);
+    double lm;
+    {
+      const double denom = alpha + (double)(W.Ltot[vv] - (alive ? 0 : 1));
+      const double logden = LP.at(alive ? vv : V + vv);
+      lm = (denom <= 0.0) ? lfn : (m + logS) - logden;
+    }
+    double s_new = LP.at(alive ? 2 * V : 2 * V + 1);   // log(ag + sg T_ne')
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (u < V) s_new = s_new + group8_bcast(lm, u);
+    const double lmass0 = LP.at(2 * V + 2 + p0);   // log((n_p0 - 1) - sg)
+    const int qc = min(q, T - 1);
+    double sc = -MVC_PM_INF;
+    bool incq = false;   // table q included in the draw (n_q' >= 1, n_q' - sigma_g > 0)
+    if (q < T) {
+      const int np = W.n_t[q] - (q == p0 ? 1 : 0);
+      const double mass = (double)np - sg;
+      if (np >= 1 && mass > 0.0) {
+        sc = (q == p0) ? lmass0 : W.lmass[q];
+        incq = true;
+      }
+    }
+    const double j0d = (double)j0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (u < V) {
+        const double self_u = group8_bcast(self, u), hy_u = group8_bcast(hy, u), h_u = group8_bcast(h, u);
+        const int j0_u = (int)group8_bcast(j0d, u);
+        const int j = W.dish[u * ts + qc];
+        double x;
+        if (j == j0_u) {
+          x = self_u;
+        } else {
+          const double *yu = C.y + u * (int)C.ystride;
+          const double *S1u = W.S1T + (size_t)u * D * s1s;
+          double G;
+          if (D == 1) {
+            G = __builtin_fma(yu[0], S1u[j], 0.0);
+          } else {
+            G = 0.0;
+            for (int d = 0; d < D; ++d) G = __builtin_fma(yu[d], S1u[d * s1s + j], G);
+          }
+          x = __builtin_fma(G + hy_u, W.cb[u * ks + j], W.c0[u * ks + j]) + h_u;
+        }
+        if (incq) sc = sc + x;
+      }
+    }
+    RUN_MARK(4);
+    double M = row8_max_all(q < T ? sc : -MVC_PM_INF);
+    if (s_new > M) M = s_new;
+    const double eq = q < T ? mvc_exp_le0(sc - M) : 0.0;   // excluded: exp(-inf) = +0
+    double x16[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x16[k] = group8_bcast(eq, k);
+#pragma unroll
+    for (int k = 8; k < 16; ++k) x16[k] = 0.0;
+    const double tot = 0.0 + pw16_seq(x16);
+    const double Wt = mvc_exp_le0(s_new - M) + tot;
+    const double r = u_i * Wt;
+    if (!(r < tot)) {
+      RUN_MARK(5);
+      return -1;   // the new table
+    }
+    const int pick = pw16_select_seq(x16, r);
+    RUN_MARK(5);
+    return pick;
+  }
   double lt[TR];   // lp of table p's dish in this lane's view
 #pragma unroll
   for (int p = 0; p < TR; ++p) lt[p] = lpj(W.dish[vv * ts + min(p, T - 1)]);
