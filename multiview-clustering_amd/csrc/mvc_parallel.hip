@@ -3779,7 +3779,8 @@ class ParallelSampler : public Sampler {
         hipLaunchKernelGGL(L.lc ? (L.lc == 3 ? (L.small ? mvc_seq_run_kernel<5> : mvc_seq_run_kernel<6>)
                                              : L.lc == 2 ? mvc_seq_run_kernel<4> : mvc_seq_run_kernel<3>)
                                 : L.tw == 1 ? mvc_seq_run_kernel<0> : mvc_seq_run_kernel<2>,
-                           dim3(1), dim3(L.lc ? kSeqLcThreads : kSeqRunThreads), (size_t)L.dyn, stream, rr.Q, L);
+                           dim3(1), dim3(L.lc == 3 && L.small ? kLaneSmallThreads : L.lc ? kSeqLcThreads : kSeqRunThreads),
+                           (size_t)L.dyn, stream, rr.Q, L);
       }
       MVC_HIP(hipGetLastError());
       dbg(repair_grid_only ? "seq_apply" : L.lc == 3 ? (L.small ? "seq_run<5>" : "seq_run<6>") : L.lc == 2 ? "seq_run<4>" : L.lc ? "seq_run<3>" : L.tw == 1 ? "seq_run<0>" : "seq_run<2>", c, s);

@@ -70,6 +70,10 @@ constexpr int kSeqRunThreads = 512, kSeqRunWaves = kSeqRunThreads / 64;
 // the lane-column run kernel: 4 waves, one per SIMD (its evaluation is issue-
 // bound; a second wave per SIMD would halve the first customer's rate)
 constexpr int kSeqLcThreads = 256;
+// the small chains' lane loop (mvc_seq_run_kernel<5>): 8 waves, two per SIMD,
+// 64 customers per step (its registers allow it; the general lane kernel <6>
+// and the lane-column kernels keep 4 waves)
+constexpr int kLaneSmallThreads = 512;
 
 // LDS layout of the run kernel's per-wave scratch (host-chosen at launch):
 // lp [V][ks] | e [ts + 16] | B, C [ts/16 + 2]; nws waves speculate.
@@ -2170,7 +2174,7 @@ __device__ __forceinline__ void seq_commit_move_split(SeqArgs &A, const SCache &
         gst(&P.S2[v * KC + j1], a1);
       }
     }
-  } else {
+  } else if (w < 4) {   // (waves past 3, in the 8-wave lane kernel, take no part)
     // wave 2: the dish the customer leaves (j0), wave 3: the one it joins (j1),
     // in every view where they differ: S1 (lanes over d), then Q and the
     // coefficients (lanes < V: coef; V <= lane < 2V: the self-removed parts),
@@ -3842,9 +3846,9 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
 // expressions, so the same values): k = v < V log(alpha_v + L_v), k = V + v
 // log(alpha_v + L_v - 1) (the own table dies), k = 2V / 2V + 1 log(ag + sg
 // T_ne) / log(ag + sg (T_ne - 1)), k = 2V + 2 + p log((n_p - 1) - sg) (the
-// own table without the customer).  Needs 2V + 2 + T <= 128.
-constexpr int kLanePre = 128;
-__shared__ double mvc_lane_pre[kSeqLcThreads / 64][kLanePre];
+// own table without the customer).  Needs 2V + 2 + T <= 64 (V <= 8, T < 32).
+constexpr int kLanePre = 64;   // 2V + 2 + T <= 64 (V <= 8, T < 32)
+__shared__ double mvc_lane_pre[kLaneSmallThreads / 64][kLanePre];
 struct LanePre {
   const double *pre;   // this wave's row
   __device__ __forceinline__ double at(int k) const { return pre[k]; }
@@ -3853,34 +3857,30 @@ struct LanePre {
 // evaluation itself (interleaved with its own work), then published into the
 // wave's row (lane_pre_publish) before the first read.
 struct LanePreVals {
-  double x[2];
+  double x;
 };
 __device__ __forceinline__ LanePreVals lane_pre_vals(const SView &W, int V, const double *hyp) {
   const int lane = threadIdx.x & 63;
   const double ag = hyp[3 * V], sg = hyp[3 * V + 1];
   const int T = *W.T, T_ne = *W.T_ne;
   LanePreVals P;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int k = 64 * h + lane;
-    double arg = 1.0;
-    if (k < 2 * V) {
-      const int v = k < V ? k : k - V;
-      arg = hyp[V + v] + (double)(W.Ltot[v] - (k < V ? 0 : 1));
-    } else if (k < 2 * V + 2) {
-      arg = ag + sg * (double)(T_ne - (k == 2 * V ? 0 : 1));
-    } else if (k < 2 * V + 2 + T) {
-      arg = (double)(W.n_t[k - 2 * V - 2] - 1) - sg;
-    }
-    P.x[h] = mvc_log(arg);
+  const int k = lane;
+  double arg = 1.0;
+  if (k < 2 * V) {
+    const int v = k < V ? k : k - V;
+    arg = hyp[V + v] + (double)(W.Ltot[v] - (k < V ? 0 : 1));
+  } else if (k < 2 * V + 2) {
+    arg = ag + sg * (double)(T_ne - (k == 2 * V ? 0 : 1));
+  } else if (k < 2 * V + 2 + T) {
+    arg = (double)(W.n_t[k - 2 * V - 2] - 1) - sg;
   }
+  P.x = mvc_log(arg);
   return P;
 }
 __device__ __forceinline__ LanePre lane_pre_publish(const LanePreVals &P) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   double *row = mvc_lane_pre[w];
-  row[lane] = P.x[0];
-  row[64 + lane] = P.x[1];
+  row[lane] = P.x;
   wave_lds_sync();
   return LanePre{row};
 }
@@ -4215,7 +4215,9 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
 // values), the per-wave candidates double-buffered by step parity.  Moves are
 // committed by the four waves (seq_commit_move_split); a birth ends the loop
 // and seq_run_body commits it on the global state, then resumes here.
-constexpr int kLaneCust = kSeqLcThreads / 8;   // customers per step
+// customers per step: 8 lanes each, every lane of the block
+template <bool kSmall>
+constexpr int lane_cust() { return (kSmall ? kLaneSmallThreads : kSeqLcThreads) / 8; }
 // kSmall (mvc_seq_run_kernel<5>, L.small): every dish list and the tables <= 8,
 // one straight-line evaluation instance and no birth commit in the kernel
 // (a birth ends the launch; mvc_seq_birth_kernel commits it), so the loop's
@@ -4223,7 +4225,8 @@ constexpr int kLaneCust = kSeqLcThreads / 8;   // customers per step
 constexpr int kLaneSmall = 8;
 template <bool kSmall>
 __device__ __forceinline__ int seq_run_loop_lane(SeqArgs &A, const SeqLds &L, const Ring &G, RunCursor &U) {
-  constexpr int kW = kSeqLcThreads / 64;
+  constexpr int kW = (kSmall ? kLaneSmallThreads : kSeqLcThreads) / 64;
+  constexpr int kLaneCust = lane_cust<kSmall>();
   int flags = 0;
   const ParState &P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -4545,7 +4548,8 @@ __device__ __forceinline__ void seq_run_body(SeqArgs &A, const SeqLds &L) {
 }
 
 template <int kMode>
-__global__ __launch_bounds__(kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(SeqArgs A, SeqLds L) {
+__global__ __launch_bounds__(kMode == 5 ? kLaneSmallThreads : kMode >= 3 ? kSeqLcThreads : kSeqRunThreads) void mvc_seq_run_kernel(
+    SeqArgs A, SeqLds L) {
   seq_run_body<kMode>(A, L);
 }
 // The same for several chains at once (one block per chain, its arguments
