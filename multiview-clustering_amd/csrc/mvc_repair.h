@@ -3518,10 +3518,27 @@ __device__ __forceinline__ void vp_build(const SeqArgs &A, const SCache &cc, con
 }
 
 // Commit the predicted moves of customers i0 .. i0 + nc - 1 (they held): the
-// overlay's values after the last of them into the LDS state and HBM, S1 and
-// S2 updated in move order (one thread per element).  Block-wide.
+// overlay's values after the last of them into the LDS state and HBM (S1 from
+// the overlay's columns: each column the overlay built for a dish with the
+// moves before and at its entry applied in move order, the values the moves'
+// sequential updates give), S2 updated in move order (one thread per view).
+// Block-wide: S1 on every wave, S2 on wave 1, the dish entries on wave 2, the
+// tables on wave 3.
+__device__ __forceinline__ bool vp_entry_final(int e, int nc, int V, int j) {
+  const int mvv = e >> 1, m = mvv / kVpV, v = mvv - m * kVpV;
+  if (!(m < nc && v < V && j >= 0)) return false;
+  bool fin = !((e & 1) == 0 && mvc_vp_ov.j[e + 1] == j);   // j0 == j1: the joined entry writes
+#pragma unroll
+  for (int m2 = 0; m2 < kVpMoves; ++m2)
+    if (m2 > m && m2 < nc) {
+      const int e2 = (m2 * kVpV + v) * 2;
+      if (mvc_vp_ov.j[e2] == j || mvc_vp_ov.j[e2 + 1] == j) fin = false;
+    }
+  return fin;
+}
 __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const VpMoves &M, int i0, int nc,
-                                          const double *const (&yr)[kVpMoves], int32_t *cnt, bool chk) {
+                                          const double *const (&yr)[kVpMoves], const double *ovs1, int32_t *cnt,
+                                          bool chk) {
   ParState &P = A.P;
   Repair *R = A.R;
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -3534,27 +3551,17 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
       ++nmv;
     }
   if (last < 0) return;
-  // S1 (threads over (v, d)) and S2 (threads over v), in move order
-  for (int e = tid; e < V * D; e += nt) {
-    const int v = e / D, d = e - v * D;
-    double *cl = cc.S1T + ((size_t)v * D + d) * ks;
-    double *col = P.S1T + ((size_t)v * D + d) * KC;
-#pragma unroll
-    for (int m = 0; m < kVpMoves; ++m)
-      if (m < nc && M.mv[m]) {
-        const int j0 = cc.dish[v * ts + M.p0[m]], j1 = cc.dish[v * ts + M.c[m]];
-        if (chk && !run_chk(j0 >= 0 && j0 < cc.Klist[v] && j1 >= 0 && j1 < cc.Klist[v], 1, i0, m, v, j0, j1,
-                            cc.Klist[v]))
-          continue;
-        if (j0 != j1) {
-          const double yd = yr[m][v * D + d];
-          const double a0 = cl[j0] - yd, a1 = cl[j1] + yd;
-          cl[j0] = a0;
-          cl[j1] = a1;
-          gst(&col[j0], a0);
-          gst(&col[j1], a1);
-        }
-      }
+  // S1: the final column of every dish a committed move changed, from the
+  // overlay entry of the last committed move touching it (threads over (entry, d))
+  for (int k = tid; k < kVpE * D; k += nt) {
+    const int e = k / D, d = k - e * D;
+    const int j = mvc_vp_ov.j[e];
+    if (!mvc_vp_ov.s1x[e] || !vp_entry_final(e, nc, V, j)) continue;
+    const int v = (e >> 1) % kVpV;
+    if (chk && !run_chk(j < cc.Klist[v], 1, i0, e, v, j, cc.Klist[v])) continue;
+    const double x = ovs1[(size_t)e * D + d];
+    cc.S1T[((size_t)v * D + d) * ks + j] = x;
+    gst(&P.S1T[((size_t)v * D + d) * KC + j], x);
   }
   if (tid >= 64 && tid < 64 + V) {
     const int v = tid - 64;
@@ -3582,13 +3589,7 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
     const int e = tid - 128, mvv = e >> 1, m = mvv / kVpV, v = mvv - m * kVpV;
     const int j = mvc_vp_ov.j[e];
     if (m < nc && v < V && j >= 0) {
-      bool fin = !((e & 1) == 0 && mvc_vp_ov.j[e + 1] == j);   // j0 == j1: the joined entry writes
-#pragma unroll
-      for (int m2 = 0; m2 < kVpMoves; ++m2)
-        if (m2 > m && m2 < nc) {
-          const int e2 = (m2 * kVpV + v) * 2;
-          if (mvc_vp_ov.j[e2] == j || mvc_vp_ov.j[e2 + 1] == j) fin = false;
-        }
+      bool fin = vp_entry_final(e, nc, V, j);
       if (chk && !run_chk(j < cc.Klist[v], 3, i0, e, v, j, cc.Klist[v])) fin = false;
       if (fin) {
         cc.d_n[v * ks + j] = mvc_vp_ov.dn[e];
@@ -3607,9 +3608,9 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
       }
     }
   }
-  // the tables (last touch), T_ne, z and the move count
-  if (tid < 2 * kVpMoves) {
-    const int m = tid >> 1, which = tid & 1;
+  // the tables (last touch), T_ne, z and the move count (wave 3)
+  if (tid >= 192 && tid < 192 + 2 * kVpMoves) {
+    const int m = (tid - 192) >> 1, which = tid & 1;
     if (m < nc && mvc_vp_ov.mv[m]) {
       const int p = which ? mvc_vp_ov.c[m] : mvc_vp_ov.p0[m];
       bool fin = true;
@@ -3627,7 +3628,7 @@ __device__ __forceinline__ void vp_commit(SeqArgs &A, const SCache &cc, const Vp
       }
       if (which == 0) gst(&P.z[i0 + m], mvc_vp_ov.c[m]);
     }
-    if (tid == 0) {
+    if (tid == 192) {
       *cc.T_ne = mvc_vp_ov.tne[last];
       gst(&R->T_ne, mvc_vp_ov.tne[last]);
       cnt[0] += nmv;
@@ -3772,7 +3773,7 @@ __device__ __forceinline__ int seq_run_loop_vp(SeqArgs &A, const SeqLds &L, cons
     // depth >= 1 here: cur < n)
     const bool pbirth = a == depth && depth > 0 && mvc_vp_ov.pcs[depth - 1] < 0;
     const int nc = pbirth ? depth - 1 : a;   // customers whose held predictions commit from the overlay
-    vp_commit(A, cc, M, i0, nc, yr, U.cnt, L.chk);
+    vp_commit(A, cc, M, i0, nc, yr, ovs1, U.cnt, L.chk);
     int mlast = -1;   // the last mover decided in this step
 #pragma unroll
     for (int k = 0; k < kVpMoves; ++k)
