@@ -3703,6 +3703,7 @@ class ParallelSampler : public Sampler {
     dim3 eg;
     bool vp_ok = true, early_mh = false;
     bool birth_retry = false;   // a capacity growth interrupted a birth: the birth kernel follows the next run kernel
+    bool birth_between = false; // the small lane loop: the birth kernel before every round but the batch's first
     int rounds = 1;
     hipEvent_t e1 = nullptr;
   };
@@ -3770,7 +3771,8 @@ class ParallelSampler : public Sampler {
         L.dyn = run_dyn(L);
         L.fill = lds_fill_byte();
         L.chk = run_check() ? 1 : 0;
-        if (L.lc == 3 && L.small && rr.birth_retry) {   // the small lane loop left a birth pending: commit it first
+        if (L.lc == 3 && L.small && (rr.birth_retry || (rr.birth_between && r > 0))) {
+          // the small lane loop left a birth pending: commit it first (a no-op without one)
           rr.birth_retry = false;
           hipLaunchKernelGGL(mvc_seq_birth_kernel, dim3(1), dim3(kSeqRunThreads), 0, stream, rr.Q);
           MVC_HIP(hipGetLastError());
@@ -3922,6 +3924,14 @@ class ParallelSampler : public Sampler {
   // the same state in the same order as repair_finish's.
   void repair_lane_tail(Chain &c, uint32_t s, RepairRun &rr) {
     if (!rs_ev) MVC_HIP(hipEventCreateWithFlags(&rs_ev, hipEventDisableTiming));
+    if (rr.L.lc == 3 && rr.L.small) {
+      // the small instance ends its launch at a birth (~0.2 per sweep): a
+      // birth launch and a second round behind the first, so such a sweep
+      // needs no second host round trip (both are no-ops after a sweep
+      // without a birth)
+      rr.rounds = 2;
+      rr.birth_between = true;
+    }
     for (;;) {
       repair_rounds(c, s, rr);
       hipLaunchKernelGGL(mvc_seq_compact_kernel, dim3(1), dim3(1024), 0, stream, rr.Q, c.pos_new, c.jmap, 1);
