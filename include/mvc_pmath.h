@@ -65,7 +65,34 @@ MVC_PM double mvc_u2d(uint64_t u) { double x; __builtin_memcpy(&x, &u, 8); retur
         K(2.505210838544172e-08), K(2.755731922398589e-07), K(2.7557319223985893e-06),             \
         K(2.48015873015873e-05), K(0.0001984126984126984), K(0.001388888888888889),                \
         K(0.008333333333333333), K(0.041666666666666664), K(0.16666666666666666))
+/* The same steps for two independent arguments interleaved in one block
+ * (each value's instructions and operands unchanged, so the same bits): two
+ * exps' dependent chains overlap where one wave per SIMD has nothing else to
+ * issue. */
+#define MVC_HORNER12X2(p, q, r, s, K0, K)                                                            \
+  asm("v_fma_f64 %0, %4, %2, %5\n\tv_fma_f64 %1, %4, %3, %5\n\t"                                       \
+      "v_fma_f64 %0, %0, %2, %6\n\tv_fma_f64 %1, %1, %3, %6\n\t"                                       \
+      "v_fma_f64 %0, %0, %2, %7\n\tv_fma_f64 %1, %1, %3, %7\n\t"                                       \
+      "v_fma_f64 %0, %0, %2, %8\n\tv_fma_f64 %1, %1, %3, %8\n\t"                                       \
+      "v_fma_f64 %0, %0, %2, %9\n\tv_fma_f64 %1, %1, %3, %9\n\t"                                       \
+      "v_fma_f64 %0, %0, %2, %10\n\tv_fma_f64 %1, %1, %3, %10\n\t"                                     \
+      "v_fma_f64 %0, %0, %2, %11\n\tv_fma_f64 %1, %1, %3, %11\n\t"                                     \
+      "v_fma_f64 %0, %0, %2, %12\n\tv_fma_f64 %1, %1, %3, %12\n\t"                                     \
+      "v_fma_f64 %0, %0, %2, %13\n\tv_fma_f64 %1, %1, %3, %13\n\t"                                     \
+      "v_fma_f64 %0, %0, %2, %14\n\tv_fma_f64 %1, %1, %3, %14\n\t"                                     \
+      "v_fma_f64 %0, %0, %2, %15\n\tv_fma_f64 %1, %1, %3, %15"                                         \
+      : "=&v"(p), "=&v"(q)                                                                         \
+      : "v"(r), "v"(s), K0(1.1470745597729725e-11), K(1.6059043836821613e-10),                     \
+        K(2.08767569878681e-09), K(2.505210838544172e-08), K(2.755731922398589e-07),               \
+        K(2.7557319223985893e-06), K(2.48015873015873e-05), K(0.0001984126984126984),              \
+        K(0.001388888888888889), K(0.008333333333333333), K(0.041666666666666664),                 \
+        K(0.16666666666666666))
 #else
+#define MVC_HORNER12X2(p, q, r, s, K0, K) \
+  do {                                    \
+    MVC_HORNER12(p, r, K0, K);            \
+    MVC_HORNER12(q, s, K0, K);            \
+  } while (0)
 #define MVC_HORNER12(p, r, K0, K)                                                                   \
   do {                                                                                              \
     p = __builtin_fma(1.1470745597729725e-11, r, 1.6059043836821613e-10);                           \
@@ -195,6 +222,36 @@ static __device__ __forceinline__ double mvc_exp_le0(double x) {
   return (x < -745.1332191019412) ? 0.0 : res;
 #else
   return mvc_exp(x);
+#endif
+}
+/* Two mvc_exp_le0 at once (MVC_HORNER12X2): the same value for each. */
+static __device__ __forceinline__ void mvc_exp_le0_x2(double x0, double x1, double &e0, double &e1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double shifter = 6755399441055744.0;
+  double kd0 = x0 * MVC_INVLN2, kd1 = x1 * MVC_INVLN2;
+  kd0 = kd0 + shifter;
+  kd1 = kd1 + shifter;
+  kd0 = kd0 - shifter;
+  kd1 = kd1 - shifter;
+  kd0 = __builtin_fmin(__builtin_fmax(kd0, -1100.0), 1100.0);
+  kd1 = __builtin_fmin(__builtin_fmax(kd1, -1100.0), 1100.0);
+  const int k0 = (int)kd0, k1 = (int)kd1;
+  double r0 = __builtin_fma(-kd0, MVC_LN2_HI, x0), r1 = __builtin_fma(-kd1, MVC_LN2_HI, x1);
+  r0 = __builtin_fma(-kd0, MVC_LN2_LO, r0);
+  r1 = __builtin_fma(-kd1, MVC_LN2_LO, r1);
+  double p0, p1;
+  MVC_HORNER12X2(p0, p1, r0, r1, "v", "v");
+  p0 = __builtin_fma(p0, r0, 0.5);
+  p1 = __builtin_fma(p1, r1, 0.5);
+  p0 = __builtin_fma(p0, r0, 1.0);
+  p1 = __builtin_fma(p1, r1, 1.0);
+  const double a0 = __builtin_fma(p0, r0, 1.0), a1 = __builtin_fma(p1, r1, 1.0);
+  const double res0 = __builtin_amdgcn_ldexp(a0, k0), res1 = __builtin_amdgcn_ldexp(a1, k1);
+  e0 = (x0 < -745.1332191019412) ? 0.0 : res0;
+  e1 = (x1 < -745.1332191019412) ? 0.0 : res1;
+#else
+  e0 = mvc_exp(x0);
+  e1 = mvc_exp(x1);
 #endif
 }
 /* mvc_exp_le0 with the Horner coefficients as SGPR operands (bitwise equal):

@@ -3990,11 +3990,16 @@ __device__ __forceinline__ int seq_resample_lane8(const SeqArgs &A, const SView 
         if (x[u] > mx) mx = x[u];
       }
     m = lfn > mx ? lfn : mx;
+    static_assert(KB % 2 == 0, "dishes in pairs");
 #pragma unroll
-    for (int u = 0; u < KB; ++u) {
-      double w = (double)l[u] - sigma;
-      if (w < 0.0) w = 0.0;
-      col[u] = col[u] + w * mvc_exp_le0(l[u] > 0 ? x[u] - m : -MVC_PM_INF);
+    for (int u = 0; u < KB; u += 2) {   // two exps interleaved (mvc_exp_le0_x2: the same values)
+      double w0 = (double)l[u] - sigma, w1 = (double)l[u + 1] - sigma;
+      if (w0 < 0.0) w0 = 0.0;
+      if (w1 < 0.0) w1 = 0.0;
+      double e0, e1;
+      mvc_exp_le0_x2(l[u] > 0 ? x[u] - m : -MVC_PM_INF, l[u + 1] > 0 ? x[u + 1] - m : -MVC_PM_INF, e0, e1);
+      col[u] = col[u] + w0 * e0;
+      col[u + 1] = col[u + 1] + w1 * e1;
     }
   } else {
     // pass 1: max over the included dishes, K_act; the first 16 lp kept
